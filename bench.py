@@ -1,0 +1,173 @@
+#!/usr/bin/env python3
+"""Benchmark: timesteps/s of the RSW 2048² FilteredAB3 fp64 step (BASELINE.json
+metric) on N MI355X, plus the roofline of the dominant kernel and the CPU
+baseline (the oracle restatement, scipy.fft on the host cores).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+N > 1 is launched by torch.distributed.run, one process per GPU.  Each rank
+steps its own 2048² problem (replicas, weak scaling) until the slab
+decomposition lands; value = all ranks' steps / max-over-ranks time.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+# SURVEY §8(d) B_alg model (fp64): b_T = 16 Ns + 8 Np per logical 2D transform
+def b_alg(model, stepper, n):
+    Ns, Np = (n // 2 + 1) * n, n * n
+    bT = 16 * Ns + 8 * Np
+    if model == "rsw":
+        return 13 * bT + (18 if stepper == "FilteredAB3" else 15) * 16 * Ns
+    if stepper == "IFMRK4":
+        return 40 * bT + 30 * 16 * Ns
+    return 10 * bT + 10 * 16 * Ns
+
+
+def cpu_baseline(model, stepper, n, budget_s=20.0, max_steps=20):
+    """Time the oracle (fp64 numpy/scipy restatement) on the host cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import sw_cases
+    import sw_oracle as O
+
+    cores = min(16, len(os.sched_getaffinity(0)))
+    O.set_fft_workers(cores)
+    p = sw_cases.case_params(f"{model}_{ {'FilteredAB3': 'fab3', 'IFMAB3': 'ifmab3', 'IFMRK4': 'ifmrk4'}[stepper]}", n)
+    pr = sw_cases.oracle_problem(p)
+    pr.set_solution(sw_cases.initial_condition(p, pr.grid))
+    pr.stepforward(3)  # the Euler start-up steps, untimed
+    t0 = time.perf_counter()
+    k = 0
+    while k < max_steps and (time.perf_counter() - t0) < budget_s:
+        pr.stepforward(1)
+        k += 1
+    dt = time.perf_counter() - t0
+    O.set_fft_workers(None)
+    return dict(value=k / dt, unit="timesteps/s", cores=cores, kind="port",
+                sample=f"{k} AB3 steps of the {n}² oracle restatement (numpy elementwise + scipy.fft "
+                       f"workers={cores}) after 3 untimed Euler steps")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--n", type=int, default=2048)
+    ap.add_argument("--model", default="rsw", choices=["rsw", "qg2"])
+    ap.add_argument("--stepper", default="FilteredAB3", choices=["FilteredAB3", "IFMAB3", "IFMRK4"])
+    ap.add_argument("--profile-steps", type=int, default=50)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_rsw2048_fab3.json"))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    def barrier_sync():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    from juliaraytracingsw_amd import drivers
+
+    if args.model == "rsw":
+        prob, P = drivers.rsw_problem(args.n, args.stepper, device=local)
+    else:
+        prob, P = drivers.qg2_problem(args.n, args.stepper, device=local)
+
+    prob.stepforward(args.warmup)
+    barrier_sync()
+    t0 = time.perf_counter()
+    prob.stepforward(args.steps)  # sw_step returns when its stream is drained
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # roofline: per-kernel HIP-event durations on libsw's stream
+    stats = prob.ctx.profile(args.profile_steps)
+    step_alg = prob.ctx.step_alg_bytes()
+    prob.close()
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    dom = max(stats, key=lambda s: s["avg_ms"] * s["launches"])
+    achieved = dom["alg_bytes"] / (dom["avg_ms"] * 1e-3) / 1e9
+    traffic = None
+    try:
+        tj = json.load(open(args.traffic_json))
+        if tj.get("config") == f"{args.model}{args.n}_{args.stepper}":
+            traffic = tj["kernels"].get(dom["name"])
+    except Exception:
+        traffic = None
+    for s in stats:
+        gbps = s["alg_bytes"] / (s["avg_ms"] * 1e-3) / 1e9
+        print(f"[bench] {s['name']:>10s}: {s['avg_ms'] * 1e3:8.1f} us/launch  x{s['launches'] / args.profile_steps:.0f}/step"
+              f"  alg {s['alg_bytes'] / 1e6:7.1f} MB  -> {gbps:7.0f} GB/s ({gbps / HBM_PEAK_GBPS:.1%} of HBM peak)",
+              file=sys.stderr)
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * args.steps / elapsed
+    balg = b_alg(args.model, args.stepper, args.n)
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.model, args.stepper, args.n)
+    out = {
+        "metric": f"timesteps/sec, {args.model.upper()} {args.n}^2 {args.stepper} fp64 (BASELINE.json metric)",
+        "value": value,
+        "unit": "timesteps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic random-phase IC (set_shafer_initial_condition!, seeded)" if args.model == "rsw"
+                else "synthetic randn PV IC (set_seed_initial_condition!, seeded)",
+        "config": {"workload": f"{args.model.upper()} {args.n}^2 {args.stepper} fp64 step, dt={P['dt']:.6g}",
+                   "grid": args.n, "parallelism": "replicas" if world > 1 else "single-gpu"},
+        "b_alg_bytes_per_step": balg,
+        "b_alg_GBps": balg * value / world / 1e9,
+        "b_alg_frac_of_peak": balg * value / world / 1e9 / HBM_PEAK_GBPS,
+        "libsw_alg_bytes_per_step": step_alg,
+        "roofline": {"bound": "hbm", "kernel": dom["name"], "achieved": achieved, "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                     "alg_bytes_per_launch": dom["alg_bytes"], "avg_us_per_launch": dom["avg_ms"] * 1e3},
+        "kernels": [{"name": s["name"], "avg_us": s["avg_ms"] * 1e3, "per_step": s["launches"] / args.profile_steps,
+                     "alg_bytes": s["alg_bytes"]} for s in stats],
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

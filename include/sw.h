@@ -1,0 +1,155 @@
+/*
+ * libsw — MI355X-native pseudo-spectral time-step core (C ABI).
+ *
+ * Drop-in boundary for the per-timestep hot path of ndefilippis/JuliaRaytracingSW
+ * (SURVEY.md §8b).  The reference plugs a time stepper into FourierFlows by
+ * defining
+ *     FourierFlows.stepforward!(sol, clock, ts::IFMAB3TimeStepper, equation,
+ *                               vars, params, grid)          utils/IFMAB3.jl:157
+ * which calls equation.calcN!(N, sol, t, clock, vars, params, grid)
+ * (rsw/RotatingShallowWater.jl:140, swqg/TwoLayerQG.jl:152).  Drivers call
+ * FF's stepforward!(prob, diags, nsteps) (rsw/RSWDriver.jl:212,
+ * swqg/TwoLayerDriver.jl:105).  Every entry point below replaces one of those
+ * seams; a Julia `ccall` shim binding them is given in INTEGRATION.md.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only; no exceptions cross the ABI.
+ *  - Return codes: 0 = ok, < 0 = error (see SW_E_*); sw_last_error() has text.
+ *  - Spectral state layout = Julia column-major (nkr, nl, nfield) of interleaved
+ *    complex (re, im) doubles: element (kr, l, f) at ((f*nl + l)*nkr + kr).
+ *    Byte-identical to a Julia Array{ComplexF64,3} `prob.sol`.
+ *  - Physical fields: Julia (nx, ny) column-major doubles, x fastest.
+ *  - The library owns all device memory.  Caller buffers are host memory and
+ *    are copied synchronously.  A context is driven by one host thread.
+ */
+#ifndef SW_H
+#define SW_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SW_ABI_VERSION 1
+
+/* models */
+#define SW_MODEL_RSW 0   /* rsw/RotatingShallowWater.jl: fields (u, v, η), 3×3 L   */
+#define SW_MODEL_QG2 1   /* swqg/TwoLayerQG.jl: fields (q1, q2), 2×2 L             */
+
+/* steppers */
+#define SW_STEP_FILTERED_AB3 0 /* FF FilteredAB3 with per-mode matvec L·sol */
+#define SW_STEP_IFMAB3       1 /* utils/IFMAB3.jl:68-169                               */
+#define SW_STEP_IFMRK4       2 /* Lawson IF-RK4, the build's definition of utils/IFMRK4.jl (A9) */
+
+/* error codes */
+#define SW_OK            0
+#define SW_E_INVALID    -1  /* bad argument / unsupported configuration   */
+#define SW_E_NOMEM      -2  /* device allocation failed                   */
+#define SW_E_HIP        -3  /* HIP runtime error                          */
+#define SW_E_COMM       -4  /* RCCL error                                 */
+#define SW_E_NAN        -5  /* NaN/Inf detected in the state after a step */
+#define SW_E_STATE      -6  /* call out of order                          */
+
+/* physical-field ids for sw_get_physical (updatevars! equivalents)
+ * RSW (rsw/RotatingShallowWater.jl:101-116): u, v, η, ζ=∂x v − ∂y u − f η
+ * QG2 (swqg/TwoLayerQG.jl:113-129), per layer (layer = id / 8): q, ψ, ζ, u, v */
+#define SW_PHYS_U     0
+#define SW_PHYS_V     1
+#define SW_PHYS_ETA   2
+#define SW_PHYS_ZETA  3
+#define SW_PHYS_Q     4
+#define SW_PHYS_PSI   5
+
+/* diagnostic ids for sw_diag */
+#define SW_DIAG_NAN   0  /* 1.0 if any NaN/Inf in the state              */
+#define SW_DIAG_KE    1  /* RSW: kinetic_energy; QG2: KE layer 1 + layer 2 */
+#define SW_DIAG_PE    2  /* potential_energy                              */
+
+typedef struct sw_config {
+  int32_t abi_version;      /* must be SW_ABI_VERSION                      */
+  int32_t model;            /* SW_MODEL_*                                  */
+  int32_t stepper;          /* SW_STEP_*                                   */
+  int32_t nx, ny;           /* grid points (powers of two, 16 … 8192)      */
+  double  Lx, Ly;           /* domain lengths                              */
+  double  aliased_fraction; /* FF TwoDGrid aliased_fraction, in (0,1)      */
+  double  dt;               /* time step                                   */
+  /* physics — RSW Params (rsw/RotatingShallowWater.jl:18-23)              */
+  double  f, Cg;            /* Coriolis, gravity-wave speed (Cg2 = Cg²)    */
+  double  nu;               /* hyperviscosity ν                            */
+  int32_t nnu;              /* hyperviscous order nν                       */
+  /* physics — QG2 Params (swqg/TwoLayerQG.jl:23-30)                       */
+  double  U, mu, F;         /* shear, bottom drag, F = 2f0²/Cg²/δρρ0       */
+  /* filter — FF makefilter kwargs (utils/IFMAB3.jl:80-84)                 */
+  int32_t use_filter;       /* IF steppers only; FilteredAB3 always filters */
+  int32_t filter_order;
+  double  filter_innerK, filter_outerK, filter_tol;
+  /* device / multi-GPU                                                    */
+  int32_t device;           /* HIP device ordinal                          */
+  int32_t check_nan;        /* if nonzero, sw_step returns SW_E_NAN on blow-up */
+  int32_t nop_calcN;        /* 1: N ≡ 0, the reference's NOPcalcN! hook
+                               (rsw/RotatingShallowWater.jl:135-138,305)    */
+  int32_t nranks, rank;     /* slab decomposition (1, 0 = single GPU)      */
+  const void* comm_unique_id; /* ncclUniqueId bytes (nranks > 1)           */
+} sw_config;
+
+typedef struct sw_ctx sw_ctx;
+
+typedef struct sw_kernel_stat {
+  char    name[48];
+  int64_t launches;
+  double  avg_ms;          /* mean HIP-event duration per launch           */
+  double  alg_bytes;       /* algorithmic HBM bytes per launch */
+} sw_kernel_stat;
+
+/* Fill *cfg with the reference defaults (RotatingShallowWater.Problem, :70-85). */
+void sw_config_default(sw_config* cfg);
+
+/* Problem(dev; …) + Equation + XTimeStepper construction
+ * (rsw/RotatingShallowWater.jl:70-99, swqg/TwoLayerQG.jl:55-90,
+ *  utils/IFMAB3.jl:68-88).  State and history start at zero, clock at 0. */
+int sw_create(sw_ctx** ctx, const sw_config* cfg);
+void sw_destroy(sw_ctx* ctx);
+const char* sw_last_error(const sw_ctx* ctx);
+
+/* sizes: nkr, nl, nfield (for the caller's buffers) */
+int sw_get_dims(const sw_ctx* ctx, int32_t* nkr, int32_t* nl, int32_t* nfield);
+
+/* set_solution! (rsw/RotatingShallowWater.jl:309-321, swqg/TwoLayerQG.jl:220-228):
+ * copies `sol` (column-major (nkr,nl,nf) complex128) and dealiases it. */
+int sw_set_state(sw_ctx* ctx, const void* sol, size_t bytes);
+/* Array(prob.sol): the (dealiased) state, aliased modes = 0. */
+int sw_get_state(const sw_ctx* ctx, void* sol, size_t bytes);
+
+int sw_set_clock(sw_ctx* ctx, double t, int64_t step);
+int sw_get_clock(const sw_ctx* ctx, double* t, int64_t* step);
+
+/* stepforward!(prob, nsteps): nsteps × stepforward!(sol, clock, ts, …). */
+int sw_step(sw_ctx* ctx, int64_t nsteps);
+
+/* equation.calcN!(N, sol, …) on a caller state (no stepping, clock untouched):
+ * N = calcN(dealias(sol)), column-major (nkr,nl,nf) complex128; aliased modes 0. */
+int sw_calcN(sw_ctx* ctx, const void* sol, void* N, size_t bytes);
+
+/* updatevars! equivalent: one physical field of the current state. */
+int sw_get_physical(sw_ctx* ctx, int32_t field_id, double* out, size_t bytes);
+
+/* Scalar diagnostics of the current state (SW_DIAG_*). */
+int sw_diag(sw_ctx* ctx, int32_t diag_id, double* out);
+
+/* Per-kernel HIP-event timing of `nsteps` steps (the state advances).
+ * Fills up to max_stats entries; *n_stats receives the count. */
+int sw_profile_steps(sw_ctx* ctx, int64_t nsteps, sw_kernel_stat* stats,
+                     int32_t max_stats, int32_t* n_stats);
+
+/* Algorithmic HBM bytes of one step of the configured path. */
+double sw_step_alg_bytes(const sw_ctx* ctx);
+
+/* Multi-GPU: write an RCCL unique id (128 bytes) for rank 0 to broadcast. */
+int sw_comm_unique_id(void* out128);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SW_H */

@@ -1,0 +1,191 @@
+"""ctypes binding of libsw.so (include/sw.h).
+
+The product path has no CPU fallback: if the HIP library is missing or fails
+to load, every entry point raises ``LibSWError`` loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+SW_ABI_VERSION = 1
+SW_MODEL_RSW, SW_MODEL_QG2 = 0, 1
+SW_STEP_FILTERED_AB3, SW_STEP_IFMAB3, SW_STEP_IFMRK4 = 0, 1, 2
+SW_OK, SW_E_INVALID, SW_E_NOMEM, SW_E_HIP, SW_E_COMM, SW_E_NAN, SW_E_STATE = 0, -1, -2, -3, -4, -5, -6
+SW_PHYS_U, SW_PHYS_V, SW_PHYS_ETA, SW_PHYS_ZETA, SW_PHYS_Q, SW_PHYS_PSI = 0, 1, 2, 3, 4, 5
+SW_DIAG_NAN, SW_DIAG_KE, SW_DIAG_PE = 0, 1, 2
+
+STEPPERS = {"FilteredAB3": SW_STEP_FILTERED_AB3, "IFMAB3": SW_STEP_IFMAB3, "IFMRK4": SW_STEP_IFMRK4}
+
+# every symbol include/sw.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "sw_config_default", "sw_create", "sw_destroy", "sw_last_error", "sw_get_dims",
+    "sw_set_state", "sw_get_state", "sw_set_clock", "sw_get_clock", "sw_step", "sw_calcN",
+    "sw_get_physical", "sw_diag", "sw_profile_steps", "sw_step_alg_bytes", "sw_comm_unique_id",
+]
+
+
+class LibSWError(RuntimeError):
+    """Raised for any libsw failure (load failure or a negative return code)."""
+
+    def __init__(self, msg, code=None):
+        super().__init__(msg)
+        self.code = code
+
+
+class SwConfig(C.Structure):
+    _fields_ = [
+        ("abi_version", C.c_int32), ("model", C.c_int32), ("stepper", C.c_int32),
+        ("nx", C.c_int32), ("ny", C.c_int32),
+        ("Lx", C.c_double), ("Ly", C.c_double), ("aliased_fraction", C.c_double), ("dt", C.c_double),
+        ("f", C.c_double), ("Cg", C.c_double), ("nu", C.c_double), ("nnu", C.c_int32),
+        ("U", C.c_double), ("mu", C.c_double), ("F", C.c_double),
+        ("use_filter", C.c_int32), ("filter_order", C.c_int32),
+        ("filter_innerK", C.c_double), ("filter_outerK", C.c_double), ("filter_tol", C.c_double),
+        ("device", C.c_int32), ("check_nan", C.c_int32), ("nop_calcN", C.c_int32), ("nranks", C.c_int32), ("rank", C.c_int32),
+        ("comm_unique_id", C.c_void_p),
+    ]
+
+
+class SwKernelStat(C.Structure):
+    _fields_ = [("name", C.c_char * 48), ("launches", C.c_int64), ("avg_ms", C.c_double),
+                ("alg_bytes", C.c_double)]
+
+
+_LIB = None
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsw.so")
+
+
+def load(path: str | None = None):
+    """Load libsw.so (once).  Raises LibSWError if it is missing."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    p = path or os.environ.get("LIBSW_PATH") or LIB_PATH
+    if not os.path.exists(p):
+        raise LibSWError(f"libsw.so not found at {p}: run __graft_entry__.build() (hipcc, gfx950)")
+    try:
+        lib = C.CDLL(p)
+    except OSError as e:  # pragma: no cover
+        raise LibSWError(f"failed to load {p}: {e}") from e
+    vp, i32, i64, dbl, sz = C.c_void_p, C.c_int32, C.c_int64, C.c_double, C.c_size_t
+    sig = {
+        "sw_config_default": (None, [C.POINTER(SwConfig)]),
+        "sw_create": (C.c_int, [C.POINTER(vp), C.POINTER(SwConfig)]),
+        "sw_destroy": (None, [vp]),
+        "sw_last_error": (C.c_char_p, [vp]),
+        "sw_get_dims": (C.c_int, [vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]),
+        "sw_set_state": (C.c_int, [vp, vp, sz]),
+        "sw_get_state": (C.c_int, [vp, vp, sz]),
+        "sw_set_clock": (C.c_int, [vp, dbl, i64]),
+        "sw_get_clock": (C.c_int, [vp, C.POINTER(dbl), C.POINTER(i64)]),
+        "sw_step": (C.c_int, [vp, i64]),
+        "sw_calcN": (C.c_int, [vp, vp, vp, sz]),
+        "sw_get_physical": (C.c_int, [vp, i32, vp, sz]),
+        "sw_diag": (C.c_int, [vp, i32, C.POINTER(dbl)]),
+        "sw_profile_steps": (C.c_int, [vp, i64, C.POINTER(SwKernelStat), i32, C.POINTER(i32)]),
+        "sw_step_alg_bytes": (dbl, [vp]),
+        "sw_comm_unique_id": (C.c_int, [vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = lib
+    return lib
+
+
+def default_config() -> SwConfig:
+    lib = load()
+    cfg = SwConfig()
+    lib.sw_config_default(C.byref(cfg))
+    return cfg
+
+
+class Context:
+    """Owning handle around one ``sw_ctx`` (one GPU, one problem)."""
+
+    def __init__(self, cfg: SwConfig):
+        self.lib = load()
+        self._h = C.c_void_p()
+        self.cfg = cfg
+        rc = self.lib.sw_create(C.byref(self._h), C.byref(cfg))
+        if rc != SW_OK:
+            msg = self.lib.sw_last_error(self._h).decode() if self._h else "sw_create failed"
+            self.lib.sw_destroy(self._h)
+            self._h = C.c_void_p()
+            raise LibSWError(f"sw_create: {msg} (code {rc})", rc)
+        nkr, nl, nf = C.c_int32(), C.c_int32(), C.c_int32()
+        self._check(self.lib.sw_get_dims(self._h, C.byref(nkr), C.byref(nl), C.byref(nf)), "sw_get_dims")
+        self.nkr, self.nl, self.nf = nkr.value, nl.value, nf.value
+
+    def _check(self, rc, what):
+        if rc != SW_OK:
+            raise LibSWError(f"{what}: {self.lib.sw_last_error(self._h).decode()} (code {rc})", rc)
+
+    def close(self):
+        if self._h:
+            self.lib.sw_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- state: numpy [nf][nl][nkr] complex128 == Julia (nkr, nl, nf) -------
+    @property
+    def state_shape(self):
+        return (self.nf, self.nl, self.nkr)
+
+    def set_state(self, sol):
+        a = np.ascontiguousarray(sol, dtype=np.complex128)
+        if a.shape != self.state_shape:
+            raise ValueError(f"state shape {a.shape} != {self.state_shape}")
+        self._check(self.lib.sw_set_state(self._h, a.ctypes.data, a.nbytes), "sw_set_state")
+
+    def get_state(self):
+        a = np.empty(self.state_shape, np.complex128)
+        self._check(self.lib.sw_get_state(self._h, a.ctypes.data, a.nbytes), "sw_get_state")
+        return a
+
+    def calcN(self, sol):
+        a = np.ascontiguousarray(sol, dtype=np.complex128)
+        out = np.empty(self.state_shape, np.complex128)
+        self._check(self.lib.sw_calcN(self._h, a.ctypes.data, out.ctypes.data, a.nbytes), "sw_calcN")
+        return out
+
+    def set_clock(self, t, step):
+        self._check(self.lib.sw_set_clock(self._h, float(t), int(step)), "sw_set_clock")
+
+    def get_clock(self):
+        t, s = C.c_double(), C.c_int64()
+        self._check(self.lib.sw_get_clock(self._h, C.byref(t), C.byref(s)), "sw_get_clock")
+        return t.value, s.value
+
+    def step(self, n=1):
+        self._check(self.lib.sw_step(self._h, int(n)), "sw_step")
+
+    def physical(self, field_id, ny, nx):
+        out = np.empty((ny, nx), np.float64)
+        self._check(self.lib.sw_get_physical(self._h, int(field_id), out.ctypes.data, out.nbytes),
+                    "sw_get_physical")
+        return out
+
+    def diag(self, diag_id):
+        v = C.c_double()
+        self._check(self.lib.sw_diag(self._h, int(diag_id), C.byref(v)), "sw_diag")
+        return v.value
+
+    def profile(self, nsteps):
+        st = (SwKernelStat * 16)()
+        n = C.c_int32()
+        self._check(self.lib.sw_profile_steps(self._h, int(nsteps), st, 16, C.byref(n)), "sw_profile_steps")
+        return [dict(name=st[i].name.decode(), launches=st[i].launches, avg_ms=st[i].avg_ms,
+                     alg_bytes=st[i].alg_bytes) for i in range(n.value)]
+
+    def step_alg_bytes(self):
+        return self.lib.sw_step_alg_bytes(self._h)

@@ -1,0 +1,532 @@
+// libsw host runtime: context lifecycle, stepper sequencing and the C ABI of
+// include/sw.h.  One HIP stream per context; every call that returns data
+// synchronises that stream.  Reference seams replaced are cited per function.
+#include "sw.h"
+#include "sw_internal.hpp"
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+using sw::Geom;
+using sw::Phys;
+
+struct KStat {
+  const char* name;
+  int64_t launches = 0;
+  double ms = 0.0;
+  double bytes = 0.0;
+};
+
+struct sw_ctx {
+  sw_config cfg{};
+  Geom g{};
+  Phys p{};
+  int nf = 0, ninv = 0, nfwd = 0;
+  hipStream_t stream = nullptr;
+  double2 *tw_x = nullptr, *tw_y = nullptr;
+  double2* sol = nullptr;                    // compact state, nf fields
+  double2* hist[3] = {nullptr, nullptr, nullptr};  // FAB3 RHS ring / IFMAB3 N ring
+  int head = 0;
+  double2 *E = nullptr, *E2 = nullptr;       // IF operators (E2 = exp(2Ldt) or exp(Ldt/2))
+  double2* rk[4] = {nullptr, nullptr, nullptr, nullptr};
+  double2* xs = nullptr;                     // RK4 stage input / scratch compact
+  double2 *minv = nullptr, *mfwd = nullptr;  // mixed-space fields
+  double2* stage = nullptr;                  // full (nkr,nl,nf) staging
+  double* dflt = nullptr;                    // physical staging / reductions
+  int* flag = nullptr;
+  double t = 0.0;
+  int64_t step = 0;
+  std::string err;
+  // profiling
+  bool prof = false;
+  std::vector<KStat> stats;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+namespace {
+
+int fail(sw_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                 \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess)                                                                \
+      return fail(ctx, SW_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));     \
+  } while (0)
+
+int ilog2(int n) {
+  int l = 0;
+  while ((1 << l) < n) ++l;
+  return l;
+}
+bool pow2(int n) { return n > 0 && (n & (n - 1)) == 0; }
+
+// FF getaliasedwavenumbers: 1-based iL = floor((1-af)/2 n) + 1,
+// iR = ceil((1+af)/2 n)
+void alias_range(int n, double af, int& iL, int& iR) {
+  const double L = (1 - af) / 2, R = (1 + af) / 2;
+  iL = (int)std::floor(L * n) + 1;
+  iR = (int)std::ceil(R * n);
+}
+
+int alloc(sw_ctx* c, void** p, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess) return fail(c, SW_E_NOMEM, std::string("hipMalloc failed: ") + hipGetErrorString(e));
+  e = hipMemsetAsync(*p, 0, bytes, c->stream);
+  if (e != hipSuccess) return fail(c, SW_E_HIP, hipGetErrorString(e));
+  return 0;
+}
+
+std::vector<double2> twiddles(int N) {
+  std::vector<double2> tw(N);
+  for (int m = 0; m < N; ++m) {
+    const long double a = 2.0L * 3.141592653589793238462643383279502884L * (long double)m / (long double)N;
+    tw[m] = make_double2((double)std::cos(a), (double)-std::sin(a));
+  }
+  return tw;
+}
+
+// --- algorithmic bytes per kernel launch ---------------------
+double live_field_bytes(const Geom& g) { return 16.0 * g.kc * g.Lr; }
+double mixed_field_bytes(const Geom& g) { return 16.0 * g.kc * g.ny; }
+
+enum KId { K_COLINV = 0, K_ROW, K_COLFWD, K_UPD, K_RK4STAGE, K_NKERN };
+const char* kname[K_NKERN] = {"col_inv", "row", "col_fwd", "update", "rk4_stage"};
+
+double kernel_bytes(const sw_ctx* c, int kid) {
+  const Geom& g = c->g;
+  const double F = live_field_bytes(g), M = mixed_field_bytes(g);
+  const int nf = c->nf;
+  switch (kid) {
+    case K_COLINV: return nf * F + c->ninv * M;
+    case K_ROW: return (c->ninv + c->nfwd) * M;
+    case K_COLFWD: return c->nfwd * M + nf * F;
+    case K_UPD:
+      if (c->cfg.stepper == SW_STEP_FILTERED_AB3) return 6 * nf * F;          // sol,N,R-1,R-2 in; sol,RHS out
+      if (c->cfg.stepper == SW_STEP_IFMAB3) return (5 * nf + 2 * nf * nf) * F;  // sol,N,N-1,N-2 in, sol out, E,E2
+      return (6 * nf + 2 * nf * nf) * F;                                      // RK4 final: u,k1..k4 in, u out, E,H
+    case K_RK4STAGE: return (3 * nf + 2 * nf * nf) * F;
+  }
+  return 0;
+}
+
+struct Timer {
+  sw_ctx* c;
+  int kid;
+  Timer(sw_ctx* c_, int k) : c(c_), kid(k) {
+    if (c->prof) (void)hipEventRecord(c->ev0, c->stream);
+  }
+  ~Timer() {
+    if (c->prof) {
+      (void)hipEventRecord(c->ev1, c->stream);
+      (void)hipEventSynchronize(c->ev1);
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
+      c->stats[kid].launches += 1;
+      c->stats[kid].ms += ms;
+    }
+  }
+};
+
+// equation.calcN!(N, X, …): col_inv -> row -> col_fwd
+void calcN(sw_ctx* c, const double2* X, double2* N) {
+  const int model = c->cfg.model;
+  if (c->cfg.nop_calcN) {  // NOPcalcN!: N .= 0
+    (void)hipMemsetAsync(N, 0, (size_t)c->nf * c->g.cfield * sizeof(double2), c->stream);
+    return;
+  }
+  {
+    Timer tm(c, K_COLINV);
+    sw::launch_col_inv(model, c->g, c->p, X, c->minv, c->tw_y, c->stream);
+  }
+  {
+    Timer tm(c, K_ROW);
+    sw::launch_row(model, c->g, c->p, c->minv, c->mfwd, c->tw_x, c->stream);
+  }
+  {
+    Timer tm(c, K_COLFWD);
+    sw::launch_col_fwd(model, c->g, c->p, c->mfwd, N, c->tw_y, c->stream);
+  }
+}
+
+// one stepforward!(sol, clock, ts, …)
+void step_once(sw_ctx* c) {
+  const int model = c->cfg.model;
+  const int st = c->cfg.stepper;
+  const int euler = c->step < 3 ? 1 : 0;
+  if (st == SW_STEP_FILTERED_AB3 || st == SW_STEP_IFMAB3) {
+    double2* N = c->hist[c->head];
+    double2* Nm1 = c->hist[(c->head + 2) % 3];
+    double2* Nm2 = c->hist[(c->head + 1) % 3];
+    calcN(c, c->sol, N);
+    Timer tm(c, K_UPD);
+    if (st == SW_STEP_FILTERED_AB3)
+      sw::launch_upd_fab3(model, c->g, c->p, c->sol, N, Nm1, Nm2, euler, c->stream);
+    else
+      sw::launch_upd_ifmab3(c->nf, c->g, c->p, c->sol, N, Nm1, Nm2, c->E, c->E2, euler, c->stream);
+    c->head = (c->head + 1) % 3;
+  } else {  // IFMRK4
+    calcN(c, c->sol, c->rk[0]);
+    {
+      Timer tm(c, K_RK4STAGE);
+      sw::launch_rk4_stage(c->nf, 1, c->g, c->p, c->sol, c->rk[0], c->E, c->E2, c->xs, c->stream);
+    }
+    calcN(c, c->xs, c->rk[1]);
+    {
+      Timer tm(c, K_RK4STAGE);
+      sw::launch_rk4_stage(c->nf, 2, c->g, c->p, c->sol, c->rk[1], c->E, c->E2, c->xs, c->stream);
+    }
+    calcN(c, c->xs, c->rk[2]);
+    {
+      Timer tm(c, K_RK4STAGE);
+      sw::launch_rk4_stage(c->nf, 3, c->g, c->p, c->sol, c->rk[2], c->E, c->E2, c->xs, c->stream);
+    }
+    calcN(c, c->xs, c->rk[3]);
+    Timer tm(c, K_UPD);
+    sw::launch_rk4_final(c->nf, c->g, c->p, c->sol, c->rk[0], c->rk[1], c->rk[2], c->rk[3], c->E,
+                         c->E2, c->stream);
+  }
+  c->t += c->cfg.dt;
+  c->step += 1;
+}
+
+size_t full_bytes(const sw_ctx* c) { return (size_t)c->nf * c->g.nkr * c->g.nl * sizeof(double2); }
+
+}  // namespace
+
+extern "C" {
+
+void sw_config_default(sw_config* cfg) {
+  std::memset(cfg, 0, sizeof(*cfg));
+  cfg->abi_version = SW_ABI_VERSION;
+  cfg->model = SW_MODEL_RSW;
+  cfg->stepper = SW_STEP_FILTERED_AB3;
+  cfg->nx = cfg->ny = 128;
+  cfg->Lx = cfg->Ly = 2 * M_PI;
+  cfg->aliased_fraction = 1.0 / 3.0;
+  cfg->dt = 5e-2;
+  cfg->f = 1.0;
+  cfg->Cg = 1.0;
+  cfg->nu = 1.0e-16;
+  cfg->nnu = 4;
+  cfg->U = 0.5;
+  cfg->mu = 1e-2;
+  cfg->F = 2 * 3.0 * 3.0 / 1.0 / 0.2;
+  cfg->use_filter = 0;
+  cfg->filter_order = 4;
+  cfg->filter_innerK = 0.65;
+  cfg->filter_outerK = 1.0;
+  cfg->filter_tol = 1e-15;
+  cfg->device = 0;
+  cfg->check_nan = 1;
+  cfg->nranks = 1;
+  cfg->rank = 0;
+}
+
+const char* sw_last_error(const sw_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int sw_create(sw_ctx** out, const sw_config* cfg) {
+  if (!out || !cfg) return SW_E_INVALID;
+  *out = nullptr;
+  if (cfg->abi_version != SW_ABI_VERSION) return SW_E_INVALID;
+  sw_ctx* c = new sw_ctx();
+  c->cfg = *cfg;
+  *out = c;
+  const sw_config& k = c->cfg;
+  if (k.model != SW_MODEL_RSW && k.model != SW_MODEL_QG2) return fail(c, SW_E_INVALID, "unknown model");
+  if (k.stepper < 0 || k.stepper > 2) return fail(c, SW_E_INVALID, "unknown stepper");
+  if (!pow2(k.nx) || !pow2(k.ny) || k.nx < 16 || k.ny < 16 || k.nx > 8192 || k.ny > 8192)
+    return fail(c, SW_E_INVALID, "nx, ny must be powers of two in [16, 8192]");
+  if (!(k.aliased_fraction > 0 && k.aliased_fraction < 1))
+    return fail(c, SW_E_INVALID, "aliased_fraction must be in (0,1)");
+  if (k.nranks != 1) return fail(c, SW_E_INVALID, "multi-GPU slab decomposition: use nranks == 1 in this build");
+  if (k.filter_order < 0) return fail(c, SW_E_INVALID, "filter_order must be >= 0");
+
+  int ndev = 0;
+  HIPCHK(c, hipGetDeviceCount(&ndev));
+  if (k.device < 0 || k.device >= ndev) return fail(c, SW_E_INVALID, "bad device ordinal");
+  HIPCHK(c, hipSetDevice(k.device));
+  HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  HIPCHK(c, hipEventCreate(&c->ev0));
+  HIPCHK(c, hipEventCreate(&c->ev1));
+
+  Geom& g = c->g;
+  g.nx = k.nx;
+  g.ny = k.ny;
+  g.log2nx = ilog2(k.nx);
+  g.log2ny = ilog2(k.ny);
+  g.nkr = k.nx / 2 + 1;
+  g.nl = k.ny;
+  int iLx, iRx, iLy, iRy;
+  alias_range(k.nx, k.aliased_fraction, iLx, iRx);
+  alias_range(k.ny, k.aliased_fraction, iLy, iRy);
+  g.kc = iLx - 1;
+  g.kcP = (g.kc + 63) / 64 * 64;
+  g.lc = iLy - 1;
+  g.lr2 = iRy;
+  g.Lr = g.lc + (k.ny - g.lr2);
+  g.LrP = (g.Lr + 7) / 8 * 8;
+  g.Lx = k.Lx;
+  g.Ly = k.Ly;
+  g.mk = (2 * M_PI / k.Lx * k.nx) / k.nx;
+  g.ml = (2 * M_PI / k.Ly * k.ny) / k.ny;
+  g.dx = k.Lx / k.nx;
+  g.dy = k.Ly / k.ny;
+  g.cfield = (long long)g.kc * g.LrP;
+  g.mfield = (long long)g.kcP * g.ny;
+  if (g.kc <= 0 || g.Lr <= 0 || g.lc > g.lr2) return fail(c, SW_E_INVALID, "degenerate dealiasing geometry");
+
+  Phys& p = c->p;
+  p.f = k.f;
+  p.Cg2 = k.Cg * k.Cg;
+  p.nu = k.nu;
+  p.nnu = k.nnu;
+  p.U = k.U;
+  p.mu = k.mu;
+  p.F = k.F;
+  p.dt = k.dt;
+  p.use_filter = (k.stepper == SW_STEP_FILTERED_AB3) ? 1 : (k.use_filter ? 1 : 0);
+  p.forder = k.filter_order;
+  p.innerK = k.filter_innerK;
+  p.decay = -std::log(k.filter_tol) / std::pow(k.filter_outerK - k.filter_innerK, (double)k.filter_order);
+
+  c->nf = k.model == SW_MODEL_RSW ? 3 : 2;
+  c->ninv = k.model == SW_MODEL_RSW ? 5 : 6;
+  c->nfwd = 4;
+
+  const size_t cb = (size_t)g.cfield * sizeof(double2);
+  const size_t mb = (size_t)g.mfield * sizeof(double2);
+  int rc;
+  if ((rc = alloc(c, (void**)&c->sol, c->nf * cb))) return rc;
+  if ((rc = alloc(c, (void**)&c->xs, c->nf * cb))) return rc;
+  if ((rc = alloc(c, (void**)&c->minv, c->ninv * mb))) return rc;
+  if ((rc = alloc(c, (void**)&c->mfwd, c->nfwd * mb))) return rc;
+  if ((rc = alloc(c, (void**)&c->stage, full_bytes(c)))) return rc;
+  if ((rc = alloc(c, (void**)&c->dflt, (size_t)g.nx * g.ny * sizeof(double)))) return rc;
+  if ((rc = alloc(c, (void**)&c->flag, 64))) return rc;
+  if (k.stepper == SW_STEP_IFMRK4) {
+    for (int i = 0; i < 4; ++i)
+      if ((rc = alloc(c, (void**)&c->rk[i], c->nf * cb))) return rc;
+  } else {
+    for (int i = 0; i < 3; ++i)
+      if ((rc = alloc(c, (void**)&c->hist[i], c->nf * cb))) return rc;
+  }
+  if (k.stepper != SW_STEP_FILTERED_AB3) {
+    const size_t eb = (size_t)c->nf * c->nf * cb;
+    if ((rc = alloc(c, (void**)&c->E, eb))) return rc;
+    if ((rc = alloc(c, (void**)&c->E2, eb))) return rc;
+    // IFMAB3: exp(L dt), exp(2 L dt) (utils/IFMAB3.jl:44-66); IFMRK4: exp(L dt), exp(L dt/2)
+    sw::launch_setup_expm(k.model, g, p, 1.0, c->E, c->stream);
+    sw::launch_setup_expm(k.model, g, p, k.stepper == SW_STEP_IFMAB3 ? 2.0 : 0.5, c->E2, c->stream);
+    HIPCHK(c, hipGetLastError());
+  }
+  {
+    auto tx = twiddles(k.nx);
+    HIPCHK(c, hipMalloc((void**)&c->tw_x, tx.size() * sizeof(double2)));
+    HIPCHK(c, hipMemcpy(c->tw_x, tx.data(), tx.size() * sizeof(double2), hipMemcpyHostToDevice));
+    auto ty = twiddles(k.ny);
+    HIPCHK(c, hipMalloc((void**)&c->tw_y, ty.size() * sizeof(double2)));
+    HIPCHK(c, hipMemcpy(c->tw_y, ty.data(), ty.size() * sizeof(double2), hipMemcpyHostToDevice));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->stats.resize(K_NKERN);
+  for (int i = 0; i < K_NKERN; ++i) c->stats[i].name = kname[i];
+  return SW_OK;
+}
+
+void sw_destroy(sw_ctx* c) {
+  if (!c) return;
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  void* ptrs[] = {c->tw_x, c->tw_y, c->sol, c->hist[0], c->hist[1], c->hist[2], c->E, c->E2,
+                  c->rk[0], c->rk[1], c->rk[2], c->rk[3], c->xs, c->minv, c->mfwd, c->stage,
+                  c->dflt, c->flag};
+  for (void* q : ptrs)
+    if (q) (void)hipFree(q);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int sw_get_dims(const sw_ctx* c, int32_t* nkr, int32_t* nl, int32_t* nf) {
+  if (!c || !c->sol) return SW_E_STATE;
+  if (nkr) *nkr = c->g.nkr;
+  if (nl) *nl = c->g.nl;
+  if (nf) *nf = c->nf;
+  return SW_OK;
+}
+
+int sw_set_state(sw_ctx* c, const void* sol, size_t bytes) {
+  if (!c || !c->sol) return SW_E_STATE;
+  if (!sol || bytes != full_bytes(c)) return fail(c, SW_E_INVALID, "sw_set_state: size mismatch");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  HIPCHK(c, hipMemcpyAsync(c->stage, sol, bytes, hipMemcpyHostToDevice, c->stream));
+  sw::launch_gather(c->nf, c->g, c->stage, c->sol, c->stream);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return SW_OK;
+}
+
+int sw_get_state(const sw_ctx* cc, void* sol, size_t bytes) {
+  sw_ctx* c = const_cast<sw_ctx*>(cc);
+  if (!c || !c->sol) return SW_E_STATE;
+  if (!sol || bytes != full_bytes(c)) return fail(c, SW_E_INVALID, "sw_get_state: size mismatch");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  sw::launch_scatter(c->nf, c->g, c->sol, c->stage, c->stream);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(sol, c->stage, bytes, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return SW_OK;
+}
+
+int sw_set_clock(sw_ctx* c, double t, int64_t step) {
+  if (!c) return SW_E_STATE;
+  if (step < 0) return fail(c, SW_E_INVALID, "negative step");
+  c->t = t;
+  c->step = step;
+  return SW_OK;
+}
+
+int sw_get_clock(const sw_ctx* c, double* t, int64_t* step) {
+  if (!c) return SW_E_STATE;
+  if (t) *t = c->t;
+  if (step) *step = c->step;
+  return SW_OK;
+}
+
+int sw_step(sw_ctx* c, int64_t nsteps) {
+  if (!c || !c->sol) return SW_E_STATE;
+  if (nsteps < 0) return fail(c, SW_E_INVALID, "negative nsteps");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  for (int64_t i = 0; i < nsteps; ++i) step_once(c);
+  HIPCHK(c, hipGetLastError());
+  if (c->cfg.check_nan && nsteps > 0) {
+    HIPCHK(c, hipMemsetAsync(c->flag, 0, sizeof(int), c->stream));
+    sw::launch_nan_check(c->nf, c->g, c->sol, c->flag, c->stream);
+    int h = 0;
+    HIPCHK(c, hipMemcpyAsync(&h, c->flag, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (h) return fail(c, SW_E_NAN, "Solution is NaN");
+  } else {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  return SW_OK;
+}
+
+int sw_calcN(sw_ctx* c, const void* sol, void* N, size_t bytes) {
+  if (!c || !c->sol) return SW_E_STATE;
+  if (!sol || !N || bytes != full_bytes(c)) return fail(c, SW_E_INVALID, "sw_calcN: size mismatch");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  double2* out = c->cfg.stepper == SW_STEP_IFMRK4 ? c->rk[3] : c->hist[c->head];
+  HIPCHK(c, hipMemcpyAsync(c->stage, sol, bytes, hipMemcpyHostToDevice, c->stream));
+  sw::launch_gather(c->nf, c->g, c->stage, c->xs, c->stream);
+  // scratch output: use the ring slot that the next step overwrites anyway
+  calcN(c, c->xs, out);
+  sw::launch_scatter(c->nf, c->g, out, c->stage, c->stream);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(N, c->stage, bytes, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return SW_OK;
+}
+
+int sw_get_physical(sw_ctx* c, int32_t fid, double* out, size_t bytes) {
+  if (!c || !c->sol) return SW_E_STATE;
+  if (!out || bytes != (size_t)c->g.nx * c->g.ny * sizeof(double))
+    return fail(c, SW_E_INVALID, "sw_get_physical: size mismatch");
+  const int id = fid & 7, layer = fid >> 3;
+  if (c->cfg.model == SW_MODEL_RSW) {
+    if (fid < 0 || fid > 3) return fail(c, SW_E_INVALID, "RSW physical ids are 0..3");
+  } else {
+    if (layer > 1 || id == SW_PHYS_ETA || id > 5) return fail(c, SW_E_INVALID, "bad QG2 physical id");
+  }
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  sw::launch_make_spec(c->cfg.model, fid, c->g, c->p, c->sol, c->xs, c->stream);
+  sw::launch_col_inv1(c->g, c->xs, c->minv, c->tw_y, c->stream);
+  sw::launch_row_c2r1(c->g, c->minv, c->dflt, c->tw_x, c->stream);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(out, c->dflt, bytes, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return SW_OK;
+}
+
+int sw_diag(sw_ctx* c, int32_t id, double* out) {
+  if (!c || !c->sol || !out) return SW_E_STATE;
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  if (id == SW_DIAG_NAN) {
+    HIPCHK(c, hipMemsetAsync(c->flag, 0, sizeof(int), c->stream));
+    sw::launch_nan_check(c->nf, c->g, c->sol, c->flag, c->stream);
+    int h = 0;
+    HIPCHK(c, hipMemcpyAsync(&h, c->flag, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    *out = h ? 1.0 : 0.0;
+    return SW_OK;
+  }
+  if (id != SW_DIAG_KE && id != SW_DIAG_PE) return fail(c, SW_E_INVALID, "unknown diagnostic");
+  HIPCHK(c, hipMemsetAsync(c->dflt, 0, 2 * sizeof(double), c->stream));
+  sw::launch_energy(c->cfg.model, c->g, c->p, c->sol, c->dflt, c->stream);
+  double acc[2] = {0, 0};
+  HIPCHK(c, hipMemcpyAsync(acc, c->dflt, sizeof(acc), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const Geom& g = c->g;
+  const double norm = g.Lx * g.Ly / ((double)g.nx * g.nx * (double)g.ny * g.ny);  // parsevalsum2
+  if (c->cfg.model == SW_MODEL_RSW) {
+    // rsw/RotatingShallowWater.jl:323-331
+    if (id == SW_DIAG_KE) *out = norm * acc[0] / (2 * g.Lx * g.Ly);
+    else *out = 0.5 * c->p.Cg2 * norm * acc[1] / (g.Lx * g.Ly);
+  } else {
+    // swqg/TwoLayerQG.jl:230-250
+    if (id == SW_DIAG_KE) *out = norm * acc[0] / (g.Lx * g.Ly);
+    else *out = 1.0 / (2 * g.Lx * g.Ly) * c->p.F * norm * acc[1];
+  }
+  return SW_OK;
+}
+
+int sw_profile_steps(sw_ctx* c, int64_t nsteps, sw_kernel_stat* out, int32_t max_stats, int32_t* n_stats) {
+  if (!c || !c->sol) return SW_E_STATE;
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  for (auto& s : c->stats) {
+    s.launches = 0;
+    s.ms = 0.0;
+  }
+  c->prof = true;
+  for (int64_t i = 0; i < nsteps; ++i) step_once(c);
+  c->prof = false;
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  int n = 0;
+  for (int i = 0; i < K_NKERN && n < max_stats; ++i) {
+    if (c->stats[i].launches == 0) continue;
+    std::snprintf(out[n].name, sizeof(out[n].name), "%s", c->stats[i].name);
+    out[n].launches = c->stats[i].launches;
+    out[n].avg_ms = c->stats[i].ms / c->stats[i].launches;
+    out[n].alg_bytes = kernel_bytes(c, i);
+    ++n;
+  }
+  if (n_stats) *n_stats = n;
+  return SW_OK;
+}
+
+double sw_step_alg_bytes(const sw_ctx* c) {
+  if (!c) return 0.0;
+  const int ncalc = c->cfg.stepper == SW_STEP_IFMRK4 ? 4 : 1;
+  double b = ncalc * (kernel_bytes(c, K_COLINV) + kernel_bytes(c, K_ROW) + kernel_bytes(c, K_COLFWD));
+  b += kernel_bytes(c, K_UPD);
+  if (c->cfg.stepper == SW_STEP_IFMRK4) b += 3 * kernel_bytes(c, K_RK4STAGE);
+  return b;
+}
+
+int sw_comm_unique_id(void* out128) {
+  if (!out128) return SW_E_INVALID;
+  return SW_E_INVALID;  // RCCL slab decomposition lands in a later build
+}
+
+}  // extern "C"

@@ -1,0 +1,884 @@
+// libsw device kernels for gfx950 (MI355X).  One pseudo-spectral step is
+//   col_inv  (compact spectral state -> y-inverse columns, "mixed" space)
+//   row      (x c2r of every field, physical products, x r2c; physical space
+//             never touches HBM)
+//   col_fwd  (y-forward columns -> N on live modes)
+//   update   (stepper combination over live modes)
+// See DESIGN.md for layouts, the roofline of each kernel and the reference
+// lines each one replaces.
+#include "sw_internal.hpp"
+#include "sw_fft.hpp"
+
+namespace sw {
+
+// block -> column mapping for the column kernels.  When one line per block and
+// the grid is a multiple of 64, the 8 columns that share each 128-B chunk of
+// the mixed layout (kr>>3 equal) are placed on blocks b, b+8, …, b+56, which
+// the dispatcher deals to one XCD, so they meet in one L2 (speed only).
+__device__ __forceinline__ int col_of_block(int b, int nb) {
+  if ((nb & 63) == 0) {
+    const int q = b >> 6, j = (b >> 3) & 7, x = b & 7;
+    return (q << 6) + (x << 3) + j;
+  }
+  return b;
+}
+
+struct LineCtx {
+  int NT, ln, t, NB;
+};
+__device__ __forceinline__ LineCtx line_ctx(int N) {
+  LineCtx c;
+  c.NT = N >> 3;
+  c.ln = threadIdx.x / c.NT;
+  c.t = threadIdx.x - c.ln * c.NT;
+  c.NB = blockDim.x / c.NT;
+  return c;
+}
+
+__device__ __forceinline__ double2 zero2() { return make_double2(0.0, 0.0); }
+
+// ===========================================================================
+// col_inv: for column kr, build the y-spectra the row pass needs, inverse FFT
+// along y (scaled by 1/(nx ny), FF's normalised c2r), store to mixed space.
+//   RSW  outputs (rsw/RotatingShallowWater.jl:147-214): 0 U, 1 V, 2 H, 3 Uy=il U, 4 Vy=il V
+//   QG2  outputs (swqg/TwoLayerQG.jl:155-176):          0 Q1, 1 Q2, 2 Ψ1, 3 Ψ2, 4 Ψy1, 5 Ψy2
+// grid: (columns, groups); RSW group f reads field f; QG2 group = layer.
+// ===========================================================================
+template <int MODEL>
+__global__ void __launch_bounds__(1024) k_col_inv(Geom g, Phys p, const double2* __restrict__ X,
+                                                  double2* __restrict__ M,
+                                                  const double2* __restrict__ tw) {
+  extern __shared__ double2 smem[];
+  const LineCtx c = line_ctx(g.ny);
+  const int kr = (c.NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * c.NB + c.ln;
+  const int grp = blockIdx.y;
+  double2* line = smem + c.ln * lds_line_elems(g.ny);
+  const bool live = kr < g.kc;
+  const double scale = 1.0 / ((double)g.nx * (double)g.ny);
+  const double k = kr * g.mk;
+  double2 v[8];
+
+  auto store = [&](int o) {
+    if (live) {
+      double2* Mo = M + (long long)o * g.mfield;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const int y = c.t + s * c.NT;
+        Mo[midx(g, kr, y)] = line[LP(y)];
+      }
+    }
+  };
+
+  if constexpr (MODEL == MODEL_RSW) {
+    const double2* Xf = X + (long long)grp * g.cfield + (long long)kr * g.LrP;
+    double2 x[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int m = c.t + s * c.NT;
+      const int j = compact_of(g, m);
+      x[s] = (live && j >= 0) ? Xf[j] : zero2();
+      v[s] = cscale(x[s], scale);
+    }
+    fft_line<+1>(v, c.t, c.NT, g.log2ny, tw, line);
+    store(grp);
+    if (grp < 2) {  // ∂y: Uy, Vy
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const int m = c.t + s * c.NT;
+        v[s] = cmul_i(x[s], lwav(g, m) * scale);
+      }
+      fft_line<+1>(v, c.t, c.NT, g.log2ny, tw, line);
+      store(3 + grp);
+    }
+  } else {
+    // streamfunctionfrompv! (swqg/TwoLayerQG.jl:101-111)
+    const double2* X1 = X + (long long)kr * g.LrP;
+    const double2* X2 = X1 + g.cfield;
+    double2 q[8], psi[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int m = c.t + s * c.NT;
+      const int j = compact_of(g, m);
+      double2 q1 = zero2(), q2 = zero2();
+      if (live && j >= 0) {
+        q1 = X1[j];
+        q2 = X2[j];
+      }
+      const double l = lwav(g, m);
+      const double K2 = k * k + l * l;
+      const double iK2 = K2 == 0.0 ? 0.0 : 1.0 / K2;
+      const double den = K2 + 2.0 * p.F;
+      const double2 qs = cadd(q1, q2);
+      const double2 qg = grp == 0 ? q1 : q2;
+      double2 ps = make_double2(-(K2 * qg.x + p.F * qs.x), -(K2 * qg.y + p.F * qs.y));
+      ps = make_double2((ps.x / den) * iK2, (ps.y / den) * iK2);
+      q[s] = qg;
+      psi[s] = ps;
+      v[s] = cscale(qg, scale);
+    }
+    fft_line<+1>(v, c.t, c.NT, g.log2ny, tw, line);
+    store(grp);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) v[s] = cscale(psi[s], scale);
+    fft_line<+1>(v, c.t, c.NT, g.log2ny, tw, line);
+    store(2 + grp);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int m = c.t + s * c.NT;
+      v[s] = cmul_i(psi[s], lwav(g, m) * scale);
+    }
+    fft_line<+1>(v, c.t, c.NT, g.log2ny, tw, line);
+    store(4 + grp);
+  }
+}
+
+// ===========================================================================
+// row: one physical row y per line.  Real fields travel in pairs a + i b
+// through one complex FFT of length nx (Z[k] = A[k] + i B[k] for k <= nx/2,
+// Z[nx-k] = conj(A[k]) + i conj(B[k]); the DC bin keeps real parts only —
+// numpy's c2r rule).
+// ===========================================================================
+__device__ __forceinline__ void load_pair(double2 (&v)[8], const LineCtx& c, const Geom& g,
+                                          const double2* __restrict__ A,
+                                          const double2* __restrict__ B, int y, bool deriv) {
+  const int half = g.nx >> 1;
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const int m = c.t + s * c.NT;
+    int kk;
+    bool cj;
+    if (m <= half) {
+      kk = m;
+      cj = false;
+    } else {
+      kk = g.nx - m;
+      cj = true;
+    }
+    double2 z = zero2();
+    if (kk < g.kc) {
+      const long long o = midx(g, kk, y);
+      double2 a = A[o];
+      double2 b = B ? B[o] : zero2();
+      if (deriv) {
+        const double kw = kk * g.mk;
+        a = cmul_i(a, kw);
+        b = cmul_i(b, kw);
+      }
+      if (kk == 0) {
+        a.y = 0.0;
+        b.y = 0.0;
+      }
+      if (cj) {
+        a = cconj(a);
+        b = cconj(b);
+      }
+      z = make_double2(a.x - b.y, a.y + b.x);  // a + i b
+    }
+    v[s] = z;
+  }
+}
+
+// After a forward FFT of z = a + i b (in LDS), write Â[k], B̂[k] for k < kc.
+__device__ __forceinline__ void store_pair(const LineCtx& c, const Geom& g, const double2* line,
+                                           double2* __restrict__ A, double2* __restrict__ B, int y) {
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const int k = c.t + s * c.NT;
+    if (k < g.kc) {
+      const double2 zk = line[LP(k)];
+      const double2 zn = line[LP((g.nx - k) & (g.nx - 1))];
+      const long long o = midx(g, k, y);
+      A[o] = make_double2(0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y));
+      // (zk - conj zn) / (2i)
+      B[o] = make_double2(0.5 * (zk.y + zn.y), -0.5 * (zk.x - zn.x));
+    }
+  }
+}
+
+template <int MODEL>
+__global__ void __launch_bounds__(1024) k_row(Geom g, Phys p, const double2* __restrict__ Mi,
+                                              double2* __restrict__ Mo,
+                                              const double2* __restrict__ tw) {
+  extern __shared__ double2 smem[];
+  const LineCtx c = line_ctx(g.nx);
+  const int y = blockIdx.x * c.NB + c.ln;
+  double2* line = smem + c.ln * lds_line_elems(g.nx);
+  const long long MF = g.mfield;
+  double2 v[8];
+  auto read_phys = [&](double2 (&w)[8]) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) w[s] = line[LP(c.t + s * c.NT)];
+  };
+
+  if constexpr (MODEL == MODEL_RSW) {
+    const double2 *U = Mi, *V = Mi + MF, *H = Mi + 2 * MF, *Uy = Mi + 3 * MF, *Vy = Mi + 4 * MF;
+    double2 uv[8], ab[8], w[8];
+    // ux + i vx
+    load_pair(v, c, g, U, V, y, true);
+    fft_line<+1>(v, c.t, c.NT, g.log2nx, tw, line);
+    read_phys(w);
+    // u + i v
+    load_pair(v, c, g, U, V, y, false);
+    fft_line<+1>(v, c.t, c.NT, g.log2nx, tw, line);
+    read_phys(uv);
+#pragma unroll
+    for (int s = 0; s < 8; ++s)  // A = u ux, B = u vx   (:172, :204)
+      ab[s] = make_double2(uv[s].x * w[s].x, uv[s].x * w[s].y);
+    // uy + i vy
+    load_pair(v, c, g, Uy, Vy, y, false);
+    fft_line<+1>(v, c.t, c.NT, g.log2nx, tw, line);
+    read_phys(w);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {  // A += v uy, B += v vy   (:181, :195)
+      ab[s].x += uv[s].y * w[s].x;
+      ab[s].y += uv[s].y * w[s].y;
+      v[s] = ab[s];
+    }
+    fft_line<-1>(v, c.t, c.NT, g.log2nx, tw, line);
+    store_pair(c, g, line, Mo, Mo + MF, y);
+    // η
+    load_pair(v, c, g, H, nullptr, y, false);
+    fft_line<+1>(v, c.t, c.NT, g.log2nx, tw, line);
+    read_phys(w);
+#pragma unroll
+    for (int s = 0; s < 8; ++s)  // C = u η, D = v η   (:218, :224)
+      v[s] = make_double2(uv[s].x * w[s].x, uv[s].y * w[s].x);
+    fft_line<-1>(v, c.t, c.NT, g.log2nx, tw, line);
+    store_pair(c, g, line, Mo + 2 * MF, Mo + 3 * MF, y);
+  } else {
+    const double2 *Q1 = Mi, *Q2 = Mi + MF, *P1 = Mi + 2 * MF, *P2 = Mi + 3 * MF,
+                  *Py1 = Mi + 4 * MF, *Py2 = Mi + 5 * MF;
+    double2 q[8], w[8];
+    // ψx1 + i ψx2
+    load_pair(v, c, g, P1, P2, y, true);
+    fft_line<+1>(v, c.t, c.NT, g.log2nx, tw, line);
+    read_phys(w);
+    load_pair(v, c, g, Q1, Q2, y, false);
+    fft_line<+1>(v, c.t, c.NT, g.log2nx, tw, line);
+    read_phys(q);
+#pragma unroll
+    for (int s = 0; s < 8; ++s)  // ψx q per layer (swqg/TwoLayerQG.jl:169)
+      v[s] = make_double2(w[s].x * q[s].x, w[s].y * q[s].y);
+    fft_line<-1>(v, c.t, c.NT, g.log2nx, tw, line);
+    store_pair(c, g, line, Mo, Mo + MF, y);
+    load_pair(v, c, g, Py1, Py2, y, false);
+    fft_line<+1>(v, c.t, c.NT, g.log2nx, tw, line);
+    read_phys(w);
+#pragma unroll
+    for (int s = 0; s < 8; ++s)  // ψy q per layer (:177)
+      v[s] = make_double2(w[s].x * q[s].x, w[s].y * q[s].y);
+    fft_line<-1>(v, c.t, c.NT, g.log2nx, tw, line);
+    store_pair(c, g, line, Mo + 2 * MF, Mo + 3 * MF, y);
+  }
+}
+
+// ===========================================================================
+// col_fwd: forward FFT along y of the row outputs, combine into N (live rows).
+//   RSW (rsw/RotatingShallowWater.jl:174-226):
+//     N0 = -F(A), N1 = -F(B), N2 = -ik F(C) - il F(D)
+//   QG2 (swqg/TwoLayerQG.jl:171,179): N_l = -il F(A_l) + ik F(B_l)
+// ===========================================================================
+template <int MODEL>
+__global__ void __launch_bounds__(1024) k_col_fwd(Geom g, Phys p, const double2* __restrict__ Mf,
+                                                  double2* __restrict__ N,
+                                                  const double2* __restrict__ tw) {
+  extern __shared__ double2 smem[];
+  const LineCtx c = line_ctx(g.ny);
+  const int kr = (c.NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * c.NB + c.ln;
+  const int grp = blockIdx.y;
+  double2* line = smem + c.ln * lds_line_elems(g.ny);
+  const bool live = kr < g.kc;
+  const double k = kr * g.mk;
+  const long long MF = g.mfield;
+  double2 v[8], acc[8];
+
+  auto load_col = [&](const double2* Mfield) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int y = c.t + s * c.NT;
+      v[s] = live ? Mfield[midx(g, kr, y)] : zero2();
+    }
+  };
+
+  int fa, fb;
+  if constexpr (MODEL == MODEL_RSW) {
+    fa = grp < 2 ? grp : 2;
+    fb = grp < 2 ? -1 : 3;
+  } else {
+    fa = grp;      // A_l
+    fb = 2 + grp;  // B_l
+  }
+  load_col(Mf + fa * MF);
+  fft_line<-1>(v, c.t, c.NT, g.log2ny, tw, line);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const int j = c.t + s * c.NT;
+    acc[s] = zero2();
+    if (j < g.Lr) {
+      const int m = lrow_of(g, j);
+      const double2 a = line[LP(m)];
+      if constexpr (MODEL == MODEL_RSW) {
+        acc[s] = (grp < 2) ? make_double2(-a.x, -a.y) : cmul_i(a, -k);
+      } else {
+        acc[s] = cmul_i(a, -lwav(g, m));
+      }
+    }
+  }
+  if (fb >= 0) {
+    load_col(Mf + fb * MF);
+    fft_line<-1>(v, c.t, c.NT, g.log2ny, tw, line);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int j = c.t + s * c.NT;
+      if (j < g.Lr) {
+        const int m = lrow_of(g, j);
+        const double2 b = line[LP(m)];
+        if constexpr (MODEL == MODEL_RSW) {
+          acc[s] = cadd(acc[s], cmul_i(b, -lwav(g, m)));
+        } else {
+          acc[s] = cadd(acc[s], cmul_i(b, k));
+        }
+      }
+    }
+  }
+  if (live) {
+    double2* Nf = N + (long long)grp * g.cfield + (long long)kr * g.LrP;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int j = c.t + s * c.NT;
+      if (j < g.Lr) Nf[j] = acc[s];
+    }
+  }
+}
+
+// ===========================================================================
+// stepper updates over live modes (one thread per mode, all fields)
+// ===========================================================================
+__device__ __forceinline__ bool mode_of(const Geom& g, long long i, int& kr, int& j) {
+  kr = (int)(i / g.LrP);
+  j = (int)(i - (long long)kr * g.LrP);
+  return kr < g.kc && j < g.Lr;
+}
+
+template <int NF>
+__device__ __forceinline__ void model_L(int model, const Phys& p, double k, double l, cplx L[NF][NF]) {
+  if constexpr (NF == 3) {
+    rsw_L(p, k, l, L);
+  } else {
+    qg2_L(p, k, l, L);
+  }
+}
+
+// FF FilteredAB3: RHS = N + L·sol; Euler for step < 3, else AB3;
+// sol .*= filter.  RHS overwrites N in place (it becomes history).
+template <int NF>
+__global__ void k_upd_fab3(Geom g, Phys p, double2* __restrict__ sol, double2* __restrict__ NR,
+                           const double2* __restrict__ Rm1, const double2* __restrict__ Rm2,
+                           int euler) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  int kr, j;
+  if (i >= g.cfield || !mode_of(g, i, kr, j)) return;
+  const double k = kr * g.mk, l = lwav(g, lrow_of(g, j));
+  cplx L[NF][NF];
+  model_L<NF>(0, p, k, l, L);
+  cplx s[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    const double2 t = sol[f * g.cfield + i];
+    s[f] = cx(t.x, t.y);
+  }
+  const double filt = filter_value(g, p, k, l);
+  const double dt = p.dt;
+#pragma unroll
+  for (int r = 0; r < NF; ++r) {
+    cplx Ls = cx(0.0);
+#pragma unroll
+    for (int cc = 0; cc < NF; ++cc) Ls = Ls + L[r][cc] * s[cc];
+    const double2 n = NR[r * g.cfield + i];
+    const cplx rhs = cx(n.x + Ls.re, n.y + Ls.im);
+    cplx upd;
+    if (euler) {
+      upd = dt * rhs;
+    } else {
+      const double2 a = Rm1[r * g.cfield + i], b = Rm2[r * g.cfield + i];
+      upd = dt * cx(23.0 / 12 * rhs.re - 16.0 / 12 * a.x + 5.0 / 12 * b.x,
+                    23.0 / 12 * rhs.im - 16.0 / 12 * a.y + 5.0 / 12 * b.y);
+    }
+    NR[r * g.cfield + i] = make_double2(rhs.re, rhs.im);
+    const cplx ns = s[r] + upd;
+    sol[r * g.cfield + i] = make_double2(ns.re * filt, ns.im * filt);
+  }
+}
+
+template <int NF>
+__device__ __forceinline__ void load_mat(const double2* __restrict__ E, long long cf, long long i,
+                                         cplx M[NF][NF]) {
+#pragma unroll
+  for (int r = 0; r < NF; ++r)
+#pragma unroll
+    for (int cc = 0; cc < NF; ++cc) {
+      const double2 t = E[(r * NF + cc) * cf + i];
+      M[r][cc] = cx(t.x, t.y);
+    }
+}
+
+template <int NF>
+__device__ __forceinline__ void load_vec(const double2* __restrict__ X, long long cf, long long i,
+                                         cplx x[NF]) {
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    const double2 t = X[f * cf + i];
+    x[f] = cx(t.x, t.y);
+  }
+}
+
+template <int NF>
+__device__ __forceinline__ void matvec(const cplx M[NF][NF], const cplx x[NF], cplx y[NF]) {
+#pragma unroll
+  for (int r = 0; r < NF; ++r) {
+    cplx s = cx(0.0);
+#pragma unroll
+    for (int cc = 0; cc < NF; ++cc) s = s + M[r][cc] * x[cc];
+    y[r] = s;
+  }
+}
+
+// utils/IFMAB3.jl:129-160: Euler for step < 3, else AB3 with E N₋₁, E2 N₋₂;
+// then sol = E·(…); filter.
+template <int NF>
+__global__ void k_upd_ifmab3(Geom g, Phys p, double2* __restrict__ sol, const double2* __restrict__ N,
+                             const double2* __restrict__ Nm1, const double2* __restrict__ Nm2,
+                             const double2* __restrict__ E, const double2* __restrict__ E2,
+                             int euler) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  int kr, j;
+  if (i >= g.cfield || !mode_of(g, i, kr, j)) return;
+  const long long cf = g.cfield;
+  cplx M[NF][NF], s[NF], n[NF], x[NF], y[NF];
+  load_mat<NF>(E, cf, i, M);
+  load_vec<NF>(sol, cf, i, s);
+  load_vec<NF>(N, cf, i, n);
+  const double dt = p.dt;
+  if (euler) {
+#pragma unroll
+    for (int f = 0; f < NF; ++f) x[f] = s[f] + dt * n[f];
+  } else {
+    cplx a[NF], b[NF], e1[NF], e2[NF], M2[NF][NF];
+    load_vec<NF>(Nm1, cf, i, a);
+    load_vec<NF>(Nm2, cf, i, b);
+    load_mat<NF>(E2, cf, i, M2);
+    matvec<NF>(M, a, e1);
+    matvec<NF>(M2, b, e2);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const cplx comb = cx(23.0 / 12 * n[f].re - 16.0 / 12 * e1[f].re + 5.0 / 12 * e2[f].re,
+                           23.0 / 12 * n[f].im - 16.0 / 12 * e1[f].im + 5.0 / 12 * e2[f].im);
+      x[f] = s[f] + dt * comb;
+    }
+  }
+  matvec<NF>(M, x, y);
+  double filt = 1.0;
+  if (p.use_filter) {
+    const double k = kr * g.mk, l = lwav(g, lrow_of(g, j));
+    filt = filter_value(g, p, k, l);
+  }
+#pragma unroll
+  for (int f = 0; f < NF; ++f) sol[f * cf + i] = make_double2(y[f].re * filt, y[f].im * filt);
+}
+
+// Lawson IF-RK4 stage inputs:
+//   which 1: x = H (u + dt/2 k1);  2: x = H u + dt/2 k2;  3: x = E u + dt H k3
+template <int NF>
+__global__ void k_rk4_stage(Geom g, Phys p, int which, const double2* __restrict__ u,
+                            const double2* __restrict__ kk, const double2* __restrict__ E,
+                            const double2* __restrict__ H, double2* __restrict__ x) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  int kr, j;
+  if (i >= g.cfield || !mode_of(g, i, kr, j)) return;
+  const long long cf = g.cfield;
+  const double dt = p.dt;
+  cplx uu[NF], kv[NF], M[NF][NF], t[NF], o[NF];
+  load_vec<NF>(u, cf, i, uu);
+  load_vec<NF>(kk, cf, i, kv);
+  if (which == 1) {
+    load_mat<NF>(H, cf, i, M);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) t[f] = uu[f] + (0.5 * dt) * kv[f];
+    matvec<NF>(M, t, o);
+  } else if (which == 2) {
+    load_mat<NF>(H, cf, i, M);
+    matvec<NF>(M, uu, t);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) o[f] = t[f] + (0.5 * dt) * kv[f];
+  } else {
+    cplx M2[NF][NF], hk[NF];
+    load_mat<NF>(E, cf, i, M);
+    load_mat<NF>(H, cf, i, M2);
+    matvec<NF>(M, uu, t);
+    matvec<NF>(M2, kv, hk);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) o[f] = t[f] + dt * hk[f];
+  }
+#pragma unroll
+  for (int f = 0; f < NF; ++f) x[f * cf + i] = make_double2(o[f].re, o[f].im);
+}
+
+// u <- E u + dt/6 (E k1 + 2 H (k2 + k3) + k4); filter
+template <int NF>
+__global__ void k_rk4_final(Geom g, Phys p, double2* __restrict__ u, const double2* __restrict__ k1,
+                            const double2* __restrict__ k2, const double2* __restrict__ k3,
+                            const double2* __restrict__ k4, const double2* __restrict__ E,
+                            const double2* __restrict__ H) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  int kr, j;
+  if (i >= g.cfield || !mode_of(g, i, kr, j)) return;
+  const long long cf = g.cfield;
+  const double dt = p.dt;
+  cplx uu[NF], a[NF], b[NF], c3[NF], d[NF], ME[NF][NF], MH[NF][NF], Eu[NF], Ek1[NF], s23[NF], H23[NF];
+  load_vec<NF>(u, cf, i, uu);
+  load_vec<NF>(k1, cf, i, a);
+  load_vec<NF>(k2, cf, i, b);
+  load_vec<NF>(k3, cf, i, c3);
+  load_vec<NF>(k4, cf, i, d);
+  load_mat<NF>(E, cf, i, ME);
+  load_mat<NF>(H, cf, i, MH);
+  matvec<NF>(ME, uu, Eu);
+  matvec<NF>(ME, a, Ek1);
+#pragma unroll
+  for (int f = 0; f < NF; ++f) s23[f] = b[f] + c3[f];
+  matvec<NF>(MH, s23, H23);
+  double filt = 1.0;
+  if (p.use_filter) filt = filter_value(g, p, kr * g.mk, lwav(g, lrow_of(g, j)));
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    const cplx comb = Ek1[f] + 2.0 * H23[f] + d[f];
+    const cplx r = Eu[f] + (dt / 6) * comb;
+    u[f * cf + i] = make_double2(r.re * filt, r.im * filt);
+  }
+}
+
+// per-mode exp(factor·dt·L) (utils/IFMAB3.jl:32-41), stored [r][c] planes
+template <int NF>
+__global__ void k_setup_expm(Geom g, Phys p, double factor, double2* __restrict__ E) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  int kr, j;
+  if (i >= g.cfield || !mode_of(g, i, kr, j)) return;
+  const double k = kr * g.mk, l = lwav(g, lrow_of(g, j));
+  cplx L[NF][NF], A[NF][NF], X[NF][NF];
+  model_L<NF>(0, p, k, l, L);
+  const double sdt = factor * p.dt;
+#pragma unroll
+  for (int r = 0; r < NF; ++r)
+#pragma unroll
+    for (int cc = 0; cc < NF; ++cc) A[r][cc] = sdt * L[r][cc];
+  expm<NF>(A, X);
+#pragma unroll
+  for (int r = 0; r < NF; ++r)
+#pragma unroll
+    for (int cc = 0; cc < NF; ++cc) E[(r * NF + cc) * g.cfield + i] = make_double2(X[r][cc].re, X[r][cc].im);
+}
+
+// ===========================================================================
+// state I/O: Julia column-major (nkr, nl, nf) <-> compact live columns
+// ===========================================================================
+__global__ void k_gather(Geom g, int nf, const double2* __restrict__ full, double2* __restrict__ cmp) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long per = (long long)g.kc * g.Lr;
+  if (i >= per * nf) return;
+  const int f = (int)(i / per);
+  const long long r = i - f * per;
+  const int j = (int)(r / g.kc), kr = (int)(r - (long long)j * g.kc);
+  const int m = lrow_of(g, j);
+  cmp[f * g.cfield + (long long)kr * g.LrP + j] = full[((long long)f * g.nl + m) * g.nkr + kr];
+}
+
+__global__ void k_scatter(Geom g, int nf, const double2* __restrict__ cmp, double2* __restrict__ full) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long per = (long long)g.nkr * g.nl;
+  if (i >= per * nf) return;
+  const int f = (int)(i / per);
+  const long long r = i - f * per;
+  const int m = (int)(r / g.nkr), kr = (int)(r - (long long)m * g.nkr);
+  const int j = compact_of(g, m);
+  double2 v = zero2();
+  if (kr < g.kc && j >= 0) v = cmp[f * g.cfield + (long long)kr * g.LrP + j];
+  full[i] = v;
+}
+
+__global__ void k_nan_check(Geom g, int nf, const double2* __restrict__ cmp, int* flag) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  int kr, j;
+  int bad = 0;
+  if (i < g.cfield && mode_of(g, i, kr, j)) {
+    for (int f = 0; f < nf; ++f) {
+      const double2 v = cmp[f * g.cfield + i];
+      if (!isfinite(v.x) || !isfinite(v.y)) bad = 1;
+    }
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
+// ===========================================================================
+// updatevars! support: one spectral field -> physical
+// ===========================================================================
+// field ids: RSW 0 u, 1 v, 2 η, 3 ζ = ik v - il u - f η (rsw/RotatingShallowWater.jl:108)
+//            QG2 layer*8 + {4 q, 5 ψ, 3 ζ = -K² ψ, 0 u = -il ψ, 1 v = ik ψ} (swqg/TwoLayerQG.jl:117-121)
+__global__ void k_make_spec(Geom g, Phys p, int model, int fid, const double2* __restrict__ sol,
+                            double2* __restrict__ out) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  int kr, j;
+  if (i >= g.cfield || !mode_of(g, i, kr, j)) return;
+  const long long cf = g.cfield;
+  const double k = kr * g.mk, l = lwav(g, lrow_of(g, j));
+  double2 r = zero2();
+  if (model == MODEL_RSW) {
+    if (fid <= 2) {
+      r = sol[fid * cf + i];
+    } else {
+      const double2 u = sol[i], v = sol[cf + i], e = sol[2 * cf + i];
+      const double2 a = cmul_i(v, k), b = cmul_i(u, l);
+      r = make_double2(a.x - b.x - p.f * e.x, a.y - b.y - p.f * e.y);
+    }
+  } else {
+    const int layer = fid >> 3, id = fid & 7;
+    const double2 q1 = sol[i], q2 = sol[cf + i];
+    const double2 qg = layer ? q2 : q1;
+    if (id == 4) {  // q
+      r = qg;
+    } else {
+      const double K2 = k * k + l * l;
+      const double iK2 = K2 == 0.0 ? 0.0 : 1.0 / K2;
+      const double den = K2 + 2.0 * p.F;
+      const double2 qs = cadd(q1, q2);
+      double2 ps = make_double2(-(K2 * qg.x + p.F * qs.x), -(K2 * qg.y + p.F * qs.y));
+      ps = make_double2((ps.x / den) * iK2, (ps.y / den) * iK2);
+      if (id == 5) r = ps;
+      else if (id == 3) r = make_double2(-K2 * ps.x, -K2 * ps.y);
+      else if (id == 0) r = cmul_i(ps, -l);
+      else if (id == 1) r = cmul_i(ps, k);
+    }
+  }
+  out[i] = r;
+}
+
+__global__ void __launch_bounds__(1024) k_col_inv1(Geom g, const double2* __restrict__ X,
+                                                   double2* __restrict__ M,
+                                                   const double2* __restrict__ tw) {
+  extern __shared__ double2 smem[];
+  const LineCtx c = line_ctx(g.ny);
+  const int kr = blockIdx.x * c.NB + c.ln;
+  double2* line = smem + c.ln * lds_line_elems(g.ny);
+  const bool live = kr < g.kc;
+  const double scale = 1.0 / ((double)g.nx * (double)g.ny);
+  const double2* Xf = X + (long long)kr * g.LrP;
+  double2 v[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const int m = c.t + s * c.NT;
+    const int j = compact_of(g, m);
+    v[s] = (live && j >= 0) ? cscale(Xf[j], scale) : zero2();
+  }
+  fft_line<+1>(v, c.t, c.NT, g.log2ny, tw, line);
+  if (live) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int y = c.t + s * c.NT;
+      M[midx(g, kr, y)] = line[LP(y)];
+    }
+  }
+}
+
+__global__ void __launch_bounds__(1024) k_row_c2r1(Geom g, const double2* __restrict__ M,
+                                                   double* __restrict__ out,
+                                                   const double2* __restrict__ tw) {
+  extern __shared__ double2 smem[];
+  const LineCtx c = line_ctx(g.nx);
+  const int y = blockIdx.x * c.NB + c.ln;
+  double2* line = smem + c.ln * lds_line_elems(g.nx);
+  double2 v[8];
+  load_pair(v, c, g, M, nullptr, y, false);
+  fft_line<+1>(v, c.t, c.NT, g.log2nx, tw, line);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const int x = c.t + s * c.NT;
+    out[(long long)y * g.nx + x] = line[LP(x)].x;
+  }
+}
+
+// Energies by Parseval over live modes (FF parsevalsum2 / parsevalsum:
+// weight 2 for 0 < kr < nx/2, 1 for kr = 0).  acc[0] = KE-sum, acc[1] = PE-sum.
+__global__ void k_energy(Geom g, Phys p, int model, const double2* __restrict__ sol, double* acc) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  int kr, j;
+  double ke = 0.0, pe = 0.0;
+  if (i < g.cfield && mode_of(g, i, kr, j)) {
+    const long long cf = g.cfield;
+    const double w = kr == 0 ? 1.0 : 2.0;
+    if (model == MODEL_RSW) {
+      const double2 u = sol[i], v = sol[cf + i], e = sol[2 * cf + i];
+      ke = w * (u.x * u.x + u.y * u.y + v.x * v.x + v.y * v.y);
+      pe = w * (e.x * e.x + e.y * e.y);
+    } else {
+      const double k = kr * g.mk, l = lwav(g, lrow_of(g, j));
+      const double K2 = k * k + l * l;
+      const double iK2 = K2 == 0.0 ? 0.0 : 1.0 / K2;
+      const double den = K2 + 2.0 * p.F;
+      const double2 q1 = sol[i], q2 = sol[cf + i];
+      const double2 qs = cadd(q1, q2);
+      double2 p1 = make_double2(-(K2 * q1.x + p.F * qs.x), -(K2 * q1.y + p.F * qs.y));
+      double2 p2 = make_double2(-(K2 * q2.x + p.F * qs.x), -(K2 * q2.y + p.F * qs.y));
+      p1 = make_double2((p1.x / den) * iK2, (p1.y / den) * iK2);
+      p2 = make_double2((p2.x / den) * iK2, (p2.y / den) * iK2);
+      ke = w * K2 * (p1.x * p1.x + p1.y * p1.y + p2.x * p2.x + p2.y * p2.y);
+      const double dx_ = p1.x - p2.x, dy_ = p1.y - p2.y;
+      pe = w * (dx_ * dx_ + dy_ * dy_);
+    }
+  }
+  // wave reduction
+  for (int off = 32; off > 0; off >>= 1) {
+    ke += __shfl_down(ke, off, 64);
+    pe += __shfl_down(pe, off, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(acc, ke);
+    atomicAdd(acc + 1, pe);
+  }
+}
+
+// ===========================================================================
+// launchers
+// ===========================================================================
+static inline int col_threads(const Geom& g, int& NB, int& nblk) {
+  const int NT = g.ny >> 3;
+  NB = NT >= 256 ? 1 : 256 / NT;
+  if (NB > g.kcP) NB = g.kcP;
+  nblk = (g.kcP + NB - 1) / NB;
+  return NB * NT;
+}
+static inline int row_threads(const Geom& g, int& NB, int& nblk) {
+  const int NT = g.nx >> 3;
+  NB = NT >= 256 ? 1 : 256 / NT;
+  if (NB > g.ny) NB = g.ny;
+  nblk = g.ny / NB;
+  return NB * NT;
+}
+
+void launch_col_inv(int model, const Geom& g, const Phys& p, const double2* X, double2* Minv,
+                    const double2* tw_y, hipStream_t s) {
+  int NB, nb;
+  const int th = col_threads(g, NB, nb);
+  const size_t sh = (size_t)NB * lds_line_elems(g.ny) * sizeof(double2);
+  const dim3 grid(nb, model == MODEL_RSW ? 3 : 2);
+  if (model == MODEL_RSW)
+    hipLaunchKernelGGL(k_col_inv<MODEL_RSW>, grid, dim3(th), sh, s, g, p, X, Minv, tw_y);
+  else
+    hipLaunchKernelGGL(k_col_inv<MODEL_QG2>, grid, dim3(th), sh, s, g, p, X, Minv, tw_y);
+}
+
+void launch_row(int model, const Geom& g, const Phys& p, const double2* Minv, double2* Mfwd,
+                const double2* tw_x, hipStream_t s) {
+  int NB, nb;
+  const int th = row_threads(g, NB, nb);
+  const size_t sh = (size_t)NB * lds_line_elems(g.nx) * sizeof(double2);
+  if (model == MODEL_RSW)
+    hipLaunchKernelGGL(k_row<MODEL_RSW>, dim3(nb), dim3(th), sh, s, g, p, Minv, Mfwd, tw_x);
+  else
+    hipLaunchKernelGGL(k_row<MODEL_QG2>, dim3(nb), dim3(th), sh, s, g, p, Minv, Mfwd, tw_x);
+}
+
+void launch_col_fwd(int model, const Geom& g, const Phys& p, const double2* Mfwd, double2* N,
+                    const double2* tw_y, hipStream_t s) {
+  int NB, nb;
+  const int th = col_threads(g, NB, nb);
+  const size_t sh = (size_t)NB * lds_line_elems(g.ny) * sizeof(double2);
+  const dim3 grid(nb, model == MODEL_RSW ? 3 : 2);
+  if (model == MODEL_RSW)
+    hipLaunchKernelGGL(k_col_fwd<MODEL_RSW>, grid, dim3(th), sh, s, g, p, Mfwd, N, tw_y);
+  else
+    hipLaunchKernelGGL(k_col_fwd<MODEL_QG2>, grid, dim3(th), sh, s, g, p, Mfwd, N, tw_y);
+}
+
+static inline dim3 mode_grid(const Geom& g) { return dim3((unsigned)((g.cfield + 255) / 256)); }
+
+void launch_upd_fab3(int model, const Geom& g, const Phys& p, double2* sol, double2* NR,
+                     const double2* Rm1, const double2* Rm2, int euler, hipStream_t s) {
+  if (model == MODEL_RSW)
+    hipLaunchKernelGGL(k_upd_fab3<3>, mode_grid(g), dim3(256), 0, s, g, p, sol, NR, Rm1, Rm2, euler);
+  else
+    hipLaunchKernelGGL(k_upd_fab3<2>, mode_grid(g), dim3(256), 0, s, g, p, sol, NR, Rm1, Rm2, euler);
+}
+
+void launch_upd_ifmab3(int nf, const Geom& g, const Phys& p, double2* sol, const double2* N,
+                       const double2* Nm1, const double2* Nm2, const double2* E, const double2* E2,
+                       int euler, hipStream_t s) {
+  if (nf == 3)
+    hipLaunchKernelGGL(k_upd_ifmab3<3>, mode_grid(g), dim3(256), 0, s, g, p, sol, N, Nm1, Nm2, E, E2, euler);
+  else
+    hipLaunchKernelGGL(k_upd_ifmab3<2>, mode_grid(g), dim3(256), 0, s, g, p, sol, N, Nm1, Nm2, E, E2, euler);
+}
+
+void launch_rk4_stage(int nf, int which, const Geom& g, const Phys& p, const double2* u,
+                      const double2* k, const double2* E, const double2* H, double2* x,
+                      hipStream_t s) {
+  if (nf == 3)
+    hipLaunchKernelGGL(k_rk4_stage<3>, mode_grid(g), dim3(256), 0, s, g, p, which, u, k, E, H, x);
+  else
+    hipLaunchKernelGGL(k_rk4_stage<2>, mode_grid(g), dim3(256), 0, s, g, p, which, u, k, E, H, x);
+}
+
+void launch_rk4_final(int nf, const Geom& g, const Phys& p, double2* u, const double2* k1,
+                      const double2* k2, const double2* k3, const double2* k4, const double2* E,
+                      const double2* H, hipStream_t s) {
+  if (nf == 3)
+    hipLaunchKernelGGL(k_rk4_final<3>, mode_grid(g), dim3(256), 0, s, g, p, u, k1, k2, k3, k4, E, H);
+  else
+    hipLaunchKernelGGL(k_rk4_final<2>, mode_grid(g), dim3(256), 0, s, g, p, u, k1, k2, k3, k4, E, H);
+}
+
+void launch_setup_expm(int model, const Geom& g, const Phys& p, double factor, double2* E,
+                       hipStream_t s) {
+  if (model == MODEL_RSW)
+    hipLaunchKernelGGL(k_setup_expm<3>, mode_grid(g), dim3(256), 0, s, g, p, factor, E);
+  else
+    hipLaunchKernelGGL(k_setup_expm<2>, mode_grid(g), dim3(256), 0, s, g, p, factor, E);
+}
+
+void launch_gather(int nf, const Geom& g, const double2* full, double2* cmp, hipStream_t s) {
+  const long long n = (long long)g.kc * g.Lr * nf;
+  hipLaunchKernelGGL(k_gather, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g, nf, full, cmp);
+}
+
+void launch_scatter(int nf, const Geom& g, const double2* cmp, double2* full, hipStream_t s) {
+  const long long n = (long long)g.nkr * g.nl * nf;
+  hipLaunchKernelGGL(k_scatter, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g, nf, cmp, full);
+}
+
+void launch_nan_check(int nf, const Geom& g, const double2* cmp, int* flag, hipStream_t s) {
+  hipLaunchKernelGGL(k_nan_check, mode_grid(g), dim3(256), 0, s, g, nf, cmp, flag);
+}
+
+void launch_make_spec(int model, int fid, const Geom& g, const Phys& p, const double2* sol,
+                      double2* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_make_spec, mode_grid(g), dim3(256), 0, s, g, p, model, fid, sol, out);
+}
+
+void launch_col_inv1(const Geom& g, const double2* X, double2* M, const double2* tw_y, hipStream_t s) {
+  int NB, nb;
+  const int th = col_threads(g, NB, nb);
+  const size_t sh = (size_t)NB * lds_line_elems(g.ny) * sizeof(double2);
+  hipLaunchKernelGGL(k_col_inv1, dim3(nb), dim3(th), sh, s, g, X, M, tw_y);
+}
+
+void launch_row_c2r1(const Geom& g, const double2* M, double* out, const double2* tw_x, hipStream_t s) {
+  int NB, nb;
+  const int th = row_threads(g, NB, nb);
+  const size_t sh = (size_t)NB * lds_line_elems(g.nx) * sizeof(double2);
+  hipLaunchKernelGGL(k_row_c2r1, dim3(nb), dim3(th), sh, s, g, M, out, tw_x);
+}
+
+void launch_energy(int model, const Geom& g, const Phys& p, const double2* sol, double* acc,
+                   hipStream_t s) {
+  hipLaunchKernelGGL(k_energy, mode_grid(g), dim3(256), 0, s, g, p, model, sol, acc);
+}
+
+}  // namespace sw

@@ -1,0 +1,155 @@
+"""Driver-side setup mirroring rsw/RSWDriver.jl and swqg/TwoLayerDriver.jl
+(SURVEY A12): parameter formulas, synthetic random-phase initial conditions
+and the frame loop.  Setup only — the per-step work is libsw's.
+"""
+from __future__ import annotations
+
+import math
+import time
+
+import numpy as np
+
+from . import _lib
+from . import rotating_shallow_water as RSW
+from . import two_layer_qg as QG2
+from .grid import TwoDGrid
+
+# rsw/RSWParameters.jl
+RSW_PARAMETERS = dict(L=2 * np.pi, f=3.0, Cg=1.0, nnu=4, nutune=20.0, cfltune=0.01, filter_order=8,
+                      aliased_fraction=1 / 3, Kg=(10, 13), ag=0.2, Kw=(0, 5), aw=0.1)
+# swqg/TwoLayerParameters.jl
+QG2_PARAMETERS = dict(L=2 * np.pi, background_Cg=1.0, f=3.0, deformation_radius=1 / 6,
+                      intervortex_radius=1.0, nnu=4, nutune=40.0, cfltune=0.025,
+                      aliased_fraction=1 / 3, ug=0.025)
+
+
+def rsw_parameters(nx, **over):
+    """rsw/RSWDriver.jl:134-148: dt = cfltune/umax·dx, ν = νtune·dx/kmax^(2nν)/dt."""
+    P = dict(RSW_PARAMETERS, **over)
+    Lx = P["L"]
+    dx = Lx / nx
+    kmax = (nx / 2 - 1) * Lx / (2 * np.pi) * (1 - P["aliased_fraction"])
+    umax = P["ag"] + P["aw"]
+    dt = P["cfltune"] / umax * dx
+    nu = P["nutune"] * dx / (kmax ** (2 * P["nnu"])) / dt
+    return dict(P, dt=dt, nu=nu, Lx=Lx)
+
+
+def qg2_compute_parameters(deformation_radius, intervortex_radius, avg_eddy_velocity, H, f0):
+    """swqg/TwoLayerDriver.jl:17-27."""
+    c1, c2 = 3.2, 0.36
+    l_star = intervortex_radius / deformation_radius
+    kappa_star = c2 / math.log(l_star / c1)
+    U = avg_eddy_velocity / l_star
+    mu = 2 * U * kappa_star / deformation_radius
+    db = 4 * f0 ** 2 * deformation_radius ** 2 / H
+    return mu, db, U
+
+
+def qg2_parameters(nx, **over):
+    """swqg/TwoLayerDriver.jl:29-63."""
+    P = dict(QG2_PARAMETERS, **over)
+    Lx = P["L"]
+    dx = Lx / nx
+    kmax = (nx / 2 - 1) * (1 - P["aliased_fraction"])
+    H = 1.0
+    mu, db, U = qg2_compute_parameters(P["deformation_radius"], P["intervortex_radius"], P["ug"], H, P["f"])
+    drr0 = db / (P["background_Cg"] / H)
+    dt = P["cfltune"] / P["ug"] * dx
+    nu = P["nutune"] * 2 * np.pi / nx / (kmax ** (2 * P["nnu"])) / dt
+    return dict(P, dt=dt, nu=nu, U=U, mu=mu, drhorho0=drr0, Lx=Lx)
+
+
+def shafer_spectra(grid: TwoDGrid, Kg, Kw, f, Cg2, rng):
+    """rsw/RSWDriver.jl:93-106,118-120: geostrophic and wave spectra with random
+    phases on the annuli, before normalisation.  Draw order: phase = 2π·U[0,1)
+    then sgn = sign(U[0,1) - 0.5), each over (nkr, nl) column-major."""
+    K2 = grid.Krsq
+    geo = (Kg[0] ** 2 <= K2) & (K2 <= Kg[1] ** 2) & (K2 > 0)
+    wav = (Kw[0] ** 2 <= K2) & (K2 <= Kw[1] ** 2) & (K2 > 0)
+    phase = 2 * np.pi * rng.random((grid.nkr, grid.nl)).T
+    sgn = np.sign(rng.random((grid.nkr, grid.nl)).T - 0.5)
+    shift = np.exp(1j * phase)
+    om = np.sqrt(f ** 2 + Cg2 * K2)
+    gamp = 1 / om
+    wamp = np.sqrt(grid.invKrsq) / (2 * om)
+    kr = np.broadcast_to(grid.kr[None, :], K2.shape)
+    l = np.broadcast_to(grid.l[:, None], K2.shape)
+    z = np.zeros(K2.shape, np.complex128)
+    ugh, vgh, egh, uwh, vwh, ewh = (z.copy() for _ in range(6))
+    egh[geo] += (gamp * f * shift)[geo]
+    ugh[geo] += (-gamp * 1j * Cg2 * l * shift)[geo]
+    vgh[geo] += (gamp * 1j * Cg2 * kr * shift)[geo]
+    ewh[wav] += (wamp * K2 * shift)[wav]
+    uwh[wav] += (wamp * (sgn * kr * om * shift + 1j * f * l * shift))[wav]
+    vwh[wav] += (wamp * (sgn * l * om * shift - 1j * f * kr * shift))[wav]
+    return (ugh, vgh, egh), (uwh, vwh, ewh)
+
+
+def _umax(prob, uh, vh):
+    """max sqrt(u² + v²) of the c2r of (uh, vh), computed by libsw's own FFTs."""
+    z = np.zeros_like(uh)
+    RSW.set_solution(prob, uh, vh, z)
+    g = prob.grid
+    u = prob.ctx.physical(_lib.SW_PHYS_U, g.ny, g.nx)
+    v = prob.ctx.physical(_lib.SW_PHYS_V, g.ny, g.nx)
+    return float(np.max(np.sqrt(u ** 2 + v ** 2)))
+
+
+def set_shafer_initial_condition(prob, Kg, Kw, ag, aw, f, Cg2, rng):
+    """rsw/RSWDriver.jl:88-132.  The Umax normalisations use libsw's c2r.
+
+    Note: the dealiasing of set_solution! happens before the c2r here, while
+    the reference c2r's the raw spectra; the annuli (K <= 13) are far inside the
+    live band, so the two agree."""
+    (ugh, vgh, egh), (uwh, vwh, ewh) = shafer_spectra(prob.grid, Kg, Kw, f, Cg2, rng)
+    s = ag / _umax(prob, ugh, vgh)
+    ugh, vgh, egh = ugh * s, vgh * s, egh * s
+    s = aw / _umax(prob, uwh, vwh)
+    uwh, vwh, ewh = uwh * s, vwh * s, ewh * s
+    RSW.set_solution(prob, ugh + uwh, vgh + vwh, egh + ewh)
+
+
+def set_seed_initial_condition(prob, rng):
+    """swqg/TwoLayerDriver.jl:10-15: q0 = 1e-2·randn(nx, ny, 2), rfft over (1,2).
+    The forward transform here is numpy's host FFT on the one-off IC (setup)."""
+    g = prob.grid
+    q0 = 1e-2 * rng.standard_normal((2, g.ny, g.nx))
+    QG2.set_solution(prob, np.fft.rfft2(q0, axes=(-2, -1)))
+
+
+def rsw_problem(nx, stepper="FilteredAB3", seed=20261015, device=0, **over):
+    """RSWDriver.initialize_problem (:134-176) on the GPU in fp64 with the named
+    stepper and the shafer random-phase IC."""
+    P = rsw_parameters(nx, **over)
+    kw = {"order": P["filter_order"]} if stepper == "FilteredAB3" else {}
+    prob = RSW.Problem("gpu", nx=nx, Lx=P["Lx"], dt=P["dt"], f=P["f"], Cg=P["Cg"], nnu=P["nnu"],
+                       nu=P["nu"], aliased_fraction=P["aliased_fraction"], stepper=stepper,
+                       use_filter=(P["nutune"] == 0), device=device, **kw)
+    rng = np.random.default_rng(seed)
+    set_shafer_initial_condition(prob, P["Kg"], P["Kw"], P["ag"], P["aw"], P["f"], P["Cg"] ** 2, rng)
+    return prob, P
+
+
+def qg2_problem(nx, stepper="IFMAB3", seed=1234, device=0, **over):
+    """TwoLayerDriver.initialize_problem (:29-68) on the GPU in fp64."""
+    P = qg2_parameters(nx, **over)
+    prob = QG2.Problem("gpu", nx=nx, Lx=P["Lx"], dt=P["dt"], f0=P["f"], Cg=P["background_Cg"],
+                       U=P["U"], drhorho0=P["drhorho0"], nnu=P["nnu"], nu=P["nu"], mu=P["mu"],
+                       aliased_fraction=P["aliased_fraction"], stepper=stepper, use_filter=False,
+                       device=device)
+    rng = np.random.default_rng(seed)
+    set_seed_initial_condition(prob, rng)
+    return prob, P
+
+
+def run_frames(prob, nframes, output_freq, on_frame=None, log_every=100):
+    """The drivers' frame loop (rsw/RSWDriver.jl:205-223): step output_freq,
+    NaN check (sw_step returns SW_E_NAN -> LibSWError), optional callback."""
+    t0 = time.time()
+    for frame in range(nframes):
+        if log_every and frame % log_every == 0:
+            print(f"step: {prob.clock.step:04d}, t: {prob.clock.t:.2f}, time: {(time.time() - t0) / 60:.2f} mins")
+        prob.stepforward(output_freq)
+        if on_frame is not None:
+            on_frame(prob, frame)

@@ -1,0 +1,95 @@
+"""Host-side mirror of the FourierFlows ``Problem`` that the reference drivers
+hold (rsw/RotatingShallowWater.jl:70-99, swqg/TwoLayerQG.jl:55-90).  All
+stepping happens in libsw on the GPU; this object only carries the handle,
+the grid description and the clock view, so driver code reads like the
+reference's (``prob.sol``, ``prob.clock``, ``stepforward!(prob, n)`` …).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+from .grid import TwoDGrid
+
+
+class Clock:
+    """FF ``Clock``: a live view of the libsw clock (t, step) plus dt."""
+
+    def __init__(self, ctx, dt):
+        self._ctx, self.dt = ctx, float(dt)
+
+    @property
+    def t(self):
+        return self._ctx.get_clock()[0]
+
+    @property
+    def step(self):
+        return self._ctx.get_clock()[1]
+
+    def set(self, t, step):
+        self._ctx.set_clock(t, step)
+
+
+class Problem:
+    """A model + stepper instance resident on one GPU."""
+
+    def __init__(self, model, *, nx, ny, Lx, Ly, dt, aliased_fraction, stepper, params,
+                 use_filter=False, filter_kw=None, device=0, check_nan=True, T=np.float64,
+                 nop_calcN=False):
+        if np.dtype(T) != np.float64:
+            raise _lib.LibSWError("this build computes in fp64 (T=Float64) only")
+        if stepper not in _lib.STEPPERS:
+            raise ValueError(f"unknown stepper {stepper!r}; expected one of {list(_lib.STEPPERS)}")
+        fk = dict(order=4, innerK=0.65, outerK=1.0, tol=1e-15)
+        unknown = set(filter_kw or {}) - set(fk)
+        if unknown:
+            raise TypeError(f"unknown stepper kwargs {sorted(unknown)}")
+        fk.update(filter_kw or {})
+        cfg = _lib.default_config()
+        cfg.model = model
+        cfg.stepper = _lib.STEPPERS[stepper]
+        cfg.nx, cfg.ny = int(nx), int(ny)
+        cfg.Lx, cfg.Ly = float(Lx), float(Ly)
+        cfg.aliased_fraction = float(aliased_fraction)
+        cfg.dt = float(dt)
+        for k, v in params.items():
+            setattr(cfg, k, v)
+        cfg.use_filter = 1 if use_filter else 0
+        cfg.filter_order = int(fk["order"])
+        cfg.filter_innerK = float(fk["innerK"])
+        cfg.filter_outerK = float(fk["outerK"])
+        cfg.filter_tol = float(fk["tol"])
+        cfg.device = int(device)
+        cfg.check_nan = 1 if check_nan else 0
+        cfg.nop_calcN = 1 if nop_calcN else 0
+        self.ctx = _lib.Context(cfg)
+        self.model = model
+        self.stepper = stepper
+        self.grid = TwoDGrid(nx, Lx, ny, Ly, aliased_fraction)
+        self.clock = Clock(self.ctx, dt)
+        self.params = dict(params)
+
+    # FF prob.sol (a host copy; assignment uploads and dealiases)
+    @property
+    def sol(self):
+        return self.ctx.get_state()
+
+    @sol.setter
+    def sol(self, value):
+        self.ctx.set_state(value)
+
+    def stepforward(self, nsteps=1):
+        """FF ``stepforward!(prob, nsteps)`` (rsw/RSWDriver.jl:212)."""
+        self.ctx.step(nsteps)
+
+    def calcN(self, sol):
+        """``equation.calcN!(N, sol, …)`` on a caller state (no stepping)."""
+        return self.ctx.calcN(sol)
+
+    def close(self):
+        self.ctx.close()
+
+
+def stepforward(prob: Problem, nsteps: int = 1):
+    """``stepforward!(prob, nsteps)``."""
+    prob.stepforward(nsteps)

@@ -1,0 +1,59 @@
+"""``TwoLayerQG`` module mirror (swqg/TwoLayerQG.jl).
+
+Same names, argument meaning and defaults as the reference's ``Problem``
+(:55-72), including F = 2 f0²/Cg²/δρρ0 (:79) and the Complex{Float32} literal
+quirk of its linear operator (:189-193), which libsw reproduces bit for bit.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+from .problem import Problem as _Problem, stepforward  # noqa: F401
+
+
+def Problem(dev="gpu", *, nx=128, ny=None, Lx=2 * np.pi, Ly=None, U=0.5, mu=1e-2, nu=1e-6, nnu=4,
+            f0=3.0, Cg=1.0, drhorho0=0.2, stepper="IFMAB3", dt=5e-2, aliased_fraction=1 / 3,
+            T=np.float64, use_filter=False, device=0, check_nan=True, nop_calcN=False, **stepper_kwargs):
+    """``TwoLayerQG.Problem(dev; nx, ny, Lx, Ly, U, μ, ν, nν, f0, Cg, δρρ0, stepper,
+    dt, aliased_fraction, T, use_filter, stepper_kwargs...)`` (:55-90).
+
+    Note: the reference defaults to T=Float32; this build computes in fp64
+    (BASELINE parity precision) and rejects other T.
+    """
+    if dev not in ("gpu", "GPU", "GPU()"):
+        raise _lib.LibSWError("libsw runs on the GPU only (dev='gpu')")
+    ny = nx if ny is None else ny
+    Ly = Lx if Ly is None else Ly
+    F = 2 * f0 ** 2 / Cg ** 2 / drhorho0
+    params = dict(U=float(U), mu=float(mu), nu=float(nu), nnu=int(nnu), F=float(F))
+    prob = _Problem(_lib.SW_MODEL_QG2, nx=nx, ny=ny, Lx=Lx, Ly=Ly, dt=dt,
+                    aliased_fraction=aliased_fraction, stepper=stepper, params=params,
+                    use_filter=use_filter, filter_kw=stepper_kwargs, device=device,
+                    check_nan=check_nan, T=T, nop_calcN=nop_calcN)
+    return prob
+
+
+def set_solution(prob, q0h):
+    """``set_solution!(prob, q0h)`` (:220-228): upload + dealias."""
+    prob.sol = np.asarray(q0h)
+
+
+def updatevars(prob):
+    """``updatevars!(prob)`` (:113-129): q, ψ, ζ, u, v per layer, shape [2][ny][nx]."""
+    g = prob.grid
+    out = {}
+    for name, fid in (("q", _lib.SW_PHYS_Q), ("psi", _lib.SW_PHYS_PSI), ("zeta", _lib.SW_PHYS_ZETA),
+                      ("u", _lib.SW_PHYS_U), ("v", _lib.SW_PHYS_V)):
+        out[name] = np.stack([prob.ctx.physical(layer * 8 + fid, g.ny, g.nx) for layer in (0, 1)])
+    return out
+
+
+def kinetic_energy(prob):
+    """``kinetic_energy(prob)`` (:230-240), summed over both layers, of the dealiased state."""
+    return prob.ctx.diag(_lib.SW_DIAG_KE)
+
+
+def potential_energy(prob):
+    """``potential_energy(prob)`` (:244-250)."""
+    return prob.ctx.diag(_lib.SW_DIAG_PE)

@@ -1,0 +1,583 @@
+"""CPU oracle for the pseudo-spectral time-step hot path (TEST INFRASTRUCTURE ONLY).
+
+This module is the *checker*, never the product.  Only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+it.  The product path (``juliaraytracingsw_amd`` + ``libsw.so``) never calls
+into this file and fails loudly when the HIP library is missing.
+
+It is a plain fp64 numpy/scipy restatement of the reference algorithm, written
+to mirror the reference op sequence one broadcast / one transform at a time:
+
+* FourierFlows.jl ``TwoDGrid`` / ``dealias!`` / ``makefilter`` / FFT plan
+  semantics (FF is not vendored in the reference; formulas restated from its
+  call sites).
+* ``rsw/RotatingShallowWater.jl`` calcN! (140-230), L (242-307).
+* ``swqg/TwoLayerQG.jl`` streamfunctionfrompv! (101-111), calcN! (152-182),
+  L_kernel! (184-198) including its Complex{Float32} literal quirk.
+* ``utils/IFMAB3.jl`` (9-11, 26-30, 125-169) and FF ``FilteredAB3`` (A7, with
+  ``addlinearterm!`` generalised to the per-mode matvec).
+* ``utils/IFMRK4.jl`` structure (13-22, 157-163) -> Lawson IF-RK4.
+* Driver parameter formulas and initial conditions: ``rsw/RSWDriver.jl:88-176``,
+  ``swqg/TwoLayerDriver.jl:10-68``.
+
+Parity pinning.  The reference cannot run here (no Julia / FourierFlows /
+FFTW).  This restatement is pinned by every known answer the
+reference holds for the path: the Julia ``exp`` of ``Lop(1,1)``
+(rsw/Notebooks/MatrixExponentialTest.ipynb:64,197-199), the per-mode matvec
+assertion (same notebook :498), the ``TwoDGrid`` display (:17-20) and the
+``dt``/``ν`` driver numbers (rsw/Notebooks/RSW_Test.ipynb:228-229), plus the
+analytic known answers listed in SURVEY §8c (linear exactness of IFMAB3 via the
+reference's NOPcalcN! hook, energy conservation of the linear propagator,
+convergence order).  No reference test pins a *stepped* nonlinear state, so
+stepped-state parity against FourierFlows itself is "parity unpinned"; the
+GPU path is checked against this restatement.
+
+Array layout: numpy C order ``[field][l][kr]`` == Julia column-major
+``(nkr, nl, nfield)`` byte for byte.  Physical ``[y][x]`` == Julia ``(nx, ny)``.
+"""
+from __future__ import annotations
+
+import math
+import numpy as np
+
+try:  # scipy's batched expm is the oracle's matrix exponential
+    import scipy.linalg as _sla
+except Exception:  # pragma: no cover
+    _sla = None
+
+# FFT backend: numpy (default, used for golden vectors) or scipy.fft with a
+# worker pool (the timed CPU-baseline leg in bench.py)
+_FFT_WORKERS = None
+
+
+def set_fft_workers(n):
+    """Use scipy.fft with ``n`` threads for the transforms (None: numpy.fft)."""
+    global _FFT_WORKERS
+    _FFT_WORKERS = n
+
+
+def _irfft2(a, s):
+    if _FFT_WORKERS:
+        import scipy.fft as sf
+        return sf.irfft2(a, s=s, axes=(-2, -1), workers=_FFT_WORKERS)
+    return np.fft.irfft2(a, s=s, axes=(-2, -1))
+
+
+def _rfft2(a):
+    if _FFT_WORKERS:
+        import scipy.fft as sf
+        return sf.rfft2(a, axes=(-2, -1), workers=_FFT_WORKERS)
+    return np.fft.rfft2(a, axes=(-2, -1))
+
+
+# utils/IFMAB3.jl:9-11
+AB3H1 = 23 / 12
+AB3H2 = 16 / 12
+AB3H3 = 5 / 12
+
+
+# --------------------------------------------------------------------------
+# FourierFlows TwoDGrid restatement
+# --------------------------------------------------------------------------
+def aliased_index_range(n: int, aliased_fraction: float):
+    """FF ``getaliasedwavenumbers``: 1-based (iL, iR) of the aliased band.
+
+    L = (1-af)/2, R = (1+af)/2, iL = floor(L n) + 1, iR = ceil(R n)
+    (SURVEY A1).  kralias = iL:nkr, lalias = iL:iR (1-based, inclusive).
+    """
+    if not (0.0 < aliased_fraction < 1.0):
+        raise ValueError("aliased_fraction must be in (0, 1)")
+    L = (1 - aliased_fraction) / 2
+    R = (1 + aliased_fraction) / 2
+    iL = math.floor(L * n) + 1
+    iR = math.ceil(R * n)
+    return iL, iR
+
+
+class TwoDGrid:
+    """Restatement of FF ``TwoDGrid(dev; nx, Lx, ny, Ly, aliased_fraction, T)``.
+
+    Called at rsw/RotatingShallowWater.jl:87 and swqg/TwoLayerQG.jl:75.
+    """
+
+    def __init__(self, nx, Lx=2 * np.pi, ny=None, Ly=None, aliased_fraction=1 / 3):
+        ny = nx if ny is None else ny
+        Ly = Lx if Ly is None else Ly
+        if nx % 2 or ny % 2:
+            raise ValueError("nx, ny must be even")
+        self.nx, self.ny, self.Lx, self.Ly = int(nx), int(ny), float(Lx), float(Ly)
+        self.aliased_fraction = float(aliased_fraction)
+        self.dx = self.Lx / self.nx
+        self.dy = self.Ly / self.ny
+        self.x = -self.Lx / 2 + self.dx * np.arange(self.nx)
+        self.y = -self.Ly / 2 + self.dy * np.arange(self.ny)
+        self.nkr = self.nx // 2 + 1
+        self.nl = self.ny
+        # rfftfreq(nx, 2π/Lx*nx) / fftfreq(ny, 2π/Ly*ny): element j = j*(fs/n)
+        mk = (2 * np.pi / self.Lx * self.nx) / self.nx
+        ml = (2 * np.pi / self.Ly * self.ny) / self.ny
+        self.kr = np.arange(self.nkr) * mk
+        lidx = np.concatenate([np.arange(0, self.ny // 2), np.arange(-self.ny // 2, 0)])
+        self.l = lidx * ml
+        self.Krsq = self.kr[None, :] ** 2 + self.l[:, None] ** 2
+        with np.errstate(divide="ignore"):
+            self.invKrsq = np.where(self.Krsq == 0, 0.0, 1.0 / self.Krsq)
+        # dealias index ranges (0-based, half-open)
+        iLx, _ = aliased_index_range(self.nx, self.aliased_fraction)
+        iLy, iRy = aliased_index_range(self.ny, self.aliased_fraction)
+        self.kralias = (iLx - 1, self.nkr)        # zeroed kr columns
+        self.lalias = (iLy - 1, iRy)              # zeroed l rows [a, b)
+        mask = np.ones((self.nl, self.nkr), dtype=bool)
+        mask[:, self.kralias[0]:self.kralias[1]] = False
+        mask[self.lalias[0]:self.lalias[1], :] = False
+        self.live = mask
+        # number of live kr columns and live l rows
+        self.kc = self.kralias[0]
+        self.live_rows = np.concatenate(
+            [np.arange(0, self.lalias[0]), np.arange(self.lalias[1], self.ny)])
+
+    def dealias(self, fh):
+        """FF ``dealias!(fh, grid)`` in place."""
+        fh[..., :, self.kralias[0]:self.kralias[1]] = 0
+        fh[..., self.lalias[0]:self.lalias[1], :] = 0
+        return fh
+
+    # FF rfftplan semantics
+    def irfft(self, fh):
+        """``ldiv!(u, grid.rfftplan, uh)``: normalised c2r (numpy rule for
+        non-Hermitian DC/Nyquist columns: c2c along l then c2r along x)."""
+        return _irfft2(fh, (self.ny, self.nx))
+
+    def rfft(self, f):
+        """``mul!(uh, grid.rfftplan, u)``: unnormalised r2c."""
+        return _rfft2(f)
+
+
+def makefilter(grid: TwoDGrid, order=4, innerK=0.65, outerK=1.0, tol=1e-15):
+    """FF ``makefilter(grid; realvars=true, order, innerK, outerK, tol)`` (A8)."""
+    K = np.sqrt((grid.kr[None, :] * grid.dx / np.pi) ** 2
+                + (grid.l[:, None] * grid.dy / np.pi) ** 2)
+    decay = -np.log(tol) / (outerK - innerK) ** order
+    filt = np.exp(-decay * (K - innerK) ** order)
+    filt[K < innerK] = 1.0
+    return filt
+
+
+def expm_batched(A):
+    """Per-mode matrix exponential (utils/IFMAB3.jl:26-30 ``mapslices(exp, …)``)."""
+    if _sla is None:  # pragma: no cover
+        raise RuntimeError("scipy is required for the oracle's expm")
+    sh = A.shape
+    flat = A.reshape(-1, sh[-2], sh[-1])
+    out = _sla.expm(flat)
+    return out.reshape(sh)
+
+
+def mvmul(A, x):
+    """``mvmul!`` (utils/IFMAB3.jl:90-100, 124-127): y[…,r] = Σ_c A[…,r,c] x[…,c].
+
+    ``A`` has shape [nl, nkr, nf, nf]; ``x`` has shape [nf, nl, nkr]."""
+    return np.einsum("lkrc,clk->rlk", A, x)
+
+
+# --------------------------------------------------------------------------
+# Rotating shallow water (rsw/RotatingShallowWater.jl)
+# --------------------------------------------------------------------------
+class RSWParams:
+    """rsw/RotatingShallowWater.jl:18-23 (ν, nν, f, Cg2)."""
+
+    def __init__(self, nu, nnu, f, Cg):
+        self.nu, self.nnu, self.f, self.Cg2 = float(nu), int(nnu), float(f), float(Cg) ** 2
+
+
+def rsw_L(grid: TwoDGrid, p: RSWParams):
+    """Per-mode 3×3 L (rsw/RotatingShallowWater.jl:242-289), shape [nl,nkr,3,3]."""
+    D = -p.nu * grid.Krsq ** p.nnu
+    k = np.broadcast_to(grid.kr[None, :], D.shape)
+    l = np.broadcast_to(grid.l[:, None], D.shape)
+    L = np.zeros(D.shape + (3, 3), dtype=np.complex128)
+    L[..., 0, 0] = D
+    L[..., 0, 1] = p.f
+    L[..., 0, 2] = -1j * k * p.Cg2
+    L[..., 1, 0] = -p.f
+    L[..., 1, 1] = D
+    L[..., 1, 2] = -1j * l * p.Cg2
+    L[..., 2, 0] = -1j * k
+    L[..., 2, 1] = -1j * l
+    L[..., 2, 2] = D
+    return L
+
+
+def rsw_calcN(sol, grid: TwoDGrid, p: RSWParams):
+    """rsw/RotatingShallowWater.jl:140-230, op for op.  ``sol`` is dealiased
+    IN PLACE (line 141), exactly as the reference does."""
+    grid.dealias(sol)
+    kr = grid.kr[None, :]
+    l = grid.l[:, None]
+    uh, vh, etah = sol[0].copy(), sol[1].copy(), sol[2].copy()
+    N = np.empty_like(sol)
+    u = grid.irfft(uh)                                   # :154-156
+    v = grid.irfft(vh)                                   # :159-161
+    uux = grid.irfft(1j * kr * uh) * u                   # :170-172
+    N[0] = -grid.rfft(uux)                               # :173-174
+    vvy = grid.irfft(1j * l * vh) * v                    # :179-181
+    N[1] = -grid.rfft(vvy)                               # :182-183
+    vuy = grid.irfft(1j * l * uh) * v                    # :193-195
+    N[0] += -grid.rfft(vuy)                              # :196-197
+    uvx = grid.irfft(1j * kr * vh) * u                   # :202-204
+    N[1] += -grid.rfft(uvx)                              # :205-206
+    eta = grid.irfft(etah)                               # :212-214
+    N[2] = -1j * kr * grid.rfft(u * eta)                 # :218-220
+    N[2] += -1j * l * grid.rfft(v * eta)                 # :224-226
+    return N
+
+
+def rsw_NOPcalcN(sol, grid, p):
+    """rsw/RotatingShallowWater.jl:135-138 (N .= 0) — the linear-only hook."""
+    return np.zeros_like(sol)
+
+
+def rsw_updatevars(sol, grid: TwoDGrid, p: RSWParams):
+    """rsw/RotatingShallowWater.jl:101-116 -> dict of physical fields."""
+    grid.dealias(sol)
+    kr = grid.kr[None, :]
+    l = grid.l[:, None]
+    zh = 1j * kr * sol[1] - 1j * l * sol[0] - p.f * sol[2]
+    return {"u": grid.irfft(sol[0]), "v": grid.irfft(sol[1]),
+            "eta": grid.irfft(sol[2]), "zeta": grid.irfft(zh)}
+
+
+def parsevalsum2(uh, grid: TwoDGrid):
+    """FF ``parsevalsum2`` (copy at thomasyamada/ThomasYamada.jl:319-331)."""
+    U = np.abs(uh) ** 2
+    s = 2 * U.sum() - U[:, 0].sum()
+    if grid.nx % 2 == 0:
+        s -= U[:, -1].sum()
+    norm = grid.Lx * grid.Ly / (grid.nx ** 2 * grid.ny ** 2)
+    return norm * s
+
+
+def rsw_energies(sol, grid, p):
+    """KE, PE (rsw/RotatingShallowWater.jl:323-336) of the dealiased state."""
+    s = grid.dealias(sol.copy())
+    KE = (parsevalsum2(s[0], grid) + parsevalsum2(s[1], grid)) / (2 * grid.Lx * grid.Ly)
+    PE = 0.5 * p.Cg2 * parsevalsum2(s[2], grid) / (grid.Lx * grid.Ly)
+    return KE, PE
+
+
+# --------------------------------------------------------------------------
+# Two-layer QG (swqg/TwoLayerQG.jl)
+# --------------------------------------------------------------------------
+class QG2Params:
+    """swqg/TwoLayerQG.jl:23-30, F = 2 f0²/Cg²/δρρ0 (:79)."""
+
+    def __init__(self, U, mu, nu, nnu, f0=3.0, Cg=1.0, drhorho0=0.2, F=None):
+        self.U, self.mu, self.nu, self.nnu = float(U), float(mu), float(nu), int(nnu)
+        self.F = float(2 * f0 ** 2 / Cg ** 2 / drhorho0) if F is None else float(F)
+
+
+def qg2_streamfunction(qh, grid: TwoDGrid, p: QG2Params):
+    """swqg/TwoLayerQG.jl:101-111 (same evaluation order)."""
+    K2 = grid.Krsq
+    q1, q2 = qh[0], qh[1]
+    psi = np.empty_like(qh)
+    psi[0] = -(K2 * q1 + p.F * (q1 + q2))
+    psi[1] = -(K2 * q2 + p.F * (q1 + q2))
+    psi /= K2 + 2 * p.F
+    psi *= grid.invKrsq
+    return psi
+
+
+def qg2_L(grid: TwoDGrid, p: QG2Params):
+    """swqg/TwoLayerQG.jl:184-206, with the Complex{Float32} literal quirk
+    (SURVEY A11): PV_term, drag_term and the Sinv numerators are rounded to
+    fp32 before being widened back to fp64.  Shape [nl, nkr, 2, 2]."""
+    k = np.broadcast_to(grid.kr[None, :], grid.Krsq.shape).astype(np.float64)
+    K2 = k ** 2 + np.broadcast_to(grid.l[:, None], grid.Krsq.shape) ** 2
+    with np.errstate(divide="ignore"):
+        K2inv = np.where(K2 == 0, 0.0, 1.0 / K2)
+    D = -p.nu * grid.Krsq ** p.nnu
+    f32 = np.float32
+    pv1_im = (((-2.0 * k) * p.F) * p.U).astype(f32).astype(np.float64)
+    pv2_im = (((2.0 * k) * p.F) * p.U).astype(f32).astype(np.float64)
+    drag2 = (p.mu * K2).astype(f32).astype(np.float64)
+    psi_re = [np.zeros_like(K2), drag2]
+    psi_im = [pv1_im, pv2_im]
+    a = ((-K2) - p.F).astype(f32).astype(np.float64)
+    b = np.full_like(K2, f32(-p.F), dtype=np.float64)
+    den = K2 + 2 * p.F
+    S = [[(a / den) * K2inv, (b / den) * K2inv],
+         [(b / den) * K2inv, (a / den) * K2inv]]
+    L = np.zeros(K2.shape + (2, 2), dtype=np.complex128)
+    for r in range(2):
+        for c in range(2):
+            L[..., r, c] = psi_re[r] * S[r][c] + 1j * (psi_im[r] * S[r][c])
+    L[..., 0, 0] = (L[..., 0, 0].real + D) + 1j * (L[..., 0, 0].imag + (-k * p.U))
+    L[..., 1, 1] = (L[..., 1, 1].real + D) + 1j * (L[..., 1, 1].imag + (k * p.U))
+    return L
+
+
+def qg2_calcN(sol, grid: TwoDGrid, p: QG2Params):
+    """swqg/TwoLayerQG.jl:152-182 (batched over both layers), sol dealiased in place."""
+    grid.dealias(sol)
+    kr = grid.kr[None, :]
+    l = grid.l[:, None]
+    qh = sol.copy()
+    psih = qg2_streamfunction(qh, grid, p)
+    q = grid.irfft(qh)                                   # :157-159
+    psixq = grid.irfft(1j * kr * psih) * q               # :167-169
+    N = -1j * l * grid.rfft(psixq)                       # :170-171
+    psiyq = grid.irfft(1j * l * psih) * q                # :175-177
+    N += 1j * kr * grid.rfft(psiyq)                      # :178-179
+    return N
+
+
+def qg2_energies(sol, grid, p):
+    """KE per layer and PE (swqg/TwoLayerQG.jl:230-252); reads sol as is."""
+    psih = qg2_streamfunction(sol, grid, p)
+    a = grid.Krsq * np.abs(psih) ** 2
+
+    def parsevalsum(fh):
+        s = 2 * fh.sum() - fh[:, 0].sum()
+        if grid.nx % 2 == 0:
+            s -= fh[:, -1].sum()
+        return (grid.Lx * grid.Ly / (grid.nx ** 2 * grid.ny ** 2)) * s.real
+
+    KE1 = parsevalsum(a[0]) / (grid.Lx * grid.Ly)
+    KE2 = parsevalsum(a[1]) / (grid.Lx * grid.Ly)
+    PE = 1 / (2 * grid.Lx * grid.Ly) * p.F * parsevalsum(np.abs(psih[0] - psih[1]) ** 2)
+    return (KE1, KE2), PE
+
+
+# --------------------------------------------------------------------------
+# Time steppers
+# --------------------------------------------------------------------------
+class Clock:
+    def __init__(self, dt):
+        self.dt, self.t, self.step = float(dt), 0.0, 0
+
+
+class FilteredAB3:
+    """FF ``FilteredAB3TimeStepper`` with ``addlinearterm!`` generalised to the
+    per-mode matvec.  Filter kwargs as keywords."""
+
+    def __init__(self, L, grid, nf, order=4, innerK=0.65, outerK=1.0, tol=1e-15):
+        self.L = L
+        self.filter = makefilter(grid, order=order, innerK=innerK, outerK=outerK, tol=tol)[None]
+        shape = (nf, grid.nl, grid.nkr)
+        self.RHS = np.zeros(shape, np.complex128)
+        self.RHSm1 = np.zeros(shape, np.complex128)
+        self.RHSm2 = np.zeros(shape, np.complex128)
+
+    def stepforward(self, sol, clock, calcN, grid, params):
+        self.RHS = calcN(sol, grid, params)
+        self.RHS += mvmul(self.L, sol)                  # addlinearterm! (matvec)
+        if clock.step < 3:
+            sol += clock.dt * self.RHS
+        else:
+            sol += clock.dt * (AB3H1 * self.RHS - AB3H2 * self.RHSm1 + AB3H3 * self.RHSm2)
+        sol *= self.filter
+        clock.t += clock.dt
+        clock.step += 1
+        self.RHSm2 = self.RHSm1.copy()
+        self.RHSm1 = self.RHS.copy()
+
+
+class IFMAB3:
+    """utils/IFMAB3.jl:68-88, 128-169 (CPU method)."""
+
+    def __init__(self, L, dt, grid, nf, use_filter=False, diagonal=False, **filter_kw):
+        self.expLdt = expm_batched(L * dt)
+        self.exp2Ldt = expm_batched(L * 2 * dt)
+        shape = (nf, grid.nl, grid.nkr)
+        self.N = np.zeros(shape, np.complex128)
+        self.Nm1 = np.zeros(shape, np.complex128)
+        self.Nm2 = np.zeros(shape, np.complex128)
+        if use_filter:
+            self.filter = makefilter(grid, **filter_kw)[None]
+        else:
+            self.filter = np.ones((1, grid.nl, grid.nkr))
+
+    def stepforward(self, sol, clock, calcN, grid, params):
+        self.N = calcN(sol, grid, params)                            # :158
+        if clock.step < 3:                                           # :130-132
+            sol += clock.dt * self.N
+            sol[...] = mvmul(self.expLdt, sol)
+        else:                                                        # :134-137
+            eN1 = mvmul(self.expLdt, self.Nm1)
+            e2N2 = mvmul(self.exp2Ldt, self.Nm2)
+            sol += clock.dt * (AB3H1 * self.N - AB3H2 * eN1 + AB3H3 * e2N2)
+            sol[...] = mvmul(self.expLdt, sol)
+        sol *= self.filter                                           # :160
+        clock.t += clock.dt
+        clock.step += 1
+        self.Nm2 = self.Nm1.copy()                                   # :165-166
+        self.Nm1 = self.N.copy()
+
+
+class IFMRK4:
+    """Lawson integrating-factor RK4, the build's definition of the draft
+    utils/IFMRK4.jl (struct fields expLdt, expL½dt, k₁..k₄, filter at :13-22;
+    four calcN! evaluations at :157-163).  SURVEY §8a A9:
+      k1 = N(u); k2 = N(H(u + dt/2 k1)); k3 = N(H u + dt/2 k2);
+      k4 = N(E u + dt H k3); u <- E u + dt/6 (E k1 + 2H(k2 + k3) + k4); filter.
+    """
+
+    def __init__(self, L, dt, grid, nf, use_filter=False, **filter_kw):
+        self.expLdt = expm_batched(L * dt)
+        self.expLhdt = expm_batched(L * 0.5 * dt)
+        if use_filter:
+            self.filter = makefilter(grid, **filter_kw)[None]
+        else:
+            self.filter = np.ones((1, grid.nl, grid.nkr))
+
+    def stepforward(self, sol, clock, calcN, grid, params):
+        dt = clock.dt
+        E, H = self.expLdt, self.expLhdt
+        k1 = calcN(sol, grid, params)                 # dealiases sol in place
+        x = mvmul(H, sol + 0.5 * dt * k1)
+        k2 = calcN(x, grid, params)
+        x = mvmul(H, sol) + 0.5 * dt * k2
+        k3 = calcN(x, grid, params)
+        x = mvmul(E, sol) + dt * mvmul(H, k3)
+        k4 = calcN(x, grid, params)
+        sol[...] = mvmul(E, sol) + dt / 6 * (mvmul(E, k1) + 2 * mvmul(H, k2 + k3) + k4)
+        sol *= self.filter
+        clock.t += dt
+        clock.step += 1
+
+
+# --------------------------------------------------------------------------
+# Problems and driver formulas
+# --------------------------------------------------------------------------
+class Problem:
+    """Mirror of ``RotatingShallowWater.Problem`` / ``TwoLayerQG.Problem`` for
+    the oracle (model in {"rsw", "qg2"}, stepper in {"FilteredAB3", "IFMAB3",
+    "IFMRK4"}, or "NOP" calcN for the linear-only check)."""
+
+    def __init__(self, model, stepper, nx, dt, Lx=2 * np.pi, aliased_fraction=1 / 3,
+                 params=None, use_filter=False, calcN=None, **filter_kw):
+        self.grid = TwoDGrid(nx, Lx, aliased_fraction=aliased_fraction)
+        self.params = params
+        self.model = model
+        if model == "rsw":
+            self.nf = 3
+            self.L = rsw_L(self.grid, params)
+            self.calcN = rsw_calcN if calcN is None else calcN
+        elif model == "qg2":
+            self.nf = 2
+            self.L = qg2_L(self.grid, params)
+            self.calcN = qg2_calcN if calcN is None else calcN
+        else:
+            raise ValueError(model)
+        self.clock = Clock(dt)
+        if stepper == "FilteredAB3":
+            self.ts = FilteredAB3(self.L, self.grid, self.nf, **filter_kw)
+        elif stepper == "IFMAB3":
+            self.ts = IFMAB3(self.L, dt, self.grid, self.nf, use_filter=use_filter, **filter_kw)
+        elif stepper == "IFMRK4":
+            self.ts = IFMRK4(self.L, dt, self.grid, self.nf, use_filter=use_filter, **filter_kw)
+        else:
+            raise ValueError(stepper)
+        self.sol = np.zeros((self.nf, self.grid.nl, self.grid.nkr), np.complex128)
+
+    def set_solution(self, solh):
+        """set_solution! (rsw/RotatingShallowWater.jl:309-321): copies then
+        updatevars! which dealiases the state in place (:104)."""
+        self.sol[...] = solh
+        self.grid.dealias(self.sol)
+
+    def stepforward(self, nsteps=1):
+        for _ in range(nsteps):
+            self.ts.stepforward(self.sol, self.clock, self.calcN, self.grid, self.params)
+
+
+def rsw_driver_params(nx, Lx=2 * np.pi, aliased_fraction=1 / 3, nnu=4, nutune=20.0,
+                      cfltune=0.01, ag=0.2, aw=0.1):
+    """rsw/RSWDriver.jl:134-148 (defaults from rsw/RSWParameters.jl)."""
+    dx = Lx / nx
+    kmax = (nx / 2 - 1) * Lx / (2 * np.pi) * (1 - aliased_fraction)
+    umax = ag + aw
+    dt = cfltune / umax * dx
+    nu = nutune * dx / (kmax ** (2 * nnu)) / dt
+    return dt, nu
+
+
+def qg2_compute_parameters(deformation_radius, intervortex_radius, avg_eddy_velocity, H, f0):
+    """swqg/TwoLayerDriver.jl:17-27."""
+    c1, c2 = 3.2, 0.36
+    l_star = intervortex_radius / deformation_radius
+    kappa_star = c2 / np.log(l_star / c1)
+    U = avg_eddy_velocity / l_star
+    mu = 2 * U * kappa_star / deformation_radius
+    db = 4 * f0 ** 2 * deformation_radius ** 2 / H
+    return mu, db, U
+
+
+def qg2_driver_params(nx, Lx=2 * np.pi, aliased_fraction=1 / 3, nnu=4, nutune=40.0,
+                      cfltune=0.025, ug=0.025, f=3.0, Cg=1.0, rd=1 / 6, lv=1.0, H=1.0):
+    """swqg/TwoLayerDriver.jl:29-63 (defaults from swqg/TwoLayerParameters.jl)."""
+    dx = Lx / nx
+    kmax = (nx / 2 - 1) * (1 - aliased_fraction)
+    mu, db, U = qg2_compute_parameters(rd, lv, ug, H, f)
+    drr0 = db / (Cg / H)
+    dt = cfltune / ug * dx
+    nu = nutune * 2 * np.pi / nx / (kmax ** (2 * nnu)) / dt
+    F = 2 * f ** 2 / Cg ** 2 / drr0
+    return dict(dt=dt, nu=nu, U=U, mu=mu, drhorho0=drr0, F=F, f0=f, Cg=Cg)
+
+
+def shafer_ic_parts(grid: TwoDGrid, Kg, Kw, f, Cg2, rng):
+    """Spectral pieces of ``set_shafer_initial_condition!`` before the Umax
+    normalisation (rsw/RSWDriver.jl:93-106, 118-120).  Julia's RNG stream is
+    not reproducible here: ``rng`` is a numpy Generator (seeded by the caller)
+    drawing phase = 2π·U[0,1) then sgn = sign(U[0,1) - 0.5), each over
+    (nkr, nl) in Julia column-major order."""
+    K2 = grid.Krsq
+    geo = (Kg[0] ** 2 <= K2) & (K2 <= Kg[1] ** 2) & (K2 > 0)
+    wav = (Kw[0] ** 2 <= K2) & (K2 <= Kw[1] ** 2) & (K2 > 0)
+    phase = 2 * np.pi * rng.random((grid.nkr, grid.nl)).T
+    sgn = np.sign(rng.random((grid.nkr, grid.nl)).T - 0.5)
+    shift = np.exp(1j * phase)
+    om = np.sqrt(f ** 2 + Cg2 * K2)
+    gamp = 1 / om
+    with np.errstate(divide="ignore", invalid="ignore"):
+        wamp = np.sqrt(grid.invKrsq) / (2 * om)
+    kr = np.broadcast_to(grid.kr[None, :], K2.shape)
+    l = np.broadcast_to(grid.l[:, None], K2.shape)
+    z = np.zeros(K2.shape, np.complex128)
+    ugh, vgh, egh = z.copy(), z.copy(), z.copy()
+    uwh, vwh, ewh = z.copy(), z.copy(), z.copy()
+    egh[geo] += (gamp * f * shift)[geo]
+    ugh[geo] += (-gamp * 1j * Cg2 * l * shift)[geo]
+    vgh[geo] += (gamp * 1j * Cg2 * kr * shift)[geo]
+    ewh[wav] += (wamp * K2 * shift)[wav]
+    uwh[wav] += (wamp * (sgn * kr * om * shift + 1j * f * l * shift))[wav]
+    vwh[wav] += (wamp * (sgn * l * om * shift - 1j * f * kr * shift))[wav]
+    return (ugh, vgh, egh), (uwh, vwh, ewh)
+
+
+def shafer_ic(grid: TwoDGrid, Kg, Kw, ag, aw, f, Cg2, rng):
+    """rsw/RSWDriver.jl:88-132 with numpy's c2r for the Umax normalisation."""
+    (ugh, vgh, egh), (uwh, vwh, ewh) = shafer_ic_parts(grid, Kg, Kw, f, Cg2, rng)
+    ug, vg = grid.irfft(ugh), grid.irfft(vgh)
+    Umax = np.max(np.sqrt(ug ** 2 + vg ** 2))
+    ugh, vgh, egh = ugh * (ag / Umax), vgh * (ag / Umax), egh * (ag / Umax)
+    uw, vw = grid.irfft(uwh), grid.irfft(vwh)
+    Umax = np.max(np.sqrt(uw ** 2 + vw ** 2))
+    uwh, vwh, ewh = uwh * (aw / Umax), vwh * (aw / Umax), ewh * (aw / Umax)
+    return np.stack([ugh + uwh, vgh + vwh, egh + ewh])
+
+
+def qg2_seed_ic(grid: TwoDGrid, rng):
+    """swqg/TwoLayerDriver.jl:10-15: q0 = 1e-2·randn(nx, ny, 2); rfft over (1,2)."""
+    q0 = 1e-2 * rng.standard_normal((2, grid.ny, grid.nx))
+    return grid.rfft(q0)
+
+
+def parity_error(a, b, grid: TwoDGrid):
+    """SURVEY §8c metric: max|a-b| / max|b| over the dealias-masked state."""
+    m = grid.live[None]
+    den = np.max(np.abs(np.where(m, b, 0)))
+    num = np.max(np.abs(np.where(m, a - b, 0)))
+    return num / den if den > 0 else num

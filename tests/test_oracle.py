@@ -1,0 +1,211 @@
+"""CPU tests: pin the oracle restatement to every known answer the reference
+holds for this path plus analytic known answers, and check
+the committed golden fixtures against it."""
+import glob
+import json
+import os
+
+import numpy as np
+import pytest
+
+import sw_cases
+import sw_oracle as O
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+# --- known answers from the reference's own notebooks -----------------------
+def test_expm_known_answer():
+    """rsw/Notebooks/MatrixExponentialTest.ipynb:64 (Lop) and :197-199 (printed exp)."""
+    k = l = 1
+    Lop = np.array([[0, 1, 1j * k], [-1, 0, 1j * l], [-1j * k, -1j * l, 0]])
+    E = O.expm_batched(Lop[None])[0]
+    ref = np.array([
+        [1.0, 1.7182818284590455, 1.7182818284590453j],
+        [-0.6321205588285577, 1.0, 0.6321205588285577j],
+        [-0.6321205588285578j, -1.7182818284590453j, 2.0861612696304874],
+    ])
+    assert np.max(np.abs(E - ref)) <= 4 * np.finfo(float).eps
+
+
+def test_mvmul_assertion():
+    """MatrixExponentialTest.ipynb:498: A[1,1,:,:]*orig_x[1,1,:] ≈ x[1,1,:] after
+    the in-place per-mode matvec (utils/IFMAB3.jl:90-100)."""
+    rng = np.random.default_rng(0)
+    A = rng.random((4, 5, 3, 3)) + 1j * rng.random((4, 5, 3, 3))
+    x = rng.random((3, 4, 5)) + 1j * rng.random((3, 4, 5))
+    y = O.mvmul(A, x)
+    np.testing.assert_allclose(y[:, 0, 0], A[0, 0] @ x[:, 0, 0], rtol=1e-14)
+
+
+def test_grid_display():
+    """MatrixExponentialTest.ipynb:17-20: TwoDGrid(Lx=2π, nx=128) display."""
+    g = O.TwoDGrid(128)
+    assert g.dx == 0.04908738521234052
+    assert g.x[0] == -3.141592653589793
+    assert abs(g.x[-1] - 3.0925052683774528) <= 4e-16
+    assert g.aliased_fraction == 0.3333333333333333
+
+
+def test_driver_dt_nu_known_answer():
+    """rsw/Notebooks/RSW_Test.ipynb:206 formulas, printed at :228-229."""
+    nx, Lx = 512, 2 * np.pi
+    dx = Lx / nx
+    kmax = nx / 2 - 1
+    cfltune, umax = 0.1, 0.3
+    nutune = 1 / cfltune
+    dt = cfltune / umax * dx
+    nu = nutune * 2 * np.pi / nx / (kmax ** (2 * 4)) / dt
+    assert nu == 1.6780303489894543e-18
+    assert dt == 0.00409061543436171
+
+
+def test_rsw_driver_params_2048():
+    """rsw/RSWDriver.jl:134-148 at the BASELINE sizes."""
+    dt, nu = O.rsw_driver_params(2048)
+    assert dt == 1.0226538585904273e-4
+    assert abs(nu / 1.281965e-20 - 1) < 1e-6
+    dt, nu = O.rsw_driver_params(1024)
+    assert dt == 2.0453077171808545e-4
+    assert abs(nu / 3.307609e-18 - 1) < 1e-6
+
+
+def test_qg2_driver_params():
+    """swqg/TwoLayerDriver.jl:17-63 (U=0.0041667, μ=0.0286347, F=18, dt=2π/N)."""
+    P = O.qg2_driver_params(2048)
+    assert abs(P["U"] - 0.0041667) < 1e-7
+    assert abs(P["mu"] - 0.0286347) < 1e-7
+    assert P["F"] == 18.0
+    assert abs(P["dt"] - 2 * np.pi / 2048) < 1e-18
+    assert abs(P["nu"] / 8.546e-22 - 1) < 1e-3
+
+
+def test_dealias_ranges():
+    """FF getaliasedwavenumbers: N=2048 -> kralias 683:1025, lalias 683:1366."""
+    g = O.TwoDGrid(2048)
+    assert g.kralias == (682, 1025) and g.lalias == (682, 1366)
+    assert g.kc == 682 and len(g.live_rows) == 1364
+    assert g.live.sum() == 682 * 1364
+
+
+def test_qg2_L_float32_quirk():
+    """swqg/TwoLayerQG.jl:189-193: PV/drag/Sinv literals are Complex{Float32}."""
+    g = O.TwoDGrid(64)
+    p = O.QG2Params(0.0041666, 0.02863, 1e-10, 4, F=18.0)
+    L = O.qg2_L(g, p)
+    k, l = 5, 7
+    K2 = k * k + l * l
+    pv2 = float(np.float32(((2.0 * k) * p.F) * p.U))
+    a = float(np.float32(-K2 - p.F))
+    S11 = (a / (K2 + 2 * p.F)) * (1 / K2)
+    D = -p.nu * K2 ** 4
+    drag = float(np.float32(p.mu * K2))
+    assert L[l, k, 1, 1] == complex(drag * S11 + D, pv2 * S11 + k * p.U)
+    # the quirk is visible at the 1e-9 level against an all-fp64 evaluation
+    S11_64 = (-K2 - p.F) / (K2 + 2 * p.F) / K2
+    assert abs(pv2 * S11 - (2 * k * p.F * p.U) * S11_64) > 0
+
+
+# --- analytic known answers --------------------------------------------------
+def _rsw_linear_problem(stepper, n=32, nu=0.0, dt=0.01):
+    params = O.RSWParams(nu, 4, 3.0, 1.0)
+    pr = O.Problem("rsw", stepper, n, dt, params=params, calcN=O.rsw_NOPcalcN)
+    rng = np.random.default_rng(3)
+    ic = rng.standard_normal(pr.sol.shape) + 1j * rng.standard_normal(pr.sol.shape)
+    pr.set_solution(ic)
+    return pr
+
+
+def test_ifmab3_linear_exactness():
+    """NOPcalcN! hook (rsw/RotatingShallowWater.jl:135-138): IFMAB3 gives exp(L t)·sol0."""
+    pr = _rsw_linear_problem("IFMAB3", nu=1e-6)
+    sol0 = pr.sol.copy()
+    pr.stepforward(7)
+    exact = O.mvmul(O.expm_batched(pr.L * (7 * pr.clock.dt)), sol0)
+    assert O.parity_error(pr.sol, exact, pr.grid) < 1e-12
+
+
+def test_linear_energy_conservation():
+    """diag(1,1,Cg²)·L is anti-Hermitian at ν=0, so KE+PE is conserved by exp(L t)."""
+    pr = _rsw_linear_problem("IFMRK4", nu=0.0, dt=0.05)
+    e0 = sum(O.rsw_energies(pr.sol, pr.grid, pr.params))
+    pr.stepforward(50)
+    e1 = sum(O.rsw_energies(pr.sol, pr.grid, pr.params))
+    assert abs(e1 / e0 - 1) < 1e-12
+
+
+def test_fab3_linear_third_order():
+    """FilteredAB3 on the linear problem converges at third order to exp(L t)."""
+    errs = []
+    for dt in (0.02, 0.01):
+        params = O.RSWParams(0.0, 4, 3.0, 1.0)
+        pr = O.Problem("rsw", "FilteredAB3", 32, dt, params=params, calcN=O.rsw_NOPcalcN,
+                       innerK=10.0, outerK=11.0)  # filter ≡ 1
+        rng = np.random.default_rng(3)
+        ic = np.zeros(pr.sol.shape, complex)
+        ic[:, 1:4, 1:4] = rng.standard_normal((3, 3, 3))
+        pr.set_solution(ic)
+        sol0 = pr.sol.copy()
+        nsteps = int(round(0.4 / dt))
+        pr.stepforward(nsteps)
+        exact = O.mvmul(O.expm_batched(pr.L * (nsteps * dt)), sol0)
+        errs.append(np.max(np.abs(pr.sol - exact)))
+    # Euler start-up steps are first order per step but only 3 of them: the
+    # global error is dominated by O(dt²) from them; check ≥ 2nd order
+    assert errs[0] / errs[1] > 3.5
+
+
+def test_ifmrk4_fourth_order():
+    """Lawson IF-RK4 converges at fourth order on the nonlinear RSW
+    step (ν = 0, live modes; aliased modes are dead)."""
+    p = dict(sw_cases.case_params("rsw_ifmrk4", 32), nu=0.0)
+    sols = {}
+    for dt in (0.02, 0.01, 0.0025):
+        p2 = dict(p, dt=dt)
+        pr = sw_cases.oracle_problem(p2)
+        pr.set_solution(sw_cases.initial_condition(p2, pr.grid))
+        pr.stepforward(int(round(0.16 / dt)))
+        sols[dt] = pr.grid.dealias(pr.sol.copy())
+    e1 = np.max(np.abs(sols[0.02] - sols[0.0025]))
+    e2 = np.max(np.abs(sols[0.01] - sols[0.0025]))
+    assert e1 / e2 > 12  # 4th order: (16·(1 - 1/512)/(1 - 1/16)) ≈ 17
+
+
+def test_kr0_column_hermitian_part_preserved():
+    """The physical fields depend only on the Hermitian part of the kr=0 column
+    (numpy c2r rule); N is Hermitian there."""
+    p = sw_cases.case_params("rsw_fab3", 32)
+    pr = sw_cases.oracle_problem(p)
+    pr.set_solution(sw_cases.initial_condition(p, pr.grid))
+    N = pr.calcN(pr.sol.copy(), pr.grid, pr.params)
+    col = N[:, :, 0]
+    l = np.arange(32)
+    live = pr.grid.live[:, 0] & pr.grid.live[(-l) % 32, 0]
+    herm = np.conj(col[:, (-l) % 32])
+    assert np.max(np.abs((col - herm)[:, live])) < 1e-12 * np.max(np.abs(col))
+
+
+# --- golden fixtures -----------------------------------------------------------
+GOLDEN_FILES = sorted(glob.glob(os.path.join(GOLDEN, "*.npz")))
+
+
+def test_golden_present():
+    assert len(GOLDEN_FILES) == 2 * len(sw_cases.CASES)
+
+
+@pytest.mark.parametrize("fn", GOLDEN_FILES, ids=[os.path.basename(f) for f in GOLDEN_FILES])
+def test_oracle_reproduces_golden(fn):
+    d = np.load(fn)  # allow_pickle=False (data only)
+    p = json.loads(str(d["params"]))
+    pr = sw_cases.oracle_problem(p)
+    ic = sw_cases.initial_condition(p, pr.grid)
+    pr.set_solution(ic)
+    assert np.array_equal(pr.sol, d["ic"])
+    N0 = pr.calcN(pr.sol.copy(), pr.grid, pr.params)
+    assert O.parity_error(N0, d["N0"], pr.grid) < 1e-13
+    done = 0
+    for key in sorted((k for k in d.files if k.startswith("sol")), key=lambda k: int(k[3:])):
+        s = int(key[3:])
+        pr.stepforward(s - done)
+        done = s
+        assert O.parity_error(pr.sol, d[key], pr.grid) < 1e-12, key
