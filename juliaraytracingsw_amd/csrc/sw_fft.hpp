@@ -1,14 +1,16 @@
 // Device-side fp64 FFT primitive for gfx950: one power-of-two transform of
 // length N per "line", NT = N/8 threads per line, 8 complex points per thread,
-// Stockham autosort radix-8 stages (plus one radix-4/2 stage) exchanged
-// through LDS.  Twiddles come from a per-length global table W_N^m, which is
-// L1/L2 resident.
+// Stockham autosort stages (one leading radix-2/4 stage when log2 N is not a
+// multiple of 3, then radix-8 stages) exchanged through LDS.
 //
-// Register convention: on entry thread t of a line holds v[s] = x[t + s*NT]
-// (s = 0..7); on exit the transform sits in the line's LDS buffer in natural
-// order (index via LP()).  DIR = -1: forward exp(-2πi jk/N); DIR = +1: inverse,
-// unnormalised.  These transforms replace FF's rfftplan (CUFFT/FFTW) calls,
-// SURVEY A2.
+// Register convention: on entry thread t of a line holds v[s] = x[t + s*NT];
+// on exit it holds v[s] = X[t + s*NT] (natural order).  The last radix-8
+// stage already leaves its outputs at t + r*NT, so no final LDS round trip
+// is made; callers that write LDS after fft_line must lds_barrier() first.
+// DIR = -1: forward exp(-2πi jk/N); DIR = +1: inverse, unnormalised.
+// Twiddles: one table load W_N^e per radix-8 butterfly, the other six powers
+// by complex multiplication (≤ 3 roundings deep).  These transforms replace
+// FF's rfftplan (CUFFT/FFTW) calls, SURVEY A2.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -47,7 +49,7 @@ __device__ __forceinline__ void dft4(double2& x0, double2& x1, double2& x2, doub
   x3 = csub(s1, s3);
 }
 
-// in-place DFT-8 on v[0..7] (natural order in, natural order out)
+// in-place DFT-8 (natural order in, natural order out)
 template <int DIR>
 __device__ __forceinline__ void dft8(double2& v0, double2& v1, double2& v2, double2& v3,
                                      double2& v4, double2& v5, double2& v6, double2& v7) {
@@ -69,47 +71,14 @@ __device__ __forceinline__ double2 twiddle(const double2* __restrict__ tw, int m
   return dir < 0 ? w : cconj(w);
 }
 
-// One Stockham stage of radix R = 2^lR (8, 4 or 2) with current sub-length
-// Ns = 2^lNs.  v[] holds x[t + s*NT]; results are stored to LDS.
-template <int DIR, int lR>
-__device__ __forceinline__ void stockham_stage(double2 (&v)[8], int t, int NT, int log2N, int lNs,
-                                               const double2* __restrict__ tw,
-                                               double2* __restrict__ line) {
-  constexpr int R = 1 << lR;
-  constexpr int B = 8 / R;  // butterflies per thread
-  const int Nsm1 = (1 << lNs) - 1;
-  const int lts = log2N - lNs - lR;  // log2 of N/(Ns*R)
-#pragma unroll
-  for (int h = 0; h < B; ++h) {
-    const int j = t + h * NT;
-    const int k = j & Nsm1;
-    double2 x[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) x[r] = v[h + r * B];
-    if (lNs > 0) {
-#pragma unroll
-      for (int r = 1; r < R; ++r) x[r] = cmul(x[r], twiddle(tw, (r * k) << lts, DIR));
-    }
-    if constexpr (R == 8) {
-      dft8<DIR>(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]);
-    } else if constexpr (R == 4) {
-      dft4<DIR>(x[0], x[1], x[2], x[3]);
-    } else {
-      dft2<DIR>(x[0], x[1]);
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) v[h + r * B] = x[r];
-  }
-  __syncthreads();  // every thread has consumed its inputs (in-place LDS)
-#pragma unroll
-  for (int h = 0; h < B; ++h) {
-    const int j = t + h * NT;
-    const int k = j & Nsm1;
-    const int idxD = ((j >> lNs) << (lNs + lR)) + k;
-#pragma unroll
-    for (int r = 0; r < R; ++r) line[LP(idxD + (r << lNs))] = v[h + r * B];
-  }
-  __syncthreads();
+// Workgroup barrier that orders LDS only.  __syncthreads() also waits for
+// every outstanding global load/store (vmcnt(0)), which would stall each FFT
+// stage behind the previous pass's HBM stores; the LDS exchange needs only
+// lgkmcnt(0) before the barrier.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 }
 
 __device__ __forceinline__ void load_line(double2 (&v)[8], int t, int NT, const double2* __restrict__ line) {
@@ -117,7 +86,59 @@ __device__ __forceinline__ void load_line(double2 (&v)[8], int t, int NT, const 
   for (int s = 0; s < 8; ++s) v[s] = line[LP(t + s * NT)];
 }
 
-// Full transform.  v holds x[t + s*NT] on entry; result in `line` (natural order).
+// Leading radix-2 (lR = 1) or radix-4 (lR = 2) stage, Ns = 1 (no twiddles).
+template <int DIR, int lR>
+__device__ __forceinline__ void first_stage_small(double2 (&v)[8], int t, int NT,
+                                                  double2* __restrict__ line) {
+  constexpr int R = 1 << lR;
+  constexpr int B = 8 / R;  // butterflies per thread
+#pragma unroll
+  for (int h = 0; h < B; ++h) {
+    if constexpr (R == 4) {
+      dft4<DIR>(v[h], v[h + B], v[h + 2 * B], v[h + 3 * B]);
+    } else {
+      dft2<DIR>(v[h], v[h + B]);
+    }
+  }
+  lds_barrier();  // every thread has consumed the previous LDS contents
+#pragma unroll
+  for (int h = 0; h < B; ++h) {
+    const int j = t + h * NT;  // Ns = 1: idxD = j*R
+#pragma unroll
+    for (int r = 0; r < R; ++r) line[LP(j * R + r)] = v[h + r * B];
+  }
+  lds_barrier();
+}
+
+// Radix-8 Stockham stage with sub-length Ns = 2^lNs (one butterfly per thread).
+// last == true: outputs stay in registers (they land at t + r*NT).
+template <int DIR>
+__device__ __forceinline__ void radix8_stage(double2 (&v)[8], int t, int log2N, int lNs,
+                                             const double2* __restrict__ tw,
+                                             double2* __restrict__ line, bool last) {
+  const int k = t & ((1 << lNs) - 1);
+  if (lNs > 0) {
+    const double2 w1 = twiddle(tw, k << (log2N - lNs - 3), DIR);
+    const double2 w2 = cmul(w1, w1), w3 = cmul(w2, w1), w4 = cmul(w2, w2);
+    const double2 w5 = cmul(w4, w1), w6 = cmul(w3, w3), w7 = cmul(w4, w3);
+    v[1] = cmul(v[1], w1);
+    v[2] = cmul(v[2], w2);
+    v[3] = cmul(v[3], w3);
+    v[4] = cmul(v[4], w4);
+    v[5] = cmul(v[5], w5);
+    v[6] = cmul(v[6], w6);
+    v[7] = cmul(v[7], w7);
+  }
+  dft8<DIR>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
+  if (last) return;
+  lds_barrier();  // in-place LDS: everyone has loaded this stage's inputs
+  const int idxD = ((t >> lNs) << (lNs + 3)) + k;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) line[LP(idxD + (r << lNs))] = v[r];
+  lds_barrier();
+}
+
+// Full transform.  v holds x[t + s*NT] on entry and X[t + s*NT] on exit.
 // All threads of the block must call this (it contains barriers).
 template <int DIR>
 __device__ __forceinline__ void fft_line(double2 (&v)[8], int t, int NT, int log2N,
@@ -125,18 +146,19 @@ __device__ __forceinline__ void fft_line(double2 (&v)[8], int t, int NT, int log
   int lNs = 0;
   const int rem = log2N % 3;
   if (rem == 1) {
-    stockham_stage<DIR, 1>(v, t, NT, log2N, lNs, tw, line);
-    lNs += 1;
+    first_stage_small<DIR, 1>(v, t, NT, line);
+    lNs = 1;
     load_line(v, t, NT, line);
   } else if (rem == 2) {
-    stockham_stage<DIR, 2>(v, t, NT, log2N, lNs, tw, line);
-    lNs += 2;
+    first_stage_small<DIR, 2>(v, t, NT, line);
+    lNs = 2;
     load_line(v, t, NT, line);
   }
   while (true) {
-    stockham_stage<DIR, 3>(v, t, NT, log2N, lNs, tw, line);
+    const bool last = lNs + 3 >= log2N;
+    radix8_stage<DIR>(v, t, log2N, lNs, tw, line, last);
+    if (last) break;
     lNs += 3;
-    if (lNs >= log2N) break;
     load_line(v, t, NT, line);
   }
 }

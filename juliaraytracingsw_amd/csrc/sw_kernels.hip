@@ -44,8 +44,8 @@ __device__ __forceinline__ double2 zero2() { return make_double2(0.0, 0.0); }
 //   QG2  outputs (swqg/TwoLayerQG.jl:155-176):          0 Q1, 1 Q2, 2 Ψ1, 3 Ψ2, 4 Ψy1, 5 Ψy2
 // grid: (columns, groups); RSW group f reads field f; QG2 group = layer.
 // ===========================================================================
-template <int MODEL>
-__global__ void __launch_bounds__(1024) k_col_inv(Geom g, Phys p, const double2* __restrict__ X,
+template <int MODEL, int MAXT>
+__global__ void __launch_bounds__(MAXT) k_col_inv(Geom g, Phys p, const double2* __restrict__ X,
                                                   double2* __restrict__ M,
                                                   const double2* __restrict__ tw) {
   extern __shared__ double2 smem[];
@@ -58,25 +58,26 @@ __global__ void __launch_bounds__(1024) k_col_inv(Geom g, Phys p, const double2*
   const double k = kr * g.mk;
   double2 v[8];
 
-  auto store = [&](int o) {
+  auto store = [&](int o) {  // fft_line leaves Y[t + s*NT] in v[s]
     if (live) {
       double2* Mo = M + (long long)o * g.mfield;
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        const int y = c.t + s * c.NT;
-        Mo[midx(g, kr, y)] = line[LP(y)];
-      }
+      for (int s = 0; s < 8; ++s) Mo[midx(g, kr, c.t + s * c.NT)] = v[s];
     }
   };
 
+  // loads are unconditional from a clamped in-bounds address, then selected:
+  // a branch around each load would serialise them (one vmcnt(0) per element)
+  const int krc = live ? kr : g.kc - 1;
   if constexpr (MODEL == MODEL_RSW) {
-    const double2* Xf = X + (long long)grp * g.cfield + (long long)kr * g.LrP;
+    const double2* Xf = X + (long long)grp * g.cfield + (long long)krc * g.LrP;
     double2 x[8];
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       const int m = c.t + s * c.NT;
       const int j = compact_of(g, m);
-      x[s] = (live && j >= 0) ? Xf[j] : zero2();
+      const double2 t = Xf[j >= 0 ? j : 0];
+      x[s] = (live && j >= 0) ? t : zero2();
       v[s] = cscale(x[s], scale);
     }
     fft_line<+1>(v, c.t, c.NT, g.log2ny, tw, line);
@@ -92,17 +93,18 @@ __global__ void __launch_bounds__(1024) k_col_inv(Geom g, Phys p, const double2*
     }
   } else {
     // streamfunctionfrompv! (swqg/TwoLayerQG.jl:101-111)
-    const double2* X1 = X + (long long)kr * g.LrP;
+    const double2* X1 = X + (long long)krc * g.LrP;
     const double2* X2 = X1 + g.cfield;
     double2 q[8], psi[8];
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       const int m = c.t + s * c.NT;
       const int j = compact_of(g, m);
-      double2 q1 = zero2(), q2 = zero2();
-      if (live && j >= 0) {
-        q1 = X1[j];
-        q2 = X2[j];
+      const int jc = j >= 0 ? j : 0;
+      double2 q1 = X1[jc], q2 = X2[jc];
+      if (!(live && j >= 0)) {
+        q1 = zero2();
+        q2 = zero2();
       }
       const double l = lwav(g, m);
       const double K2 = k * k + l * l;
@@ -142,45 +144,47 @@ __device__ __forceinline__ void load_pair(double2 (&v)[8], const LineCtx& c, con
                                           const double2* __restrict__ A,
                                           const double2* __restrict__ B, int y, bool deriv) {
   const int half = g.nx >> 1;
+  double2 a[8], b[8];
+  int kk[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {  // issue every load first (clamped, unconditional)
+    const int m = c.t + s * c.NT;
+    kk[s] = m <= half ? m : g.nx - m;
+    const long long o = midx(g, kk[s] < g.kc ? kk[s] : 0, y);
+    a[s] = A[o];
+    b[s] = B ? B[o] : zero2();
+  }
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
     const int m = c.t + s * c.NT;
-    int kk;
-    bool cj;
-    if (m <= half) {
-      kk = m;
-      cj = false;
-    } else {
-      kk = g.nx - m;
-      cj = true;
+    double2 aa = a[s], bb = b[s];
+    if (deriv) {
+      const double kw = kk[s] * g.mk;
+      aa = cmul_i(aa, kw);
+      bb = cmul_i(bb, kw);
     }
-    double2 z = zero2();
-    if (kk < g.kc) {
-      const long long o = midx(g, kk, y);
-      double2 a = A[o];
-      double2 b = B ? B[o] : zero2();
-      if (deriv) {
-        const double kw = kk * g.mk;
-        a = cmul_i(a, kw);
-        b = cmul_i(b, kw);
-      }
-      if (kk == 0) {
-        a.y = 0.0;
-        b.y = 0.0;
-      }
-      if (cj) {
-        a = cconj(a);
-        b = cconj(b);
-      }
-      z = make_double2(a.x - b.y, a.y + b.x);  // a + i b
+    if (kk[s] == 0) {
+      aa.y = 0.0;
+      bb.y = 0.0;
     }
-    v[s] = z;
+    if (m > half) {
+      aa = cconj(aa);
+      bb = cconj(bb);
+    }
+    const double2 z = make_double2(aa.x - bb.y, aa.y + bb.x);  // a + i b
+    v[s] = kk[s] < g.kc ? z : zero2();
   }
 }
 
-// After a forward FFT of z = a + i b (in LDS), write Â[k], B̂[k] for k < kc.
-__device__ __forceinline__ void store_pair(const LineCtx& c, const Geom& g, const double2* line,
-                                           double2* __restrict__ A, double2* __restrict__ B, int y) {
+// After a forward FFT of z = a + i b (Z[t + s*NT] in v), write Â[k], B̂[k]
+// for k < kc.  Needs Z[nx-k] from a mirror thread: one LDS round trip.
+__device__ __forceinline__ void store_pair(const double2 (&v)[8], const LineCtx& c, const Geom& g,
+                                           double2* line, double2* __restrict__ A,
+                                           double2* __restrict__ B, int y) {
+  lds_barrier();  // previous LDS readers are done
+#pragma unroll
+  for (int s = 0; s < 8; ++s) line[LP(c.t + s * c.NT)] = v[s];
+  lds_barrier();
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
     const int k = c.t + s * c.NT;
@@ -195,8 +199,8 @@ __device__ __forceinline__ void store_pair(const LineCtx& c, const Geom& g, cons
   }
 }
 
-template <int MODEL>
-__global__ void __launch_bounds__(1024) k_row(Geom g, Phys p, const double2* __restrict__ Mi,
+template <int MODEL, int MAXT>
+__global__ void __launch_bounds__(MAXT) k_row(Geom g, Phys p, const double2* __restrict__ Mi,
                                               double2* __restrict__ Mo,
                                               const double2* __restrict__ tw) {
   extern __shared__ double2 smem[];
@@ -205,70 +209,66 @@ __global__ void __launch_bounds__(1024) k_row(Geom g, Phys p, const double2* __r
   double2* line = smem + c.ln * lds_line_elems(g.nx);
   const long long MF = g.mfield;
   double2 v[8];
+  // fft_line leaves z[x = t + s*NT] in v[s]
   auto read_phys = [&](double2 (&w)[8]) {
 #pragma unroll
-    for (int s = 0; s < 8; ++s) w[s] = line[LP(c.t + s * c.NT)];
+    for (int s = 0; s < 8; ++s) w[s] = v[s];
   };
 
   if constexpr (MODEL == MODEL_RSW) {
     const double2 *U = Mi, *V = Mi + MF, *H = Mi + 2 * MF, *Uy = Mi + 3 * MF, *Vy = Mi + 4 * MF;
-    double2 uv[8], ab[8], w[8];
-    // ux + i vx
-    load_pair(v, c, g, U, V, y, true);
-    fft_line<+1>(v, c.t, c.NT, g.log2nx, tw, line);
-    read_phys(w);
+    double2 uv[8], ab[8];
     // u + i v
     load_pair(v, c, g, U, V, y, false);
     fft_line<+1>(v, c.t, c.NT, g.log2nx, tw, line);
     read_phys(uv);
+    // ux + i vx:  A = u ux, B = u vx   (:172, :204)
+    load_pair(v, c, g, U, V, y, true);
+    fft_line<+1>(v, c.t, c.NT, g.log2nx, tw, line);
+    read_phys(v);
 #pragma unroll
-    for (int s = 0; s < 8; ++s)  // A = u ux, B = u vx   (:172, :204)
-      ab[s] = make_double2(uv[s].x * w[s].x, uv[s].x * w[s].y);
-    // uy + i vy
+    for (int s = 0; s < 8; ++s) ab[s] = make_double2(uv[s].x * v[s].x, uv[s].x * v[s].y);
+    // uy + i vy:  A += v uy, B += v vy   (:181, :195)
     load_pair(v, c, g, Uy, Vy, y, false);
     fft_line<+1>(v, c.t, c.NT, g.log2nx, tw, line);
-    read_phys(w);
+    read_phys(v);
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {  // A += v uy, B += v vy   (:181, :195)
-      ab[s].x += uv[s].y * w[s].x;
-      ab[s].y += uv[s].y * w[s].y;
-      v[s] = ab[s];
-    }
+    for (int s = 0; s < 8; ++s)
+      v[s] = make_double2(ab[s].x + uv[s].y * v[s].x, ab[s].y + uv[s].y * v[s].y);
     fft_line<-1>(v, c.t, c.NT, g.log2nx, tw, line);
-    store_pair(c, g, line, Mo, Mo + MF, y);
-    // η
+    store_pair(v, c, g, line, Mo, Mo + MF, y);
+    // η:  C = u η, D = v η   (:218, :224)
     load_pair(v, c, g, H, nullptr, y, false);
     fft_line<+1>(v, c.t, c.NT, g.log2nx, tw, line);
-    read_phys(w);
+    read_phys(v);
 #pragma unroll
-    for (int s = 0; s < 8; ++s)  // C = u η, D = v η   (:218, :224)
-      v[s] = make_double2(uv[s].x * w[s].x, uv[s].y * w[s].x);
+    for (int s = 0; s < 8; ++s) v[s] = make_double2(uv[s].x * v[s].x, uv[s].y * v[s].x);
     fft_line<-1>(v, c.t, c.NT, g.log2nx, tw, line);
-    store_pair(c, g, line, Mo + 2 * MF, Mo + 3 * MF, y);
+    store_pair(v, c, g, line, Mo + 2 * MF, Mo + 3 * MF, y);
   } else {
     const double2 *Q1 = Mi, *Q2 = Mi + MF, *P1 = Mi + 2 * MF, *P2 = Mi + 3 * MF,
                   *Py1 = Mi + 4 * MF, *Py2 = Mi + 5 * MF;
-    double2 q[8], w[8];
-    // ψx1 + i ψx2
-    load_pair(v, c, g, P1, P2, y, true);
-    fft_line<+1>(v, c.t, c.NT, g.log2nx, tw, line);
-    read_phys(w);
+    double2 q[8];
+    // q1 + i q2
     load_pair(v, c, g, Q1, Q2, y, false);
     fft_line<+1>(v, c.t, c.NT, g.log2nx, tw, line);
     read_phys(q);
+    // ψx1 + i ψx2;  ψx q per layer (swqg/TwoLayerQG.jl:169)
+    load_pair(v, c, g, P1, P2, y, true);
+    fft_line<+1>(v, c.t, c.NT, g.log2nx, tw, line);
+    read_phys(v);
 #pragma unroll
-    for (int s = 0; s < 8; ++s)  // ψx q per layer (swqg/TwoLayerQG.jl:169)
-      v[s] = make_double2(w[s].x * q[s].x, w[s].y * q[s].y);
+    for (int s = 0; s < 8; ++s) v[s] = make_double2(v[s].x * q[s].x, v[s].y * q[s].y);
     fft_line<-1>(v, c.t, c.NT, g.log2nx, tw, line);
-    store_pair(c, g, line, Mo, Mo + MF, y);
+    store_pair(v, c, g, line, Mo, Mo + MF, y);
+    // ψy q per layer (:177)
     load_pair(v, c, g, Py1, Py2, y, false);
     fft_line<+1>(v, c.t, c.NT, g.log2nx, tw, line);
-    read_phys(w);
+    read_phys(v);
 #pragma unroll
-    for (int s = 0; s < 8; ++s)  // ψy q per layer (:177)
-      v[s] = make_double2(w[s].x * q[s].x, w[s].y * q[s].y);
+    for (int s = 0; s < 8; ++s) v[s] = make_double2(v[s].x * q[s].x, v[s].y * q[s].y);
     fft_line<-1>(v, c.t, c.NT, g.log2nx, tw, line);
-    store_pair(c, g, line, Mo + 2 * MF, Mo + 3 * MF, y);
+    store_pair(v, c, g, line, Mo + 2 * MF, Mo + 3 * MF, y);
   }
 }
 
@@ -278,8 +278,8 @@ __global__ void __launch_bounds__(1024) k_row(Geom g, Phys p, const double2* __r
 //     N0 = -F(A), N1 = -F(B), N2 = -ik F(C) - il F(D)
 //   QG2 (swqg/TwoLayerQG.jl:171,179): N_l = -il F(A_l) + ik F(B_l)
 // ===========================================================================
-template <int MODEL>
-__global__ void __launch_bounds__(1024) k_col_fwd(Geom g, Phys p, const double2* __restrict__ Mf,
+template <int MODEL, int MAXT>
+__global__ void __launch_bounds__(MAXT) k_col_fwd(Geom g, Phys p, const double2* __restrict__ Mf,
                                                   double2* __restrict__ N,
                                                   const double2* __restrict__ tw) {
   extern __shared__ double2 smem[];
@@ -296,7 +296,8 @@ __global__ void __launch_bounds__(1024) k_col_fwd(Geom g, Phys p, const double2*
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       const int y = c.t + s * c.NT;
-      v[s] = live ? Mfield[midx(g, kr, y)] : zero2();
+      const double2 t = Mfield[midx(g, kr, y)];  // kr < kcP: always in bounds
+      v[s] = live ? t : zero2();
     }
   };
 
@@ -308,20 +309,16 @@ __global__ void __launch_bounds__(1024) k_col_fwd(Geom g, Phys p, const double2*
     fa = grp;      // A_l
     fb = 2 + grp;  // B_l
   }
+  // fft_line leaves F[m = t + s*NT] in v[s]; only live rows are written
   load_col(Mf + fa * MF);
   fft_line<-1>(v, c.t, c.NT, g.log2ny, tw, line);
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
-    const int j = c.t + s * c.NT;
-    acc[s] = zero2();
-    if (j < g.Lr) {
-      const int m = lrow_of(g, j);
-      const double2 a = line[LP(m)];
-      if constexpr (MODEL == MODEL_RSW) {
-        acc[s] = (grp < 2) ? make_double2(-a.x, -a.y) : cmul_i(a, -k);
-      } else {
-        acc[s] = cmul_i(a, -lwav(g, m));
-      }
+    const double2 a = v[s];
+    if constexpr (MODEL == MODEL_RSW) {
+      acc[s] = (grp < 2) ? make_double2(-a.x, -a.y) : cmul_i(a, -k);
+    } else {
+      acc[s] = cmul_i(a, -lwav(g, c.t + s * c.NT));
     }
   }
   if (fb >= 0) {
@@ -329,15 +326,11 @@ __global__ void __launch_bounds__(1024) k_col_fwd(Geom g, Phys p, const double2*
     fft_line<-1>(v, c.t, c.NT, g.log2ny, tw, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      const int j = c.t + s * c.NT;
-      if (j < g.Lr) {
-        const int m = lrow_of(g, j);
-        const double2 b = line[LP(m)];
-        if constexpr (MODEL == MODEL_RSW) {
-          acc[s] = cadd(acc[s], cmul_i(b, -lwav(g, m)));
-        } else {
-          acc[s] = cadd(acc[s], cmul_i(b, k));
-        }
+      const int m = c.t + s * c.NT;
+      if constexpr (MODEL == MODEL_RSW) {
+        acc[s] = cadd(acc[s], cmul_i(v[s], -lwav(g, m)));
+      } else {
+        acc[s] = cadd(acc[s], cmul_i(v[s], k));
       }
     }
   }
@@ -345,8 +338,8 @@ __global__ void __launch_bounds__(1024) k_col_fwd(Geom g, Phys p, const double2*
     double2* Nf = N + (long long)grp * g.cfield + (long long)kr * g.LrP;
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      const int j = c.t + s * c.NT;
-      if (j < g.Lr) Nf[j] = acc[s];
+      const int j = compact_of(g, c.t + s * c.NT);
+      if (j >= 0) Nf[j] = acc[s];
     }
   }
 }
@@ -661,7 +654,8 @@ __global__ void k_make_spec(Geom g, Phys p, int model, int fid, const double2* _
   out[i] = r;
 }
 
-__global__ void __launch_bounds__(1024) k_col_inv1(Geom g, const double2* __restrict__ X,
+template <int MAXT>
+__global__ void __launch_bounds__(MAXT) k_col_inv1(Geom g, const double2* __restrict__ X,
                                                    double2* __restrict__ M,
                                                    const double2* __restrict__ tw) {
   extern __shared__ double2 smem[];
@@ -670,25 +664,24 @@ __global__ void __launch_bounds__(1024) k_col_inv1(Geom g, const double2* __rest
   double2* line = smem + c.ln * lds_line_elems(g.ny);
   const bool live = kr < g.kc;
   const double scale = 1.0 / ((double)g.nx * (double)g.ny);
-  const double2* Xf = X + (long long)kr * g.LrP;
+  const double2* Xf = X + (long long)(live ? kr : g.kc - 1) * g.LrP;
   double2 v[8];
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
     const int m = c.t + s * c.NT;
     const int j = compact_of(g, m);
-    v[s] = (live && j >= 0) ? cscale(Xf[j], scale) : zero2();
+    const double2 t = Xf[j >= 0 ? j : 0];
+    v[s] = (live && j >= 0) ? cscale(t, scale) : zero2();
   }
   fft_line<+1>(v, c.t, c.NT, g.log2ny, tw, line);
   if (live) {
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const int y = c.t + s * c.NT;
-      M[midx(g, kr, y)] = line[LP(y)];
-    }
+    for (int s = 0; s < 8; ++s) M[midx(g, kr, c.t + s * c.NT)] = v[s];
   }
 }
 
-__global__ void __launch_bounds__(1024) k_row_c2r1(Geom g, const double2* __restrict__ M,
+template <int MAXT>
+__global__ void __launch_bounds__(MAXT) k_row_c2r1(Geom g, const double2* __restrict__ M,
                                                    double* __restrict__ out,
                                                    const double2* __restrict__ tw) {
   extern __shared__ double2 smem[];
@@ -699,10 +692,7 @@ __global__ void __launch_bounds__(1024) k_row_c2r1(Geom g, const double2* __rest
   load_pair(v, c, g, M, nullptr, y, false);
   fft_line<+1>(v, c.t, c.NT, g.log2nx, tw, line);
 #pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    const int x = c.t + s * c.NT;
-    out[(long long)y * g.nx + x] = line[LP(x)].x;
-  }
+  for (int s = 0; s < 8; ++s) out[(long long)y * g.nx + c.t + s * c.NT] = v[s].x;
 }
 
 // Energies by Parseval over live modes (FF parsevalsum2 / parsevalsum:
@@ -763,16 +753,23 @@ static inline int row_threads(const Geom& g, int& NB, int& nblk) {
   return NB * NT;
 }
 
+// Launch with the instantiation whose __launch_bounds__ matches the block:
+// 256-thread blocks may use up to 256 VGPRs (no spills in the fused row pass).
 void launch_col_inv(int model, const Geom& g, const Phys& p, const double2* X, double2* Minv,
                     const double2* tw_y, hipStream_t s) {
   int NB, nb;
   const int th = col_threads(g, NB, nb);
   const size_t sh = (size_t)NB * lds_line_elems(g.ny) * sizeof(double2);
   const dim3 grid(nb, model == MODEL_RSW ? 3 : 2);
-  if (model == MODEL_RSW)
-    hipLaunchKernelGGL(k_col_inv<MODEL_RSW>, grid, dim3(th), sh, s, g, p, X, Minv, tw_y);
-  else
-    hipLaunchKernelGGL(k_col_inv<MODEL_QG2>, grid, dim3(th), sh, s, g, p, X, Minv, tw_y);
+  if (model == MODEL_RSW) {
+    if (th <= 256) hipLaunchKernelGGL((k_col_inv<MODEL_RSW, 256>), grid, dim3(th), sh, s, g, p, X, Minv, tw_y);
+    else if (th <= 512) hipLaunchKernelGGL((k_col_inv<MODEL_RSW, 512>), grid, dim3(th), sh, s, g, p, X, Minv, tw_y);
+    else hipLaunchKernelGGL((k_col_inv<MODEL_RSW, 1024>), grid, dim3(th), sh, s, g, p, X, Minv, tw_y);
+  } else {
+    if (th <= 256) hipLaunchKernelGGL((k_col_inv<MODEL_QG2, 256>), grid, dim3(th), sh, s, g, p, X, Minv, tw_y);
+    else if (th <= 512) hipLaunchKernelGGL((k_col_inv<MODEL_QG2, 512>), grid, dim3(th), sh, s, g, p, X, Minv, tw_y);
+    else hipLaunchKernelGGL((k_col_inv<MODEL_QG2, 1024>), grid, dim3(th), sh, s, g, p, X, Minv, tw_y);
+  }
 }
 
 void launch_row(int model, const Geom& g, const Phys& p, const double2* Minv, double2* Mfwd,
@@ -780,10 +777,15 @@ void launch_row(int model, const Geom& g, const Phys& p, const double2* Minv, do
   int NB, nb;
   const int th = row_threads(g, NB, nb);
   const size_t sh = (size_t)NB * lds_line_elems(g.nx) * sizeof(double2);
-  if (model == MODEL_RSW)
-    hipLaunchKernelGGL(k_row<MODEL_RSW>, dim3(nb), dim3(th), sh, s, g, p, Minv, Mfwd, tw_x);
-  else
-    hipLaunchKernelGGL(k_row<MODEL_QG2>, dim3(nb), dim3(th), sh, s, g, p, Minv, Mfwd, tw_x);
+  if (model == MODEL_RSW) {
+    if (th <= 256) hipLaunchKernelGGL((k_row<MODEL_RSW, 256>), dim3(nb), dim3(th), sh, s, g, p, Minv, Mfwd, tw_x);
+    else if (th <= 512) hipLaunchKernelGGL((k_row<MODEL_RSW, 512>), dim3(nb), dim3(th), sh, s, g, p, Minv, Mfwd, tw_x);
+    else hipLaunchKernelGGL((k_row<MODEL_RSW, 1024>), dim3(nb), dim3(th), sh, s, g, p, Minv, Mfwd, tw_x);
+  } else {
+    if (th <= 256) hipLaunchKernelGGL((k_row<MODEL_QG2, 256>), dim3(nb), dim3(th), sh, s, g, p, Minv, Mfwd, tw_x);
+    else if (th <= 512) hipLaunchKernelGGL((k_row<MODEL_QG2, 512>), dim3(nb), dim3(th), sh, s, g, p, Minv, Mfwd, tw_x);
+    else hipLaunchKernelGGL((k_row<MODEL_QG2, 1024>), dim3(nb), dim3(th), sh, s, g, p, Minv, Mfwd, tw_x);
+  }
 }
 
 void launch_col_fwd(int model, const Geom& g, const Phys& p, const double2* Mfwd, double2* N,
@@ -792,10 +794,15 @@ void launch_col_fwd(int model, const Geom& g, const Phys& p, const double2* Mfwd
   const int th = col_threads(g, NB, nb);
   const size_t sh = (size_t)NB * lds_line_elems(g.ny) * sizeof(double2);
   const dim3 grid(nb, model == MODEL_RSW ? 3 : 2);
-  if (model == MODEL_RSW)
-    hipLaunchKernelGGL(k_col_fwd<MODEL_RSW>, grid, dim3(th), sh, s, g, p, Mfwd, N, tw_y);
-  else
-    hipLaunchKernelGGL(k_col_fwd<MODEL_QG2>, grid, dim3(th), sh, s, g, p, Mfwd, N, tw_y);
+  if (model == MODEL_RSW) {
+    if (th <= 256) hipLaunchKernelGGL((k_col_fwd<MODEL_RSW, 256>), grid, dim3(th), sh, s, g, p, Mfwd, N, tw_y);
+    else if (th <= 512) hipLaunchKernelGGL((k_col_fwd<MODEL_RSW, 512>), grid, dim3(th), sh, s, g, p, Mfwd, N, tw_y);
+    else hipLaunchKernelGGL((k_col_fwd<MODEL_RSW, 1024>), grid, dim3(th), sh, s, g, p, Mfwd, N, tw_y);
+  } else {
+    if (th <= 256) hipLaunchKernelGGL((k_col_fwd<MODEL_QG2, 256>), grid, dim3(th), sh, s, g, p, Mfwd, N, tw_y);
+    else if (th <= 512) hipLaunchKernelGGL((k_col_fwd<MODEL_QG2, 512>), grid, dim3(th), sh, s, g, p, Mfwd, N, tw_y);
+    else hipLaunchKernelGGL((k_col_fwd<MODEL_QG2, 1024>), grid, dim3(th), sh, s, g, p, Mfwd, N, tw_y);
+  }
 }
 
 static inline dim3 mode_grid(const Geom& g) { return dim3((unsigned)((g.cfield + 255) / 256)); }
@@ -866,14 +873,16 @@ void launch_col_inv1(const Geom& g, const double2* X, double2* M, const double2*
   int NB, nb;
   const int th = col_threads(g, NB, nb);
   const size_t sh = (size_t)NB * lds_line_elems(g.ny) * sizeof(double2);
-  hipLaunchKernelGGL(k_col_inv1, dim3(nb), dim3(th), sh, s, g, X, M, tw_y);
+  if (th <= 256) hipLaunchKernelGGL(k_col_inv1<256>, dim3(nb), dim3(th), sh, s, g, X, M, tw_y);
+  else hipLaunchKernelGGL(k_col_inv1<1024>, dim3(nb), dim3(th), sh, s, g, X, M, tw_y);
 }
 
 void launch_row_c2r1(const Geom& g, const double2* M, double* out, const double2* tw_x, hipStream_t s) {
   int NB, nb;
   const int th = row_threads(g, NB, nb);
   const size_t sh = (size_t)NB * lds_line_elems(g.nx) * sizeof(double2);
-  hipLaunchKernelGGL(k_row_c2r1, dim3(nb), dim3(th), sh, s, g, M, out, tw_x);
+  if (th <= 256) hipLaunchKernelGGL(k_row_c2r1<256>, dim3(nb), dim3(th), sh, s, g, M, out, tw_x);
+  else hipLaunchKernelGGL(k_row_c2r1<1024>, dim3(nb), dim3(th), sh, s, g, M, out, tw_x);
 }
 
 void launch_energy(int model, const Geom& g, const Phys& p, const double2* sol, double* acc,
