@@ -244,8 +244,8 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   const sw_config& k = c->cfg;
   if (k.model != SW_MODEL_RSW && k.model != SW_MODEL_QG2) return fail(c, SW_E_INVALID, "unknown model");
   if (k.stepper < 0 || k.stepper > 2) return fail(c, SW_E_INVALID, "unknown stepper");
-  if (!pow2(k.nx) || !pow2(k.ny) || k.nx < 16 || k.ny < 16 || k.nx > 8192 || k.ny > 8192)
-    return fail(c, SW_E_INVALID, "nx, ny must be powers of two in [16, 8192]");
+  if (!pow2(k.nx) || !pow2(k.ny) || k.nx < 32 || k.ny < 32 || k.nx > 8192 || k.ny > 8192)
+    return fail(c, SW_E_INVALID, "nx, ny must be powers of two in [32, 8192]");
   if (!(k.aliased_fraction > 0 && k.aliased_fraction < 1))
     return fail(c, SW_E_INVALID, "aliased_fraction must be in (0,1)");
   if (k.nranks != 1) return fail(c, SW_E_INVALID, "multi-GPU slab decomposition: use nranks == 1 in this build");

@@ -40,8 +40,9 @@ __host__ __device__ inline int compact_of(const Geom& g, int m) {
 __host__ __device__ inline double lwav(const Geom& g, int m) {
   return (double)(m < (g.ny >> 1) ? m : m - g.ny) * g.ml;
 }
-__host__ __device__ inline long long midx(const Geom& g, int kr, int y) {
-  return ((long long)(kr >> 3) * g.ny + y) * 8 + (kr & 7);
+// element offset inside one mixed field (< 2^31 for nx, ny <= 8192)
+__host__ __device__ inline int midx(const Geom& g, int kr, int y) {
+  return ((kr >> 3) * g.ny + y) * 8 + (kr & 7);
 }
 
 // integer power x^n (n >= 0) by repeated squaring

@@ -23,15 +23,31 @@ __device__ __forceinline__ int col_of_block(int b, int nb) {
   return b;
 }
 
-struct LineCtx {
-  int NT, ln, t, NB;
+// minimum waves per SIMD requested from the register allocator
+#ifndef SW_MINW_FFT
+#define SW_MINW_FFT 2
+#endif
+#define SW_MINW(L) (Blk<L>::THREADS >= 1024 ? 4 : SW_MINW_FFT)
+
+// threads per block: one line of NT = N/8 threads, or several short lines
+// packed into 256 threads
+template <int LOG2N>
+struct Blk {
+  static constexpr int NT = FftPlan<LOG2N>::NT;
+  // at most 32 lines, so that NB divides ny (>= 32) and kcP (multiple of 64)
+  static constexpr int NB = NT >= 256 ? 1 : (256 / NT > 32 ? 32 : 256 / NT);
+  static constexpr int THREADS = NB * NT;
 };
-__device__ __forceinline__ LineCtx line_ctx(int N) {
+
+struct LineCtx {
+  int ln, t;
+};
+template <int LOG2N>
+__device__ __forceinline__ LineCtx line_ctx() {
+  constexpr int NT = FftPlan<LOG2N>::NT;
   LineCtx c;
-  c.NT = N >> 3;
-  c.ln = threadIdx.x / c.NT;
-  c.t = threadIdx.x - c.ln * c.NT;
-  c.NB = blockDim.x / c.NT;
+  c.ln = threadIdx.x / NT;
+  c.t = threadIdx.x - c.ln * NT;
   return c;
 }
 
@@ -44,15 +60,19 @@ __device__ __forceinline__ double2 zero2() { return make_double2(0.0, 0.0); }
 //   QG2  outputs (swqg/TwoLayerQG.jl:155-176):          0 Q1, 1 Q2, 2 Ψ1, 3 Ψ2, 4 Ψy1, 5 Ψy2
 // grid: (columns, groups); RSW group f reads field f; QG2 group = layer.
 // ===========================================================================
-template <int MODEL, int MAXT>
-__global__ void __launch_bounds__(MAXT) k_col_inv(Geom g, Phys p, const double2* __restrict__ X,
-                                                  double2* __restrict__ M,
-                                                  const double2* __restrict__ tw) {
+template <int MODEL, int LOG2N>
+__global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
+    k_col_inv(Geom g, Phys p, const double2* __restrict__ X, double2* __restrict__ M,
+              const double2* __restrict__ tw) {
+  using B = Blk<LOG2N>;
+  constexpr int NT = B::NT;
   extern __shared__ double2 smem[];
-  const LineCtx c = line_ctx(g.ny);
-  const int kr = (c.NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * c.NB + c.ln;
+  const LineCtx c = line_ctx<LOG2N>();
+  const int kr = (B::NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * B::NB + c.ln;
   const int grp = blockIdx.y;
-  double2* line = smem + c.ln * lds_line_elems(g.ny);
+  double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
+  Twiddles<LOG2N> tws;
+  tws.load(c.t, tw);
   const bool live = kr < g.kc;
   const double scale = 1.0 / ((double)g.nx * (double)g.ny);
   const double k = kr * g.mk;
@@ -62,7 +82,7 @@ __global__ void __launch_bounds__(MAXT) k_col_inv(Geom g, Phys p, const double2*
     if (live) {
       double2* Mo = M + (long long)o * g.mfield;
 #pragma unroll
-      for (int s = 0; s < 8; ++s) Mo[midx(g, kr, c.t + s * c.NT)] = v[s];
+      for (int s = 0; s < 8; ++s) Mo[midx(g, kr, c.t + s * NT)] = v[s];
     }
   };
 
@@ -74,31 +94,28 @@ __global__ void __launch_bounds__(MAXT) k_col_inv(Geom g, Phys p, const double2*
     double2 x[8];
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      const int m = c.t + s * c.NT;
+      const int m = c.t + s * NT;
       const int j = compact_of(g, m);
       const double2 t = Xf[j >= 0 ? j : 0];
       x[s] = (live && j >= 0) ? t : zero2();
       v[s] = cscale(x[s], scale);
     }
-    fft_line<+1>(v, c.t, c.NT, g.log2ny, tw, line);
+    fft_line<LOG2N, +1>(v, c.t, tws, line);
     store(grp);
     if (grp < 2) {  // ∂y: Uy, Vy
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        const int m = c.t + s * c.NT;
-        v[s] = cmul_i(x[s], lwav(g, m) * scale);
-      }
-      fft_line<+1>(v, c.t, c.NT, g.log2ny, tw, line);
+      for (int s = 0; s < 8; ++s) v[s] = cmul_i(x[s], lwav(g, c.t + s * NT) * scale);
+      fft_line<LOG2N, +1>(v, c.t, tws, line);
       store(3 + grp);
     }
   } else {
     // streamfunctionfrompv! (swqg/TwoLayerQG.jl:101-111)
     const double2* X1 = X + (long long)krc * g.LrP;
     const double2* X2 = X1 + g.cfield;
-    double2 q[8], psi[8];
+    double2 psi[8];
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      const int m = c.t + s * c.NT;
+      const int m = c.t + s * NT;
       const int j = compact_of(g, m);
       const int jc = j >= 0 ? j : 0;
       double2 q1 = X1[jc], q2 = X2[jc];
@@ -113,23 +130,18 @@ __global__ void __launch_bounds__(MAXT) k_col_inv(Geom g, Phys p, const double2*
       const double2 qs = cadd(q1, q2);
       const double2 qg = grp == 0 ? q1 : q2;
       double2 ps = make_double2(-(K2 * qg.x + p.F * qs.x), -(K2 * qg.y + p.F * qs.y));
-      ps = make_double2((ps.x / den) * iK2, (ps.y / den) * iK2);
-      q[s] = qg;
-      psi[s] = ps;
+      psi[s] = make_double2((ps.x / den) * iK2, (ps.y / den) * iK2);
       v[s] = cscale(qg, scale);
     }
-    fft_line<+1>(v, c.t, c.NT, g.log2ny, tw, line);
+    fft_line<LOG2N, +1>(v, c.t, tws, line);
     store(grp);
 #pragma unroll
     for (int s = 0; s < 8; ++s) v[s] = cscale(psi[s], scale);
-    fft_line<+1>(v, c.t, c.NT, g.log2ny, tw, line);
+    fft_line<LOG2N, +1>(v, c.t, tws, line);
     store(2 + grp);
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const int m = c.t + s * c.NT;
-      v[s] = cmul_i(psi[s], lwav(g, m) * scale);
-    }
-    fft_line<+1>(v, c.t, c.NT, g.log2ny, tw, line);
+    for (int s = 0; s < 8; ++s) v[s] = cmul_i(psi[s], lwav(g, c.t + s * NT) * scale);
+    fft_line<LOG2N, +1>(v, c.t, tws, line);
     store(4 + grp);
   }
 }
@@ -140,23 +152,24 @@ __global__ void __launch_bounds__(MAXT) k_col_inv(Geom g, Phys p, const double2*
 // Z[nx-k] = conj(A[k]) + i conj(B[k]); the DC bin keeps real parts only —
 // numpy's c2r rule).
 // ===========================================================================
-__device__ __forceinline__ void load_pair(double2 (&v)[8], const LineCtx& c, const Geom& g,
+template <int LOG2N>
+__device__ __forceinline__ void load_pair(double2 (&v)[8], int t, const Geom& g,
                                           const double2* __restrict__ A,
                                           const double2* __restrict__ B, int y, bool deriv) {
-  const int half = g.nx >> 1;
+  constexpr int N = 1 << LOG2N, NT = N / 8, half = N / 2;
   double2 a[8], b[8];
   int kk[8];
 #pragma unroll
   for (int s = 0; s < 8; ++s) {  // issue every load first (clamped, unconditional)
-    const int m = c.t + s * c.NT;
-    kk[s] = m <= half ? m : g.nx - m;
-    const long long o = midx(g, kk[s] < g.kc ? kk[s] : 0, y);
+    const int m = t + s * NT;
+    kk[s] = m <= half ? m : N - m;
+    const int o = midx(g, kk[s] < g.kc ? kk[s] : 0, y);
     a[s] = A[o];
     b[s] = B ? B[o] : zero2();
   }
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
-    const int m = c.t + s * c.NT;
+    const int m = t + s * NT;
     double2 aa = a[s], bb = b[s];
     if (deriv) {
       const double kw = kk[s] * g.mk;
@@ -178,20 +191,22 @@ __device__ __forceinline__ void load_pair(double2 (&v)[8], const LineCtx& c, con
 
 // After a forward FFT of z = a + i b (Z[t + s*NT] in v), write Â[k], B̂[k]
 // for k < kc.  Needs Z[nx-k] from a mirror thread: one LDS round trip.
-__device__ __forceinline__ void store_pair(const double2 (&v)[8], const LineCtx& c, const Geom& g,
+template <int LOG2N>
+__device__ __forceinline__ void store_pair(const double2 (&v)[8], int t, const Geom& g,
                                            double2* line, double2* __restrict__ A,
                                            double2* __restrict__ B, int y) {
+  constexpr int N = 1 << LOG2N, NT = N / 8;
   lds_barrier();  // previous LDS readers are done
 #pragma unroll
-  for (int s = 0; s < 8; ++s) line[LP(c.t + s * c.NT)] = v[s];
+  for (int s = 0; s < 8; ++s) line[LP(t + s * NT)] = v[s];
   lds_barrier();
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
-    const int k = c.t + s * c.NT;
+    const int k = t + s * NT;
     if (k < g.kc) {
-      const double2 zk = line[LP(k)];
-      const double2 zn = line[LP((g.nx - k) & (g.nx - 1))];
-      const long long o = midx(g, k, y);
+      const double2 zk = v[s];
+      const double2 zn = line[LP((N - k) & (N - 1))];
+      const int o = midx(g, k, y);
       A[o] = make_double2(0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y));
       // (zk - conj zn) / (2i)
       B[o] = make_double2(0.5 * (zk.y + zn.y), -0.5 * (zk.x - zn.x));
@@ -199,76 +214,71 @@ __device__ __forceinline__ void store_pair(const double2 (&v)[8], const LineCtx&
   }
 }
 
-template <int MODEL, int MAXT>
-__global__ void __launch_bounds__(MAXT) k_row(Geom g, Phys p, const double2* __restrict__ Mi,
-                                              double2* __restrict__ Mo,
-                                              const double2* __restrict__ tw) {
+template <int MODEL, int LOG2N>
+__global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
+    k_row(Geom g, Phys p, const double2* __restrict__ Mi, double2* __restrict__ Mo,
+          const double2* __restrict__ tw) {
+  using Bk = Blk<LOG2N>;
   extern __shared__ double2 smem[];
-  const LineCtx c = line_ctx(g.nx);
-  const int y = blockIdx.x * c.NB + c.ln;
-  double2* line = smem + c.ln * lds_line_elems(g.nx);
+  const LineCtx c = line_ctx<LOG2N>();
+  const int y = blockIdx.x * Bk::NB + c.ln;
+  double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
+  Twiddles<LOG2N> tws;
+  tws.load(c.t, tw);
   const long long MF = g.mfield;
   double2 v[8];
-  // fft_line leaves z[x = t + s*NT] in v[s]
-  auto read_phys = [&](double2 (&w)[8]) {
-#pragma unroll
-    for (int s = 0; s < 8; ++s) w[s] = v[s];
-  };
 
   if constexpr (MODEL == MODEL_RSW) {
     const double2 *U = Mi, *V = Mi + MF, *H = Mi + 2 * MF, *Uy = Mi + 3 * MF, *Vy = Mi + 4 * MF;
     double2 uv[8], ab[8];
-    // u + i v
-    load_pair(v, c, g, U, V, y, false);
-    fft_line<+1>(v, c.t, c.NT, g.log2nx, tw, line);
-    read_phys(uv);
+    // u + i v   (fft_line leaves z[x = t + s*NT] in v[s])
+    load_pair<LOG2N>(v, c.t, g, U, V, y, false);
+    fft_line<LOG2N, +1>(v, c.t, tws, line);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) uv[s] = v[s];
     // ux + i vx:  A = u ux, B = u vx   (:172, :204)
-    load_pair(v, c, g, U, V, y, true);
-    fft_line<+1>(v, c.t, c.NT, g.log2nx, tw, line);
-    read_phys(v);
+    load_pair<LOG2N>(v, c.t, g, U, V, y, true);
+    fft_line<LOG2N, +1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) ab[s] = make_double2(uv[s].x * v[s].x, uv[s].x * v[s].y);
     // uy + i vy:  A += v uy, B += v vy   (:181, :195)
-    load_pair(v, c, g, Uy, Vy, y, false);
-    fft_line<+1>(v, c.t, c.NT, g.log2nx, tw, line);
-    read_phys(v);
+    load_pair<LOG2N>(v, c.t, g, Uy, Vy, y, false);
+    fft_line<LOG2N, +1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s)
       v[s] = make_double2(ab[s].x + uv[s].y * v[s].x, ab[s].y + uv[s].y * v[s].y);
-    fft_line<-1>(v, c.t, c.NT, g.log2nx, tw, line);
-    store_pair(v, c, g, line, Mo, Mo + MF, y);
+    fft_line<LOG2N, -1>(v, c.t, tws, line);
+    store_pair<LOG2N>(v, c.t, g, line, Mo, Mo + MF, y);
     // η:  C = u η, D = v η   (:218, :224)
-    load_pair(v, c, g, H, nullptr, y, false);
-    fft_line<+1>(v, c.t, c.NT, g.log2nx, tw, line);
-    read_phys(v);
+    load_pair<LOG2N>(v, c.t, g, H, nullptr, y, false);
+    fft_line<LOG2N, +1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) v[s] = make_double2(uv[s].x * v[s].x, uv[s].y * v[s].x);
-    fft_line<-1>(v, c.t, c.NT, g.log2nx, tw, line);
-    store_pair(v, c, g, line, Mo + 2 * MF, Mo + 3 * MF, y);
+    fft_line<LOG2N, -1>(v, c.t, tws, line);
+    store_pair<LOG2N>(v, c.t, g, line, Mo + 2 * MF, Mo + 3 * MF, y);
   } else {
     const double2 *Q1 = Mi, *Q2 = Mi + MF, *P1 = Mi + 2 * MF, *P2 = Mi + 3 * MF,
                   *Py1 = Mi + 4 * MF, *Py2 = Mi + 5 * MF;
     double2 q[8];
     // q1 + i q2
-    load_pair(v, c, g, Q1, Q2, y, false);
-    fft_line<+1>(v, c.t, c.NT, g.log2nx, tw, line);
-    read_phys(q);
+    load_pair<LOG2N>(v, c.t, g, Q1, Q2, y, false);
+    fft_line<LOG2N, +1>(v, c.t, tws, line);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) q[s] = v[s];
     // ψx1 + i ψx2;  ψx q per layer (swqg/TwoLayerQG.jl:169)
-    load_pair(v, c, g, P1, P2, y, true);
-    fft_line<+1>(v, c.t, c.NT, g.log2nx, tw, line);
-    read_phys(v);
+    load_pair<LOG2N>(v, c.t, g, P1, P2, y, true);
+    fft_line<LOG2N, +1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) v[s] = make_double2(v[s].x * q[s].x, v[s].y * q[s].y);
-    fft_line<-1>(v, c.t, c.NT, g.log2nx, tw, line);
-    store_pair(v, c, g, line, Mo, Mo + MF, y);
+    fft_line<LOG2N, -1>(v, c.t, tws, line);
+    store_pair<LOG2N>(v, c.t, g, line, Mo, Mo + MF, y);
     // ψy q per layer (:177)
-    load_pair(v, c, g, Py1, Py2, y, false);
-    fft_line<+1>(v, c.t, c.NT, g.log2nx, tw, line);
-    read_phys(v);
+    load_pair<LOG2N>(v, c.t, g, Py1, Py2, y, false);
+    fft_line<LOG2N, +1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) v[s] = make_double2(v[s].x * q[s].x, v[s].y * q[s].y);
-    fft_line<-1>(v, c.t, c.NT, g.log2nx, tw, line);
-    store_pair(v, c, g, line, Mo + 2 * MF, Mo + 3 * MF, y);
+    fft_line<LOG2N, -1>(v, c.t, tws, line);
+    store_pair<LOG2N>(v, c.t, g, line, Mo + 2 * MF, Mo + 3 * MF, y);
   }
 }
 
@@ -278,15 +288,19 @@ __global__ void __launch_bounds__(MAXT) k_row(Geom g, Phys p, const double2* __r
 //     N0 = -F(A), N1 = -F(B), N2 = -ik F(C) - il F(D)
 //   QG2 (swqg/TwoLayerQG.jl:171,179): N_l = -il F(A_l) + ik F(B_l)
 // ===========================================================================
-template <int MODEL, int MAXT>
-__global__ void __launch_bounds__(MAXT) k_col_fwd(Geom g, Phys p, const double2* __restrict__ Mf,
-                                                  double2* __restrict__ N,
-                                                  const double2* __restrict__ tw) {
+template <int MODEL, int LOG2N>
+__global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
+    k_col_fwd(Geom g, Phys p, const double2* __restrict__ Mf, double2* __restrict__ N,
+              const double2* __restrict__ tw) {
+  using B = Blk<LOG2N>;
+  constexpr int NT = B::NT;
   extern __shared__ double2 smem[];
-  const LineCtx c = line_ctx(g.ny);
-  const int kr = (c.NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * c.NB + c.ln;
+  const LineCtx c = line_ctx<LOG2N>();
+  const int kr = (B::NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * B::NB + c.ln;
   const int grp = blockIdx.y;
-  double2* line = smem + c.ln * lds_line_elems(g.ny);
+  double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
+  Twiddles<LOG2N> tws;
+  tws.load(c.t, tw);
   const bool live = kr < g.kc;
   const double k = kr * g.mk;
   const long long MF = g.mfield;
@@ -295,8 +309,7 @@ __global__ void __launch_bounds__(MAXT) k_col_fwd(Geom g, Phys p, const double2*
   auto load_col = [&](const double2* Mfield) {
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      const int y = c.t + s * c.NT;
-      const double2 t = Mfield[midx(g, kr, y)];  // kr < kcP: always in bounds
+      const double2 t = Mfield[midx(g, kr, c.t + s * NT)];  // kr < kcP: always in bounds
       v[s] = live ? t : zero2();
     }
   };
@@ -311,22 +324,22 @@ __global__ void __launch_bounds__(MAXT) k_col_fwd(Geom g, Phys p, const double2*
   }
   // fft_line leaves F[m = t + s*NT] in v[s]; only live rows are written
   load_col(Mf + fa * MF);
-  fft_line<-1>(v, c.t, c.NT, g.log2ny, tw, line);
+  fft_line<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
     const double2 a = v[s];
     if constexpr (MODEL == MODEL_RSW) {
       acc[s] = (grp < 2) ? make_double2(-a.x, -a.y) : cmul_i(a, -k);
     } else {
-      acc[s] = cmul_i(a, -lwav(g, c.t + s * c.NT));
+      acc[s] = cmul_i(a, -lwav(g, c.t + s * NT));
     }
   }
   if (fb >= 0) {
     load_col(Mf + fb * MF);
-    fft_line<-1>(v, c.t, c.NT, g.log2ny, tw, line);
+    fft_line<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      const int m = c.t + s * c.NT;
+      const int m = c.t + s * NT;
       if constexpr (MODEL == MODEL_RSW) {
         acc[s] = cadd(acc[s], cmul_i(v[s], -lwav(g, m)));
       } else {
@@ -338,7 +351,7 @@ __global__ void __launch_bounds__(MAXT) k_col_fwd(Geom g, Phys p, const double2*
     double2* Nf = N + (long long)grp * g.cfield + (long long)kr * g.LrP;
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      const int j = compact_of(g, c.t + s * c.NT);
+      const int j = compact_of(g, c.t + s * NT);
       if (j >= 0) Nf[j] = acc[s];
     }
   }
@@ -654,45 +667,52 @@ __global__ void k_make_spec(Geom g, Phys p, int model, int fid, const double2* _
   out[i] = r;
 }
 
-template <int MAXT>
-__global__ void __launch_bounds__(MAXT) k_col_inv1(Geom g, const double2* __restrict__ X,
-                                                   double2* __restrict__ M,
-                                                   const double2* __restrict__ tw) {
+template <int LOG2N>
+__global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
+    k_col_inv1(Geom g, const double2* __restrict__ X, double2* __restrict__ M,
+               const double2* __restrict__ tw) {
+  using B = Blk<LOG2N>;
+  constexpr int NT = B::NT;
   extern __shared__ double2 smem[];
-  const LineCtx c = line_ctx(g.ny);
-  const int kr = blockIdx.x * c.NB + c.ln;
-  double2* line = smem + c.ln * lds_line_elems(g.ny);
+  const LineCtx c = line_ctx<LOG2N>();
+  const int kr = blockIdx.x * B::NB + c.ln;
+  double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
+  Twiddles<LOG2N> tws;
+  tws.load(c.t, tw);
   const bool live = kr < g.kc;
   const double scale = 1.0 / ((double)g.nx * (double)g.ny);
   const double2* Xf = X + (long long)(live ? kr : g.kc - 1) * g.LrP;
   double2 v[8];
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
-    const int m = c.t + s * c.NT;
-    const int j = compact_of(g, m);
+    const int j = compact_of(g, c.t + s * NT);
     const double2 t = Xf[j >= 0 ? j : 0];
     v[s] = (live && j >= 0) ? cscale(t, scale) : zero2();
   }
-  fft_line<+1>(v, c.t, c.NT, g.log2ny, tw, line);
+  fft_line<LOG2N, +1>(v, c.t, tws, line);
   if (live) {
 #pragma unroll
-    for (int s = 0; s < 8; ++s) M[midx(g, kr, c.t + s * c.NT)] = v[s];
+    for (int s = 0; s < 8; ++s) M[midx(g, kr, c.t + s * NT)] = v[s];
   }
 }
 
-template <int MAXT>
-__global__ void __launch_bounds__(MAXT) k_row_c2r1(Geom g, const double2* __restrict__ M,
-                                                   double* __restrict__ out,
-                                                   const double2* __restrict__ tw) {
+template <int LOG2N>
+__global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
+    k_row_c2r1(Geom g, const double2* __restrict__ M, double* __restrict__ out,
+               const double2* __restrict__ tw) {
+  using B = Blk<LOG2N>;
+  constexpr int NT = B::NT;
   extern __shared__ double2 smem[];
-  const LineCtx c = line_ctx(g.nx);
-  const int y = blockIdx.x * c.NB + c.ln;
-  double2* line = smem + c.ln * lds_line_elems(g.nx);
+  const LineCtx c = line_ctx<LOG2N>();
+  const int y = blockIdx.x * B::NB + c.ln;
+  double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
+  Twiddles<LOG2N> tws;
+  tws.load(c.t, tw);
   double2 v[8];
-  load_pair(v, c, g, M, nullptr, y, false);
-  fft_line<+1>(v, c.t, c.NT, g.log2nx, tw, line);
+  load_pair<LOG2N>(v, c.t, g, M, nullptr, y, false);
+  fft_line<LOG2N, +1>(v, c.t, tws, line);
 #pragma unroll
-  for (int s = 0; s < 8; ++s) out[(long long)y * g.nx + c.t + s * c.NT] = v[s].x;
+  for (int s = 0; s < 8; ++s) out[(long long)y * g.nx + c.t + s * NT] = v[s].x;
 }
 
 // Energies by Parseval over live modes (FF parsevalsum2 / parsevalsum:
@@ -738,71 +758,92 @@ __global__ void k_energy(Geom g, Phys p, int model, const double2* __restrict__ 
 // ===========================================================================
 // launchers
 // ===========================================================================
-static inline int col_threads(const Geom& g, int& NB, int& nblk) {
-  const int NT = g.ny >> 3;
-  NB = NT >= 256 ? 1 : 256 / NT;
-  if (NB > g.kcP) NB = g.kcP;
-  nblk = (g.kcP + NB - 1) / NB;
-  return NB * NT;
-}
-static inline int row_threads(const Geom& g, int& NB, int& nblk) {
-  const int NT = g.nx >> 3;
-  NB = NT >= 256 ? 1 : 256 / NT;
-  if (NB > g.ny) NB = g.ny;
-  nblk = g.ny / NB;
-  return NB * NT;
+// host-side: dispatch the LOG2N instantiation (N = 32 … 8192)
+#define SW_LOG2_CASES(X) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13)
+
+template <template <int> class F, typename... Args>
+static void dispatch_log2(int log2n, Args&&... args) {
+  switch (log2n) {
+#define SW_CASE(L) \
+  case L:          \
+    F<L>::run(args...); \
+    break;
+    SW_LOG2_CASES(SW_CASE)
+#undef SW_CASE
+    default:
+      break;
+  }
 }
 
-// Launch with the instantiation whose __launch_bounds__ matches the block:
-// 256-thread blocks may use up to 256 VGPRs (no spills in the fused row pass).
+template <int L>
+static int col_blocks(const Geom& g) {
+  return (g.kcP + Blk<L>::NB - 1) / Blk<L>::NB;
+}
+template <int L>
+static int row_blocks(const Geom& g) {
+  return g.ny / Blk<L>::NB;
+}
+template <int L>
+static size_t lds_bytes() {
+  return (size_t)Blk<L>::NB * FftPlan<L>::LDS * sizeof(double2);
+}
+
+template <int L>
+struct ColInvL {
+  static void run(int model, const Geom& g, const Phys& p, const double2* X, double2* M,
+                  const double2* tw, hipStream_t s) {
+    const dim3 grid(col_blocks<L>(g), model == MODEL_RSW ? 3 : 2);
+    if (model == MODEL_RSW)
+      hipLaunchKernelGGL((k_col_inv<MODEL_RSW, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw);
+    else
+      hipLaunchKernelGGL((k_col_inv<MODEL_QG2, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw);
+  }
+};
+template <int L>
+struct RowL {
+  static void run(int model, const Geom& g, const Phys& p, const double2* Mi, double2* Mo,
+                  const double2* tw, hipStream_t s) {
+    if (model == MODEL_RSW)
+      hipLaunchKernelGGL((k_row<MODEL_RSW, L>), dim3(row_blocks<L>(g)), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, Mi, Mo, tw);
+    else
+      hipLaunchKernelGGL((k_row<MODEL_QG2, L>), dim3(row_blocks<L>(g)), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, Mi, Mo, tw);
+  }
+};
+template <int L>
+struct ColFwdL {
+  static void run(int model, const Geom& g, const Phys& p, const double2* Mf, double2* N,
+                  const double2* tw, hipStream_t s) {
+    const dim3 grid(col_blocks<L>(g), model == MODEL_RSW ? 3 : 2);
+    if (model == MODEL_RSW)
+      hipLaunchKernelGGL((k_col_fwd<MODEL_RSW, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, Mf, N, tw);
+    else
+      hipLaunchKernelGGL((k_col_fwd<MODEL_QG2, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, Mf, N, tw);
+  }
+};
+template <int L>
+struct ColInv1L {
+  static void run(const Geom& g, const double2* X, double2* M, const double2* tw, hipStream_t s) {
+    hipLaunchKernelGGL((k_col_inv1<L>), dim3(col_blocks<L>(g)), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, X, M, tw);
+  }
+};
+template <int L>
+struct RowC2r1L {
+  static void run(const Geom& g, const double2* M, double* out, const double2* tw, hipStream_t s) {
+    hipLaunchKernelGGL((k_row_c2r1<L>), dim3(row_blocks<L>(g)), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, M, out, tw);
+  }
+};
+
 void launch_col_inv(int model, const Geom& g, const Phys& p, const double2* X, double2* Minv,
                     const double2* tw_y, hipStream_t s) {
-  int NB, nb;
-  const int th = col_threads(g, NB, nb);
-  const size_t sh = (size_t)NB * lds_line_elems(g.ny) * sizeof(double2);
-  const dim3 grid(nb, model == MODEL_RSW ? 3 : 2);
-  if (model == MODEL_RSW) {
-    if (th <= 256) hipLaunchKernelGGL((k_col_inv<MODEL_RSW, 256>), grid, dim3(th), sh, s, g, p, X, Minv, tw_y);
-    else if (th <= 512) hipLaunchKernelGGL((k_col_inv<MODEL_RSW, 512>), grid, dim3(th), sh, s, g, p, X, Minv, tw_y);
-    else hipLaunchKernelGGL((k_col_inv<MODEL_RSW, 1024>), grid, dim3(th), sh, s, g, p, X, Minv, tw_y);
-  } else {
-    if (th <= 256) hipLaunchKernelGGL((k_col_inv<MODEL_QG2, 256>), grid, dim3(th), sh, s, g, p, X, Minv, tw_y);
-    else if (th <= 512) hipLaunchKernelGGL((k_col_inv<MODEL_QG2, 512>), grid, dim3(th), sh, s, g, p, X, Minv, tw_y);
-    else hipLaunchKernelGGL((k_col_inv<MODEL_QG2, 1024>), grid, dim3(th), sh, s, g, p, X, Minv, tw_y);
-  }
+  dispatch_log2<ColInvL>(g.log2ny, model, g, p, X, Minv, tw_y, s);
 }
-
 void launch_row(int model, const Geom& g, const Phys& p, const double2* Minv, double2* Mfwd,
                 const double2* tw_x, hipStream_t s) {
-  int NB, nb;
-  const int th = row_threads(g, NB, nb);
-  const size_t sh = (size_t)NB * lds_line_elems(g.nx) * sizeof(double2);
-  if (model == MODEL_RSW) {
-    if (th <= 256) hipLaunchKernelGGL((k_row<MODEL_RSW, 256>), dim3(nb), dim3(th), sh, s, g, p, Minv, Mfwd, tw_x);
-    else if (th <= 512) hipLaunchKernelGGL((k_row<MODEL_RSW, 512>), dim3(nb), dim3(th), sh, s, g, p, Minv, Mfwd, tw_x);
-    else hipLaunchKernelGGL((k_row<MODEL_RSW, 1024>), dim3(nb), dim3(th), sh, s, g, p, Minv, Mfwd, tw_x);
-  } else {
-    if (th <= 256) hipLaunchKernelGGL((k_row<MODEL_QG2, 256>), dim3(nb), dim3(th), sh, s, g, p, Minv, Mfwd, tw_x);
-    else if (th <= 512) hipLaunchKernelGGL((k_row<MODEL_QG2, 512>), dim3(nb), dim3(th), sh, s, g, p, Minv, Mfwd, tw_x);
-    else hipLaunchKernelGGL((k_row<MODEL_QG2, 1024>), dim3(nb), dim3(th), sh, s, g, p, Minv, Mfwd, tw_x);
-  }
+  dispatch_log2<RowL>(g.log2nx, model, g, p, Minv, Mfwd, tw_x, s);
 }
-
 void launch_col_fwd(int model, const Geom& g, const Phys& p, const double2* Mfwd, double2* N,
                     const double2* tw_y, hipStream_t s) {
-  int NB, nb;
-  const int th = col_threads(g, NB, nb);
-  const size_t sh = (size_t)NB * lds_line_elems(g.ny) * sizeof(double2);
-  const dim3 grid(nb, model == MODEL_RSW ? 3 : 2);
-  if (model == MODEL_RSW) {
-    if (th <= 256) hipLaunchKernelGGL((k_col_fwd<MODEL_RSW, 256>), grid, dim3(th), sh, s, g, p, Mfwd, N, tw_y);
-    else if (th <= 512) hipLaunchKernelGGL((k_col_fwd<MODEL_RSW, 512>), grid, dim3(th), sh, s, g, p, Mfwd, N, tw_y);
-    else hipLaunchKernelGGL((k_col_fwd<MODEL_RSW, 1024>), grid, dim3(th), sh, s, g, p, Mfwd, N, tw_y);
-  } else {
-    if (th <= 256) hipLaunchKernelGGL((k_col_fwd<MODEL_QG2, 256>), grid, dim3(th), sh, s, g, p, Mfwd, N, tw_y);
-    else if (th <= 512) hipLaunchKernelGGL((k_col_fwd<MODEL_QG2, 512>), grid, dim3(th), sh, s, g, p, Mfwd, N, tw_y);
-    else hipLaunchKernelGGL((k_col_fwd<MODEL_QG2, 1024>), grid, dim3(th), sh, s, g, p, Mfwd, N, tw_y);
-  }
+  dispatch_log2<ColFwdL>(g.log2ny, model, g, p, Mfwd, N, tw_y, s);
 }
 
 static inline dim3 mode_grid(const Geom& g) { return dim3((unsigned)((g.cfield + 255) / 256)); }
@@ -870,19 +911,11 @@ void launch_make_spec(int model, int fid, const Geom& g, const Phys& p, const do
 }
 
 void launch_col_inv1(const Geom& g, const double2* X, double2* M, const double2* tw_y, hipStream_t s) {
-  int NB, nb;
-  const int th = col_threads(g, NB, nb);
-  const size_t sh = (size_t)NB * lds_line_elems(g.ny) * sizeof(double2);
-  if (th <= 256) hipLaunchKernelGGL(k_col_inv1<256>, dim3(nb), dim3(th), sh, s, g, X, M, tw_y);
-  else hipLaunchKernelGGL(k_col_inv1<1024>, dim3(nb), dim3(th), sh, s, g, X, M, tw_y);
+  dispatch_log2<ColInv1L>(g.log2ny, g, X, M, tw_y, s);
 }
 
 void launch_row_c2r1(const Geom& g, const double2* M, double* out, const double2* tw_x, hipStream_t s) {
-  int NB, nb;
-  const int th = row_threads(g, NB, nb);
-  const size_t sh = (size_t)NB * lds_line_elems(g.nx) * sizeof(double2);
-  if (th <= 256) hipLaunchKernelGGL(k_row_c2r1<256>, dim3(nb), dim3(th), sh, s, g, M, out, tw_x);
-  else hipLaunchKernelGGL(k_row_c2r1<1024>, dim3(nb), dim3(th), sh, s, g, M, out, tw_x);
+  dispatch_log2<RowC2r1L>(g.log2nx, g, M, out, tw_x, s);
 }
 
 void launch_energy(int model, const Geom& g, const Phys& p, const double2* sol, double* acc,
