@@ -90,6 +90,9 @@ typedef struct sw_config {
   int32_t check_nan;        /* if nonzero, sw_step returns SW_E_NAN on blow-up */
   int32_t nop_calcN;        /* 1: N ≡ 0, the reference's NOPcalcN! hook
                                (rsw/RotatingShallowWater.jl:135-138,305)    */
+  int32_t unfused;          /* debug/reference: separate col_fwd + update +
+                               col_inv kernels instead of the fused column
+                               pass (results are bitwise identical)        */
   int32_t nranks, rank;     /* slab decomposition (1, 0 = single GPU)      */
   const void* comm_unique_id; /* ncclUniqueId bytes (nranks > 1)           */
 } sw_config;

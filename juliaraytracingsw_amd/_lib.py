@@ -44,7 +44,8 @@ class SwConfig(C.Structure):
         ("U", C.c_double), ("mu", C.c_double), ("F", C.c_double),
         ("use_filter", C.c_int32), ("filter_order", C.c_int32),
         ("filter_innerK", C.c_double), ("filter_outerK", C.c_double), ("filter_tol", C.c_double),
-        ("device", C.c_int32), ("check_nan", C.c_int32), ("nop_calcN", C.c_int32), ("nranks", C.c_int32), ("rank", C.c_int32),
+        ("device", C.c_int32), ("check_nan", C.c_int32), ("nop_calcN", C.c_int32), ("unfused", C.c_int32),
+        ("nranks", C.c_int32), ("rank", C.c_int32),
         ("comm_unique_id", C.c_void_p),
     ]
 

@@ -8,8 +8,10 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
+#include <utility>
 #include <vector>
 
 using sw::Geom;
@@ -30,11 +32,15 @@ struct sw_ctx {
   hipStream_t stream = nullptr;
   double2 *tw_x = nullptr, *tw_y = nullptr;
   double2* sol = nullptr;                    // compact state, nf fields
+  double2* sol2 = nullptr;                   // FilteredAB3: the other state buffer (ping-pong)
   double2* hist[3] = {nullptr, nullptr, nullptr};  // FAB3 RHS ring / IFMAB3 N ring
   int head = 0;
   double2 *E = nullptr, *E2 = nullptr;       // IF operators (E2 = exp(2Ldt) or exp(Ldt/2))
-  double2* rk[4] = {nullptr, nullptr, nullptr, nullptr};
-  double2* xs = nullptr;                     // RK4 stage input / scratch compact
+  double2* acc = nullptr;                    // IFMRK4 running stage combination
+  double2* nbuf = nullptr;                   // unfused IFMRK4: calcN output
+  double2* xs = nullptr;                     // stage input / scratch compact
+  bool mixed_valid = false;                  // minv == col_inv(sol) (fused pipeline primed)
+  bool fuse_all = false;                     // SW_FUSE_ALL=1: fused pass for every pair (experiments)
   double2 *minv = nullptr, *mfwd = nullptr;  // mixed-space fields
   double2* stage = nullptr;                  // full (nkr,nl,nf) staging
   double* dflt = nullptr;                    // physical staging / reductions
@@ -99,8 +105,20 @@ std::vector<double2> twiddles(int N) {
 double live_field_bytes(const Geom& g) { return 16.0 * g.kc * g.Lr; }
 double mixed_field_bytes(const Geom& g) { return 16.0 * g.kc * g.ny; }
 
-enum KId { K_COLINV = 0, K_ROW, K_COLFWD, K_UPD, K_RK4STAGE, K_NKERN };
-const char* kname[K_NKERN] = {"col_inv", "row", "col_fwd", "update", "rk4_stage"};
+enum KId { K_COLINV = 0, K_ROW, K_COLFWD, K_UPD, K_COLSTEP, K_NKERN };
+const char* kname[K_NKERN] = {"col_inv", "row", "col_fwd", "update", "col_step"};
+
+// state/history bytes of one stepper op per live mode, in live-field units
+// (reads + writes; AB3 steady state; IFMRK4 averaged over its four stages)
+double op_fields(const sw_ctx* c) {
+  const int nf = c->nf, st = c->cfg.stepper;
+  if (st == SW_STEP_FILTERED_AB3) return 3 * nf + 2 * nf;          // sol,R-1,R-2 in; sol,RHS out
+  if (st == SW_STEP_IFMAB3) return 3 * nf + 2 * nf * nf + 2 * nf;  // sol,N-1,N-2,E,E2 in; sol,N out
+  // stages: 1 u,E,H in / acc out; 2 u,acc,H in / acc out; 3 u,acc,E,H in / acc out; 4 u,acc,E in / u out
+  const double s1 = nf + 2 * nf * nf + nf, s2 = 2 * nf + nf * nf + nf, s3 = 2 * nf + 2 * nf * nf + nf,
+               s4 = 2 * nf + nf * nf + nf;
+  return (s1 + s2 + s3 + s4) / 4;
+}
 
 double kernel_bytes(const sw_ctx* c, int kid) {
   const Geom& g = c->g;
@@ -110,11 +128,8 @@ double kernel_bytes(const sw_ctx* c, int kid) {
     case K_COLINV: return nf * F + c->ninv * M;
     case K_ROW: return (c->ninv + c->nfwd) * M;
     case K_COLFWD: return c->nfwd * M + nf * F;
-    case K_UPD:
-      if (c->cfg.stepper == SW_STEP_FILTERED_AB3) return 6 * nf * F;          // sol,N,R-1,R-2 in; sol,RHS out
-      if (c->cfg.stepper == SW_STEP_IFMAB3) return (5 * nf + 2 * nf * nf) * F;  // sol,N,N-1,N-2 in, sol out, E,E2
-      return (6 * nf + 2 * nf * nf) * F;                                      // RK4 final: u,k1..k4 in, u out, E,H
-    case K_RK4STAGE: return (3 * nf + 2 * nf * nf) * F;
+    case K_UPD: return (op_fields(c) + nf) * F;  // + N read
+    case K_COLSTEP: return c->nfwd * M + op_fields(c) * F + c->ninv * M;
   }
   return 0;
 }
@@ -158,42 +173,64 @@ void calcN(sw_ctx* c, const double2* X, double2* N) {
   }
 }
 
-// one stepforward!(sol, clock, ts, …)
-void step_once(sw_ctx* c) {
+// one stepforward!(sol, clock, ts, …).  Fused pipeline: the column pass of
+// stage s also produces the inverse transforms the row pass of stage s+1
+// needs, so a primed step is row -> col_step (two launches).
+// The fused column pass is used where it wins (measured): RSW FilteredAB3,
+// whose update splits by field.  Other model/stepper pairs run the separate
+// col_inv / row / col_fwd / update kernels (the fused generic k_col_step keeps
+// all N fields live and spills on gfx950 at 2048²).
+bool use_fused(const sw_ctx* c) {
+  if (c->cfg.unfused || c->cfg.nop_calcN) return false;
+  if (c->fuse_all) return true;
+  return c->cfg.model == SW_MODEL_RSW && c->cfg.stepper == SW_STEP_FILTERED_AB3;
+}
+
+void run_stage(sw_ctx* c, int op, const sw::StepPtrs& a, const double2* X) {
   const int model = c->cfg.model;
+  if (use_fused(c)) {
+    if (!c->mixed_valid) {
+      Timer tm(c, K_COLINV);
+      sw::launch_col_inv(model, c->g, c->p, X, c->minv, c->tw_y, c->stream);
+    }
+    {
+      Timer tm(c, K_ROW);
+      sw::launch_row(model, c->g, c->p, c->minv, c->mfwd, c->tw_x, c->stream);
+    }
+    Timer tm(c, K_COLSTEP);
+    sw::launch_col_step(model, op, c->g, c->p, a, c->mfwd, c->minv, c->tw_y, c->stream);
+    c->mixed_valid = true;  // minv now holds the next stage's inverse transforms
+  } else {
+    double2* N = (op == sw::OP_RK4) ? c->nbuf : a.h0;
+    calcN(c, X, N);
+    Timer tm(c, K_UPD);
+    sw::launch_step_elem(c->nf, op, c->g, c->p, a, N, c->xs, c->stream);
+    c->mixed_valid = false;
+  }
+}
+
+void step_once(sw_ctx* c) {
   const int st = c->cfg.stepper;
-  const int euler = c->step < 3 ? 1 : 0;
+  sw::StepPtrs a{};
+  a.sol = c->sol;
+  a.sol_out = (st == SW_STEP_FILTERED_AB3) ? c->sol2 : c->sol;
+  a.E = c->E;
+  a.E2 = c->E2;
+  a.xs = c->xs;
+  a.euler = c->step < 3 ? 1 : 0;
   if (st == SW_STEP_FILTERED_AB3 || st == SW_STEP_IFMAB3) {
-    double2* N = c->hist[c->head];
-    double2* Nm1 = c->hist[(c->head + 2) % 3];
-    double2* Nm2 = c->hist[(c->head + 1) % 3];
-    calcN(c, c->sol, N);
-    Timer tm(c, K_UPD);
-    if (st == SW_STEP_FILTERED_AB3)
-      sw::launch_upd_fab3(model, c->g, c->p, c->sol, N, Nm1, Nm2, euler, c->stream);
-    else
-      sw::launch_upd_ifmab3(c->nf, c->g, c->p, c->sol, N, Nm1, Nm2, c->E, c->E2, euler, c->stream);
-    c->head = (c->head + 1) % 3;
+    a.h0 = c->hist[c->head];
+    a.h1 = c->hist[(c->head + 2) % 3];
+    a.h2 = c->hist[(c->head + 1) % 3];
+    run_stage(c, st == SW_STEP_FILTERED_AB3 ? sw::OP_FAB3 : sw::OP_IFMAB3, a, c->sol);
+    c->head = (c->head + 1) % 3;  // RHS₋₂ <- RHS₋₁ <- RHS by rotation (utils/IFMAB3.jl:165-166)
+    if (st == SW_STEP_FILTERED_AB3) std::swap(c->sol, c->sol2);
   } else {  // IFMRK4
-    calcN(c, c->sol, c->rk[0]);
-    {
-      Timer tm(c, K_RK4STAGE);
-      sw::launch_rk4_stage(c->nf, 1, c->g, c->p, c->sol, c->rk[0], c->E, c->E2, c->xs, c->stream);
+    a.h0 = c->acc;
+    for (int stage = 1; stage <= 4; ++stage) {
+      a.stage = stage;
+      run_stage(c, sw::OP_RK4, a, stage == 1 ? c->sol : c->xs);
     }
-    calcN(c, c->xs, c->rk[1]);
-    {
-      Timer tm(c, K_RK4STAGE);
-      sw::launch_rk4_stage(c->nf, 2, c->g, c->p, c->sol, c->rk[1], c->E, c->E2, c->xs, c->stream);
-    }
-    calcN(c, c->xs, c->rk[2]);
-    {
-      Timer tm(c, K_RK4STAGE);
-      sw::launch_rk4_stage(c->nf, 3, c->g, c->p, c->sol, c->rk[2], c->E, c->E2, c->xs, c->stream);
-    }
-    calcN(c, c->xs, c->rk[3]);
-    Timer tm(c, K_UPD);
-    sw::launch_rk4_final(c->nf, c->g, c->p, c->sol, c->rk[0], c->rk[1], c->rk[2], c->rk[3], c->E,
-                         c->E2, c->stream);
   }
   c->t += c->cfg.dt;
   c->step += 1;
@@ -308,14 +345,16 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   int rc;
   if ((rc = alloc(c, (void**)&c->sol, c->nf * cb))) return rc;
   if ((rc = alloc(c, (void**)&c->xs, c->nf * cb))) return rc;
+  if (k.stepper == SW_STEP_FILTERED_AB3)
+    if ((rc = alloc(c, (void**)&c->sol2, c->nf * cb))) return rc;
   if ((rc = alloc(c, (void**)&c->minv, c->ninv * mb))) return rc;
   if ((rc = alloc(c, (void**)&c->mfwd, c->nfwd * mb))) return rc;
   if ((rc = alloc(c, (void**)&c->stage, full_bytes(c)))) return rc;
   if ((rc = alloc(c, (void**)&c->dflt, (size_t)g.nx * g.ny * sizeof(double)))) return rc;
   if ((rc = alloc(c, (void**)&c->flag, 64))) return rc;
   if (k.stepper == SW_STEP_IFMRK4) {
-    for (int i = 0; i < 4; ++i)
-      if ((rc = alloc(c, (void**)&c->rk[i], c->nf * cb))) return rc;
+    if ((rc = alloc(c, (void**)&c->acc, c->nf * cb))) return rc;
+    if ((rc = alloc(c, (void**)&c->nbuf, c->nf * cb))) return rc;
   } else {
     for (int i = 0; i < 3; ++i)
       if ((rc = alloc(c, (void**)&c->hist[i], c->nf * cb))) return rc;
@@ -338,6 +377,7 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
     HIPCHK(c, hipMemcpy(c->tw_y, ty.data(), ty.size() * sizeof(double2), hipMemcpyHostToDevice));
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (const char* e = std::getenv("SW_FUSE_ALL")) c->fuse_all = e[0] == '1';
   c->stats.resize(K_NKERN);
   for (int i = 0; i < K_NKERN; ++i) c->stats[i].name = kname[i];
   return SW_OK;
@@ -346,9 +386,8 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
 void sw_destroy(sw_ctx* c) {
   if (!c) return;
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* ptrs[] = {c->tw_x, c->tw_y, c->sol, c->hist[0], c->hist[1], c->hist[2], c->E, c->E2,
-                  c->rk[0], c->rk[1], c->rk[2], c->rk[3], c->xs, c->minv, c->mfwd, c->stage,
-                  c->dflt, c->flag};
+  void* ptrs[] = {c->tw_x, c->tw_y, c->sol, c->sol2, c->hist[0], c->hist[1], c->hist[2], c->E, c->E2,
+                  c->acc, c->nbuf, c->xs, c->minv, c->mfwd, c->stage, c->dflt, c->flag};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -371,6 +410,7 @@ int sw_set_state(sw_ctx* c, const void* sol, size_t bytes) {
   HIPCHK(c, hipSetDevice(c->cfg.device));
   HIPCHK(c, hipMemcpyAsync(c->stage, sol, bytes, hipMemcpyHostToDevice, c->stream));
   sw::launch_gather(c->nf, c->g, c->stage, c->sol, c->stream);
+  c->mixed_valid = false;
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return SW_OK;
@@ -426,7 +466,8 @@ int sw_calcN(sw_ctx* c, const void* sol, void* N, size_t bytes) {
   if (!c || !c->sol) return SW_E_STATE;
   if (!sol || !N || bytes != full_bytes(c)) return fail(c, SW_E_INVALID, "sw_calcN: size mismatch");
   HIPCHK(c, hipSetDevice(c->cfg.device));
-  double2* out = c->cfg.stepper == SW_STEP_IFMRK4 ? c->rk[3] : c->hist[c->head];
+  double2* out = c->cfg.stepper == SW_STEP_IFMRK4 ? c->nbuf : c->hist[c->head];
+  c->mixed_valid = false;  // minv / mfwd are used as scratch
   HIPCHK(c, hipMemcpyAsync(c->stage, sol, bytes, hipMemcpyHostToDevice, c->stream));
   sw::launch_gather(c->nf, c->g, c->stage, c->xs, c->stream);
   // scratch output: use the ring slot that the next step overwrites anyway
@@ -449,6 +490,7 @@ int sw_get_physical(sw_ctx* c, int32_t fid, double* out, size_t bytes) {
     if (layer > 1 || id == SW_PHYS_ETA || id > 5) return fail(c, SW_E_INVALID, "bad QG2 physical id");
   }
   HIPCHK(c, hipSetDevice(c->cfg.device));
+  c->mixed_valid = false;  // minv is used as scratch
   sw::launch_make_spec(c->cfg.model, fid, c->g, c->p, c->sol, c->xs, c->stream);
   sw::launch_col_inv1(c->g, c->xs, c->minv, c->tw_y, c->stream);
   sw::launch_row_c2r1(c->g, c->minv, c->dflt, c->tw_x, c->stream);
@@ -517,11 +559,11 @@ int sw_profile_steps(sw_ctx* c, int64_t nsteps, sw_kernel_stat* out, int32_t max
 
 double sw_step_alg_bytes(const sw_ctx* c) {
   if (!c) return 0.0;
-  const int ncalc = c->cfg.stepper == SW_STEP_IFMRK4 ? 4 : 1;
-  double b = ncalc * (kernel_bytes(c, K_COLINV) + kernel_bytes(c, K_ROW) + kernel_bytes(c, K_COLFWD));
-  b += kernel_bytes(c, K_UPD);
-  if (c->cfg.stepper == SW_STEP_IFMRK4) b += 3 * kernel_bytes(c, K_RK4STAGE);
-  return b;
+  const int nstage = c->cfg.stepper == SW_STEP_IFMRK4 ? 4 : 1;
+  if (!use_fused(c))
+    return nstage * (kernel_bytes(c, K_COLINV) + kernel_bytes(c, K_ROW) + kernel_bytes(c, K_COLFWD) +
+                     kernel_bytes(c, K_UPD));
+  return nstage * (kernel_bytes(c, K_ROW) + kernel_bytes(c, K_COLSTEP));  // primed pipeline
 }
 
 int sw_comm_unique_id(void* out128) {

@@ -17,6 +17,12 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+// No implicit FMA contraction anywhere in libsw's device code: every kernel
+// that evaluates the same formula rounds it the same way (the fused column
+// pass is bitwise identical to the separate kernels).  Complex products use
+// explicit fma below.
+#pragma clang fp contract(off)
+
 namespace sw {
 
 // padded LDS index: one pad element every 8 complex (breaks the 128-B
@@ -27,7 +33,7 @@ __host__ __device__ constexpr int lds_line_elems(int N) { return N + N / 8; }
 __device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
 __device__ __forceinline__ double2 cmul(double2 a, double2 b) {
-  return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+  return make_double2(__builtin_fma(a.x, b.x, -(a.y * b.y)), __builtin_fma(a.x, b.y, a.y * b.x));
 }
 __device__ __forceinline__ double2 cconj(double2 a) { return make_double2(a.x, -a.y); }
 __device__ __forceinline__ double2 cscale(double2 a, double s) { return make_double2(a.x * s, a.y * s); }

@@ -4,6 +4,10 @@
 #include <stdint.h>
 #include <stddef.h>
 
+// No implicit FMA contraction in libsw: the same formula rounds the same way
+// in every kernel (and on the host), so kernel fusion never changes results.
+#pragma clang fp contract(off)
+
 namespace sw {
 
 enum { MODEL_RSW = 0, MODEL_QG2 = 1 };
@@ -231,17 +235,24 @@ void launch_row(int model, const Geom& g, const Phys& p, const double2* Minv, do
                 const double2* tw_x, hipStream_t s);
 void launch_col_fwd(int model, const Geom& g, const Phys& p, const double2* Mfwd, double2* N,
                     const double2* tw_y, hipStream_t s);
-void launch_upd_fab3(int model, const Geom& g, const Phys& p, double2* sol, double2* NR,
-                     const double2* Rm1, const double2* Rm2, int euler, hipStream_t s);
-void launch_upd_ifmab3(int nf, const Geom& g, const Phys& p, double2* sol, const double2* N,
-                       const double2* Nm1, const double2* Nm2, const double2* E, const double2* E2,
-                       int euler, hipStream_t s);
-void launch_rk4_stage(int nf, int which, const Geom& g, const Phys& p, const double2* u,
-                      const double2* k, const double2* E, const double2* H, double2* x,
-                      hipStream_t s);
-void launch_rk4_final(int nf, const Geom& g, const Phys& p, double2* u, const double2* k1,
-                      const double2* k2, const double2* k3, const double2* k4, const double2* E,
-                      const double2* H, hipStream_t s);
+// Pointers of one stepper stage (see sw_kernels.hip).
+struct StepPtrs {
+  const double2* sol;  // state in
+  double2* sol_out;    // state out (FilteredAB3: the other buffer; else == sol)
+  double2* h0;
+  const double2* h1;
+  const double2* h2;
+  const double2* E;
+  const double2* E2;
+  double2* xs;        // IFMRK4 stages 1-3: the stage input written for the next calcN
+  int euler;
+  int stage;
+};
+enum { OP_FAB3 = 0, OP_IFMAB3 = 1, OP_RK4 = 2 };
+void launch_col_step(int model, int op, const Geom& g, const Phys& p, const StepPtrs& a,
+                     const double2* Mf, double2* Minv, const double2* tw_y, hipStream_t s);
+void launch_step_elem(int nf, int op, const Geom& g, const Phys& p, const StepPtrs& a,
+                      const double2* N, double2* xs, hipStream_t s);
 void launch_setup_expm(int model, const Geom& g, const Phys& p, double factor, double2* E,
                        hipStream_t s);
 void launch_gather(int nf, const Geom& g, const double2* full, double2* compact, hipStream_t s);

@@ -358,7 +358,8 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
 }
 
 // ===========================================================================
-// stepper updates over live modes (one thread per mode, all fields)
+// stepper updates: per-mode operations shared by the elementwise kernels and
+// the fused column kernel (identical arithmetic on both paths)
 // ===========================================================================
 __device__ __forceinline__ bool mode_of(const Geom& g, long long i, int& kr, int& j) {
   kr = (int)(i / g.LrP);
@@ -367,52 +368,11 @@ __device__ __forceinline__ bool mode_of(const Geom& g, long long i, int& kr, int
 }
 
 template <int NF>
-__device__ __forceinline__ void model_L(int model, const Phys& p, double k, double l, cplx L[NF][NF]) {
+__device__ __forceinline__ void model_L(const Phys& p, double k, double l, cplx L[NF][NF]) {
   if constexpr (NF == 3) {
     rsw_L(p, k, l, L);
   } else {
     qg2_L(p, k, l, L);
-  }
-}
-
-// FF FilteredAB3: RHS = N + L·sol; Euler for step < 3, else AB3;
-// sol .*= filter.  RHS overwrites N in place (it becomes history).
-template <int NF>
-__global__ void k_upd_fab3(Geom g, Phys p, double2* __restrict__ sol, double2* __restrict__ NR,
-                           const double2* __restrict__ Rm1, const double2* __restrict__ Rm2,
-                           int euler) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  int kr, j;
-  if (i >= g.cfield || !mode_of(g, i, kr, j)) return;
-  const double k = kr * g.mk, l = lwav(g, lrow_of(g, j));
-  cplx L[NF][NF];
-  model_L<NF>(0, p, k, l, L);
-  cplx s[NF];
-#pragma unroll
-  for (int f = 0; f < NF; ++f) {
-    const double2 t = sol[f * g.cfield + i];
-    s[f] = cx(t.x, t.y);
-  }
-  const double filt = filter_value(g, p, k, l);
-  const double dt = p.dt;
-#pragma unroll
-  for (int r = 0; r < NF; ++r) {
-    cplx Ls = cx(0.0);
-#pragma unroll
-    for (int cc = 0; cc < NF; ++cc) Ls = Ls + L[r][cc] * s[cc];
-    const double2 n = NR[r * g.cfield + i];
-    const cplx rhs = cx(n.x + Ls.re, n.y + Ls.im);
-    cplx upd;
-    if (euler) {
-      upd = dt * rhs;
-    } else {
-      const double2 a = Rm1[r * g.cfield + i], b = Rm2[r * g.cfield + i];
-      upd = dt * cx(23.0 / 12 * rhs.re - 16.0 / 12 * a.x + 5.0 / 12 * b.x,
-                    23.0 / 12 * rhs.im - 16.0 / 12 * a.y + 5.0 / 12 * b.y);
-    }
-    NR[r * g.cfield + i] = make_double2(rhs.re, rhs.im);
-    const cplx ns = s[r] + upd;
-    sol[r * g.cfield + i] = make_double2(ns.re * filt, ns.im * filt);
   }
 }
 
@@ -439,7 +399,15 @@ __device__ __forceinline__ void load_vec(const double2* __restrict__ X, long lon
 }
 
 template <int NF>
+__device__ __forceinline__ void store_vec(double2* __restrict__ X, long long cf, long long i,
+                                          const cplx x[NF]) {
+#pragma unroll
+  for (int f = 0; f < NF; ++f) X[f * cf + i] = make_double2(x[f].re, x[f].im);
+}
+
+template <int NF>
 __device__ __forceinline__ void matvec(const cplx M[NF][NF], const cplx x[NF], cplx y[NF]) {
+#pragma clang fp contract(off)
 #pragma unroll
   for (int r = 0; r < NF; ++r) {
     cplx s = cx(0.0);
@@ -449,117 +417,423 @@ __device__ __forceinline__ void matvec(const cplx M[NF][NF], const cplx x[NF], c
   }
 }
 
-// utils/IFMAB3.jl:129-160: Euler for step < 3, else AB3 with E N₋₁, E2 N₋₂;
-// then sol = E·(…); filter.
-template <int NF>
-__global__ void k_upd_ifmab3(Geom g, Phys p, double2* __restrict__ sol, const double2* __restrict__ N,
-                             const double2* __restrict__ Nm1, const double2* __restrict__ Nm2,
-                             const double2* __restrict__ E, const double2* __restrict__ E2,
-                             int euler) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  int kr, j;
-  if (i >= g.cfield || !mode_of(g, i, kr, j)) return;
+// StepPtrs (sw_internal.hpp): h0 receives this step's history entry
+// (FAB3: RHS, IFMAB3: N, RK4: the running combination acc).
+
+// FF FilteredAB3 for field F of one mode:
+//   RHS_F = N_F + (L·sol)_F;  x_F = sol_F + dt·(Euler | AB3);  x_F *= filter.
+// Reads the old state (all fields, for L·sol) from a.sol and writes the new
+// field to a.sol_out (a separate buffer, so fields can be updated one by one).
+template <int NF, int F>
+__device__ __forceinline__ cplx op_fab3_field(const Geom& g, const Phys& p, const StepPtrs& a,
+                                              long long i, double k, double l, cplx n) {
+#pragma clang fp contract(off)
   const long long cf = g.cfield;
-  cplx M[NF][NF], s[NF], n[NF], x[NF], y[NF];
-  load_mat<NF>(E, cf, i, M);
-  load_vec<NF>(sol, cf, i, s);
-  load_vec<NF>(N, cf, i, n);
+  cplx L[NF][NF], s[NF];
+  model_L<NF>(p, k, l, L);
+  load_vec<NF>(a.sol, cf, i, s);
+  const double filt = filter_value(g, p, k, l);
   const double dt = p.dt;
-  if (euler) {
+  cplx Ls = cx(0.0);
 #pragma unroll
-    for (int f = 0; f < NF; ++f) x[f] = s[f] + dt * n[f];
+  for (int cc = 0; cc < NF; ++cc) Ls = Ls + L[F][cc] * s[cc];
+  const cplx rhs = cx(n.re + Ls.re, n.im + Ls.im);
+  cplx x;
+  if (a.euler) {
+    x = s[F] + dt * rhs;
   } else {
-    cplx a[NF], b[NF], e1[NF], e2[NF], M2[NF][NF];
-    load_vec<NF>(Nm1, cf, i, a);
-    load_vec<NF>(Nm2, cf, i, b);
-    load_mat<NF>(E2, cf, i, M2);
-    matvec<NF>(M, a, e1);
-    matvec<NF>(M2, b, e2);
+    const double2 r1 = a.h1[F * cf + i], r2 = a.h2[F * cf + i];
+    x = s[F] + dt * cx(23.0 / 12 * rhs.re - 16.0 / 12 * r1.x + 5.0 / 12 * r2.x,
+                       23.0 / 12 * rhs.im - 16.0 / 12 * r1.y + 5.0 / 12 * r2.y);
+  }
+  x = cx(x.re * filt, x.im * filt);
+  a.h0[F * cf + i] = make_double2(rhs.re, rhs.im);
+  a.sol_out[F * cf + i] = make_double2(x.re, x.im);
+  return x;
+}
+
+template <int NF>
+__device__ __forceinline__ void op_fab3(const Geom& g, const Phys& p, const StepPtrs& a, long long i,
+                                        double k, double l, const cplx n[NF], cplx x[NF]) {
+  x[0] = op_fab3_field<NF, 0>(g, p, a, i, k, l, n[0]);
+  x[1] = op_fab3_field<NF, 1>(g, p, a, i, k, l, n[1]);
+  if constexpr (NF == 3) x[2] = op_fab3_field<NF, 2>(g, p, a, i, k, l, n[2]);
+}
+
+// utils/IFMAB3.jl:129-160: Euler for step < 3, else AB3 with E N₋₁, E2 N₋₂;
+// then sol = E·(…); filter.  N becomes history.
+template <int NF>
+__device__ __forceinline__ void op_ifmab3(const Geom& g, const Phys& p, const StepPtrs& a, long long i,
+                                          double k, double l, const cplx n[NF], cplx x[NF]) {
+#pragma clang fp contract(off)
+  const long long cf = g.cfield;
+  cplx M[NF][NF], s[NF], y[NF];
+  load_mat<NF>(a.E, cf, i, M);
+  load_vec<NF>(a.sol, cf, i, s);
+  const double dt = p.dt;
+  if (a.euler) {
+#pragma unroll
+    for (int f = 0; f < NF; ++f) y[f] = s[f] + dt * n[f];
+  } else {
+    cplx r1[NF], r2[NF], e1[NF], e2[NF], M2[NF][NF];
+    load_vec<NF>(a.h1, cf, i, r1);
+    load_vec<NF>(a.h2, cf, i, r2);
+    load_mat<NF>(a.E2, cf, i, M2);
+    matvec<NF>(M, r1, e1);
+    matvec<NF>(M2, r2, e2);
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+      y[f] = s[f] + dt * cx(23.0 / 12 * n[f].re - 16.0 / 12 * e1[f].re + 5.0 / 12 * e2[f].re,
+                            23.0 / 12 * n[f].im - 16.0 / 12 * e1[f].im + 5.0 / 12 * e2[f].im);
+  }
+  matvec<NF>(M, y, x);
+  if (p.use_filter) {
+    const double filt = filter_value(g, p, k, l);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) x[f] = cx(x[f].re * filt, x[f].im * filt);
+  }
+  store_vec<NF>(a.h0, cf, i, n);
+  store_vec<NF>(a.sol_out, cf, i, x);
+}
+
+// Lawson IF-RK4, one calcN result per stage:
+//   1: k1 -> acc = E k1;          x = H (u + dt/2 k1)
+//   2: k2 -> acc += 2 H k2;       x = H u + dt/2 k2
+//   3: k3 -> acc += 2 H k3;       x = E u + dt H k3
+//   4: k4 -> u = E u + dt/6 (acc + k4), filtered;  x = u
+template <int NF>
+__device__ __forceinline__ void op_rk4(const Geom& g, const Phys& p, const StepPtrs& a, long long i,
+                                       double k, double l, const cplx n[NF], cplx x[NF]) {
+#pragma clang fp contract(off)
+  const long long cf = g.cfield;
+  const double dt = p.dt;
+  cplx u[NF], M[NF][NF], t[NF], acc[NF];
+  load_vec<NF>(a.sol, cf, i, u);
+  if (a.stage == 1) {
+    load_mat<NF>(a.E, cf, i, M);
+    matvec<NF>(M, n, acc);
+    load_mat<NF>(a.E2, cf, i, M);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) t[f] = u[f] + (0.5 * dt) * n[f];
+    matvec<NF>(M, t, x);
+    store_vec<NF>(a.h0, cf, i, acc);
+  } else if (a.stage == 2 || a.stage == 3) {
+    cplx hk[NF];
+    load_vec<NF>(a.h0, cf, i, acc);
+    load_mat<NF>(a.E2, cf, i, M);
+    matvec<NF>(M, n, hk);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) acc[f] = acc[f] + 2.0 * hk[f];
+    if (a.stage == 2) {
+      matvec<NF>(M, u, t);
+#pragma unroll
+      for (int f = 0; f < NF; ++f) x[f] = t[f] + (0.5 * dt) * n[f];
+    } else {
+      load_mat<NF>(a.E, cf, i, M);
+      matvec<NF>(M, u, t);
+#pragma unroll
+      for (int f = 0; f < NF; ++f) x[f] = t[f] + dt * hk[f];
+    }
+    store_vec<NF>(a.h0, cf, i, acc);
+  } else {
+    load_vec<NF>(a.h0, cf, i, acc);
+    load_mat<NF>(a.E, cf, i, M);
+    matvec<NF>(M, u, t);
+    double filt = 1.0;
+    if (p.use_filter) filt = filter_value(g, p, k, l);
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
-      const cplx comb = cx(23.0 / 12 * n[f].re - 16.0 / 12 * e1[f].re + 5.0 / 12 * e2[f].re,
-                           23.0 / 12 * n[f].im - 16.0 / 12 * e1[f].im + 5.0 / 12 * e2[f].im);
-      x[f] = s[f] + dt * comb;
+      const cplx r = t[f] + (dt / 6) * (acc[f] + n[f]);
+      x[f] = cx(r.re * filt, r.im * filt);
+    }
+    store_vec<NF>(a.sol_out, cf, i, x);
+  }
+}
+
+template <int NF, int OP>
+__device__ __forceinline__ void step_op(const Geom& g, const Phys& p, const StepPtrs& a, long long i,
+                                        double k, double l, const cplx n[NF], cplx x[NF]) {
+  if constexpr (OP == OP_FAB3) op_fab3<NF>(g, p, a, i, k, l, n, x);
+  else if constexpr (OP == OP_IFMAB3) op_ifmab3<NF>(g, p, a, i, k, l, n, x);
+  else op_rk4<NF>(g, p, a, i, k, l, n, x);
+}
+
+// Elementwise (unfused) stepper kernel: N from memory; the stage input x is
+// written to xs (RK4 stages 1-3) for a separate col_inv.
+template <int NF, int OP>
+__global__ void k_step_elem(Geom g, Phys p, StepPtrs a, const double2* __restrict__ N,
+                            double2* __restrict__ xs) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  int kr, j;
+  if (i >= g.cfield || !mode_of(g, i, kr, j)) return;
+  const double k = kr * g.mk, l = lwav(g, lrow_of(g, j));
+  cplx n[NF], x[NF];
+  load_vec<NF>(N, g.cfield, i, n);
+  step_op<NF, OP>(g, p, a, i, k, l, n, x);
+  if (OP == OP_RK4 && a.stage < 4) store_vec<NF>(a.xs, g.cfield, i, x);
+}
+
+// ===========================================================================
+// col_step: the fused column pass of one stepper stage.  For column kr:
+//   forward y-FFTs of the row outputs -> N (registers, never in HBM)
+//   -> stepper op per live mode (state/history read and written once)
+//   -> the next calcN's inverse y-FFTs straight from registers -> mixed space.
+// Replaces col_fwd + update + col_inv of the next step.
+// ===========================================================================
+// keep the state/history loads of at most SW_SLOT_GROUP slots in flight
+#ifndef SW_SLOT_GROUP
+#define SW_SLOT_GROUP 2
+#endif
+#define SW_SLOT_FENCE(s) \
+  if (((s) + 1) % SW_SLOT_GROUP == 0) __builtin_amdgcn_sched_barrier(0)
+
+template <int MODEL, int LOG2N, int OP>
+__global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
+    k_col_step(Geom g, Phys p, StepPtrs a, const double2* __restrict__ Mf,
+               double2* __restrict__ Minv, const double2* __restrict__ tw) {
+  using B = Blk<LOG2N>;
+  constexpr int NT = B::NT;
+  constexpr int NF = MODEL == MODEL_RSW ? 3 : 2;
+  extern __shared__ double2 smem[];
+  const LineCtx c = line_ctx<LOG2N>();
+  const int kr = (B::NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * B::NB + c.ln;
+  double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
+  Twiddles<LOG2N> tws;
+  tws.load(c.t, tw);
+  const bool live = kr < g.kc;
+  const double k = kr * g.mk;
+  const long long MF = g.mfield;
+  double2 v[8];
+
+  auto load_col = [&](const double2* Mfield) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const double2 t = Mfield[midx(g, kr, c.t + s * NT)];  // kr < kcP: in bounds
+      v[s] = live ? t : zero2();
+    }
+  };
+
+  // forward y-FFT of row output fi, folded into N_f with the model's multiplier
+  auto fwd_into = [&](double2 (&n)[8], int fi, int mult, bool first) {
+    // mult: 0 -> -F, 1 -> -ik F, 2 -> -il F, 3 -> +ik F
+    load_col(Mf + fi * MF);
+    fft_line<LOG2N, -1>(v, c.t, tws, line);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      double2 t;
+      if (mult == 0) t = make_double2(-v[s].x, -v[s].y);
+      else if (mult == 1) t = cmul_i(v[s], -k);
+      else if (mult == 2) t = cmul_i(v[s], -lwav(g, c.t + s * NT));
+      else t = cmul_i(v[s], k);
+      n[s] = first ? t : cadd(n[s], t);
+    }
+  };
+  // N_f (rsw/RotatingShallowWater.jl:174-226, swqg/TwoLayerQG.jl:171,179)
+  auto compute_N = [&](double2 (&n)[8], int f) {
+    if constexpr (MODEL == MODEL_RSW) {
+      if (f < 2) {
+        fwd_into(n, f, 0, true);
+      } else {
+        fwd_into(n, 2, 1, true);
+        fwd_into(n, 3, 2, false);
+      }
+    } else {
+      fwd_into(n, f, 2, true);
+      fwd_into(n, 2 + f, 3, false);
+    }
+  };
+
+  if constexpr (OP == OP_FAB3) {
+    // FilteredAB3 updates field f from N_f alone: no N array is kept
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      double2 n[8];
+      compute_N(n, f);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const int m = c.t + s * NT;
+        const int j = compact_of(g, m);
+        if (live && j >= 0) {
+          const long long i = (long long)kr * g.LrP + j;
+          const cplx nf = cx(n[s].x, n[s].y);
+          if (f == 0) op_fab3_field<NF, 0>(g, p, a, i, k, lwav(g, m), nf);
+          else if (f == 1) op_fab3_field<NF, 1>(g, p, a, i, k, lwav(g, m), nf);
+          else op_fab3_field<NF, (NF == 3 ? 2 : 1)>(g, p, a, i, k, lwav(g, m), nf);
+        }
+        SW_SLOT_FENCE(s);
+      }
+    }
+  } else {
+    double2 X[NF][8];
+#pragma unroll
+    for (int f = 0; f < NF; ++f) compute_N(X[f], f);
+    // stepper op on the live modes of this column; it stores the next calcN
+    // input (new state, or the RK4 stage input in xs), which the inverse phase
+    // reads back (same thread, same addresses, L2-hot)
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int m = c.t + s * NT;
+      const int j = compact_of(g, m);
+      if (live && j >= 0) {
+        cplx n[NF], x[NF];
+#pragma unroll
+        for (int f = 0; f < NF; ++f) n[f] = cx(X[f][s].x, X[f][s].y);
+        const long long i = (long long)kr * g.LrP + j;
+        step_op<NF, OP>(g, p, a, i, k, lwav(g, m), n, x);
+        if (OP == OP_RK4 && a.stage < 4) store_vec<NF>(a.xs, g.cfield, i, x);
+      }
+      SW_SLOT_FENCE(s);
     }
   }
-  matvec<NF>(M, x, y);
-  double filt = 1.0;
-  if (p.use_filter) {
-    const double k = kr * g.mk, l = lwav(g, lrow_of(g, j));
-    filt = filter_value(g, p, k, l);
-  }
+  const double2* Xs = (OP == OP_RK4 && a.stage < 4) ? a.xs : a.sol_out;
+  const double2* Xc = Xs + (long long)(live ? kr : g.kc - 1) * g.LrP;
+  auto load_x = [&](int f, double2 (&x)[8]) {
 #pragma unroll
-  for (int f = 0; f < NF; ++f) sol[f * cf + i] = make_double2(y[f].re * filt, y[f].im * filt);
-}
+    for (int s = 0; s < 8; ++s) {
+      const int j = compact_of(g, c.t + s * NT);
+      const double2 t = Xc[f * g.cfield + (j >= 0 ? j : 0)];
+      x[s] = (live && j >= 0) ? t : zero2();
+    }
+  };
 
-// Lawson IF-RK4 stage inputs:
-//   which 1: x = H (u + dt/2 k1);  2: x = H u + dt/2 k2;  3: x = E u + dt H k3
-template <int NF>
-__global__ void k_rk4_stage(Geom g, Phys p, int which, const double2* __restrict__ u,
-                            const double2* __restrict__ kk, const double2* __restrict__ E,
-                            const double2* __restrict__ H, double2* __restrict__ x) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  int kr, j;
-  if (i >= g.cfield || !mode_of(g, i, kr, j)) return;
-  const long long cf = g.cfield;
-  const double dt = p.dt;
-  cplx uu[NF], kv[NF], M[NF][NF], t[NF], o[NF];
-  load_vec<NF>(u, cf, i, uu);
-  load_vec<NF>(kk, cf, i, kv);
-  if (which == 1) {
-    load_mat<NF>(H, cf, i, M);
+  // ---- inverse for the next calcN (same outputs as k_col_inv)
+  const double scale = 1.0 / ((double)g.nx * (double)g.ny);
+  auto store = [&](int o) {
+    if (live) {
+      double2* Mo = Minv + (long long)o * MF;
 #pragma unroll
-    for (int f = 0; f < NF; ++f) t[f] = uu[f] + (0.5 * dt) * kv[f];
-    matvec<NF>(M, t, o);
-  } else if (which == 2) {
-    load_mat<NF>(H, cf, i, M);
-    matvec<NF>(M, uu, t);
+      for (int s = 0; s < 8; ++s) Mo[midx(g, kr, c.t + s * NT)] = v[s];
+    }
+  };
+  if constexpr (MODEL == MODEL_RSW) {
 #pragma unroll
-    for (int f = 0; f < NF; ++f) o[f] = t[f] + (0.5 * dt) * kv[f];
+    for (int f = 0; f < 3; ++f) {
+      double2 x[8];
+      load_x(f, x);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) v[s] = cscale(x[s], scale);
+      fft_line<LOG2N, +1>(v, c.t, tws, line);
+      store(f);
+      if (f < 2) {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) v[s] = cmul_i(x[s], lwav(g, c.t + s * NT) * scale);
+        fft_line<LOG2N, +1>(v, c.t, tws, line);
+        store(3 + f);
+      }
+    }
   } else {
-    cplx M2[NF][NF], hk[NF];
-    load_mat<NF>(E, cf, i, M);
-    load_mat<NF>(H, cf, i, M2);
-    matvec<NF>(M, uu, t);
-    matvec<NF>(M2, kv, hk);
+    double2 q1[8], q2[8];
+    load_x(0, q1);
+    load_x(1, q2);
 #pragma unroll
-    for (int f = 0; f < NF; ++f) o[f] = t[f] + dt * hk[f];
+    for (int f = 0; f < 2; ++f) {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) v[s] = cscale(f ? q2[s] : q1[s], scale);
+      fft_line<LOG2N, +1>(v, c.t, tws, line);
+      store(f);
+      double2 psi[8];
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {  // streamfunctionfrompv! (swqg/TwoLayerQG.jl:101-111)
+        const double l = lwav(g, c.t + s * NT);
+        const double K2 = k * k + l * l;
+        const double iK2 = K2 == 0.0 ? 0.0 : 1.0 / K2;
+        const double den = K2 + 2.0 * p.F;
+        const double2 qs = cadd(q1[s], q2[s]);
+        const double2 qg = f ? q2[s] : q1[s];
+        const double2 ps = make_double2(-(K2 * qg.x + p.F * qs.x), -(K2 * qg.y + p.F * qs.y));
+        psi[s] = make_double2((ps.x / den) * iK2, (ps.y / den) * iK2);
+        v[s] = cscale(psi[s], scale);
+      }
+      fft_line<LOG2N, +1>(v, c.t, tws, line);
+      store(2 + f);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) v[s] = cmul_i(psi[s], lwav(g, c.t + s * NT) * scale);
+      fft_line<LOG2N, +1>(v, c.t, tws, line);
+      store(4 + f);
+    }
   }
-#pragma unroll
-  for (int f = 0; f < NF; ++f) x[f * cf + i] = make_double2(o[f].re, o[f].im);
 }
 
-// u <- E u + dt/6 (E k1 + 2 H (k2 + k3) + k4); filter
-template <int NF>
-__global__ void k_rk4_final(Geom g, Phys p, double2* __restrict__ u, const double2* __restrict__ k1,
-                            const double2* __restrict__ k2, const double2* __restrict__ k3,
-                            const double2* __restrict__ k4, const double2* __restrict__ E,
-                            const double2* __restrict__ H) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  int kr, j;
-  if (i >= g.cfield || !mode_of(g, i, kr, j)) return;
-  const long long cf = g.cfield;
-  const double dt = p.dt;
-  cplx uu[NF], a[NF], b[NF], c3[NF], d[NF], ME[NF][NF], MH[NF][NF], Eu[NF], Ek1[NF], s23[NF], H23[NF];
-  load_vec<NF>(u, cf, i, uu);
-  load_vec<NF>(k1, cf, i, a);
-  load_vec<NF>(k2, cf, i, b);
-  load_vec<NF>(k3, cf, i, c3);
-  load_vec<NF>(k4, cf, i, d);
-  load_mat<NF>(E, cf, i, ME);
-  load_mat<NF>(H, cf, i, MH);
-  matvec<NF>(ME, uu, Eu);
-  matvec<NF>(ME, a, Ek1);
+// ===========================================================================
+// col_step_fab3 (RSW FilteredAB3): one block per (column, field f).  The
+// FilteredAB3 update of field f needs N_f alone (plus the old state for L·sol),
+// and the next calcN's inverse transforms of field f need only the new field f:
+//   f=0: N0 = -F(A)            -> u   -> U, Uy
+//   f=1: N1 = -F(B)            -> v   -> V, Vy
+//   f=2: N2 = -ik F(C) - il F(D) -> η -> H
+// three y-FFTs per block, N never in HBM, old/new state in separate buffers.
+// ===========================================================================
+template <int LOG2N>
+__global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
+    k_col_step_fab3_rsw(Geom g, Phys p, StepPtrs a, const double2* __restrict__ Mf,
+                        double2* __restrict__ Minv, const double2* __restrict__ tw) {
+  using B = Blk<LOG2N>;
+  constexpr int NT = B::NT;
+  extern __shared__ double2 smem[];
+  const LineCtx c = line_ctx<LOG2N>();
+  const int kr = (B::NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * B::NB + c.ln;
+  const int f = blockIdx.y;
+  double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
+  Twiddles<LOG2N> tws;
+  tws.load(c.t, tw);
+  const bool live = kr < g.kc;
+  const double k = kr * g.mk;
+  const long long MF = g.mfield;
+  double2 v[8], n[8];
+
+  auto load_col = [&](const double2* Mfield) {
 #pragma unroll
-  for (int f = 0; f < NF; ++f) s23[f] = b[f] + c3[f];
-  matvec<NF>(MH, s23, H23);
-  double filt = 1.0;
-  if (p.use_filter) filt = filter_value(g, p, kr * g.mk, lwav(g, lrow_of(g, j)));
+    for (int s = 0; s < 8; ++s) {
+      const double2 t = Mfield[midx(g, kr, c.t + s * NT)];  // kr < kcP: in bounds
+      v[s] = live ? t : zero2();
+    }
+  };
+  // ---- N_f (rsw/RotatingShallowWater.jl:174-226)
+  load_col(Mf + (f < 2 ? f : 2) * MF);
+  fft_line<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
-  for (int f = 0; f < NF; ++f) {
-    const cplx comb = Ek1[f] + 2.0 * H23[f] + d[f];
-    const cplx r = Eu[f] + (dt / 6) * comb;
-    u[f * cf + i] = make_double2(r.re * filt, r.im * filt);
+  for (int s = 0; s < 8; ++s) n[s] = (f < 2) ? make_double2(-v[s].x, -v[s].y) : cmul_i(v[s], -k);
+  if (f == 2) {
+    load_col(Mf + 3 * MF);
+    fft_line<LOG2N, -1>(v, c.t, tws, line);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) n[s] = cadd(n[s], cmul_i(v[s], -lwav(g, c.t + s * NT)));
+  }
+  // ---- FilteredAB3 update of field f on the live modes; x = new field f
+  double2 x[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const int m = c.t + s * NT;
+    const int j = compact_of(g, m);
+    x[s] = zero2();
+    if (live && j >= 0) {
+      const long long i = (long long)kr * g.LrP + j;
+      const cplx nf = cx(n[s].x, n[s].y);
+      cplx r;
+      if (f == 0) r = op_fab3_field<3, 0>(g, p, a, i, k, lwav(g, m), nf);
+      else if (f == 1) r = op_fab3_field<3, 1>(g, p, a, i, k, lwav(g, m), nf);
+      else r = op_fab3_field<3, 2>(g, p, a, i, k, lwav(g, m), nf);
+      x[s] = make_double2(r.re, r.im);
+    }
+  }
+  // ---- inverse transforms of field f for the next calcN (as k_col_inv)
+  const double scale = 1.0 / ((double)g.nx * (double)g.ny);
+  auto store = [&](int o) {
+    if (live) {
+      double2* Mo = Minv + (long long)o * MF;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) Mo[midx(g, kr, c.t + s * NT)] = v[s];
+    }
+  };
+#pragma unroll
+  for (int s = 0; s < 8; ++s) v[s] = cscale(x[s], scale);
+  fft_line<LOG2N, +1>(v, c.t, tws, line);
+  store(f);
+  if (f < 2) {  // ∂y: Uy, Vy
+#pragma unroll
+    for (int s = 0; s < 8; ++s) v[s] = cmul_i(x[s], lwav(g, c.t + s * NT) * scale);
+    fft_line<LOG2N, +1>(v, c.t, tws, line);
+    store(3 + f);
   }
 }
 
@@ -571,7 +845,7 @@ __global__ void k_setup_expm(Geom g, Phys p, double factor, double2* __restrict_
   if (i >= g.cfield || !mode_of(g, i, kr, j)) return;
   const double k = kr * g.mk, l = lwav(g, lrow_of(g, j));
   cplx L[NF][NF], A[NF][NF], X[NF][NF];
-  model_L<NF>(0, p, k, l, L);
+  model_L<NF>(p, k, l, L);
   const double sdt = factor * p.dt;
 #pragma unroll
   for (int r = 0; r < NF; ++r)
@@ -848,39 +1122,45 @@ void launch_col_fwd(int model, const Geom& g, const Phys& p, const double2* Mfwd
 
 static inline dim3 mode_grid(const Geom& g) { return dim3((unsigned)((g.cfield + 255) / 256)); }
 
-void launch_upd_fab3(int model, const Geom& g, const Phys& p, double2* sol, double2* NR,
-                     const double2* Rm1, const double2* Rm2, int euler, hipStream_t s) {
-  if (model == MODEL_RSW)
-    hipLaunchKernelGGL(k_upd_fab3<3>, mode_grid(g), dim3(256), 0, s, g, p, sol, NR, Rm1, Rm2, euler);
-  else
-    hipLaunchKernelGGL(k_upd_fab3<2>, mode_grid(g), dim3(256), 0, s, g, p, sol, NR, Rm1, Rm2, euler);
+template <int L>
+struct ColStepL {
+  static void run(int model, int op, const Geom& g, const Phys& p, const StepPtrs& a,
+                  const double2* Mf, double2* Minv, const double2* tw, hipStream_t s) {
+    const dim3 grid(col_blocks<L>(g)), blk(Blk<L>::THREADS);
+    const size_t sh = lds_bytes<L>();
+#define SW_CS(M, O) hipLaunchKernelGGL((k_col_step<M, L, O>), grid, blk, sh, s, g, p, a, Mf, Minv, tw)
+    if (model == MODEL_RSW) {
+      if (op == OP_FAB3)
+        hipLaunchKernelGGL((k_col_step_fab3_rsw<L>), dim3(col_blocks<L>(g), 3), blk, sh, s, g, p, a, Mf, Minv, tw);
+      else if (op == OP_IFMAB3) SW_CS(MODEL_RSW, OP_IFMAB3);
+      else SW_CS(MODEL_RSW, OP_RK4);
+    } else {
+      if (op == OP_FAB3) SW_CS(MODEL_QG2, OP_FAB3);
+      else if (op == OP_IFMAB3) SW_CS(MODEL_QG2, OP_IFMAB3);
+      else SW_CS(MODEL_QG2, OP_RK4);
+    }
+#undef SW_CS
+  }
+};
+
+void launch_col_step(int model, int op, const Geom& g, const Phys& p, const StepPtrs& a,
+                     const double2* Mf, double2* Minv, const double2* tw_y, hipStream_t s) {
+  dispatch_log2<ColStepL>(g.log2ny, model, op, g, p, a, Mf, Minv, tw_y, s);
 }
 
-void launch_upd_ifmab3(int nf, const Geom& g, const Phys& p, double2* sol, const double2* N,
-                       const double2* Nm1, const double2* Nm2, const double2* E, const double2* E2,
-                       int euler, hipStream_t s) {
-  if (nf == 3)
-    hipLaunchKernelGGL(k_upd_ifmab3<3>, mode_grid(g), dim3(256), 0, s, g, p, sol, N, Nm1, Nm2, E, E2, euler);
-  else
-    hipLaunchKernelGGL(k_upd_ifmab3<2>, mode_grid(g), dim3(256), 0, s, g, p, sol, N, Nm1, Nm2, E, E2, euler);
-}
-
-void launch_rk4_stage(int nf, int which, const Geom& g, const Phys& p, const double2* u,
-                      const double2* k, const double2* E, const double2* H, double2* x,
-                      hipStream_t s) {
-  if (nf == 3)
-    hipLaunchKernelGGL(k_rk4_stage<3>, mode_grid(g), dim3(256), 0, s, g, p, which, u, k, E, H, x);
-  else
-    hipLaunchKernelGGL(k_rk4_stage<2>, mode_grid(g), dim3(256), 0, s, g, p, which, u, k, E, H, x);
-}
-
-void launch_rk4_final(int nf, const Geom& g, const Phys& p, double2* u, const double2* k1,
-                      const double2* k2, const double2* k3, const double2* k4, const double2* E,
-                      const double2* H, hipStream_t s) {
-  if (nf == 3)
-    hipLaunchKernelGGL(k_rk4_final<3>, mode_grid(g), dim3(256), 0, s, g, p, u, k1, k2, k3, k4, E, H);
-  else
-    hipLaunchKernelGGL(k_rk4_final<2>, mode_grid(g), dim3(256), 0, s, g, p, u, k1, k2, k3, k4, E, H);
+void launch_step_elem(int nf, int op, const Geom& g, const Phys& p, const StepPtrs& a,
+                      const double2* N, double2* xs, hipStream_t s) {
+#define SW_SE(F, O) hipLaunchKernelGGL((k_step_elem<F, O>), mode_grid(g), dim3(256), 0, s, g, p, a, N, xs)
+  if (nf == 3) {
+    if (op == OP_FAB3) SW_SE(3, OP_FAB3);
+    else if (op == OP_IFMAB3) SW_SE(3, OP_IFMAB3);
+    else SW_SE(3, OP_RK4);
+  } else {
+    if (op == OP_FAB3) SW_SE(2, OP_FAB3);
+    else if (op == OP_IFMAB3) SW_SE(2, OP_IFMAB3);
+    else SW_SE(2, OP_RK4);
+  }
+#undef SW_SE
 }
 
 void launch_setup_expm(int model, const Geom& g, const Phys& p, double factor, double2* E,

@@ -35,7 +35,7 @@ class Problem:
 
     def __init__(self, model, *, nx, ny, Lx, Ly, dt, aliased_fraction, stepper, params,
                  use_filter=False, filter_kw=None, device=0, check_nan=True, T=np.float64,
-                 nop_calcN=False):
+                 nop_calcN=False, unfused=False):
         if np.dtype(T) != np.float64:
             raise _lib.LibSWError("this build computes in fp64 (T=Float64) only")
         if stepper not in _lib.STEPPERS:
@@ -62,6 +62,7 @@ class Problem:
         cfg.device = int(device)
         cfg.check_nan = 1 if check_nan else 0
         cfg.nop_calcN = 1 if nop_calcN else 0
+        cfg.unfused = 1 if unfused else 0
         self.ctx = _lib.Context(cfg)
         self.model = model
         self.stepper = stepper

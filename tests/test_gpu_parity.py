@@ -101,6 +101,30 @@ def test_nop_calcN_linear_exactness():
     prob.close()
 
 
+@pytest.mark.parametrize("fuse_all", [False, True])
+@pytest.mark.parametrize("name", sw_cases.CASES)
+def test_fused_equals_unfused(name, fuse_all, monkeypatch):
+    """The fused column pass (col_fwd + update + next col_inv in one kernel) and
+    the reference sequence of separate kernels give bitwise-identical states.
+    fuse_all: also force the generic fused kernel on every model/stepper pair."""
+    if fuse_all:
+        monkeypatch.setenv("SW_FUSE_ALL", "1")
+    p = sw_cases.case_params(name, 128)
+    pr = sw_cases.oracle_problem(p)
+    pr.set_solution(sw_cases.initial_condition(p, pr.grid))
+    a = sw_cases.libsw_problem(p)
+    monkeypatch.delenv("SW_FUSE_ALL", raising=False)
+    b = sw_cases.libsw_problem(p, unfused=True)
+    a.sol = pr.sol
+    b.sol = pr.sol
+    for n in (2, 3, 4):  # Euler start-up, then AB3, crossing sw_step calls
+        a.stepforward(n)
+        b.stepforward(n)
+        assert np.array_equal(a.sol, b.sol), n
+    a.close()
+    b.close()
+
+
 def test_determinism_2048():
     """Same inputs -> bitwise-identical state (no atomics on the data path)."""
     from juliaraytracingsw_amd import drivers
