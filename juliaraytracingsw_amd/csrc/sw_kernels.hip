@@ -771,8 +771,20 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   constexpr int NT = B::NT;
   extern __shared__ double2 smem[];
   const LineCtx c = line_ctx<LOG2N>();
-  const int kr = (B::NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * B::NB + c.ln;
-  const int f = blockIdx.y;
+  int kr, f;
+  if (B::NB == 1) {
+    // 1-D grid of 3*kcP blocks.  The 3 fields of the 8 columns that share each
+    // 128-B chunk of the mixed layout (24 blocks) sit on one XCD label
+    // (b % 8) within 192 consecutive block ids: they meet in one L2, where the
+    // other fields' reads of the old state and the chunk writes coalesce
+    // (speed only; any placement is correct).
+    const int b = blockIdx.x, q = b / 192, r = b - q * 192, x = r & 7, jj = r >> 3;
+    f = jj % 3;
+    kr = q * 64 + x * 8 + jj / 3;
+  } else {
+    kr = blockIdx.x * B::NB + c.ln;
+    f = blockIdx.y;
+  }
   double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
   Twiddles<LOG2N> tws;
   tws.load(c.t, tw);
@@ -1131,7 +1143,9 @@ struct ColStepL {
 #define SW_CS(M, O) hipLaunchKernelGGL((k_col_step<M, L, O>), grid, blk, sh, s, g, p, a, Mf, Minv, tw)
     if (model == MODEL_RSW) {
       if (op == OP_FAB3)
-        hipLaunchKernelGGL((k_col_step_fab3_rsw<L>), dim3(col_blocks<L>(g), 3), blk, sh, s, g, p, a, Mf, Minv, tw);
+        hipLaunchKernelGGL((k_col_step_fab3_rsw<L>),
+                           Blk<L>::NB == 1 ? dim3(3 * col_blocks<L>(g)) : dim3(col_blocks<L>(g), 3), blk, sh,
+                           s, g, p, a, Mf, Minv, tw);
       else if (op == OP_IFMAB3) SW_CS(MODEL_RSW, OP_IFMAB3);
       else SW_CS(MODEL_RSW, OP_RK4);
     } else {
