@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SW_ABI_VERSION 1
+#define SW_ABI_VERSION 2
 
 /* models */
 #define SW_MODEL_RSW 0   /* rsw/RotatingShallowWater.jl: fields (u, v, η), 3×3 L   */
@@ -93,8 +93,15 @@ typedef struct sw_config {
   int32_t unfused;          /* debug/reference: separate col_fwd + update +
                                col_inv kernels instead of the fused column
                                pass (results are bitwise identical)        */
-  int32_t nranks, rank;     /* slab decomposition (1, 0 = single GPU)      */
-  const void* comm_unique_id; /* ncclUniqueId bytes (nranks > 1)           */
+  /* slab decomposition: the grid is split into nranks slabs
+   * (kr columns for the column passes, y rows for the row pass).
+   *   local_slabs <= 1: this process holds slab `rank` on `device`; the
+   *     transposes are RCCL all-to-alls over comm_unique_id (nranks > 1).
+   *   local_slabs == nranks: this process holds every slab on `device`; the
+   *     transposes are device copies (same data movement, one GPU).
+   * nranks must be a power of two with ny / nranks >= 32.                 */
+  int32_t nranks, rank, local_slabs;
+  const void* comm_unique_id; /* ncclUniqueId bytes (128), from sw_comm_unique_id */
 } sw_config;
 
 typedef struct sw_ctx sw_ctx;
@@ -149,7 +156,8 @@ int sw_profile_steps(sw_ctx* ctx, int64_t nsteps, sw_kernel_stat* stats,
 /* Algorithmic HBM bytes of one step of the configured path. */
 double sw_step_alg_bytes(const sw_ctx* ctx);
 
-/* Multi-GPU: write an RCCL unique id (128 bytes) for rank 0 to broadcast. */
+/* Multi-GPU: write an RCCL unique id (128 bytes); rank 0 calls it and
+ * broadcasts the bytes to every rank before sw_create. */
 int sw_comm_unique_id(void* out128);
 
 #ifdef __cplusplus

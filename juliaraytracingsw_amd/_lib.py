@@ -10,7 +10,7 @@ import os
 
 import numpy as np
 
-SW_ABI_VERSION = 1
+SW_ABI_VERSION = 2
 SW_MODEL_RSW, SW_MODEL_QG2 = 0, 1
 SW_STEP_FILTERED_AB3, SW_STEP_IFMAB3, SW_STEP_IFMRK4 = 0, 1, 2
 SW_OK, SW_E_INVALID, SW_E_NOMEM, SW_E_HIP, SW_E_COMM, SW_E_NAN, SW_E_STATE = 0, -1, -2, -3, -4, -5, -6
@@ -45,7 +45,7 @@ class SwConfig(C.Structure):
         ("use_filter", C.c_int32), ("filter_order", C.c_int32),
         ("filter_innerK", C.c_double), ("filter_outerK", C.c_double), ("filter_tol", C.c_double),
         ("device", C.c_int32), ("check_nan", C.c_int32), ("nop_calcN", C.c_int32), ("unfused", C.c_int32),
-        ("nranks", C.c_int32), ("rank", C.c_int32),
+        ("nranks", C.c_int32), ("rank", C.c_int32), ("local_slabs", C.c_int32),
         ("comm_unique_id", C.c_void_p),
     ]
 
@@ -103,6 +103,15 @@ def default_config() -> SwConfig:
     cfg = SwConfig()
     lib.sw_config_default(C.byref(cfg))
     return cfg
+
+
+def comm_unique_id() -> bytes:
+    """RCCL unique id (128 bytes) for rank 0 to broadcast (sw_comm_unique_id)."""
+    buf = C.create_string_buffer(128)
+    rc = load().sw_comm_unique_id(buf)
+    if rc != SW_OK:
+        raise LibSWError(f"sw_comm_unique_id failed (code {rc})", rc)
+    return buf.raw
 
 
 class Context:

@@ -34,7 +34,8 @@ def build_lib(verbose=False, force=False, out=OUT, extra_flags=()):
         return out
     cmd = [hipcc_path(), "-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC", "-shared",
            "-Wno-unused-result", f"-I{os.path.join(ROOT, 'include')}", "-o", out + ".tmp",
-           *extra_flags, *[os.path.join(CSRC, s) for s in SOURCES]]
+           *extra_flags, *[os.path.join(CSRC, s) for s in SOURCES],
+           "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
     if verbose:
         print(" ".join(cmd))
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -1,11 +1,14 @@
-// libsw host runtime: context lifecycle, stepper sequencing and the C ABI of
-// include/sw.h.  One HIP stream per context; every call that returns data
-// synchronises that stream.  Reference seams replaced are cited per function.
+// libsw host runtime: context lifecycle, slab decomposition, stepper
+// sequencing and the C ABI of include/sw.h.  One HIP stream per context;
+// every call that returns data synchronises that stream.  Reference seams
+// replaced are cited per function.
 #include "sw.h"
 #include "sw_internal.hpp"
 
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -21,28 +24,40 @@ struct KStat {
   const char* name;
   int64_t launches = 0;
   double ms = 0.0;
-  double bytes = 0.0;
+};
+
+// Device buffers of one slab.  With one slab the two
+// phases of each mixed array are the same buffer (mic == mir, mfr == mfc).
+struct Slab {
+  Geom g{};
+  double2* sol = nullptr;                    // compact state, nf fields
+  double2* sol2 = nullptr;                   // FilteredAB3: the other state buffer (ping-pong)
+  double2* hist[3] = {nullptr, nullptr, nullptr};  // FAB3 RHS ring / IFMAB3 N ring
+  double2 *E = nullptr, *E2 = nullptr;       // IF operators (E2 = exp(2Ldt) or exp(Ldt/2))
+  double2* acc = nullptr;                    // IFMRK4 running stage combination
+  double2* nbuf = nullptr;                   // unfused IFMRK4 / sw_calcN: calcN output
+  double2* xs = nullptr;                     // stage input / scratch compact
+  double2* mic = nullptr;                    // calcN inputs, column phase (col_inv / col_step out)
+  double2* mir = nullptr;                    // calcN inputs, row phase (row in)
+  double2* mfr = nullptr;                    // row outputs, row phase
+  double2* mfc = nullptr;                    // row outputs, column phase (col_fwd / col_step in)
 };
 
 struct sw_ctx {
   sw_config cfg{};
-  Geom g{};
   Phys p{};
   int nf = 0, ninv = 0, nfwd = 0;
+  int P = 1;                                 // slabs in the decomposition
+  bool rccl = false;                         // one slab per process, RCCL transposes
+  ncclComm_t comm = nullptr;
   hipStream_t stream = nullptr;
   double2 *tw_x = nullptr, *tw_y = nullptr;
-  double2* sol = nullptr;                    // compact state, nf fields
-  double2* sol2 = nullptr;                   // FilteredAB3: the other state buffer (ping-pong)
-  double2* hist[3] = {nullptr, nullptr, nullptr};  // FAB3 RHS ring / IFMAB3 N ring
+  std::vector<Slab> sl;                      // slabs held by this process
   int head = 0;
-  double2 *E = nullptr, *E2 = nullptr;       // IF operators (E2 = exp(2Ldt) or exp(Ldt/2))
-  double2* acc = nullptr;                    // IFMRK4 running stage combination
-  double2* nbuf = nullptr;                   // unfused IFMRK4: calcN output
-  double2* xs = nullptr;                     // stage input / scratch compact
-  bool mixed_valid = false;                  // minv == col_inv(sol) (fused pipeline primed)
+  bool mixed_valid = false;                  // mir == transposed col_inv(sol) (fused pipeline primed)
   bool fuse_all = false;                     // SW_FUSE_ALL=1: fused pass for every pair (experiments)
-  double2 *minv = nullptr, *mfwd = nullptr;  // mixed-space fields
   double2* stage = nullptr;                  // full (nkr,nl,nf) staging
+  double2* gbuf = nullptr;                   // RCCL: all-gathered compact slabs
   double* dflt = nullptr;                    // physical staging / reductions
   int* flag = nullptr;
   double t = 0.0;
@@ -68,6 +83,13 @@ int fail(sw_ctx* c, int code, const std::string& msg) {
       return fail(ctx, SW_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));     \
   } while (0)
 
+#define NCCLCHK(ctx, expr)                                                               \
+  do {                                                                                   \
+    ncclResult_t r_ = (expr);                                                            \
+    if (r_ != ncclSuccess)                                                               \
+      return fail(ctx, SW_E_COMM, std::string(#expr) + ": " + ncclGetErrorString(r_));   \
+  } while (0)
+
 int ilog2(int n) {
   int l = 0;
   while ((1 << l) < n) ++l;
@@ -81,6 +103,54 @@ void alias_range(int n, double af, int& iL, int& iR) {
   const double L = (1 - af) / 2, R = (1 + af) / 2;
   iL = (int)std::floor(L * n) + 1;
   iR = (int)std::ceil(R * n);
+}
+
+// lines per block of the column kernels (Blk<log2ny>::NB in sw_kernels.hip)
+int col_lines_per_block(int ny) {
+  const int NT = ny / 8;
+  return NT >= 256 ? 1 : std::min(256 / NT, 32);
+}
+
+// geometry of slab s of P
+Geom make_geom(const sw_config& k, int P, int s) {
+  Geom g{};
+  g.nx = k.nx;
+  g.ny = k.ny;
+  g.log2nx = ilog2(k.nx);
+  g.log2ny = ilog2(k.ny);
+  g.nkr = k.nx / 2 + 1;
+  g.nl = k.ny;
+  int iLx, iRx, iLy, iRy;
+  alias_range(k.nx, k.aliased_fraction, iLx, iRx);
+  alias_range(k.ny, k.aliased_fraction, iLy, iRy);
+  g.kc = iLx - 1;
+  g.lc = iLy - 1;
+  g.lr2 = iRy;
+  g.Lr = g.lc + (k.ny - g.lr2);
+  g.LrP = (g.Lr + 7) / 8 * 8;
+  g.Lx = k.Lx;
+  g.Ly = k.Ly;
+  g.mk = (2 * M_PI / k.Lx * k.nx) / k.nx;
+  g.ml = (2 * M_PI / k.Ly * k.ny) / k.ny;
+  g.dx = k.Lx / k.nx;
+  g.dy = k.Ly / k.ny;
+  g.nslab = P;
+  g.slab = s;
+  if (P == 1) {
+    g.kcl = (g.kc + 63) / 64 * 64;  // XCD-aware column mapping needs multiples of 64
+  } else {
+    const int gran = std::max(8, col_lines_per_block(k.ny));
+    g.kcl = ((g.kc + P - 1) / P + gran - 1) / gran * gran;
+  }
+  g.ntl = g.kcl / 8;
+  g.kr0 = s * g.kcl;
+  g.kcn = std::max(0, std::min(g.kcl, g.kc - g.kr0));
+  g.nyl = k.ny / P;
+  g.log2nyl = ilog2(g.nyl);
+  g.y0 = s * g.nyl;
+  g.cfield = (long long)std::max(g.kcn, 1) * g.LrP;
+  g.mfield = (long long)g.kcl * g.ny;
+  return g;
 }
 
 int alloc(sw_ctx* c, void** p, size_t bytes) {
@@ -101,12 +171,15 @@ std::vector<double2> twiddles(int N) {
   return tw;
 }
 
-// --- algorithmic bytes per kernel launch (DESIGN.md §4) ---------------------
-double live_field_bytes(const Geom& g) { return 16.0 * g.kc * g.Lr; }
-double mixed_field_bytes(const Geom& g) { return 16.0 * g.kc * g.ny; }
+// --- algorithmic bytes per kernel launch (DESIGN.md §3) ---------------------
+// summed over the slabs this process holds; F = live compact field,
+// Mc = live mixed field in the column phase, Mr = in the row phase
+double live_field_bytes(const Geom& g) { return 16.0 * g.kcn * g.Lr; }
+double mixed_col_bytes(const Geom& g) { return 16.0 * g.kcn * g.ny; }
+double mixed_row_bytes(const Geom& g) { return 16.0 * g.kc * g.nyl; }
 
-enum KId { K_COLINV = 0, K_ROW, K_COLFWD, K_UPD, K_COLSTEP, K_NKERN };
-const char* kname[K_NKERN] = {"col_inv", "row", "col_fwd", "update", "col_step"};
+enum KId { K_COLINV = 0, K_ROW, K_COLFWD, K_UPD, K_COLSTEP, K_XCHG, K_NKERN };
+const char* kname[K_NKERN] = {"col_inv", "row", "col_fwd", "update", "col_step", "transpose"};
 
 // state/history bytes of one stepper op per live mode, in live-field units
 // (reads + writes; AB3 steady state; IFMRK4 averaged over its four stages)
@@ -121,17 +194,23 @@ double op_fields(const sw_ctx* c) {
 }
 
 double kernel_bytes(const sw_ctx* c, int kid) {
-  const Geom& g = c->g;
-  const double F = live_field_bytes(g), M = mixed_field_bytes(g);
-  const int nf = c->nf;
-  switch (kid) {
-    case K_COLINV: return nf * F + c->ninv * M;
-    case K_ROW: return (c->ninv + c->nfwd) * M;
-    case K_COLFWD: return c->nfwd * M + nf * F;
-    case K_UPD: return (op_fields(c) + nf) * F;  // + N read
-    case K_COLSTEP: return c->nfwd * M + op_fields(c) * F + c->ninv * M;
+  double b = 0.0;
+  for (const Slab& s : c->sl) {
+    const Geom& g = s.g;
+    const double F = live_field_bytes(g), Mc = mixed_col_bytes(g), Mr = mixed_row_bytes(g);
+    const int nf = c->nf;
+    switch (kid) {
+      case K_COLINV: b += nf * F + c->ninv * Mc; break;
+      case K_ROW: b += (c->ninv + c->nfwd) * Mr; break;
+      case K_COLFWD: b += c->nfwd * Mc + nf * F; break;
+      case K_UPD: b += (op_fields(c) + nf) * F; break;  // + N read
+      case K_COLSTEP: b += c->nfwd * Mc + op_fields(c) * F + c->ninv * Mc; break;
+      case K_XCHG:  // bytes leaving this slab in one inverse + one forward transpose
+        b += (double)(c->ninv + c->nfwd) * (c->P - 1) * g.kcl * g.nyl * 16.0;
+        break;
+    }
   }
-  return 0;
+  return b;
 }
 
 struct Timer {
@@ -152,25 +231,69 @@ struct Timer {
   }
 };
 
-// equation.calcN!(N, X, …): col_inv -> row -> col_fwd
-void calcN(sw_ctx* c, const double2* X, double2* N) {
+// The transpose between the column and the row passes: block q
+// of every source slab p goes to block p of slab q.  inv: column-phase calcN
+// inputs -> row phase; fwd: row outputs -> column phase.  The blocks are
+// contiguous in both layouts, so no pack/unpack kernels exist.
+int transpose(sw_ctx* c, bool inv, int nfields) {
+  if (c->P == 1) return 0;
+  Timer tm(c, K_XCHG);
+  const Geom& g0 = c->sl[0].g;
+  const size_t blk = (size_t)g0.kcl * g0.nyl;  // elements per (slab pair, field)
+  const long long MF = g0.mfield;
+  if (!c->rccl) {
+    for (int o = 0; o < nfields; ++o)
+      for (int p = 0; p < c->P; ++p)
+        for (int q = 0; q < c->P; ++q) {
+          const double2* src = (inv ? c->sl[p].mic : c->sl[p].mfr) + o * MF + q * blk;
+          double2* dst = (inv ? c->sl[q].mir : c->sl[q].mfc) + o * MF + p * blk;
+          HIPCHK(c, hipMemcpyAsync(dst, src, blk * sizeof(double2), hipMemcpyDeviceToDevice, c->stream));
+        }
+    return 0;
+  }
+  const Slab& s = c->sl[0];
+  const int me = g0.slab;
+  NCCLCHK(c, ncclGroupStart());
+  for (int o = 0; o < nfields; ++o) {
+    const double2* src = (inv ? s.mic : s.mfr) + o * MF;
+    double2* dst = (inv ? s.mir : s.mfc) + o * MF;
+    for (int q = 0; q < c->P; ++q) {
+      if (q == me) {
+        HIPCHK(c, hipMemcpyAsync(dst + me * blk, src + me * blk, blk * sizeof(double2),
+                                 hipMemcpyDeviceToDevice, c->stream));
+      } else {
+        NCCLCHK(c, ncclSend(src + q * blk, 2 * blk, ncclDouble, q, c->comm, c->stream));
+        NCCLCHK(c, ncclRecv(dst + q * blk, 2 * blk, ncclDouble, q, c->comm, c->stream));
+      }
+    }
+  }
+  NCCLCHK(c, ncclGroupEnd());
+  return 0;
+}
+
+// equation.calcN!(N, X, …): col_inv -> transpose -> row -> transpose -> col_fwd
+int calcN(sw_ctx* c, double2* Slab::*X, double2* Slab::*N) {
   const int model = c->cfg.model;
   if (c->cfg.nop_calcN) {  // NOPcalcN!: N .= 0
-    (void)hipMemsetAsync(N, 0, (size_t)c->nf * c->g.cfield * sizeof(double2), c->stream);
-    return;
+    for (Slab& s : c->sl)
+      HIPCHK(c, hipMemsetAsync(s.*N, 0, (size_t)c->nf * s.g.cfield * sizeof(double2), c->stream));
+    return 0;
   }
   {
     Timer tm(c, K_COLINV);
-    sw::launch_col_inv(model, c->g, c->p, X, c->minv, c->tw_y, c->stream);
+    for (Slab& s : c->sl) sw::launch_col_inv(model, s.g, c->p, s.*X, s.mic, c->tw_y, c->stream);
   }
+  if (int rc = transpose(c, true, c->ninv)) return rc;
   {
     Timer tm(c, K_ROW);
-    sw::launch_row(model, c->g, c->p, c->minv, c->mfwd, c->tw_x, c->stream);
+    for (Slab& s : c->sl) sw::launch_row(model, s.g, c->p, s.mir, s.mfr, c->tw_x, c->stream);
   }
+  if (int rc = transpose(c, false, c->nfwd)) return rc;
   {
     Timer tm(c, K_COLFWD);
-    sw::launch_col_fwd(model, c->g, c->p, c->mfwd, N, c->tw_y, c->stream);
+    for (Slab& s : c->sl) sw::launch_col_fwd(model, s.g, c->p, s.mfc, s.*N, c->tw_y, c->stream);
   }
+  return 0;
 }
 
 // one stepforward!(sol, clock, ts, …).  Fused pipeline: the column pass of
@@ -186,57 +309,152 @@ bool use_fused(const sw_ctx* c) {
   return c->cfg.model == SW_MODEL_RSW && c->cfg.stepper == SW_STEP_FILTERED_AB3;
 }
 
-void run_stage(sw_ctx* c, int op, const sw::StepPtrs& a, const double2* X) {
+sw::StepPtrs step_ptrs(const sw_ctx* c, const Slab& s) {
+  const int st = c->cfg.stepper;
+  sw::StepPtrs a{};
+  a.sol = s.sol;
+  a.sol_out = (st == SW_STEP_FILTERED_AB3) ? s.sol2 : s.sol;
+  a.E = s.E;
+  a.E2 = s.E2;
+  a.xs = s.xs;
+  a.euler = c->step < 3 ? 1 : 0;
+  if (st == SW_STEP_IFMRK4) {
+    a.h0 = s.acc;
+  } else {
+    a.h0 = s.hist[c->head];
+    a.h1 = s.hist[(c->head + 2) % 3];
+    a.h2 = s.hist[(c->head + 1) % 3];
+  }
+  return a;
+}
+
+int run_stage(sw_ctx* c, int op, int stage, double2* Slab::*X) {
   const int model = c->cfg.model;
   if (use_fused(c)) {
     if (!c->mixed_valid) {
-      Timer tm(c, K_COLINV);
-      sw::launch_col_inv(model, c->g, c->p, X, c->minv, c->tw_y, c->stream);
+      {
+        Timer tm(c, K_COLINV);
+        for (Slab& s : c->sl) sw::launch_col_inv(model, s.g, c->p, s.*X, s.mic, c->tw_y, c->stream);
+      }
+      if (int rc = transpose(c, true, c->ninv)) return rc;
     }
     {
       Timer tm(c, K_ROW);
-      sw::launch_row(model, c->g, c->p, c->minv, c->mfwd, c->tw_x, c->stream);
+      for (Slab& s : c->sl) sw::launch_row(model, s.g, c->p, s.mir, s.mfr, c->tw_x, c->stream);
     }
-    Timer tm(c, K_COLSTEP);
-    sw::launch_col_step(model, op, c->g, c->p, a, c->mfwd, c->minv, c->tw_y, c->stream);
-    c->mixed_valid = true;  // minv now holds the next stage's inverse transforms
+    if (int rc = transpose(c, false, c->nfwd)) return rc;
+    {
+      Timer tm(c, K_COLSTEP);
+      for (Slab& s : c->sl) {
+        sw::StepPtrs a = step_ptrs(c, s);
+        a.stage = stage;
+        sw::launch_col_step(model, op, s.g, c->p, a, s.mfc, s.mic, c->tw_y, c->stream);
+      }
+    }
+    if (int rc = transpose(c, true, c->ninv)) return rc;
+    c->mixed_valid = true;  // mir now holds the next stage's inverse transforms
   } else {
-    double2* N = (op == sw::OP_RK4) ? c->nbuf : a.h0;
-    calcN(c, X, N);
+    // AB3 steppers: calcN writes straight into this step's history slot, which
+    // the update then overwrites in place (N -> RHS or N); nbuf aliases it
+    if (op != sw::OP_RK4)
+      for (Slab& s : c->sl) s.nbuf = s.hist[c->head];
+    if (int rc = calcN(c, X, &Slab::nbuf)) return rc;
     Timer tm(c, K_UPD);
-    sw::launch_step_elem(c->nf, op, c->g, c->p, a, N, c->xs, c->stream);
+    for (Slab& s : c->sl) {
+      sw::StepPtrs a = step_ptrs(c, s);
+      a.stage = stage;
+      sw::launch_step_elem(c->nf, op, s.g, c->p, a, s.nbuf, s.xs, c->stream);
+    }
     c->mixed_valid = false;
   }
+  return 0;
 }
 
-void step_once(sw_ctx* c) {
+int step_once(sw_ctx* c) {
   const int st = c->cfg.stepper;
-  sw::StepPtrs a{};
-  a.sol = c->sol;
-  a.sol_out = (st == SW_STEP_FILTERED_AB3) ? c->sol2 : c->sol;
-  a.E = c->E;
-  a.E2 = c->E2;
-  a.xs = c->xs;
-  a.euler = c->step < 3 ? 1 : 0;
   if (st == SW_STEP_FILTERED_AB3 || st == SW_STEP_IFMAB3) {
-    a.h0 = c->hist[c->head];
-    a.h1 = c->hist[(c->head + 2) % 3];
-    a.h2 = c->hist[(c->head + 1) % 3];
-    run_stage(c, st == SW_STEP_FILTERED_AB3 ? sw::OP_FAB3 : sw::OP_IFMAB3, a, c->sol);
+    if (int rc = run_stage(c, st == SW_STEP_FILTERED_AB3 ? sw::OP_FAB3 : sw::OP_IFMAB3, 0, &Slab::sol))
+      return rc;
     c->head = (c->head + 1) % 3;  // RHS₋₂ <- RHS₋₁ <- RHS by rotation (utils/IFMAB3.jl:165-166)
-    if (st == SW_STEP_FILTERED_AB3) std::swap(c->sol, c->sol2);
+    if (st == SW_STEP_FILTERED_AB3)
+      for (Slab& s : c->sl) std::swap(s.sol, s.sol2);
   } else {  // IFMRK4
-    a.h0 = c->acc;
-    for (int stage = 1; stage <= 4; ++stage) {
-      a.stage = stage;
-      run_stage(c, sw::OP_RK4, a, stage == 1 ? c->sol : c->xs);
-    }
+    for (int stage = 1; stage <= 4; ++stage)
+      if (int rc = run_stage(c, sw::OP_RK4, stage, stage == 1 ? &Slab::sol : &Slab::xs)) return rc;
   }
   c->t += c->cfg.dt;
   c->step += 1;
+  return 0;
 }
 
-size_t full_bytes(const sw_ctx* c) { return (size_t)c->nf * c->g.nkr * c->g.nl * sizeof(double2); }
+size_t full_bytes(const sw_ctx* c) {
+  const Geom& g = c->sl[0].g;
+  return (size_t)c->nf * g.nkr * g.nl * sizeof(double2);
+}
+
+// columns of the full (nkr, nl) array written by slab q's scatter
+void scatter_cols(const Geom& g, int& lo, int& hi) {
+  lo = std::min(g.kr0, g.nkr);
+  hi = (g.slab == g.nslab - 1) ? g.nkr : std::min(g.kr0 + g.kcl, g.nkr);
+}
+
+// c->stage <- the full (nkr, nl, nf) array of the per-slab compact field set
+int collect_full(sw_ctx* c, double2* Slab::*X) {
+  if (!c->rccl) {
+    for (Slab& s : c->sl) {
+      int lo, hi;
+      scatter_cols(s.g, lo, hi);
+      sw::launch_scatter(c->nf, s.g, lo, hi, s.*X, c->stage, c->stream);
+    }
+    HIPCHK(c, hipGetLastError());
+    return 0;
+  }
+  // RCCL: all-gather every slab's compact fields, padded to kcl columns
+  const Slab& s = c->sl[0];
+  const size_t fpad = (size_t)s.g.kcl * s.g.LrP, slot = (size_t)c->nf * fpad;
+  double2* mine = c->gbuf + (size_t)s.g.slab * slot;
+  for (int f = 0; f < c->nf; ++f)
+    HIPCHK(c, hipMemcpyAsync(mine + f * fpad, s.*X + f * s.g.cfield, s.g.cfield * sizeof(double2),
+                             hipMemcpyDeviceToDevice, c->stream));
+  NCCLCHK(c, ncclAllGather(mine, c->gbuf, 2 * slot, ncclDouble, c->comm, c->stream));
+  for (int q = 0; q < c->P; ++q) {
+    Geom gq = make_geom(c->cfg, c->P, q);
+    gq.cfield = (long long)fpad;
+    int lo, hi;
+    scatter_cols(gq, lo, hi);
+    sw::launch_scatter(c->nf, gq, lo, hi, c->gbuf + (size_t)q * slot, c->stage, c->stream);
+  }
+  HIPCHK(c, hipGetLastError());
+  return 0;
+}
+
+template <typename T>
+int allreduce(sw_ctx* c, T* dev, size_t n, ncclRedOp_t op) {
+  if (!c->rccl) return 0;
+  const ncclDataType_t dt = sizeof(T) == 8 ? ncclDouble : ncclInt32;
+  NCCLCHK(c, ncclAllReduce(dev, dev, n, dt, op, c->comm, c->stream));
+  return 0;
+}
+
+int nan_flag(sw_ctx* c, int& h) {
+  HIPCHK(c, hipMemsetAsync(c->flag, 0, sizeof(int), c->stream));
+  for (Slab& s : c->sl) sw::launch_nan_check(c->nf, s.g, s.sol, c->flag, c->stream);
+  HIPCHK(c, hipGetLastError());
+  if (int rc = allreduce(c, c->flag, 1, ncclMax)) return rc;
+  h = 0;
+  HIPCHK(c, hipMemcpyAsync(&h, c->flag, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+void free_slab(Slab& s) {
+  void* ptrs[] = {s.sol, s.sol2, s.hist[0], s.hist[1], s.hist[2], s.E, s.E2, s.acc, s.xs, s.mic, s.mfr};
+  for (void* q : ptrs)
+    if (q) (void)hipFree(q);
+  if (s.nbuf && s.nbuf != s.hist[0] && s.nbuf != s.hist[1] && s.nbuf != s.hist[2]) (void)hipFree(s.nbuf);
+  if (s.mir && s.mir != s.mic) (void)hipFree(s.mir);
+  if (s.mfc && s.mfc != s.mfr) (void)hipFree(s.mfc);
+}
 
 }  // namespace
 
@@ -267,6 +485,7 @@ void sw_config_default(sw_config* cfg) {
   cfg->check_nan = 1;
   cfg->nranks = 1;
   cfg->rank = 0;
+  cfg->local_slabs = 1;
 }
 
 const char* sw_last_error(const sw_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
@@ -285,8 +504,17 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
     return fail(c, SW_E_INVALID, "nx, ny must be powers of two in [32, 8192]");
   if (!(k.aliased_fraction > 0 && k.aliased_fraction < 1))
     return fail(c, SW_E_INVALID, "aliased_fraction must be in (0,1)");
-  if (k.nranks != 1) return fail(c, SW_E_INVALID, "multi-GPU slab decomposition: use nranks == 1 in this build");
   if (k.filter_order < 0) return fail(c, SW_E_INVALID, "filter_order must be >= 0");
+  const int P = k.nranks;
+  if (!pow2(P) || k.ny / P < 32)
+    return fail(c, SW_E_INVALID, "nranks must be a power of two with ny / nranks >= 32");
+  const int nlocal = k.local_slabs <= 1 ? 1 : k.local_slabs;
+  if (nlocal != 1 && nlocal != P) return fail(c, SW_E_INVALID, "local_slabs must be 1 or nranks");
+  if (P > 1 && nlocal == 1 && (k.rank < 0 || k.rank >= P)) return fail(c, SW_E_INVALID, "bad rank");
+  if (P > 1 && nlocal == 1 && !k.comm_unique_id)
+    return fail(c, SW_E_INVALID, "nranks > 1 with one slab per process needs comm_unique_id");
+  c->P = P;
+  c->rccl = P > 1 && nlocal == 1;
 
   int ndev = 0;
   HIPCHK(c, hipGetDeviceCount(&ndev));
@@ -295,32 +523,18 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   HIPCHK(c, hipEventCreate(&c->ev0));
   HIPCHK(c, hipEventCreate(&c->ev1));
+  if (c->rccl) {
+    ncclUniqueId id;
+    std::memcpy(&id, k.comm_unique_id, sizeof(id));
+    NCCLCHK(c, ncclCommInitRank(&c->comm, P, id, k.rank));
+  }
 
-  Geom& g = c->g;
-  g.nx = k.nx;
-  g.ny = k.ny;
-  g.log2nx = ilog2(k.nx);
-  g.log2ny = ilog2(k.ny);
-  g.nkr = k.nx / 2 + 1;
-  g.nl = k.ny;
-  int iLx, iRx, iLy, iRy;
-  alias_range(k.nx, k.aliased_fraction, iLx, iRx);
-  alias_range(k.ny, k.aliased_fraction, iLy, iRy);
-  g.kc = iLx - 1;
-  g.kcP = (g.kc + 63) / 64 * 64;
-  g.lc = iLy - 1;
-  g.lr2 = iRy;
-  g.Lr = g.lc + (k.ny - g.lr2);
-  g.LrP = (g.Lr + 7) / 8 * 8;
-  g.Lx = k.Lx;
-  g.Ly = k.Ly;
-  g.mk = (2 * M_PI / k.Lx * k.nx) / k.nx;
-  g.ml = (2 * M_PI / k.Ly * k.ny) / k.ny;
-  g.dx = k.Lx / k.nx;
-  g.dy = k.Ly / k.ny;
-  g.cfield = (long long)g.kc * g.LrP;
-  g.mfield = (long long)g.kcP * g.ny;
-  if (g.kc <= 0 || g.Lr <= 0 || g.lc > g.lr2) return fail(c, SW_E_INVALID, "degenerate dealiasing geometry");
+  c->sl.resize(nlocal);
+  for (int i = 0; i < nlocal; ++i) c->sl[i].g = make_geom(k, P, c->rccl ? k.rank : i);
+  {
+    const Geom& g = c->sl[0].g;
+    if (g.kc <= 0 || g.Lr <= 0 || g.lc > g.lr2) return fail(c, SW_E_INVALID, "degenerate dealiasing geometry");
+  }
 
   Phys& p = c->p;
   p.f = k.f;
@@ -340,34 +554,46 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   c->ninv = k.model == SW_MODEL_RSW ? 5 : 6;
   c->nfwd = 4;
 
-  const size_t cb = (size_t)g.cfield * sizeof(double2);
-  const size_t mb = (size_t)g.mfield * sizeof(double2);
   int rc;
-  if ((rc = alloc(c, (void**)&c->sol, c->nf * cb))) return rc;
-  if ((rc = alloc(c, (void**)&c->xs, c->nf * cb))) return rc;
-  if (k.stepper == SW_STEP_FILTERED_AB3)
-    if ((rc = alloc(c, (void**)&c->sol2, c->nf * cb))) return rc;
-  if ((rc = alloc(c, (void**)&c->minv, c->ninv * mb))) return rc;
-  if ((rc = alloc(c, (void**)&c->mfwd, c->nfwd * mb))) return rc;
+  for (Slab& s : c->sl) {
+    const Geom& g = s.g;
+    const size_t cb = (size_t)g.cfield * sizeof(double2);
+    const size_t mb = (size_t)g.mfield * sizeof(double2);
+    if ((rc = alloc(c, (void**)&s.sol, c->nf * cb))) return rc;
+    if ((rc = alloc(c, (void**)&s.xs, c->nf * cb))) return rc;
+    if (k.stepper == SW_STEP_FILTERED_AB3)
+      if ((rc = alloc(c, (void**)&s.sol2, c->nf * cb))) return rc;
+    if ((rc = alloc(c, (void**)&s.mic, c->ninv * mb))) return rc;
+    if ((rc = alloc(c, (void**)&s.mfr, c->nfwd * mb))) return rc;
+    s.mir = s.mic;
+    s.mfc = s.mfr;
+    if (P > 1) {
+      if ((rc = alloc(c, (void**)&s.mir, c->ninv * mb))) return rc;
+      if ((rc = alloc(c, (void**)&s.mfc, c->nfwd * mb))) return rc;
+    }
+    if (k.stepper == SW_STEP_IFMRK4) {
+      if ((rc = alloc(c, (void**)&s.acc, c->nf * cb))) return rc;
+      if ((rc = alloc(c, (void**)&s.nbuf, c->nf * cb))) return rc;
+    } else {
+      for (int i = 0; i < 3; ++i)
+        if ((rc = alloc(c, (void**)&s.hist[i], c->nf * cb))) return rc;
+    }
+    if (k.stepper != SW_STEP_FILTERED_AB3) {
+      const size_t eb = (size_t)c->nf * c->nf * cb;
+      if ((rc = alloc(c, (void**)&s.E, eb))) return rc;
+      if ((rc = alloc(c, (void**)&s.E2, eb))) return rc;
+      // IFMAB3: exp(L dt), exp(2 L dt) (utils/IFMAB3.jl:44-66); IFMRK4: exp(L dt), exp(L dt/2)
+      sw::launch_setup_expm(k.model, g, p, 1.0, s.E, c->stream);
+      sw::launch_setup_expm(k.model, g, p, k.stepper == SW_STEP_IFMAB3 ? 2.0 : 0.5, s.E2, c->stream);
+      HIPCHK(c, hipGetLastError());
+    }
+  }
+  const Geom& g = c->sl[0].g;
   if ((rc = alloc(c, (void**)&c->stage, full_bytes(c)))) return rc;
   if ((rc = alloc(c, (void**)&c->dflt, (size_t)g.nx * g.ny * sizeof(double)))) return rc;
   if ((rc = alloc(c, (void**)&c->flag, 64))) return rc;
-  if (k.stepper == SW_STEP_IFMRK4) {
-    if ((rc = alloc(c, (void**)&c->acc, c->nf * cb))) return rc;
-    if ((rc = alloc(c, (void**)&c->nbuf, c->nf * cb))) return rc;
-  } else {
-    for (int i = 0; i < 3; ++i)
-      if ((rc = alloc(c, (void**)&c->hist[i], c->nf * cb))) return rc;
-  }
-  if (k.stepper != SW_STEP_FILTERED_AB3) {
-    const size_t eb = (size_t)c->nf * c->nf * cb;
-    if ((rc = alloc(c, (void**)&c->E, eb))) return rc;
-    if ((rc = alloc(c, (void**)&c->E2, eb))) return rc;
-    // IFMAB3: exp(L dt), exp(2 L dt) (utils/IFMAB3.jl:44-66); IFMRK4: exp(L dt), exp(L dt/2)
-    sw::launch_setup_expm(k.model, g, p, 1.0, c->E, c->stream);
-    sw::launch_setup_expm(k.model, g, p, k.stepper == SW_STEP_IFMAB3 ? 2.0 : 0.5, c->E2, c->stream);
-    HIPCHK(c, hipGetLastError());
-  }
+  if (c->rccl)
+    if ((rc = alloc(c, (void**)&c->gbuf, (size_t)P * c->nf * g.kcl * g.LrP * sizeof(double2)))) return rc;
   {
     auto tx = twiddles(k.nx);
     HIPCHK(c, hipMalloc((void**)&c->tw_x, tx.size() * sizeof(double2)));
@@ -386,30 +612,33 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
 void sw_destroy(sw_ctx* c) {
   if (!c) return;
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* ptrs[] = {c->tw_x, c->tw_y, c->sol, c->sol2, c->hist[0], c->hist[1], c->hist[2], c->E, c->E2,
-                  c->acc, c->nbuf, c->xs, c->minv, c->mfwd, c->stage, c->dflt, c->flag};
+  for (Slab& s : c->sl) free_slab(s);
+  void* ptrs[] = {c->tw_x, c->tw_y, c->stage, c->gbuf, c->dflt, c->flag};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
+  if (c->comm) (void)ncclCommDestroy(c->comm);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
 
+static bool ready(const sw_ctx* c) { return c && !c->sl.empty() && c->sl[0].sol && c->stage; }
+
 int sw_get_dims(const sw_ctx* c, int32_t* nkr, int32_t* nl, int32_t* nf) {
-  if (!c || !c->sol) return SW_E_STATE;
-  if (nkr) *nkr = c->g.nkr;
-  if (nl) *nl = c->g.nl;
+  if (!ready(c)) return SW_E_STATE;
+  if (nkr) *nkr = c->sl[0].g.nkr;
+  if (nl) *nl = c->sl[0].g.nl;
   if (nf) *nf = c->nf;
   return SW_OK;
 }
 
 int sw_set_state(sw_ctx* c, const void* sol, size_t bytes) {
-  if (!c || !c->sol) return SW_E_STATE;
+  if (!ready(c)) return SW_E_STATE;
   if (!sol || bytes != full_bytes(c)) return fail(c, SW_E_INVALID, "sw_set_state: size mismatch");
   HIPCHK(c, hipSetDevice(c->cfg.device));
   HIPCHK(c, hipMemcpyAsync(c->stage, sol, bytes, hipMemcpyHostToDevice, c->stream));
-  sw::launch_gather(c->nf, c->g, c->stage, c->sol, c->stream);
+  for (Slab& s : c->sl) sw::launch_gather(c->nf, s.g, c->stage, s.sol, c->stream);
   c->mixed_valid = false;
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -418,11 +647,10 @@ int sw_set_state(sw_ctx* c, const void* sol, size_t bytes) {
 
 int sw_get_state(const sw_ctx* cc, void* sol, size_t bytes) {
   sw_ctx* c = const_cast<sw_ctx*>(cc);
-  if (!c || !c->sol) return SW_E_STATE;
+  if (!ready(c)) return SW_E_STATE;
   if (!sol || bytes != full_bytes(c)) return fail(c, SW_E_INVALID, "sw_get_state: size mismatch");
   HIPCHK(c, hipSetDevice(c->cfg.device));
-  sw::launch_scatter(c->nf, c->g, c->sol, c->stage, c->stream);
-  HIPCHK(c, hipGetLastError());
+  if (int rc = collect_full(c, &Slab::sol)) return rc;
   HIPCHK(c, hipMemcpyAsync(sol, c->stage, bytes, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return SW_OK;
@@ -444,17 +672,15 @@ int sw_get_clock(const sw_ctx* c, double* t, int64_t* step) {
 }
 
 int sw_step(sw_ctx* c, int64_t nsteps) {
-  if (!c || !c->sol) return SW_E_STATE;
+  if (!ready(c)) return SW_E_STATE;
   if (nsteps < 0) return fail(c, SW_E_INVALID, "negative nsteps");
   HIPCHK(c, hipSetDevice(c->cfg.device));
-  for (int64_t i = 0; i < nsteps; ++i) step_once(c);
+  for (int64_t i = 0; i < nsteps; ++i)
+    if (int rc = step_once(c)) return rc;
   HIPCHK(c, hipGetLastError());
   if (c->cfg.check_nan && nsteps > 0) {
-    HIPCHK(c, hipMemsetAsync(c->flag, 0, sizeof(int), c->stream));
-    sw::launch_nan_check(c->nf, c->g, c->sol, c->flag, c->stream);
     int h = 0;
-    HIPCHK(c, hipMemcpyAsync(&h, c->flag, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (int rc = nan_flag(c, h)) return rc;
     if (h) return fail(c, SW_E_NAN, "Solution is NaN");
   } else {
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -463,25 +689,27 @@ int sw_step(sw_ctx* c, int64_t nsteps) {
 }
 
 int sw_calcN(sw_ctx* c, const void* sol, void* N, size_t bytes) {
-  if (!c || !c->sol) return SW_E_STATE;
+  if (!ready(c)) return SW_E_STATE;
   if (!sol || !N || bytes != full_bytes(c)) return fail(c, SW_E_INVALID, "sw_calcN: size mismatch");
   HIPCHK(c, hipSetDevice(c->cfg.device));
-  double2* out = c->cfg.stepper == SW_STEP_IFMRK4 ? c->nbuf : c->hist[c->head];
-  c->mixed_valid = false;  // minv / mfwd are used as scratch
+  c->mixed_valid = false;  // mixed arrays are used as scratch
   HIPCHK(c, hipMemcpyAsync(c->stage, sol, bytes, hipMemcpyHostToDevice, c->stream));
-  sw::launch_gather(c->nf, c->g, c->stage, c->xs, c->stream);
-  // scratch output: use the ring slot that the next step overwrites anyway
-  calcN(c, c->xs, out);
-  sw::launch_scatter(c->nf, c->g, out, c->stage, c->stream);
-  HIPCHK(c, hipGetLastError());
+  for (Slab& s : c->sl) {
+    sw::launch_gather(c->nf, s.g, c->stage, s.xs, c->stream);
+    // scratch output: the ring slot that the next step overwrites anyway
+    if (c->cfg.stepper != SW_STEP_IFMRK4) s.nbuf = s.hist[c->head];
+  }
+  if (int rc = calcN(c, &Slab::xs, &Slab::nbuf)) return rc;
+  if (int rc = collect_full(c, &Slab::nbuf)) return rc;
   HIPCHK(c, hipMemcpyAsync(N, c->stage, bytes, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return SW_OK;
 }
 
 int sw_get_physical(sw_ctx* c, int32_t fid, double* out, size_t bytes) {
-  if (!c || !c->sol) return SW_E_STATE;
-  if (!out || bytes != (size_t)c->g.nx * c->g.ny * sizeof(double))
+  if (!ready(c)) return SW_E_STATE;
+  const Geom& g0 = c->sl[0].g;
+  if (!out || bytes != (size_t)g0.nx * g0.ny * sizeof(double))
     return fail(c, SW_E_INVALID, "sw_get_physical: size mismatch");
   const int id = fid & 7, layer = fid >> 3;
   if (c->cfg.model == SW_MODEL_RSW) {
@@ -490,35 +718,41 @@ int sw_get_physical(sw_ctx* c, int32_t fid, double* out, size_t bytes) {
     if (layer > 1 || id == SW_PHYS_ETA || id > 5) return fail(c, SW_E_INVALID, "bad QG2 physical id");
   }
   HIPCHK(c, hipSetDevice(c->cfg.device));
-  c->mixed_valid = false;  // minv is used as scratch
-  sw::launch_make_spec(c->cfg.model, fid, c->g, c->p, c->sol, c->xs, c->stream);
-  sw::launch_col_inv1(c->g, c->xs, c->minv, c->tw_y, c->stream);
-  sw::launch_row_c2r1(c->g, c->minv, c->dflt, c->tw_x, c->stream);
+  c->mixed_valid = false;  // mixed arrays are used as scratch
+  for (Slab& s : c->sl) {
+    sw::launch_make_spec(c->cfg.model, fid, s.g, c->p, s.sol, s.xs, c->stream);
+    sw::launch_col_inv1(s.g, s.xs, s.mic, c->tw_y, c->stream);
+  }
+  if (int rc = transpose(c, true, 1)) return rc;
+  for (Slab& s : c->sl) sw::launch_row_c2r1(s.g, s.mir, c->dflt, c->tw_x, c->stream);
   HIPCHK(c, hipGetLastError());
+  if (c->rccl) {
+    const size_t rows = (size_t)g0.nyl * g0.nx;
+    NCCLCHK(c, ncclAllGather(c->dflt + (size_t)g0.y0 * g0.nx, c->dflt, rows, ncclDouble, c->comm, c->stream));
+  }
   HIPCHK(c, hipMemcpyAsync(out, c->dflt, bytes, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return SW_OK;
 }
 
 int sw_diag(sw_ctx* c, int32_t id, double* out) {
-  if (!c || !c->sol || !out) return SW_E_STATE;
+  if (!ready(c) || !out) return SW_E_STATE;
   HIPCHK(c, hipSetDevice(c->cfg.device));
   if (id == SW_DIAG_NAN) {
-    HIPCHK(c, hipMemsetAsync(c->flag, 0, sizeof(int), c->stream));
-    sw::launch_nan_check(c->nf, c->g, c->sol, c->flag, c->stream);
     int h = 0;
-    HIPCHK(c, hipMemcpyAsync(&h, c->flag, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (int rc = nan_flag(c, h)) return rc;
     *out = h ? 1.0 : 0.0;
     return SW_OK;
   }
   if (id != SW_DIAG_KE && id != SW_DIAG_PE) return fail(c, SW_E_INVALID, "unknown diagnostic");
   HIPCHK(c, hipMemsetAsync(c->dflt, 0, 2 * sizeof(double), c->stream));
-  sw::launch_energy(c->cfg.model, c->g, c->p, c->sol, c->dflt, c->stream);
+  for (Slab& s : c->sl) sw::launch_energy(c->cfg.model, s.g, c->p, s.sol, c->dflt, c->stream);
+  HIPCHK(c, hipGetLastError());
+  if (int rc = allreduce(c, c->dflt, 2, ncclSum)) return rc;
   double acc[2] = {0, 0};
   HIPCHK(c, hipMemcpyAsync(acc, c->dflt, sizeof(acc), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  const Geom& g = c->g;
+  const Geom& g = c->sl[0].g;
   const double norm = g.Lx * g.Ly / ((double)g.nx * g.nx * (double)g.ny * g.ny);  // parsevalsum2
   if (c->cfg.model == SW_MODEL_RSW) {
     // rsw/RotatingShallowWater.jl:323-331
@@ -533,15 +767,17 @@ int sw_diag(sw_ctx* c, int32_t id, double* out) {
 }
 
 int sw_profile_steps(sw_ctx* c, int64_t nsteps, sw_kernel_stat* out, int32_t max_stats, int32_t* n_stats) {
-  if (!c || !c->sol) return SW_E_STATE;
+  if (!ready(c)) return SW_E_STATE;
   HIPCHK(c, hipSetDevice(c->cfg.device));
   for (auto& s : c->stats) {
     s.launches = 0;
     s.ms = 0.0;
   }
   c->prof = true;
-  for (int64_t i = 0; i < nsteps; ++i) step_once(c);
+  int rc = 0;
+  for (int64_t i = 0; i < nsteps && !rc; ++i) rc = step_once(c);
   c->prof = false;
+  if (rc) return rc;
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
   int n = 0;
@@ -550,7 +786,8 @@ int sw_profile_steps(sw_ctx* c, int64_t nsteps, sw_kernel_stat* out, int32_t max
     std::snprintf(out[n].name, sizeof(out[n].name), "%s", c->stats[i].name);
     out[n].launches = c->stats[i].launches;
     out[n].avg_ms = c->stats[i].ms / c->stats[i].launches;
-    out[n].alg_bytes = kernel_bytes(c, i);
+    // one transpose stat = one direction; kernel_bytes(K_XCHG) counts both
+    out[n].alg_bytes = i == K_XCHG ? kernel_bytes(c, i) / 2 : kernel_bytes(c, i);
     ++n;
   }
   if (n_stats) *n_stats = n;
@@ -558,7 +795,7 @@ int sw_profile_steps(sw_ctx* c, int64_t nsteps, sw_kernel_stat* out, int32_t max
 }
 
 double sw_step_alg_bytes(const sw_ctx* c) {
-  if (!c) return 0.0;
+  if (!ready(c)) return 0.0;
   const int nstage = c->cfg.stepper == SW_STEP_IFMRK4 ? 4 : 1;
   if (!use_fused(c))
     return nstage * (kernel_bytes(c, K_COLINV) + kernel_bytes(c, K_ROW) + kernel_bytes(c, K_COLFWD) +
@@ -568,7 +805,11 @@ double sw_step_alg_bytes(const sw_ctx* c) {
 
 int sw_comm_unique_id(void* out128) {
   if (!out128) return SW_E_INVALID;
-  return SW_E_INVALID;  // RCCL slab decomposition lands in a later build
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return SW_E_COMM;
+  std::memcpy(out128, &id, sizeof(id));
+  return SW_OK;
 }
 
 }  // extern "C"

@@ -13,18 +13,32 @@ namespace sw {
 enum { MODEL_RSW = 0, MODEL_QG2 = 1 };
 enum { ST_FAB3 = 0, ST_IFMAB3 = 1, ST_IFMRK4 = 2 };
 
-// Grid geometry in the layouts of DESIGN.md §2.
-//  compact spectral field: [kr][j], kr < kc, j < Lr live rows, column stride LrP
-//  mixed (x-spectral / y-physical) field: [kr/8][y][kr%8], kr < kcP
+// Grid geometry of one slab in the layouts of DESIGN.md §2 and §6.
+// Slab s of P owns kr columns [kr0, kr0 + kcl) in the column passes and
+// physical rows [y0, y0 + nyl) in the row pass (P = 1: kr0 = y0 = 0,
+// kcl = roundup(kc, 64), nyl = ny).
+//  compact spectral field: [krl][j], krl < kcn live local columns, j < Lr live
+//    rows, column stride LrP
+//  mixed field, column phase (local column krl, any y):
+//    [y / nyl][krl / 8][y % nyl][krl % 8]             -> midc()
+//  mixed field, row phase (any global column kr < P*kcl, local row yl):
+//    [kr / 8][yl][kr % 8]                             -> midx()
+//  Block q of the column-phase array (rows of slab q) is exactly the block
+//  slab q holds for this slab's columns in its row-phase array, so the
+//  transpose between the passes is a plain all-to-all of contiguous blocks.
 struct Geom {
   int nx, ny, log2nx, log2ny;
   int nkr, nl;
-  int kc, kcP;        // live kr columns [0, kc); padded to kcP (multiple of 64)
+  int kc;             // global live kr columns [0, kc)
   int lc, lr2, Lr, LrP;  // live l rows [0, lc) ∪ [lr2, ny); count Lr; stride LrP
   double mk, ml;      // kr = i*mk, l = (signed j)*ml
   double dx, dy, Lx, Ly;
-  long long cfield;   // elements per compact field  = kc*LrP
-  long long mfield;   // elements per mixed field    = kcP*ny
+  // slab decomposition
+  int nslab, slab;    // P, this slab
+  int kr0, kcn, kcl, ntl;  // first global column, live local columns, local columns (multiple of 8), kcl/8
+  int y0, nyl, log2nyl;    // first row, local rows
+  long long cfield;   // elements per compact field  = max(kcn,1)*LrP
+  long long mfield;   // elements per mixed field    = kcl*ny = (P*kcl)*nyl
 };
 
 struct Phys {
@@ -44,9 +58,14 @@ __host__ __device__ inline int compact_of(const Geom& g, int m) {
 __host__ __device__ inline double lwav(const Geom& g, int m) {
   return (double)(m < (g.ny >> 1) ? m : m - g.ny) * g.ml;
 }
-// element offset inside one mixed field (< 2^31 for nx, ny <= 8192)
-__host__ __device__ inline int midx(const Geom& g, int kr, int y) {
-  return ((kr >> 3) * g.ny + y) * 8 + (kr & 7);
+// element offsets inside one mixed field (< 2^31 for nx, ny <= 8192)
+// row phase: global column kr, local row yl
+__host__ __device__ inline int midx(const Geom& g, int kr, int yl) {
+  return ((kr >> 3) * g.nyl + yl) * 8 + (kr & 7);
+}
+// column phase: local column krl, global row y
+__host__ __device__ inline int midc(const Geom& g, int krl, int y) {
+  return (((y >> g.log2nyl) * g.ntl + (krl >> 3)) * g.nyl + (y & (g.nyl - 1))) * 8 + (krl & 7);
 }
 
 // integer power x^n (n >= 0) by repeated squaring
@@ -256,7 +275,8 @@ void launch_step_elem(int nf, int op, const Geom& g, const Phys& p, const StepPt
 void launch_setup_expm(int model, const Geom& g, const Phys& p, double factor, double2* E,
                        hipStream_t s);
 void launch_gather(int nf, const Geom& g, const double2* full, double2* compact, hipStream_t s);
-void launch_scatter(int nf, const Geom& g, const double2* compact, double2* full, hipStream_t s);
+void launch_scatter(int nf, const Geom& g, int lo, int hi, const double2* compact, double2* full,
+                    hipStream_t s);
 void launch_nan_check(int nf, const Geom& g, const double2* compact, int* flag, hipStream_t s);
 void launch_make_spec(int model, int field_id, const Geom& g, const Phys& p, const double2* sol,
                       double2* out, hipStream_t s);

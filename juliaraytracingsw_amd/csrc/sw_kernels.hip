@@ -34,7 +34,8 @@ __device__ __forceinline__ int col_of_block(int b, int nb) {
 template <int LOG2N>
 struct Blk {
   static constexpr int NT = FftPlan<LOG2N>::NT;
-  // at most 32 lines, so that NB divides ny (>= 32) and kcP (multiple of 64)
+  // at most 32 lines, so that NB divides the local rows (>= 32) and the local
+  // columns (a multiple of NB)
   static constexpr int NB = NT >= 256 ? 1 : (256 / NT > 32 ? 32 : 256 / NT);
   static constexpr int THREADS = NB * NT;
 };
@@ -68,27 +69,28 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   constexpr int NT = B::NT;
   extern __shared__ double2 smem[];
   const LineCtx c = line_ctx<LOG2N>();
-  const int kr = (B::NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * B::NB + c.ln;
+  const int krl = (B::NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * B::NB + c.ln;
   const int grp = blockIdx.y;
+  const bool live = krl < g.kcn;
+  if (B::NB == 1 && !live) return;  // padding column: nobody reads it
   double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
   Twiddles<LOG2N> tws;
   tws.load(c.t, tw);
-  const bool live = kr < g.kc;
   const double scale = 1.0 / ((double)g.nx * (double)g.ny);
-  const double k = kr * g.mk;
+  const double k = (g.kr0 + krl) * g.mk;
   double2 v[8];
 
   auto store = [&](int o) {  // fft_line leaves Y[t + s*NT] in v[s]
     if (live) {
       double2* Mo = M + (long long)o * g.mfield;
 #pragma unroll
-      for (int s = 0; s < 8; ++s) Mo[midx(g, kr, c.t + s * NT)] = v[s];
+      for (int s = 0; s < 8; ++s) Mo[midc(g, krl, c.t + s * NT)] = v[s];
     }
   };
 
   // loads are unconditional from a clamped in-bounds address, then selected:
   // a branch around each load would serialise them (one vmcnt(0) per element)
-  const int krc = live ? kr : g.kc - 1;
+  const int krc = live ? krl : 0;
   if constexpr (MODEL == MODEL_RSW) {
     const double2* Xf = X + (long long)grp * g.cfield + (long long)krc * g.LrP;
     double2 x[8];
@@ -296,20 +298,22 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   constexpr int NT = B::NT;
   extern __shared__ double2 smem[];
   const LineCtx c = line_ctx<LOG2N>();
-  const int kr = (B::NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * B::NB + c.ln;
+  const int krl = (B::NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * B::NB + c.ln;
   const int grp = blockIdx.y;
+  const bool live = krl < g.kcn;
+  if (B::NB == 1 && !live) return;
+  const int krA = krl < g.kcl ? krl : g.kcl - 1;  // in-bounds address
   double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
   Twiddles<LOG2N> tws;
   tws.load(c.t, tw);
-  const bool live = kr < g.kc;
-  const double k = kr * g.mk;
+  const double k = (g.kr0 + krl) * g.mk;
   const long long MF = g.mfield;
   double2 v[8], acc[8];
 
   auto load_col = [&](const double2* Mfield) {
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      const double2 t = Mfield[midx(g, kr, c.t + s * NT)];  // kr < kcP: always in bounds
+      const double2 t = Mfield[midc(g, krA, c.t + s * NT)];
       v[s] = live ? t : zero2();
     }
   };
@@ -348,7 +352,7 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     }
   }
   if (live) {
-    double2* Nf = N + (long long)grp * g.cfield + (long long)kr * g.LrP;
+    double2* Nf = N + (long long)grp * g.cfield + (long long)krl * g.LrP;
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       const int j = compact_of(g, c.t + s * NT);
@@ -361,10 +365,12 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
 // stepper updates: per-mode operations shared by the elementwise kernels and
 // the fused column kernel (identical arithmetic on both paths)
 // ===========================================================================
+// compact index i -> global column kr, live row j; false for padding
 __device__ __forceinline__ bool mode_of(const Geom& g, long long i, int& kr, int& j) {
-  kr = (int)(i / g.LrP);
-  j = (int)(i - (long long)kr * g.LrP);
-  return kr < g.kc && j < g.Lr;
+  const int krl = (int)(i / g.LrP);
+  j = (int)(i - (long long)krl * g.LrP);
+  kr = g.kr0 + krl;
+  return krl < g.kcn && j < g.Lr;
 }
 
 template <int NF>
@@ -596,19 +602,21 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   constexpr int NF = MODEL == MODEL_RSW ? 3 : 2;
   extern __shared__ double2 smem[];
   const LineCtx c = line_ctx<LOG2N>();
-  const int kr = (B::NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * B::NB + c.ln;
+  const int krl = (B::NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * B::NB + c.ln;
+  const bool live = krl < g.kcn;
+  if (B::NB == 1 && !live) return;
+  const int krA = krl < g.kcl ? krl : g.kcl - 1;
   double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
   Twiddles<LOG2N> tws;
   tws.load(c.t, tw);
-  const bool live = kr < g.kc;
-  const double k = kr * g.mk;
+  const double k = (g.kr0 + krl) * g.mk;
   const long long MF = g.mfield;
   double2 v[8];
 
   auto load_col = [&](const double2* Mfield) {
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      const double2 t = Mfield[midx(g, kr, c.t + s * NT)];  // kr < kcP: in bounds
+      const double2 t = Mfield[midc(g, krA, c.t + s * NT)];
       v[s] = live ? t : zero2();
     }
   };
@@ -654,7 +662,7 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
         const int m = c.t + s * NT;
         const int j = compact_of(g, m);
         if (live && j >= 0) {
-          const long long i = (long long)kr * g.LrP + j;
+          const long long i = (long long)krl * g.LrP + j;
           const cplx nf = cx(n[s].x, n[s].y);
           if (f == 0) op_fab3_field<NF, 0>(g, p, a, i, k, lwav(g, m), nf);
           else if (f == 1) op_fab3_field<NF, 1>(g, p, a, i, k, lwav(g, m), nf);
@@ -678,7 +686,7 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
         cplx n[NF], x[NF];
 #pragma unroll
         for (int f = 0; f < NF; ++f) n[f] = cx(X[f][s].x, X[f][s].y);
-        const long long i = (long long)kr * g.LrP + j;
+        const long long i = (long long)krl * g.LrP + j;
         step_op<NF, OP>(g, p, a, i, k, lwav(g, m), n, x);
         if (OP == OP_RK4 && a.stage < 4) store_vec<NF>(a.xs, g.cfield, i, x);
       }
@@ -686,7 +694,7 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     }
   }
   const double2* Xs = (OP == OP_RK4 && a.stage < 4) ? a.xs : a.sol_out;
-  const double2* Xc = Xs + (long long)(live ? kr : g.kc - 1) * g.LrP;
+  const double2* Xc = Xs + (long long)(live ? krl : 0) * g.LrP;
   auto load_x = [&](int f, double2 (&x)[8]) {
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
@@ -702,7 +710,7 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     if (live) {
       double2* Mo = Minv + (long long)o * MF;
 #pragma unroll
-      for (int s = 0; s < 8; ++s) Mo[midx(g, kr, c.t + s * NT)] = v[s];
+      for (int s = 0; s < 8; ++s) Mo[midc(g, krl, c.t + s * NT)] = v[s];
     }
   };
   if constexpr (MODEL == MODEL_RSW) {
@@ -771,32 +779,34 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   constexpr int NT = B::NT;
   extern __shared__ double2 smem[];
   const LineCtx c = line_ctx<LOG2N>();
-  int kr, f;
-  if (B::NB == 1) {
-    // 1-D grid of 3*kcP blocks.  The 3 fields of the 8 columns that share each
-    // 128-B chunk of the mixed layout (24 blocks) sit on one XCD label
-    // (b % 8) within 192 consecutive block ids: they meet in one L2, where the
-    // other fields' reads of the old state and the chunk writes coalesce
-    // (speed only; any placement is correct).
+  int krl, f;
+  if (B::NB == 1 && gridDim.y == 1) {
+    // 1-D grid of 3*kcl blocks (kcl a multiple of 64).  The 3 fields of the 8
+    // columns that share each 128-B chunk of the mixed layout (24 blocks) sit
+    // on one XCD label (b % 8) within 192 consecutive block ids: they meet in
+    // one L2, where the other fields' reads of the old state and the chunk
+    // writes coalesce (speed only; any placement is correct).
     const int b = blockIdx.x, q = b / 192, r = b - q * 192, x = r & 7, jj = r >> 3;
     f = jj % 3;
-    kr = q * 64 + x * 8 + jj / 3;
+    krl = q * 64 + x * 8 + jj / 3;
   } else {
-    kr = blockIdx.x * B::NB + c.ln;
+    krl = blockIdx.x * B::NB + c.ln;
     f = blockIdx.y;
   }
+  const bool live = krl < g.kcn;
+  if (B::NB == 1 && !live) return;
+  const int krA = krl < g.kcl ? krl : g.kcl - 1;
   double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
   Twiddles<LOG2N> tws;
   tws.load(c.t, tw);
-  const bool live = kr < g.kc;
-  const double k = kr * g.mk;
+  const double k = (g.kr0 + krl) * g.mk;
   const long long MF = g.mfield;
   double2 v[8], n[8];
 
   auto load_col = [&](const double2* Mfield) {
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      const double2 t = Mfield[midx(g, kr, c.t + s * NT)];  // kr < kcP: in bounds
+      const double2 t = Mfield[midc(g, krA, c.t + s * NT)];
       v[s] = live ? t : zero2();
     }
   };
@@ -819,7 +829,7 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     const int j = compact_of(g, m);
     x[s] = zero2();
     if (live && j >= 0) {
-      const long long i = (long long)kr * g.LrP + j;
+      const long long i = (long long)krl * g.LrP + j;
       const cplx nf = cx(n[s].x, n[s].y);
       cplx r;
       if (f == 0) r = op_fab3_field<3, 0>(g, p, a, i, k, lwav(g, m), nf);
@@ -834,7 +844,7 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     if (live) {
       double2* Mo = Minv + (long long)o * MF;
 #pragma unroll
-      for (int s = 0; s < 8; ++s) Mo[midx(g, kr, c.t + s * NT)] = v[s];
+      for (int s = 0; s < 8; ++s) Mo[midc(g, krl, c.t + s * NT)] = v[s];
     }
   };
 #pragma unroll
@@ -873,28 +883,32 @@ __global__ void k_setup_expm(Geom g, Phys p, double factor, double2* __restrict_
 // ===========================================================================
 // state I/O: Julia column-major (nkr, nl, nf) <-> compact live columns
 // ===========================================================================
+// this slab's live columns [kr0, kr0 + kcn) of the full array
 __global__ void k_gather(Geom g, int nf, const double2* __restrict__ full, double2* __restrict__ cmp) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long per = (long long)g.kc * g.Lr;
+  const long long per = (long long)g.kcn * g.Lr;
   if (i >= per * nf) return;
   const int f = (int)(i / per);
   const long long r = i - f * per;
-  const int j = (int)(r / g.kc), kr = (int)(r - (long long)j * g.kc);
+  const int j = (int)(r / g.kcn), krl = (int)(r - (long long)j * g.kcn);
   const int m = lrow_of(g, j);
-  cmp[f * g.cfield + (long long)kr * g.LrP + j] = full[((long long)f * g.nl + m) * g.nkr + kr];
+  cmp[f * g.cfield + (long long)krl * g.LrP + j] = full[((long long)f * g.nl + m) * g.nkr + g.kr0 + krl];
 }
 
-__global__ void k_scatter(Geom g, int nf, const double2* __restrict__ cmp, double2* __restrict__ full) {
+// columns [lo, hi) of the full array from this slab (zero outside live modes)
+__global__ void k_scatter(Geom g, int nf, int lo, int hi, const double2* __restrict__ cmp,
+                          double2* __restrict__ full) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long per = (long long)g.nkr * g.nl;
+  const int w = hi - lo;
+  const long long per = (long long)w * g.nl;
   if (i >= per * nf) return;
   const int f = (int)(i / per);
   const long long r = i - f * per;
-  const int m = (int)(r / g.nkr), kr = (int)(r - (long long)m * g.nkr);
-  const int j = compact_of(g, m);
+  const int m = (int)(r / w), kr = lo + (int)(r - (long long)m * w);
+  const int j = compact_of(g, m), krl = kr - g.kr0;
   double2 v = zero2();
-  if (kr < g.kc && j >= 0) v = cmp[f * g.cfield + (long long)kr * g.LrP + j];
-  full[i] = v;
+  if (krl >= 0 && krl < g.kcn && j >= 0) v = cmp[f * g.cfield + (long long)krl * g.LrP + j];
+  full[((long long)f * g.nl + m) * g.nkr + kr] = v;
 }
 
 __global__ void k_nan_check(Geom g, int nf, const double2* __restrict__ cmp, int* flag) {
@@ -961,13 +975,14 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   constexpr int NT = B::NT;
   extern __shared__ double2 smem[];
   const LineCtx c = line_ctx<LOG2N>();
-  const int kr = blockIdx.x * B::NB + c.ln;
+  const int krl = blockIdx.x * B::NB + c.ln;
+  const bool live = krl < g.kcn;
+  if (B::NB == 1 && !live) return;
   double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
   Twiddles<LOG2N> tws;
   tws.load(c.t, tw);
-  const bool live = kr < g.kc;
   const double scale = 1.0 / ((double)g.nx * (double)g.ny);
-  const double2* Xf = X + (long long)(live ? kr : g.kc - 1) * g.LrP;
+  const double2* Xf = X + (long long)(live ? krl : 0) * g.LrP;
   double2 v[8];
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
@@ -978,7 +993,7 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   fft_line<LOG2N, +1>(v, c.t, tws, line);
   if (live) {
 #pragma unroll
-    for (int s = 0; s < 8; ++s) M[midx(g, kr, c.t + s * NT)] = v[s];
+    for (int s = 0; s < 8; ++s) M[midc(g, krl, c.t + s * NT)] = v[s];
   }
 }
 
@@ -998,7 +1013,7 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   load_pair<LOG2N>(v, c.t, g, M, nullptr, y, false);
   fft_line<LOG2N, +1>(v, c.t, tws, line);
 #pragma unroll
-  for (int s = 0; s < 8; ++s) out[(long long)y * g.nx + c.t + s * NT] = v[s].x;
+  for (int s = 0; s < 8; ++s) out[(long long)(g.y0 + y) * g.nx + c.t + s * NT] = v[s].x;
 }
 
 // Energies by Parseval over live modes (FF parsevalsum2 / parsevalsum:
@@ -1063,11 +1078,11 @@ static void dispatch_log2(int log2n, Args&&... args) {
 
 template <int L>
 static int col_blocks(const Geom& g) {
-  return (g.kcP + Blk<L>::NB - 1) / Blk<L>::NB;
+  return (g.kcl + Blk<L>::NB - 1) / Blk<L>::NB;
 }
 template <int L>
 static int row_blocks(const Geom& g) {
-  return g.ny / Blk<L>::NB;
+  return g.nyl / Blk<L>::NB;
 }
 template <int L>
 static size_t lds_bytes() {
@@ -1144,7 +1159,8 @@ struct ColStepL {
     if (model == MODEL_RSW) {
       if (op == OP_FAB3)
         hipLaunchKernelGGL((k_col_step_fab3_rsw<L>),
-                           Blk<L>::NB == 1 ? dim3(3 * col_blocks<L>(g)) : dim3(col_blocks<L>(g), 3), blk, sh,
+                           (Blk<L>::NB == 1 && g.kcl % 64 == 0) ? dim3(3 * g.kcl) : dim3(col_blocks<L>(g), 3),
+                           blk, sh,
                            s, g, p, a, Mf, Minv, tw);
       else if (op == OP_IFMAB3) SW_CS(MODEL_RSW, OP_IFMAB3);
       else SW_CS(MODEL_RSW, OP_RK4);
@@ -1186,13 +1202,15 @@ void launch_setup_expm(int model, const Geom& g, const Phys& p, double factor, d
 }
 
 void launch_gather(int nf, const Geom& g, const double2* full, double2* cmp, hipStream_t s) {
-  const long long n = (long long)g.kc * g.Lr * nf;
+  const long long n = (long long)g.kcn * g.Lr * nf;
+  if (n == 0) return;
   hipLaunchKernelGGL(k_gather, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g, nf, full, cmp);
 }
 
-void launch_scatter(int nf, const Geom& g, const double2* cmp, double2* full, hipStream_t s) {
-  const long long n = (long long)g.nkr * g.nl * nf;
-  hipLaunchKernelGGL(k_scatter, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g, nf, cmp, full);
+void launch_scatter(int nf, const Geom& g, int lo, int hi, const double2* cmp, double2* full, hipStream_t s) {
+  const long long n = (long long)(hi - lo) * g.nl * nf;
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_scatter, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g, nf, lo, hi, cmp, full);
 }
 
 void launch_nan_check(int nf, const Geom& g, const double2* cmp, int* flag, hipStream_t s) {

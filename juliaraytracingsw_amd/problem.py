@@ -6,6 +6,8 @@ reference's (``prob.sol``, ``prob.clock``, ``stepforward!(prob, n)`` …).
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import numpy as np
 
 from . import _lib
@@ -35,7 +37,8 @@ class Problem:
 
     def __init__(self, model, *, nx, ny, Lx, Ly, dt, aliased_fraction, stepper, params,
                  use_filter=False, filter_kw=None, device=0, check_nan=True, T=np.float64,
-                 nop_calcN=False, unfused=False):
+                 nop_calcN=False, unfused=False, nranks=1, rank=0, local_slabs=1,
+                 comm_unique_id=None):
         if np.dtype(T) != np.float64:
             raise _lib.LibSWError("this build computes in fp64 (T=Float64) only")
         if stepper not in _lib.STEPPERS:
@@ -63,6 +66,14 @@ class Problem:
         cfg.check_nan = 1 if check_nan else 0
         cfg.nop_calcN = 1 if nop_calcN else 0
         cfg.unfused = 1 if unfused else 0
+        # slab decomposition: nranks slabs; local_slabs == nranks
+        # holds them all on this GPU, else this process holds slab `rank` and
+        # transposes over RCCL with the broadcast comm_unique_id bytes
+        cfg.nranks, cfg.rank, cfg.local_slabs = int(nranks), int(rank), int(local_slabs)
+        self._uid = None
+        if comm_unique_id is not None:
+            self._uid = C.create_string_buffer(bytes(comm_unique_id), 128)
+            cfg.comm_unique_id = C.cast(self._uid, C.c_void_p)
         self.ctx = _lib.Context(cfg)
         self.model = model
         self.stepper = stepper

@@ -15,7 +15,7 @@ from .problem import Problem as _Problem, stepforward  # noqa: F401
 def Problem(dev="gpu", *, nx=128, ny=None, Lx=2 * np.pi, Ly=None, U=0.5, mu=1e-2, nu=1e-6, nnu=4,
             f0=3.0, Cg=1.0, drhorho0=0.2, stepper="IFMAB3", dt=5e-2, aliased_fraction=1 / 3,
             T=np.float64, use_filter=False, device=0, check_nan=True, nop_calcN=False, unfused=False,
-            **stepper_kwargs):
+            decomposition=None, **stepper_kwargs):
     """``TwoLayerQG.Problem(dev; nx, ny, Lx, Ly, U, μ, ν, nν, f0, Cg, δρρ0, stepper,
     dt, aliased_fraction, T, use_filter, stepper_kwargs...)`` (:55-90).
 
@@ -31,7 +31,8 @@ def Problem(dev="gpu", *, nx=128, ny=None, Lx=2 * np.pi, Ly=None, U=0.5, mu=1e-2
     prob = _Problem(_lib.SW_MODEL_QG2, nx=nx, ny=ny, Lx=Lx, Ly=Ly, dt=dt,
                     aliased_fraction=aliased_fraction, stepper=stepper, params=params,
                     use_filter=use_filter, filter_kw=stepper_kwargs, device=device,
-                    check_nan=check_nan, T=T, nop_calcN=nop_calcN, unfused=unfused)
+                    check_nan=check_nan, T=T, nop_calcN=nop_calcN, unfused=unfused,
+                    **(decomposition or {}))
     return prob
 
 
