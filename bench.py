@@ -3,11 +3,17 @@
 metric) on N MI355X, plus the roofline of the dominant kernel and the CPU
 baseline (the oracle restatement, scipy.fft on the host cores).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode ensemble|slab]
 
-N > 1 is launched by torch.distributed.run, one process per GPU.  Each rank
-steps its own 2048² problem (replicas, weak scaling) until the slab
-decomposition lands; value = all ranks' steps / max-over-ranks time.
+N > 1 is launched by torch.distributed.run, one process per GPU.
+  --mode ensemble (default): every rank steps its own independent 2048²
+      problem (an ensemble of seeded runs, the reference's job-array usage);
+      no collective on the data path; value = all ranks' steps / max-over-ranks
+      time; scaling "weak".
+  --mode slab: ONE problem slab-decomposed over the N GPUs, transposes as RCCL
+      all-to-alls; value = that problem's steps / time; scaling
+      "strong".  Meant for the large configurations (4096², 8192²): at 2048²
+      the transposes cost more than the step.
 """
 import argparse
 import json
@@ -66,6 +72,7 @@ def main():
     ap.add_argument("--stepper", default="FilteredAB3", choices=["FilteredAB3", "IFMAB3", "IFMRK4"])
     ap.add_argument("--profile-steps", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mode", default="ensemble", choices=["ensemble", "slab"])
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_rsw2048_fab3.json"))
     args = ap.parse_args()
 
@@ -88,12 +95,14 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    from juliaraytracingsw_amd import drivers
+    from juliaraytracingsw_amd import drivers, slab_comm
 
+    slab = args.mode == "slab" and world > 1
+    dec = slab_comm.rccl_decomposition(rank, world) if slab else None
     if args.model == "rsw":
-        prob, P = drivers.rsw_problem(args.n, args.stepper, device=local)
+        prob, P = drivers.rsw_problem(args.n, args.stepper, device=local, decomposition=dec)
     else:
-        prob, P = drivers.qg2_problem(args.n, args.stepper, device=local)
+        prob, P = drivers.qg2_problem(args.n, args.stepper, device=local, decomposition=dec)
 
     prob.stepforward(args.warmup)
     barrier_sync()
@@ -132,7 +141,7 @@ def main():
               file=sys.stderr)
 
     ms_per_step = elapsed / args.steps * 1e3
-    value = world * args.steps / elapsed
+    value = (1 if slab else world) * args.steps / elapsed
     balg = b_alg(args.model, args.stepper, args.n)
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
@@ -146,15 +155,16 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if slab else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic random-phase IC (set_shafer_initial_condition!, seeded)" if args.model == "rsw"
                 else "synthetic randn PV IC (set_seed_initial_condition!, seeded)",
         "config": {"workload": f"{args.model.upper()} {args.n}^2 {args.stepper} fp64 step, dt={P['dt']:.6g}",
-                   "grid": args.n, "parallelism": "replicas" if world > 1 else "single-gpu"},
+                   "grid": args.n,
+                   "parallelism": (f"slab{world}" if slab else f"ensemble{world}") if world > 1 else "single-gpu"},
         "b_alg_bytes_per_step": balg,
-        "b_alg_GBps": balg * value / world / 1e9,
+        "b_alg_GBps": balg * value / world / 1e9,  # per GPU
         "b_alg_frac_of_peak": balg * value / world / 1e9 / HBM_PEAK_GBPS,
         "libsw_alg_bytes_per_step": step_alg,
         "roofline": {"bound": "hbm", "kernel": dom["name"], "achieved": achieved, "peak": HBM_PEAK_GBPS,

@@ -67,6 +67,17 @@ extern "C" {
 #define SW_DIAG_KE    1  /* RSW: kinetic_energy; QG2: KE layer 1 + layer 2 */
 #define SW_DIAG_PE    2  /* potential_energy                              */
 
+/* Host-staged transport (optional, one slab per process).  When set, libsw
+ * moves every inter-slab exchange through host memory and calls
+ *     exchange(user, send, recv, block_bytes, nranks)
+ * instead of RCCL: `send` holds nranks contiguous blocks of block_bytes, block
+ * q destined for rank q; on return block p of `recv` must hold the block rank
+ * p sent to this rank (an all-to-all, e.g. MPI_Alltoall or a gloo
+ * all_to_all).  Return 0 on success.  Used where RCCL cannot run (several
+ * ranks on one GPU, CPU interconnect tests); results are bitwise identical. */
+typedef int (*sw_exchange_fn)(void* user, const void* send, void* recv, size_t block_bytes,
+                              int32_t nranks);
+
 typedef struct sw_config {
   int32_t abi_version;      /* must be SW_ABI_VERSION                      */
   int32_t model;            /* SW_MODEL_*                                  */
@@ -102,6 +113,8 @@ typedef struct sw_config {
    * nranks must be a power of two with ny / nranks >= 32.                 */
   int32_t nranks, rank, local_slabs;
   const void* comm_unique_id; /* ncclUniqueId bytes (128), from sw_comm_unique_id */
+  sw_exchange_fn exchange;    /* optional host-staged transport instead of RCCL */
+  void* exchange_user;
 } sw_config;
 
 typedef struct sw_ctx sw_ctx;

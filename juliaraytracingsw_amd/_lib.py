@@ -35,6 +35,10 @@ class LibSWError(RuntimeError):
         self.code = code
 
 
+# int exchange(void* user, const void* send, void* recv, size_t block_bytes, int32_t nranks)
+EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int32)
+
+
 class SwConfig(C.Structure):
     _fields_ = [
         ("abi_version", C.c_int32), ("model", C.c_int32), ("stepper", C.c_int32),
@@ -47,6 +51,7 @@ class SwConfig(C.Structure):
         ("device", C.c_int32), ("check_nan", C.c_int32), ("nop_calcN", C.c_int32), ("unfused", C.c_int32),
         ("nranks", C.c_int32), ("rank", C.c_int32), ("local_slabs", C.c_int32),
         ("comm_unique_id", C.c_void_p),
+        ("exchange", EXCHANGE_FN), ("exchange_user", C.c_void_p),
     ]
 
 

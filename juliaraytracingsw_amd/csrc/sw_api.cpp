@@ -48,8 +48,11 @@ struct sw_ctx {
   Phys p{};
   int nf = 0, ninv = 0, nfwd = 0;
   int P = 1;                                 // slabs in the decomposition
-  bool rccl = false;                         // one slab per process, RCCL transposes
-  ncclComm_t comm = nullptr;
+  bool dist = false;                         // one slab per process (P > 1)
+  bool hostx = false;                        // dist with the host-staged exchange hook
+  ncclComm_t comm = nullptr;                 // dist without the hook: RCCL
+  char *hsend = nullptr, *hrecv = nullptr;   // pinned staging of the host-staged exchange
+  size_t hbytes = 0;
   hipStream_t stream = nullptr;
   double2 *tw_x = nullptr, *tw_y = nullptr;
   std::vector<Slab> sl;                      // slabs held by this process
@@ -57,7 +60,7 @@ struct sw_ctx {
   bool mixed_valid = false;                  // mir == transposed col_inv(sol) (fused pipeline primed)
   bool fuse_all = false;                     // SW_FUSE_ALL=1: fused pass for every pair (experiments)
   double2* stage = nullptr;                  // full (nkr,nl,nf) staging
-  double2* gbuf = nullptr;                   // RCCL: all-gathered compact slabs
+  double2* gbuf = nullptr;                   // dist: all-gathered compact slabs
   double* dflt = nullptr;                    // physical staging / reductions
   int* flag = nullptr;
   double t = 0.0;
@@ -241,7 +244,7 @@ int transpose(sw_ctx* c, bool inv, int nfields) {
   const Geom& g0 = c->sl[0].g;
   const size_t blk = (size_t)g0.kcl * g0.nyl;  // elements per (slab pair, field)
   const long long MF = g0.mfield;
-  if (!c->rccl) {
+  if (!c->dist) {
     for (int o = 0; o < nfields; ++o)
       for (int p = 0; p < c->P; ++p)
         for (int q = 0; q < c->P; ++q) {
@@ -253,6 +256,22 @@ int transpose(sw_ctx* c, bool inv, int nfields) {
   }
   const Slab& s = c->sl[0];
   const int me = g0.slab;
+  if (c->hostx) {
+    // stage [q][field][block] so block q of every field is one contiguous
+    // message for rank q (one 2-D copy per field each way)
+    const size_t fb = blk * sizeof(double2), rowb = nfields * fb;
+    if (rowb * c->P > c->hbytes) return fail(c, SW_E_INVALID, "exchange staging too small");
+    for (int o = 0; o < nfields; ++o)
+      HIPCHK(c, hipMemcpy2DAsync(c->hsend + o * fb, rowb, (inv ? s.mic : s.mfr) + o * MF, fb, fb, c->P,
+                                 hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->cfg.exchange(c->cfg.exchange_user, c->hsend, c->hrecv, rowb, c->P) != 0)
+      return fail(c, SW_E_COMM, "exchange hook failed");
+    for (int o = 0; o < nfields; ++o)
+      HIPCHK(c, hipMemcpy2DAsync((inv ? s.mir : s.mfc) + o * MF, fb, c->hrecv + o * fb, rowb, fb, c->P,
+                                 hipMemcpyHostToDevice, c->stream));
+    return 0;
+  }
   NCCLCHK(c, ncclGroupStart());
   for (int o = 0; o < nfields; ++o) {
     const double2* src = (inv ? s.mic : s.mfr) + o * MF;
@@ -398,9 +417,26 @@ void scatter_cols(const Geom& g, int& lo, int& hi) {
   hi = (g.slab == g.nslab - 1) ? g.nkr : std::min(g.kr0 + g.kcl, g.nkr);
 }
 
+// dist: every rank's `bytes` at `mine` -> dst[rank * bytes] on every rank
+// (in place allowed: mine == dst + rank * bytes)
+int allgather(sw_ctx* c, const void* mine, void* dst, size_t bytes) {
+  if (!c->hostx) {
+    NCCLCHK(c, ncclAllGather(mine, dst, bytes, ncclUint8, c->comm, c->stream));
+    return 0;
+  }
+  if (bytes * c->P > c->hbytes) return fail(c, SW_E_INVALID, "exchange staging too small");
+  HIPCHK(c, hipMemcpyAsync(c->hsend, mine, bytes, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (int q = 1; q < c->P; ++q) std::memcpy(c->hsend + q * bytes, c->hsend, bytes);
+  if (c->cfg.exchange(c->cfg.exchange_user, c->hsend, c->hrecv, bytes, c->P) != 0)
+    return fail(c, SW_E_COMM, "exchange hook failed");
+  HIPCHK(c, hipMemcpyAsync(dst, c->hrecv, bytes * c->P, hipMemcpyHostToDevice, c->stream));
+  return 0;
+}
+
 // c->stage <- the full (nkr, nl, nf) array of the per-slab compact field set
 int collect_full(sw_ctx* c, double2* Slab::*X) {
-  if (!c->rccl) {
+  if (!c->dist) {
     for (Slab& s : c->sl) {
       int lo, hi;
       scatter_cols(s.g, lo, hi);
@@ -416,7 +452,7 @@ int collect_full(sw_ctx* c, double2* Slab::*X) {
   for (int f = 0; f < c->nf; ++f)
     HIPCHK(c, hipMemcpyAsync(mine + f * fpad, s.*X + f * s.g.cfield, s.g.cfield * sizeof(double2),
                              hipMemcpyDeviceToDevice, c->stream));
-  NCCLCHK(c, ncclAllGather(mine, c->gbuf, 2 * slot, ncclDouble, c->comm, c->stream));
+  if (int rc = allgather(c, mine, c->gbuf, slot * sizeof(double2))) return rc;
   for (int q = 0; q < c->P; ++q) {
     Geom gq = make_geom(c->cfg, c->P, q);
     gq.cfield = (long long)fpad;
@@ -428,22 +464,19 @@ int collect_full(sw_ctx* c, double2* Slab::*X) {
   return 0;
 }
 
-template <typename T>
-int allreduce(sw_ctx* c, T* dev, size_t n, ncclRedOp_t op) {
-  if (!c->rccl) return 0;
-  const ncclDataType_t dt = sizeof(T) == 8 ? ncclDouble : ncclInt32;
-  NCCLCHK(c, ncclAllReduce(dev, dev, n, dt, op, c->comm, c->stream));
-  return 0;
-}
-
 int nan_flag(sw_ctx* c, int& h) {
   HIPCHK(c, hipMemsetAsync(c->flag, 0, sizeof(int), c->stream));
   for (Slab& s : c->sl) sw::launch_nan_check(c->nf, s.g, s.sol, c->flag, c->stream);
   HIPCHK(c, hipGetLastError());
-  if (int rc = allreduce(c, c->flag, 1, ncclMax)) return rc;
-  h = 0;
-  HIPCHK(c, hipMemcpyAsync(&h, c->flag, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  int all[64] = {0};
+  const int n = c->dist ? c->P : 1;
+  if (c->dist)
+    if (int rc = allgather(c, c->flag, c->flag + 1, sizeof(int))) return rc;
+  HIPCHK(c, hipMemcpyAsync(all, c->dist ? c->flag + 1 : c->flag, n * sizeof(int), hipMemcpyDeviceToHost,
+                           c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  h = 0;
+  for (int i = 0; i < n; ++i) h |= all[i];
   return 0;
 }
 
@@ -511,10 +544,11 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   const int nlocal = k.local_slabs <= 1 ? 1 : k.local_slabs;
   if (nlocal != 1 && nlocal != P) return fail(c, SW_E_INVALID, "local_slabs must be 1 or nranks");
   if (P > 1 && nlocal == 1 && (k.rank < 0 || k.rank >= P)) return fail(c, SW_E_INVALID, "bad rank");
-  if (P > 1 && nlocal == 1 && !k.comm_unique_id)
-    return fail(c, SW_E_INVALID, "nranks > 1 with one slab per process needs comm_unique_id");
+  if (P > 1 && nlocal == 1 && !k.comm_unique_id && !k.exchange)
+    return fail(c, SW_E_INVALID, "nranks > 1 with one slab per process needs comm_unique_id or exchange");
   c->P = P;
-  c->rccl = P > 1 && nlocal == 1;
+  c->dist = P > 1 && nlocal == 1;
+  c->hostx = c->dist && k.exchange;
 
   int ndev = 0;
   HIPCHK(c, hipGetDeviceCount(&ndev));
@@ -523,14 +557,14 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   HIPCHK(c, hipEventCreate(&c->ev0));
   HIPCHK(c, hipEventCreate(&c->ev1));
-  if (c->rccl) {
+  if (c->dist && !c->hostx) {
     ncclUniqueId id;
     std::memcpy(&id, k.comm_unique_id, sizeof(id));
     NCCLCHK(c, ncclCommInitRank(&c->comm, P, id, k.rank));
   }
 
   c->sl.resize(nlocal);
-  for (int i = 0; i < nlocal; ++i) c->sl[i].g = make_geom(k, P, c->rccl ? k.rank : i);
+  for (int i = 0; i < nlocal; ++i) c->sl[i].g = make_geom(k, P, c->dist ? k.rank : i);
   {
     const Geom& g = c->sl[0].g;
     if (g.kc <= 0 || g.Lr <= 0 || g.lc > g.lr2) return fail(c, SW_E_INVALID, "degenerate dealiasing geometry");
@@ -591,9 +625,19 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   const Geom& g = c->sl[0].g;
   if ((rc = alloc(c, (void**)&c->stage, full_bytes(c)))) return rc;
   if ((rc = alloc(c, (void**)&c->dflt, (size_t)g.nx * g.ny * sizeof(double)))) return rc;
-  if ((rc = alloc(c, (void**)&c->flag, 64))) return rc;
-  if (c->rccl)
-    if ((rc = alloc(c, (void**)&c->gbuf, (size_t)P * c->nf * g.kcl * g.LrP * sizeof(double2)))) return rc;
+  if ((rc = alloc(c, (void**)&c->flag, 64 * sizeof(int)))) return rc;
+  if (c->dist) {
+    const size_t gb = (size_t)P * c->nf * g.kcl * g.LrP * sizeof(double2);
+    if ((rc = alloc(c, (void**)&c->gbuf, gb))) return rc;
+    if (c->hostx) {
+      // largest message set: a transpose, the compact all-gather or the physical rows
+      const size_t tb = (size_t)std::max(c->ninv, c->nfwd) * (size_t)g.mfield * sizeof(double2);
+      const size_t pb = (size_t)g.nx * g.ny * sizeof(double);
+      c->hbytes = std::max(tb, std::max(gb, pb));
+      HIPCHK(c, hipHostMalloc((void**)&c->hsend, c->hbytes, hipHostMallocDefault));
+      HIPCHK(c, hipHostMalloc((void**)&c->hrecv, c->hbytes, hipHostMallocDefault));
+    }
+  }
   {
     auto tx = twiddles(k.nx);
     HIPCHK(c, hipMalloc((void**)&c->tw_x, tx.size() * sizeof(double2)));
@@ -617,6 +661,8 @@ void sw_destroy(sw_ctx* c) {
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   if (c->comm) (void)ncclCommDestroy(c->comm);
+  if (c->hsend) (void)hipHostFree(c->hsend);
+  if (c->hrecv) (void)hipHostFree(c->hrecv);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -726,9 +772,9 @@ int sw_get_physical(sw_ctx* c, int32_t fid, double* out, size_t bytes) {
   if (int rc = transpose(c, true, 1)) return rc;
   for (Slab& s : c->sl) sw::launch_row_c2r1(s.g, s.mir, c->dflt, c->tw_x, c->stream);
   HIPCHK(c, hipGetLastError());
-  if (c->rccl) {
+  if (c->dist) {
     const size_t rows = (size_t)g0.nyl * g0.nx;
-    NCCLCHK(c, ncclAllGather(c->dflt + (size_t)g0.y0 * g0.nx, c->dflt, rows, ncclDouble, c->comm, c->stream));
+    if (int rc = allgather(c, c->dflt + (size_t)g0.y0 * g0.nx, c->dflt, rows * sizeof(double))) return rc;
   }
   HIPCHK(c, hipMemcpyAsync(out, c->dflt, bytes, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -748,10 +794,19 @@ int sw_diag(sw_ctx* c, int32_t id, double* out) {
   HIPCHK(c, hipMemsetAsync(c->dflt, 0, 2 * sizeof(double), c->stream));
   for (Slab& s : c->sl) sw::launch_energy(c->cfg.model, s.g, c->p, s.sol, c->dflt, c->stream);
   HIPCHK(c, hipGetLastError());
-  if (int rc = allreduce(c, c->dflt, 2, ncclSum)) return rc;
-  double acc[2] = {0, 0};
-  HIPCHK(c, hipMemcpyAsync(acc, c->dflt, sizeof(acc), hipMemcpyDeviceToHost, c->stream));
+  // per-rank partial sums, added in rank order on every rank
+  std::vector<double> part(2 * (size_t)c->P, 0.0);
+  const int nparts = c->dist ? c->P : 1;
+  if (c->dist)
+    if (int rc = allgather(c, c->dflt, c->dflt + 2, 2 * sizeof(double))) return rc;
+  HIPCHK(c, hipMemcpyAsync(part.data(), c->dflt + (c->dist ? 2 : 0), 2 * nparts * sizeof(double),
+                           hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  double acc[2] = {0, 0};
+  for (int i = 0; i < nparts; ++i) {
+    acc[0] += part[2 * i];
+    acc[1] += part[2 * i + 1];
+  }
   const Geom& g = c->sl[0].g;
   const double norm = g.Lx * g.Ly / ((double)g.nx * g.nx * (double)g.ny * g.ny);  // parsevalsum2
   if (c->cfg.model == SW_MODEL_RSW) {

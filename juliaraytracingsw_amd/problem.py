@@ -38,7 +38,7 @@ class Problem:
     def __init__(self, model, *, nx, ny, Lx, Ly, dt, aliased_fraction, stepper, params,
                  use_filter=False, filter_kw=None, device=0, check_nan=True, T=np.float64,
                  nop_calcN=False, unfused=False, nranks=1, rank=0, local_slabs=1,
-                 comm_unique_id=None):
+                 comm_unique_id=None, exchange=None):
         if np.dtype(T) != np.float64:
             raise _lib.LibSWError("this build computes in fp64 (T=Float64) only")
         if stepper not in _lib.STEPPERS:
@@ -74,6 +74,9 @@ class Problem:
         if comm_unique_id is not None:
             self._uid = C.create_string_buffer(bytes(comm_unique_id), 128)
             cfg.comm_unique_id = C.cast(self._uid, C.c_void_p)
+        self._xchg = exchange  # keep the callback alive as long as the context
+        if exchange is not None:
+            cfg.exchange = exchange
         self.ctx = _lib.Context(cfg)
         self.model = model
         self.stepper = stepper

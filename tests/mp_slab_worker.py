@@ -1,0 +1,69 @@
+"""Worker for tests/test_gpu_multiprocess.py (launched by torch.distributed.run).
+
+Every rank holds one slab of the problem in its own process and its own libsw
+context on the same GPU; the transposes go through the host-staged transport
+hook over gloo (RCCL refuses several ranks on one GPU).  Rank 0 also runs the
+undecomposed problem and checks the gathered state, calcN, physical fields
+and energies against it."""
+import argparse
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.dirname(HERE), HERE, os.path.join(os.path.dirname(HERE), "oracle")]
+
+import numpy as np  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--case", default="rsw_fab3")
+    ap.add_argument("--n", type=int, default=128)
+    ap.add_argument("--steps", type=int, default=6)
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    import sw_cases
+    import sw_oracle as O
+    from juliaraytracingsw_amd import rotating_shallow_water as RSW, slab_comm, two_layer_qg as QG2
+
+    M = RSW if a.case.startswith("rsw") else QG2
+    p = sw_cases.case_params(a.case, a.n)
+    grid = O.TwoDGrid(a.n)
+    ic = sw_cases.initial_condition(p, grid)
+    prob = sw_cases.libsw_problem(p, decomposition=slab_comm.host_decomposition(rank, world))
+    prob.sol = ic
+    N = prob.calcN(ic)
+    prob.stepforward(a.steps)
+    sol = prob.sol
+    phys = M.updatevars(prob)
+    ke, pe = M.kinetic_energy(prob), M.potential_energy(prob)
+    res = {}
+    if rank == 0:
+        ref = sw_cases.libsw_problem(p)
+        ref.sol = ic
+        Nr = ref.calcN(ic)
+        ref.stepforward(a.steps)
+        pr = M.updatevars(ref)
+        res = dict(
+            state_equal=bool(np.array_equal(sol, ref.sol)),
+            calcN_equal=bool(np.array_equal(N, Nr)),
+            physical_equal=bool(all(np.array_equal(phys[k], pr[k]) for k in pr)),
+            ke_rel=abs(ke / M.kinetic_energy(ref) - 1),
+            pe_rel=abs(pe / M.potential_energy(ref) - 1),
+            world=world,
+        )
+        ref.close()
+    prob.close()
+    dist.barrier()
+    if rank == 0:
+        with open(a.out, "w") as f:
+            json.dump(res, f)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

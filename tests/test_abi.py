@@ -59,6 +59,7 @@ def test_config_struct_layout(lib_path):
     assert cfg.abi_version == _lib.SW_ABI_VERSION
     assert cfg.filter_innerK == 0.65 and cfg.filter_outerK == 1.0 and cfg.filter_tol == 1e-15
     assert cfg.nranks == 1 and cfg.check_nan == 1 and cfg.nop_calcN == 0
+    assert cfg.rank == 0 and cfg.local_slabs == 1 and not cfg.comm_unique_id and not cfg.exchange
     assert ctypes.sizeof(_lib.SwConfig) % 8 == 0
 
 
