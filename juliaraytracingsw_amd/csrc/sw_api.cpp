@@ -585,8 +585,10 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   p.decay = -std::log(k.filter_tol) / std::pow(k.filter_outerK - k.filter_innerK, (double)k.filter_order);
 
   c->nf = k.model == SW_MODEL_RSW ? 3 : 2;
-  c->ninv = k.model == SW_MODEL_RSW ? 5 : 6;
-  c->nfwd = 4;
+  // mixed fields per calcN: RSW U,V,H,Uy in / P,K,ζu,Q,vη out;
+  // QG2 Q,Ψ,Ψy per layer in / ψx q, ψy q per layer out
+  c->ninv = k.model == SW_MODEL_RSW ? 4 : 6;
+  c->nfwd = k.model == SW_MODEL_RSW ? 5 : 4;
 
   int rc;
   for (Slab& s : c->sl) {

@@ -28,6 +28,9 @@ __device__ __forceinline__ int col_of_block(int b, int nb) {
 #define SW_MINW_FFT 2
 #endif
 #define SW_MINW(L) (Blk<L>::THREADS >= 1024 ? 4 : SW_MINW_FFT)
+#ifndef SW_MINW_ROW
+#define SW_MINW_ROW 2
+#endif
 
 // threads per block: one line of NT = N/8 threads, or several short lines
 // packed into 256 threads
@@ -57,7 +60,8 @@ __device__ __forceinline__ double2 zero2() { return make_double2(0.0, 0.0); }
 // ===========================================================================
 // col_inv: for column kr, build the y-spectra the row pass needs, inverse FFT
 // along y (scaled by 1/(nx ny), FF's normalised c2r), store to mixed space.
-//   RSW  outputs (rsw/RotatingShallowWater.jl:147-214): 0 U, 1 V, 2 H, 3 Uy=il U, 4 Vy=il V
+//   RSW  outputs (rsw/RotatingShallowWater.jl:147-214): 0 U, 1 V, 2 H, 3 Uy=il U
+//        (the row pass forms ζ̂ = ik V - Uy itself: ik is constant along a row)
 //   QG2  outputs (swqg/TwoLayerQG.jl:155-176):          0 Q1, 1 Q2, 2 Ψ1, 3 Ψ2, 4 Ψy1, 5 Ψy2
 // grid: (columns, groups); RSW group f reads field f; QG2 group = layer.
 // ===========================================================================
@@ -104,11 +108,11 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     }
     fft_line<LOG2N, +1>(v, c.t, tws, line);
     store(grp);
-    if (grp < 2) {  // ∂y: Uy, Vy
+    if (grp == 0) {  // ∂y u: Uy
 #pragma unroll
       for (int s = 0; s < 8; ++s) v[s] = cmul_i(x[s], lwav(g, c.t + s * NT) * scale);
       fft_line<LOG2N, +1>(v, c.t, tws, line);
-      store(3 + grp);
+      store(3);
     }
   } else {
     // streamfunctionfrompv! (swqg/TwoLayerQG.jl:101-111)
@@ -191,12 +195,47 @@ __device__ __forceinline__ void load_pair(double2 (&v)[8], int t, const Geom& g,
   }
 }
 
-// After a forward FFT of z = a + i b (Z[t + s*NT] in v), write Â[k], B̂[k]
-// for k < kc.  Needs Z[nx-k] from a mirror thread: one LDS round trip.
+// RSW second inverse pair: a = Ĥ, b = ζ̂ = ik V̂ - Uy (x-spectral, per element)
 template <int LOG2N>
-__device__ __forceinline__ void store_pair(const double2 (&v)[8], int t, const Geom& g,
-                                           double2* line, double2* __restrict__ A,
-                                           double2* __restrict__ B, int y) {
+__device__ __forceinline__ void load_eta_zeta(double2 (&v)[8], int t, const Geom& g,
+                                              const double2* __restrict__ H,
+                                              const double2* __restrict__ V,
+                                              const double2* __restrict__ Uy, int y) {
+  constexpr int N = 1 << LOG2N, NT = N / 8, half = N / 2;
+  double2 h[8], vv[8], uy[8];
+  int kk[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const int m = t + s * NT;
+    kk[s] = m <= half ? m : N - m;
+    const int o = midx(g, kk[s] < g.kc ? kk[s] : 0, y);
+    h[s] = H[o];
+    vv[s] = V[o];
+    uy[s] = Uy[o];
+  }
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const int m = t + s * NT;
+    double2 aa = h[s], bb = csub(cmul_i(vv[s], kk[s] * g.mk), uy[s]);
+    if (kk[s] == 0) {
+      aa.y = 0.0;
+      bb.y = 0.0;
+    }
+    if (m > half) {
+      aa = cconj(aa);
+      bb = cconj(bb);
+    }
+    const double2 z = make_double2(aa.x - bb.y, aa.y + bb.x);
+    v[s] = kk[s] < g.kc ? z : zero2();
+  }
+}
+
+// After a forward FFT of z = a + i b (Z[t + s*NT] in v), hand Â[k], B̂[k] for
+// k < kc to emit(k, Â, B̂).  Needs Z[nx-k] from a mirror thread: one LDS
+// round trip.
+template <int LOG2N, typename Emit>
+__device__ __forceinline__ void split_pair(const double2 (&v)[8], int t, const Geom& g,
+                                           double2* line, Emit emit) {
   constexpr int N = 1 << LOG2N, NT = N / 8;
   lds_barrier();  // previous LDS readers are done
 #pragma unroll
@@ -208,16 +247,26 @@ __device__ __forceinline__ void store_pair(const double2 (&v)[8], int t, const G
     if (k < g.kc) {
       const double2 zk = v[s];
       const double2 zn = line[LP((N - k) & (N - 1))];
-      const int o = midx(g, k, y);
-      A[o] = make_double2(0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y));
-      // (zk - conj zn) / (2i)
-      B[o] = make_double2(0.5 * (zk.y + zn.y), -0.5 * (zk.x - zn.x));
+      // A = (zk + conj zn) / 2,  B = (zk - conj zn) / (2i)
+      emit(k, make_double2(0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y)),
+           make_double2(0.5 * (zk.y + zn.y), -0.5 * (zk.x - zn.x)));
     }
   }
 }
 
+template <int LOG2N>
+__device__ __forceinline__ void store_pair(const double2 (&v)[8], int t, const Geom& g,
+                                           double2* line, double2* __restrict__ A,
+                                           double2* __restrict__ B, int y) {
+  split_pair<LOG2N>(v, t, g, line, [&](int k, double2 a, double2 b) {
+    const int o = midx(g, k, y);
+    A[o] = a;
+    B[o] = b;
+  });
+}
+
 template <int MODEL, int LOG2N>
-__global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
+__global__ void __launch_bounds__(Blk<LOG2N>::THREADS, Blk<LOG2N>::THREADS >= 1024 ? 4 : SW_MINW_ROW)
     k_row(Geom g, Phys p, const double2* __restrict__ Mi, double2* __restrict__ Mo,
           const double2* __restrict__ tw) {
   using Bk = Blk<LOG2N>;
@@ -231,33 +280,58 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   double2 v[8];
 
   if constexpr (MODEL == MODEL_RSW) {
-    const double2 *U = Mi, *V = Mi + MF, *H = Mi + 2 * MF, *Uy = Mi + 3 * MF, *Vy = Mi + 4 * MF;
-    double2 uv[8], ab[8];
+    // rsw/RotatingShallowWater.jl:140-230 in vorticity form:
+    //   u ux + v uy = ∂x K - ζ v,  u vx + v vy = ∂y K + ζ u,
+    //   K = (u² + v²)/2, ζ = vx - uy.
+    // Both sides agree exactly on the live (2/3-rule) modes, where every
+    // product's aliases vanish.  Outputs (x-spectral, k < kc):
+    //   0 P = -ik K̂ + (ζv)^   -> N_u = F_y(P)
+    //   1 K̂, 2 (ζu)^          -> N_v = -il F_y(K̂) - F_y((ζu)^)
+    //   3 Q = -ik (uη)^, 4 (vη)^ -> N_η = F_y(Q) - il F_y((vη)^)
+    const double2 *U = Mi, *V = Mi + MF, *H = Mi + 2 * MF, *Uy = Mi + 3 * MF;
+    double2 uv[8];
     // u + i v   (fft_line leaves z[x = t + s*NT] in v[s])
     load_pair<LOG2N>(v, c.t, g, U, V, y, false);
     fft_line<LOG2N, +1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) uv[s] = v[s];
-    // ux + i vx:  A = u ux, B = u vx   (:172, :204)
-    load_pair<LOG2N>(v, c.t, g, U, V, y, true);
+    // η + i ζ
+    load_eta_zeta<LOG2N>(v, c.t, g, H, V, Uy, y);
     fft_line<LOG2N, +1>(v, c.t, tws, line);
+    double2 pb[8];
+    double pc[8];
 #pragma unroll
-    for (int s = 0; s < 8; ++s) ab[s] = make_double2(uv[s].x * v[s].x, uv[s].x * v[s].y);
-    // uy + i vy:  A += v uy, B += v vy   (:181, :195)
-    load_pair<LOG2N>(v, c.t, g, Uy, Vy, y, false);
-    fft_line<LOG2N, +1>(v, c.t, tws, line);
-#pragma unroll
-    for (int s = 0; s < 8; ++s)
-      v[s] = make_double2(ab[s].x + uv[s].y * v[s].x, ab[s].y + uv[s].y * v[s].y);
+    for (int s = 0; s < 8; ++s) {
+      const double u = uv[s].x, w = uv[s].y, eta = v[s].x, zeta = v[s].y;
+      pb[s] = make_double2(zeta * u, u * eta);
+      pc[s] = w * eta;
+      v[s] = make_double2(0.5 * (u * u + w * w), zeta * w);
+    }
+    // K + i ζv
     fft_line<LOG2N, -1>(v, c.t, tws, line);
-    store_pair<LOG2N>(v, c.t, g, line, Mo, Mo + MF, y);
-    // η:  C = u η, D = v η   (:218, :224)
-    load_pair<LOG2N>(v, c.t, g, H, nullptr, y, false);
-    fft_line<LOG2N, +1>(v, c.t, tws, line);
+    split_pair<LOG2N>(v, c.t, g, line, [&](int k, double2 a, double2 b) {
+      const int o = midx(g, k, y);
+      Mo[o] = cadd(cmul_i(a, -(k * g.mk)), b);
+      Mo[MF + o] = a;
+    });
+    // ζu + i uη
 #pragma unroll
-    for (int s = 0; s < 8; ++s) v[s] = make_double2(uv[s].x * v[s].x, uv[s].y * v[s].x);
+    for (int s = 0; s < 8; ++s) v[s] = pb[s];
     fft_line<LOG2N, -1>(v, c.t, tws, line);
-    store_pair<LOG2N>(v, c.t, g, line, Mo + 2 * MF, Mo + 3 * MF, y);
+    split_pair<LOG2N>(v, c.t, g, line, [&](int k, double2 a, double2 b) {
+      const int o = midx(g, k, y);
+      Mo[2 * MF + o] = a;
+      Mo[3 * MF + o] = cmul_i(b, -(k * g.mk));
+    });
+    // vη (real input: the transform is the spectrum itself)
+#pragma unroll
+    for (int s = 0; s < 8; ++s) v[s] = make_double2(pc[s], 0.0);
+    fft_line<LOG2N, -1>(v, c.t, tws, line);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int k = c.t + s * Bk::NT;
+      if (k < g.kc) Mo[4 * MF + midx(g, k, y)] = v[s];
+    }
   } else {
     const double2 *Q1 = Mi, *Q2 = Mi + MF, *P1 = Mi + 2 * MF, *P2 = Mi + 3 * MF,
                   *Py1 = Mi + 4 * MF, *Py2 = Mi + 5 * MF;
@@ -286,10 +360,36 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
 
 // ===========================================================================
 // col_fwd: forward FFT along y of the row outputs, combine into N (live rows).
-//   RSW (rsw/RotatingShallowWater.jl:174-226):
-//     N0 = -F(A), N1 = -F(B), N2 = -ik F(C) - il F(D)
+// N_f is the sum of at most two forward y-transforms of row outputs, each
+// with a per-mode multiplier (nterms):
+//   RSW (rsw/RotatingShallowWater.jl:174-226, vorticity form of k_row):
+//     N_u = F(P),  N_v = -il F(K̂) - F((ζu)^),  N_η = F(Q) - il F((vη)^)
 //   QG2 (swqg/TwoLayerQG.jl:171,179): N_l = -il F(A_l) + ik F(B_l)
 // ===========================================================================
+enum { MUL_ONE = 0, MUL_NEG, MUL_NIK, MUL_NIL, MUL_PIK };
+struct NTerms {
+  int fa, ma, fb, mb;  // fb < 0: one term
+};
+template <int MODEL>
+__device__ __forceinline__ NTerms nterms(int f) {
+  if constexpr (MODEL == MODEL_RSW) {
+    if (f == 0) return NTerms{0, MUL_ONE, -1, MUL_ONE};
+    if (f == 1) return NTerms{1, MUL_NIL, 2, MUL_NEG};
+    return NTerms{3, MUL_ONE, 4, MUL_NIL};
+  } else {
+    return NTerms{f, MUL_NIL, 2 + f, MUL_PIK};
+  }
+}
+__device__ __forceinline__ double2 apply_mul(double2 a, int mul, double k, double l) {
+  switch (mul) {
+    case MUL_ONE: return a;
+    case MUL_NEG: return make_double2(-a.x, -a.y);
+    case MUL_NIK: return cmul_i(a, -k);
+    case MUL_NIL: return cmul_i(a, -l);
+    default: return cmul_i(a, k);
+  }
+}
+
 template <int MODEL, int LOG2N>
 __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     k_col_fwd(Geom g, Phys p, const double2* __restrict__ Mf, double2* __restrict__ N,
@@ -318,38 +418,17 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     }
   };
 
-  int fa, fb;
-  if constexpr (MODEL == MODEL_RSW) {
-    fa = grp < 2 ? grp : 2;
-    fb = grp < 2 ? -1 : 3;
-  } else {
-    fa = grp;      // A_l
-    fb = 2 + grp;  // B_l
-  }
+  const NTerms nt = nterms<MODEL>(grp);
   // fft_line leaves F[m = t + s*NT] in v[s]; only live rows are written
-  load_col(Mf + fa * MF);
+  load_col(Mf + nt.fa * MF);
   fft_line<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    const double2 a = v[s];
-    if constexpr (MODEL == MODEL_RSW) {
-      acc[s] = (grp < 2) ? make_double2(-a.x, -a.y) : cmul_i(a, -k);
-    } else {
-      acc[s] = cmul_i(a, -lwav(g, c.t + s * NT));
-    }
-  }
-  if (fb >= 0) {
-    load_col(Mf + fb * MF);
+  for (int s = 0; s < 8; ++s) acc[s] = apply_mul(v[s], nt.ma, k, lwav(g, c.t + s * NT));
+  if (nt.fb >= 0) {
+    load_col(Mf + nt.fb * MF);
     fft_line<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const int m = c.t + s * NT;
-      if constexpr (MODEL == MODEL_RSW) {
-        acc[s] = cadd(acc[s], cmul_i(v[s], -lwav(g, m)));
-      } else {
-        acc[s] = cadd(acc[s], cmul_i(v[s], k));
-      }
-    }
+    for (int s = 0; s < 8; ++s) acc[s] = cadd(acc[s], apply_mul(v[s], nt.mb, k, lwav(g, c.t + s * NT)));
   }
   if (live) {
     double2* Nf = N + (long long)grp * g.cfield + (long long)krl * g.LrP;
@@ -621,33 +700,18 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     }
   };
 
-  // forward y-FFT of row output fi, folded into N_f with the model's multiplier
-  auto fwd_into = [&](double2 (&n)[8], int fi, int mult, bool first) {
-    // mult: 0 -> -F, 1 -> -ik F, 2 -> -il F, 3 -> +ik F
-    load_col(Mf + fi * MF);
+  // N_f (nterms): forward y-FFTs of row outputs with per-mode multipliers
+  auto compute_N = [&](double2 (&n)[8], int f) {
+    const NTerms nt = nterms<MODEL>(f);
+    load_col(Mf + nt.fa * MF);
     fft_line<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      double2 t;
-      if (mult == 0) t = make_double2(-v[s].x, -v[s].y);
-      else if (mult == 1) t = cmul_i(v[s], -k);
-      else if (mult == 2) t = cmul_i(v[s], -lwav(g, c.t + s * NT));
-      else t = cmul_i(v[s], k);
-      n[s] = first ? t : cadd(n[s], t);
-    }
-  };
-  // N_f (rsw/RotatingShallowWater.jl:174-226, swqg/TwoLayerQG.jl:171,179)
-  auto compute_N = [&](double2 (&n)[8], int f) {
-    if constexpr (MODEL == MODEL_RSW) {
-      if (f < 2) {
-        fwd_into(n, f, 0, true);
-      } else {
-        fwd_into(n, 2, 1, true);
-        fwd_into(n, 3, 2, false);
-      }
-    } else {
-      fwd_into(n, f, 2, true);
-      fwd_into(n, 2 + f, 3, false);
+    for (int s = 0; s < 8; ++s) n[s] = apply_mul(v[s], nt.ma, k, lwav(g, c.t + s * NT));
+    if (nt.fb >= 0) {
+      load_col(Mf + nt.fb * MF);
+      fft_line<LOG2N, -1>(v, c.t, tws, line);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) n[s] = cadd(n[s], apply_mul(v[s], nt.mb, k, lwav(g, c.t + s * NT)));
     }
   };
 
@@ -722,11 +786,11 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
       for (int s = 0; s < 8; ++s) v[s] = cscale(x[s], scale);
       fft_line<LOG2N, +1>(v, c.t, tws, line);
       store(f);
-      if (f < 2) {
+      if (f == 0) {  // Uy
 #pragma unroll
         for (int s = 0; s < 8; ++s) v[s] = cmul_i(x[s], lwav(g, c.t + s * NT) * scale);
         fft_line<LOG2N, +1>(v, c.t, tws, line);
-        store(3 + f);
+        store(3);
       }
     }
   } else {
@@ -766,9 +830,9 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
 // col_step_fab3 (RSW FilteredAB3): one block per (column, field f).  The
 // FilteredAB3 update of field f needs N_f alone (plus the old state for L·sol),
 // and the next calcN's inverse transforms of field f need only the new field f:
-//   f=0: N0 = -F(A)            -> u   -> U, Uy
-//   f=1: N1 = -F(B)            -> v   -> V, Vy
-//   f=2: N2 = -ik F(C) - il F(D) -> η -> H
+//   f=0: N_u = F(P)                   -> u -> U, Uy
+//   f=1: N_v = -il F(K̂) - F((ζu)^)    -> v -> V
+//   f=2: N_η = F(Q) - il F((vη)^)     -> η -> H
 // three y-FFTs per block, N never in HBM, old/new state in separate buffers.
 // ===========================================================================
 template <int LOG2N>
@@ -810,16 +874,19 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
       v[s] = live ? t : zero2();
     }
   };
-  // ---- N_f (rsw/RotatingShallowWater.jl:174-226)
-  load_col(Mf + (f < 2 ? f : 2) * MF);
-  fft_line<LOG2N, -1>(v, c.t, tws, line);
-#pragma unroll
-  for (int s = 0; s < 8; ++s) n[s] = (f < 2) ? make_double2(-v[s].x, -v[s].y) : cmul_i(v[s], -k);
-  if (f == 2) {
-    load_col(Mf + 3 * MF);
+  // ---- N_f (rsw/RotatingShallowWater.jl:174-226; nterms)
+  {
+    const NTerms nt = nterms<MODEL_RSW>(f);
+    load_col(Mf + nt.fa * MF);
     fft_line<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
-    for (int s = 0; s < 8; ++s) n[s] = cadd(n[s], cmul_i(v[s], -lwav(g, c.t + s * NT)));
+    for (int s = 0; s < 8; ++s) n[s] = apply_mul(v[s], nt.ma, k, lwav(g, c.t + s * NT));
+    if (nt.fb >= 0) {
+      load_col(Mf + nt.fb * MF);
+      fft_line<LOG2N, -1>(v, c.t, tws, line);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) n[s] = cadd(n[s], apply_mul(v[s], nt.mb, k, lwav(g, c.t + s * NT)));
+    }
   }
   // ---- FilteredAB3 update of field f on the live modes; x = new field f
   double2 x[8];
@@ -851,11 +918,11 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   for (int s = 0; s < 8; ++s) v[s] = cscale(x[s], scale);
   fft_line<LOG2N, +1>(v, c.t, tws, line);
   store(f);
-  if (f < 2) {  // ∂y: Uy, Vy
+  if (f == 0) {  // ∂y u: Uy
 #pragma unroll
     for (int s = 0; s < 8; ++s) v[s] = cmul_i(x[s], lwav(g, c.t + s * NT) * scale);
     fft_line<LOG2N, +1>(v, c.t, tws, line);
-    store(3 + f);
+    store(3);
   }
 }
 
