@@ -19,13 +19,11 @@ enum { ST_FAB3 = 0, ST_IFMAB3 = 1, ST_IFMRK4 = 2 };
 // kcl = roundup(kc, 64), nyl = ny).
 //  compact spectral field: [krl][j], krl < kcn live local columns, j < Lr live
 //    rows, column stride LrP
-//  mixed field, column phase (local column krl, any y):
-//    [y / nyl][krl / 8][y % nyl][krl % 8]             -> midc()
-//  mixed field, row phase (any global column kr < P*kcl, local row yl):
-//    [kr / 8][yl][kr % 8]                             -> midx()
-//  Block q of the column-phase array (rows of slab q) is exactly the block
-//  slab q holds for this slab's columns in its row-phase array, so the
-//  transpose between the passes is a plain all-to-all of contiguous blocks.
+//  mixed fields: midx/midc (forward direction), midx_i/midc_i (inverse
+//    direction) below.  Block q of a column-phase array (rows of slab q) is
+//    exactly the block slab q holds for this slab's columns in its row-phase
+//    array, so the transpose between the passes is a plain all-to-all of
+//    contiguous blocks.
 struct Geom {
   int nx, ny, log2nx, log2ny;
   int nkr, nl;
@@ -58,15 +56,62 @@ __host__ __device__ inline int compact_of(const Geom& g, int m) {
 __host__ __device__ inline double lwav(const Geom& g, int m) {
   return (double)(m < (g.ny >> 1) ? m : m - g.ny) * g.ml;
 }
-// element offsets inside one mixed field (< 2^31 for nx, ny <= 8192)
-// row phase: global column kr, local row yl
-__host__ __device__ inline int midx(const Geom& g, int kr, int yl) {
-  return ((kr >> 3) * g.nyl + yl) * 8 + (kr & 7);
+// Element offsets inside one mixed field (< 2^31 for nx, ny <= 8192).  A
+// 128-B line holds a tile of A columns kr × B = 8/A rows y (16-B elements, kr
+// fastest).  The row pass touches 16·A bytes of a line, the column pass
+// 16·B; the blocks that share a line are placed on one XCD (col_of_block),
+// where L2 stitches the line.  Measured on MI355X at 2048² (tools/sweep.sh,
+// DESIGN.md §2): 2×4 tiles in both directions beat whole-line rows (8×1) or
+// whole-line columns (1×8) by 11 % per step, because a pass that touches
+// 16 B of each line pays for the whole line in L1 fills and L2 requests.
+//  column phase (local column krl, any y): block q = y / nyl, then the tile
+//    offset of (krl, y % nyl) inside the block
+//  row phase (global kr = p kcl + krl, local row yl): block p, then the tile
+//    offset of (krl, yl)
+//  so block q of the column-phase array (rows of slab q) is byte for byte
+//  block p of slab q's row-phase array.
+// The forward fields (row outputs) use A = SW_TILE_F with their lines in
+// column order, the inverse fields (column outputs) A = SW_TILE_I with their
+// lines in row order.
+#ifndef SW_TILE_F
+#define SW_TILE_F 2
+#endif
+#ifndef SW_TILE_I
+#define SW_TILE_I 2
+#endif
+// line order: 0 = [y / B][kr / A] (a row's lines contiguous), 1 = [kr / A][y / B]
+#ifndef SW_LORD_F
+#define SW_LORD_F 1
+#endif
+#ifndef SW_LORD_I
+#define SW_LORD_I 0
+#endif
+template <int A, int ORD>
+__host__ __device__ inline int mtile_local(const Geom& g, int krl, int yl) {
+  // (krl, yl) inside one slab-pair block of kcl columns × nyl rows
+  constexpr int B = 8 / A;
+  const int line = ORD == 0 ? (yl / B) * (g.kcl / A) + krl / A : (krl / A) * (g.nyl / B) + yl / B;
+  return line * 8 + (yl % B) * A + krl % A;
 }
-// column phase: local column krl, global row y
-__host__ __device__ inline int midc(const Geom& g, int krl, int y) {
-  return (((y >> g.log2nyl) * g.ntl + (krl >> 3)) * g.nyl + (y & (g.nyl - 1))) * 8 + (krl & 7);
+template <int A, int ORD>
+__host__ __device__ inline int mtile_c(const Geom& g, int krl, int y) {
+  return (y >> g.log2nyl) * g.nyl * g.kcl + mtile_local<A, ORD>(g, krl, y & (g.nyl - 1));
 }
+template <int A, int ORD>
+__host__ __device__ inline int mtile_x(const Geom& g, int kr, int yl) {
+  int p = 0, krl = kr;
+  if (g.nslab > 1) {
+    p = kr / g.kcl;
+    krl = kr - p * g.kcl;
+  }
+  return p * g.nyl * g.kcl + mtile_local<A, ORD>(g, krl, yl);
+}
+// forward fields: row phase / column phase
+__host__ __device__ inline int midx(const Geom& g, int kr, int yl) { return mtile_x<SW_TILE_F, SW_LORD_F>(g, kr, yl); }
+__host__ __device__ inline int midc(const Geom& g, int krl, int y) { return mtile_c<SW_TILE_F, SW_LORD_F>(g, krl, y); }
+// inverse fields: column phase / row phase
+__host__ __device__ inline int midc_i(const Geom& g, int krl, int y) { return mtile_c<SW_TILE_I, SW_LORD_I>(g, krl, y); }
+__host__ __device__ inline int midx_i(const Geom& g, int kr, int yl) { return mtile_x<SW_TILE_I, SW_LORD_I>(g, kr, yl); }
 
 // integer power x^n (n >= 0) by repeated squaring
 __host__ __device__ inline double ipow(double x, int n) {

@@ -11,10 +11,10 @@
 
 namespace sw {
 
-// block -> column mapping for the column kernels.  When one line per block and
-// the grid is a multiple of 64, the 8 columns that share each 128-B chunk of
-// the mixed layout (kr>>3 equal) are placed on blocks b, b+8, …, b+56, which
-// the dispatcher deals to one XCD, so they meet in one L2 (speed only).
+// block -> line mapping.  When one line per block and the grid is a multiple
+// of 64, the 8 lines (columns, or rows in the row pass) that share each 128-B
+// chunk of a mixed layout are placed on blocks b, b+8, …, b+56, which the
+// dispatcher deals to one XCD, so they meet in one L2 (speed only).
 __device__ __forceinline__ int col_of_block(int b, int nb) {
   if ((nb & 63) == 0) {
     const int q = b >> 6, j = (b >> 3) & 7, x = b & 7;
@@ -88,7 +88,7 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     if (live) {
       double2* Mo = M + (long long)o * g.mfield;
 #pragma unroll
-      for (int s = 0; s < 8; ++s) Mo[midc(g, krl, c.t + s * NT)] = v[s];
+      for (int s = 0; s < 8; ++s) Mo[midc_i(g, krl, c.t + s * NT)] = v[s];
     }
   };
 
@@ -169,7 +169,7 @@ __device__ __forceinline__ void load_pair(double2 (&v)[8], int t, const Geom& g,
   for (int s = 0; s < 8; ++s) {  // issue every load first (clamped, unconditional)
     const int m = t + s * NT;
     kk[s] = m <= half ? m : N - m;
-    const int o = midx(g, kk[s] < g.kc ? kk[s] : 0, y);
+    const int o = midx_i(g, kk[s] < g.kc ? kk[s] : 0, y);
     a[s] = A[o];
     b[s] = B ? B[o] : zero2();
   }
@@ -208,7 +208,7 @@ __device__ __forceinline__ void load_eta_zeta(double2 (&v)[8], int t, const Geom
   for (int s = 0; s < 8; ++s) {
     const int m = t + s * NT;
     kk[s] = m <= half ? m : N - m;
-    const int o = midx(g, kk[s] < g.kc ? kk[s] : 0, y);
+    const int o = midx_i(g, kk[s] < g.kc ? kk[s] : 0, y);
     h[s] = H[o];
     vv[s] = V[o];
     uy[s] = Uy[o];
@@ -272,7 +272,7 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, Blk<LOG2N>::THREADS >= 10
   using Bk = Blk<LOG2N>;
   extern __shared__ double2 smem[];
   const LineCtx c = line_ctx<LOG2N>();
-  const int y = blockIdx.x * Bk::NB + c.ln;
+  const int y = (Bk::NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * Bk::NB + c.ln;
   double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
   Twiddles<LOG2N> tws;
   tws.load(c.t, tw);
@@ -774,7 +774,7 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     if (live) {
       double2* Mo = Minv + (long long)o * MF;
 #pragma unroll
-      for (int s = 0; s < 8; ++s) Mo[midc(g, krl, c.t + s * NT)] = v[s];
+      for (int s = 0; s < 8; ++s) Mo[midc_i(g, krl, c.t + s * NT)] = v[s];
     }
   };
   if constexpr (MODEL == MODEL_RSW) {
@@ -911,7 +911,7 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     if (live) {
       double2* Mo = Minv + (long long)o * MF;
 #pragma unroll
-      for (int s = 0; s < 8; ++s) Mo[midc(g, krl, c.t + s * NT)] = v[s];
+      for (int s = 0; s < 8; ++s) Mo[midc_i(g, krl, c.t + s * NT)] = v[s];
     }
   };
 #pragma unroll
@@ -1060,7 +1060,7 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   fft_line<LOG2N, +1>(v, c.t, tws, line);
   if (live) {
 #pragma unroll
-    for (int s = 0; s < 8; ++s) M[midc(g, krl, c.t + s * NT)] = v[s];
+    for (int s = 0; s < 8; ++s) M[midc_i(g, krl, c.t + s * NT)] = v[s];
   }
 }
 
@@ -1072,7 +1072,7 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   constexpr int NT = B::NT;
   extern __shared__ double2 smem[];
   const LineCtx c = line_ctx<LOG2N>();
-  const int y = blockIdx.x * B::NB + c.ln;
+  const int y = (B::NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * B::NB + c.ln;
   double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
   Twiddles<LOG2N> tws;
   tws.load(c.t, tw);

@@ -1,8 +1,8 @@
 """CPU rehearsal of libsw's slab-decomposed calcN (TEST INFRASTRUCTURE).
 
 One rank of the decomposition of DESIGN.md §6, written with numpy FFTs but
-with exactly libsw's data movement: the column-phase mixed layout
-[q][tile][yl][8], the row-phase layout [tile][yl][8], the staging order
+with exactly libsw's data movement and field set: the tiled mixed layouts of
+sw_internal.hpp (mtile_c / mtile_x, both directions), the staging order
 [peer][field][block] of the host-staged transport and the product's own
 exchange hook (``juliaraytracingsw_amd.slab_comm.torch_exchange``) moving
 the blocks between processes.  RSW calcN (rsw/RotatingShallowWater.jl:140-230)
@@ -25,12 +25,59 @@ def _exchange(hook, send: np.ndarray, P: int) -> np.ndarray:
     return recv
 
 
+# libsw's tile shapes (sw_internal.hpp): (kr extent A of a 128-B line, line order)
+TILE_F, LORD_F = 2, 1  # forward fields (row outputs)
+TILE_I, LORD_I = 2, 0  # inverse fields (column outputs)
+
+
+def _tile_local(krl, yl, A, order, kcl, nyl):
+    """mtile_local: element offset of (krl, yl) inside one kcl x nyl block."""
+    B = 8 // A
+    line = (yl // B) * (kcl // A) + krl // A if order == 0 else (krl // A) * (nyl // B) + yl // B
+    return line * 8 + (yl % B) * A + krl % A
+
+
+def _to_col_phase(X, A, order, P, nyl):
+    """[y][krl] (ny x kcl) -> the column-phase buffer (mtile_c), blocks q contiguous."""
+    ny, kcl = X.shape
+    y, krl = np.meshgrid(np.arange(ny), np.arange(kcl), indexing="ij")
+    off = (y // nyl) * nyl * kcl + _tile_local(krl, y % nyl, A, order, kcl, nyl)
+    buf = np.empty(ny * kcl, X.dtype)
+    buf[off.ravel()] = X.ravel()
+    return buf.reshape(P, nyl * kcl)
+
+
+def _from_row_phase(blocks, A, order, kcl, nyl):
+    """blocks [p][nyl*kcl] (mtile_x) -> [yl][kr] (nyl x P*kcl)."""
+    P = blocks.shape[0]
+    yl, kr = np.meshgrid(np.arange(nyl), np.arange(P * kcl), indexing="ij")
+    off = (kr // kcl) * nyl * kcl + _tile_local(kr % kcl, yl, A, order, kcl, nyl)
+    return blocks.reshape(-1)[off]
+
+
+def _to_row_phase(Y, A, order, kcl, nyl):
+    """[yl][kr] (nyl x P*kcl) -> blocks [q][nyl*kcl] (mtile_x), block q = slab q's columns."""
+    P = Y.shape[1] // kcl
+    yl, kr = np.meshgrid(np.arange(nyl), np.arange(P * kcl), indexing="ij")
+    off = (kr // kcl) * nyl * kcl + _tile_local(kr % kcl, yl, A, order, kcl, nyl)
+    buf = np.empty(P * nyl * kcl, Y.dtype)
+    buf[off.ravel()] = Y.ravel()
+    return buf.reshape(P, nyl * kcl)
+
+
+def _from_col_phase(blocks, A, order, kcl, nyl):
+    """blocks [q][nyl*kcl] (mtile_c) -> [y][krl] (ny x kcl)."""
+    P = blocks.shape[0]
+    y, krl = np.meshgrid(np.arange(P * nyl), np.arange(kcl), indexing="ij")
+    off = (y // nyl) * nyl * kcl + _tile_local(krl, y % nyl, A, order, kcl, nyl)
+    return blocks.reshape(-1)[off]
+
+
 def slab_calcN_rsw(sol, grid, P, r, hook):
     """N on slab r's live columns: (3, ny, kcn) complex, plus kr0."""
     nx, ny = grid.nx, grid.ny
     geo = slab_geometry(nx, ny, grid.aliased_fraction, P, r)
     kc, kcl, kr0, kcn, nyl = geo["kc"], geo["kcl"], geo["kr0"], geo["kcn"], geo["nyl"]
-    ntl = kcl // 8
     kr_all = grid.kr  # (nkr,)
     l = grid.l        # (ny,)
     scale = 1.0 / (nx * ny)
@@ -39,15 +86,16 @@ def slab_calcN_rsw(sol, grid, P, r, hook):
     S = np.zeros((3, ny, kcl), complex)
     S[:, :, :kcn] = grid.dealias(sol.copy())[:, :, kr0:kr0 + kcn]
     U, V, H = S
-    inv_in = [U, V, H, 1j * l[:, None] * U, 1j * l[:, None] * V]
+    # inverse fields U, V, H, Uy (sw_kernels.hip k_col_inv)
+    inv_in = [U, V, H, 1j * l[:, None] * U]
     colph = [np.fft.ifft(X, axis=0) * ny * scale for X in inv_in]  # unnormalised inverse / (nx ny)
-    # [y][krl] -> [q][tile][yl][8]; staging [q][field][...]
-    send = np.stack([c.reshape(P, nyl, ntl, 8).transpose(0, 2, 1, 3) for c in colph], axis=1)
-    recv = _exchange(hook, send, P)  # [p][field][tile][yl][8]
+    # inverse-direction layout midc_i; staging [q][field][block]
+    send = np.stack([_to_col_phase(c, TILE_I, LORD_I, P, nyl) for c in colph], axis=1)
+    recv = _exchange(hook, send, P)  # [p][field][block]
 
-    # --- row phase: [global tile][yl][8] -> [yl][kr]
+    # --- row phase (midx_i) -> [yl][kr]
     def row_field(f):
-        t = recv[:, f].reshape(P * ntl, nyl, 8).transpose(1, 0, 2).reshape(nyl, P * kcl)
+        t = _from_row_phase(recv[:, f], TILE_I, LORD_I, kcl, nyl)
         full = np.zeros((nyl, nx // 2 + 1), complex)
         full[:, :kc] = t[:, :kc]
         return full
@@ -55,27 +103,32 @@ def slab_calcN_rsw(sol, grid, P, r, hook):
     def phys(Xh):  # unnormalised c2r along x (numpy rule: DC imaginary part dropped)
         return np.fft.irfft(Xh, n=nx, axis=1) * nx
 
-    Ur, Vr, Hr, Uyr, Vyr = (row_field(f) for f in range(5))
+    Ur, Vr, Hr, Uyr = (row_field(f) for f in range(4))
     ik = 1j * kr_all[None, :]
     u, v, eta = phys(Ur), phys(Vr), phys(Hr)
-    ux, vx, uy, vy = phys(ik * Ur), phys(ik * Vr), phys(Uyr), phys(Vyr)
-    prods = [u * ux + v * uy, u * vx + v * vy, u * eta, v * eta]
+    zeta = phys(ik * Vr - Uyr)
+
+    def spec(a):
+        return np.fft.rfft(a, axis=1)
+
+    # vorticity form (k_row): P = -ik K^ + (ζv)^, K^, (ζu)^, Q = -ik (uη)^, (vη)^
+    Kh = spec(0.5 * (u * u + v * v))
+    outs = [-ik * Kh + spec(zeta * v), Kh, spec(zeta * u), -ik * spec(u * eta), spec(v * eta)]
     fwd = []
-    for a in prods:
+    for a in outs:
         Y = np.zeros((nyl, P * kcl), complex)
-        Y[:, :kc] = np.fft.rfft(a, axis=1)[:, :kc]
-        fwd.append(Y.reshape(nyl, P * ntl, 8).transpose(1, 0, 2))  # [tile][yl][8]
-    # block q = tiles of slab q
-    send = np.stack([f.reshape(P, ntl, nyl, 8) for f in fwd], axis=1)  # [q][field][tile][yl][8]
-    recv = _exchange(hook, send, P)  # [p][field][tile][yl][8]
+        Y[:, :kc] = a[:, :kc]
+        fwd.append(_to_row_phase(Y, TILE_F, LORD_F, kcl, nyl))  # midx: [q][block]
+    send = np.stack(fwd, axis=1)  # [q][field][block]
+    recv = _exchange(hook, send, P)  # [p][field][block]
 
-    # --- column phase: [p][tile][yl][8] -> [y][krl], forward y-FFT, combine
+    # --- column phase (midc) -> [y][krl], forward y-FFT, combine
     def col_field(f):
-        return recv[:, f].transpose(0, 2, 1, 3).reshape(ny, kcl)
+        return _from_col_phase(recv[:, f], TILE_F, LORD_F, kcl, nyl)
 
-    FA, FB, FC, FD = (np.fft.fft(col_field(f), axis=0) for f in range(4))
-    k = np.arange(kr0, kr0 + kcl) * kr_all[1]  # global wavenumbers of the local columns
-    N = np.stack([-FA, -FB, -1j * k[None, :] * FC - 1j * l[:, None] * FD])[:, :, :kcn]
+    FP, FK, FZU, FQ, FVE = (np.fft.fft(col_field(f), axis=0) for f in range(5))
+    il = 1j * l[:, None]
+    N = np.stack([FP, -il * FK - FZU, FQ - il * FVE])[:, :, :kcn]
     return N, kr0
 
 
