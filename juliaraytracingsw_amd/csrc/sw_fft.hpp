@@ -123,11 +123,12 @@ __device__ __forceinline__ void load_line(double2 (&v)[8], int t, const double2*
   for (int s = 0; s < 8; ++s) v[s] = line[(NT % 8 == 0) ? LP(t) + s * (NT + NT / 8) : LP(t + s * NT)];
 }
 
-// Full transform.  v holds x[t + s*NT] on entry and X[t + s*NT] on exit.
-// All threads of the block must call this (it contains barriers).
-template <int LOG2N, int DIR>
-__device__ __forceinline__ void fft_line(double2 (&v)[8], int t, const Twiddles<LOG2N>& tws,
-                                         double2* __restrict__ line) {
+// C independent transforms of one line each, sharing every barrier (C LDS
+// line buffers, `stride` complex apart).  v[c] holds x[t + s*NT] on entry and
+// X[t + s*NT] on exit.  All threads of the block must call this (barriers).
+template <int LOG2N, int DIR, int C>
+__device__ __forceinline__ void fft_lines(double2 (&v)[C][8], int t, const Twiddles<LOG2N>& tws,
+                                          double2* __restrict__ line, int stride) {
   using P = FftPlan<LOG2N>;
   constexpr int NT = P::NT;
   // Opaque copy of the stage twiddles: keeps the compiler from sharing the
@@ -140,31 +141,42 @@ __device__ __forceinline__ void fft_line(double2 (&v)[8], int t, const Twiddles<
     asm volatile("" : "+v"(tw1[i].x), "+v"(tw1[i].y));
   }
   if constexpr (P::REM == 2) {  // radix-4, Ns = 1: butterflies j = t, t + NT
-    dft4<DIR>(v[0], v[2], v[4], v[6]);
-    dft4<DIR>(v[1], v[3], v[5], v[7]);
-    lds_barrier();
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int j = t + h * NT;
-      const int base = 4 * j + (j >> 1);  // LP(4j + r) = 4j + r + (j >> 1), r < 4
-#pragma unroll
-      for (int r = 0; r < 4; ++r) line[base + r] = v[h + 2 * r];
+    for (int c = 0; c < C; ++c) {
+      dft4<DIR>(v[c][0], v[c][2], v[c][4], v[c][6]);
+      dft4<DIR>(v[c][1], v[c][3], v[c][5], v[c][7]);
     }
     lds_barrier();
-    load_line<LOG2N>(v, t, line);
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int j = t + h * NT;
+        const int base = 4 * j + (j >> 1);  // LP(4j + r) = 4j + r + (j >> 1), r < 4
+#pragma unroll
+        for (int r = 0; r < 4; ++r) line[c * stride + base + r] = v[c][h + 2 * r];
+      }
+    lds_barrier();
+#pragma unroll
+    for (int c = 0; c < C; ++c) load_line<LOG2N>(v[c], t, line + c * stride);
   } else if constexpr (P::REM == 1) {  // radix-2, Ns = 1: butterflies j = t + h*NT, h < 4
 #pragma unroll
-    for (int h = 0; h < 4; ++h) dft2<DIR>(v[h], v[h + 4]);
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int h = 0; h < 4; ++h) dft2<DIR>(v[c][h], v[c][h + 4]);
     lds_barrier();
 #pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      const int j = t + h * NT;
-      const int base = 2 * j + (j >> 2);  // LP(2j + r) = 2j + r + (j >> 2), r < 2
-      line[base] = v[h];
-      line[base + 1] = v[h + 4];
-    }
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const int j = t + h * NT;
+        const int base = 2 * j + (j >> 2);  // LP(2j + r) = 2j + r + (j >> 2), r < 2
+        line[c * stride + base] = v[c][h];
+        line[c * stride + base + 1] = v[c][h + 4];
+      }
     lds_barrier();
-    load_line<LOG2N>(v, t, line);
+#pragma unroll
+    for (int c = 0; c < C; ++c) load_line<LOG2N>(v[c], t, line + c * stride);
   }
   // radix-8 stages
   constexpr int S0 = P::REM ? P::REM : 0;
@@ -176,29 +188,45 @@ __device__ __forceinline__ void fft_line(double2 (&v)[8], int t, const Twiddles<
       const double2 w1 = DIR < 0 ? tw1[ti] : cconj(tw1[ti]);
       const double2 w2 = cmul(w1, w1), w3 = cmul(w2, w1), w4 = cmul(w2, w2);
       const double2 w5 = cmul(w4, w1), w6 = cmul(w3, w3), w7 = cmul(w4, w3);
-      v[1] = cmul(v[1], w1);
-      v[2] = cmul(v[2], w2);
-      v[3] = cmul(v[3], w3);
-      v[4] = cmul(v[4], w4);
-      v[5] = cmul(v[5], w5);
-      v[6] = cmul(v[6], w6);
-      v[7] = cmul(v[7], w7);
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        v[c][1] = cmul(v[c][1], w1);
+        v[c][2] = cmul(v[c][2], w2);
+        v[c][3] = cmul(v[c][3], w3);
+        v[c][4] = cmul(v[c][4], w4);
+        v[c][5] = cmul(v[c][5], w5);
+        v[c][6] = cmul(v[c][6], w6);
+        v[c][7] = cmul(v[c][7], w7);
+      }
     }
-    dft8<DIR>(v);
+#pragma unroll
+    for (int c = 0; c < C; ++c) dft8<DIR>(v[c]);
     if (lNs + 3 >= LOG2N) break;  // last stage: outputs already at t + r*NT
     lds_barrier();                // in-place LDS: everyone has loaded this stage's inputs
     const int idxD = ((t >> lNs) << (lNs + 3)) + k;
-    if (lNs >= 3) {
-      const int base = LP(idxD);
 #pragma unroll
-      for (int r = 0; r < 8; ++r) line[base + r * (Ns + Ns / 8)] = v[r];
-    } else {
+    for (int c = 0; c < C; ++c) {
+      if (lNs >= 3) {
+        const int base = LP(idxD);
 #pragma unroll
-      for (int r = 0; r < 8; ++r) line[LP(idxD + r * Ns)] = v[r];
+        for (int r = 0; r < 8; ++r) line[c * stride + base + r * (Ns + Ns / 8)] = v[c][r];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) line[c * stride + LP(idxD + r * Ns)] = v[c][r];
+      }
     }
     lds_barrier();
-    load_line<LOG2N>(v, t, line);
+#pragma unroll
+    for (int c = 0; c < C; ++c) load_line<LOG2N>(v[c], t, line + c * stride);
   }
+}
+
+// Full transform.  v holds x[t + s*NT] on entry and X[t + s*NT] on exit.
+// All threads of the block must call this (it contains barriers).
+template <int LOG2N, int DIR>
+__device__ __forceinline__ void fft_line(double2 (&v)[8], int t, const Twiddles<LOG2N>& tws,
+                                         double2* __restrict__ line) {
+  fft_lines<LOG2N, DIR, 1>(reinterpret_cast<double2(&)[1][8]>(v), t, tws, line, 0);
 }
 
 }  // namespace sw

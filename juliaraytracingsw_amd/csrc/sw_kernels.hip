@@ -254,6 +254,33 @@ __device__ __forceinline__ void split_pair(const double2 (&v)[8], int t, const G
   }
 }
 
+// split_pair for C transforms at once (C line buffers `stride` apart, one
+// barrier pair): emit(c, k, Â, B̂).
+template <int LOG2N, int C, typename Emit>
+__device__ __forceinline__ void split_pairs(const double2 (&v)[C][8], int t, const Geom& g,
+                                            double2* line, int stride, Emit emit) {
+  constexpr int N = 1 << LOG2N, NT = N / 8;
+  lds_barrier();
+#pragma unroll
+  for (int c = 0; c < C; ++c)
+#pragma unroll
+    for (int s = 0; s < 8; ++s) line[c * stride + LP(t + s * NT)] = v[c][s];
+  lds_barrier();
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const int k = t + s * NT;
+    if (k < g.kc) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const double2 zk = v[c][s];
+        const double2 zn = line[c * stride + LP((N - k) & (N - 1))];
+        emit(c, k, make_double2(0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y)),
+             make_double2(0.5 * (zk.y + zn.y), -0.5 * (zk.x - zn.x)));
+      }
+    }
+  }
+}
+
 template <int LOG2N>
 __device__ __forceinline__ void store_pair(const double2 (&v)[8], int t, const Geom& g,
                                            double2* line, double2* __restrict__ A,
@@ -265,6 +292,9 @@ __device__ __forceinline__ void store_pair(const double2 (&v)[8], int t, const G
   });
 }
 
+// LDS line buffers per row of k_row (RSW transforms pairs of lines together)
+__host__ __device__ constexpr int row_lds_lines(int model) { return model == MODEL_RSW ? 2 : 1; }
+
 template <int MODEL, int LOG2N>
 __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, Blk<LOG2N>::THREADS >= 1024 ? 4 : SW_MINW_ROW)
     k_row(Geom g, Phys p, const double2* __restrict__ Mi, double2* __restrict__ Mo,
@@ -273,7 +303,7 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, Blk<LOG2N>::THREADS >= 10
   extern __shared__ double2 smem[];
   const LineCtx c = line_ctx<LOG2N>();
   const int y = (Bk::NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * Bk::NB + c.ln;
-  double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
+  double2* line = smem + c.ln * row_lds_lines(MODEL) * FftPlan<LOG2N>::LDS;
   Twiddles<LOG2N> tws;
   tws.load(c.t, tw);
   const long long MF = g.mfield;
@@ -289,43 +319,35 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, Blk<LOG2N>::THREADS >= 10
     //   1 K̂, 2 (ζu)^          -> N_v = -il F_y(K̂) - F_y((ζu)^)
     //   3 Q = -ik (uη)^, 4 (vη)^ -> N_η = F_y(Q) - il F_y((vη)^)
     const double2 *U = Mi, *V = Mi + MF, *H = Mi + 2 * MF, *Uy = Mi + 3 * MF;
-    double2 uv[8];
-    // u + i v   (fft_line leaves z[x = t + s*NT] in v[s])
-    load_pair<LOG2N>(v, c.t, g, U, V, y, false);
-    fft_line<LOG2N, +1>(v, c.t, tws, line);
-#pragma unroll
-    for (int s = 0; s < 8; ++s) uv[s] = v[s];
-    // η + i ζ
-    load_eta_zeta<LOG2N>(v, c.t, g, H, V, Uy, y);
-    fft_line<LOG2N, +1>(v, c.t, tws, line);
-    double2 pb[8];
+    constexpr int LS = FftPlan<LOG2N>::LDS;  // two line buffers per row
+    double2 w[2][8];
+    // u + i v and η + i ζ, transformed together (fft_lines leaves z[x = t + s*NT])
+    load_pair<LOG2N>(w[0], c.t, g, U, V, y, false);
+    load_eta_zeta<LOG2N>(w[1], c.t, g, H, V, Uy, y);
+    fft_lines<LOG2N, +1, 2>(w, c.t, tws, line, LS);
     double pc[8];
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      const double u = uv[s].x, w = uv[s].y, eta = v[s].x, zeta = v[s].y;
-      pb[s] = make_double2(zeta * u, u * eta);
-      pc[s] = w * eta;
-      v[s] = make_double2(0.5 * (u * u + w * w), zeta * w);
+      const double u = w[0][s].x, vv = w[0][s].y, eta = w[1][s].x, zeta = w[1][s].y;
+      pc[s] = vv * eta;
+      w[0][s] = make_double2(0.5 * (u * u + vv * vv), zeta * vv);  // K + i ζv
+      w[1][s] = make_double2(zeta * u, u * eta);                   // ζu + i uη
     }
-    // K + i ζv
-    fft_line<LOG2N, -1>(v, c.t, tws, line);
-    split_pair<LOG2N>(v, c.t, g, line, [&](int k, double2 a, double2 b) {
+    fft_lines<LOG2N, -1, 2>(w, c.t, tws, line, LS);
+    split_pairs<LOG2N, 2>(w, c.t, g, line, LS, [&](int cc, int k, double2 a, double2 b) {
       const int o = midx(g, k, y);
-      Mo[o] = cadd(cmul_i(a, -(k * g.mk)), b);
-      Mo[MF + o] = a;
-    });
-    // ζu + i uη
-#pragma unroll
-    for (int s = 0; s < 8; ++s) v[s] = pb[s];
-    fft_line<LOG2N, -1>(v, c.t, tws, line);
-    split_pair<LOG2N>(v, c.t, g, line, [&](int k, double2 a, double2 b) {
-      const int o = midx(g, k, y);
-      Mo[2 * MF + o] = a;
-      Mo[3 * MF + o] = cmul_i(b, -(k * g.mk));
+      if (cc == 0) {
+        Mo[o] = cadd(cmul_i(a, -(k * g.mk)), b);
+        Mo[MF + o] = a;
+      } else {
+        Mo[2 * MF + o] = a;
+        Mo[3 * MF + o] = cmul_i(b, -(k * g.mk));
+      }
     });
     // vη (real input: the transform is the spectrum itself)
 #pragma unroll
     for (int s = 0; s < 8; ++s) v[s] = make_double2(pc[s], 0.0);
+    lds_barrier();  // split_pairs' mirror reads are done
     fft_line<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
@@ -1172,9 +1194,11 @@ struct RowL {
   static void run(int model, const Geom& g, const Phys& p, const double2* Mi, double2* Mo,
                   const double2* tw, hipStream_t s) {
     if (model == MODEL_RSW)
-      hipLaunchKernelGGL((k_row<MODEL_RSW, L>), dim3(row_blocks<L>(g)), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, Mi, Mo, tw);
+      hipLaunchKernelGGL((k_row<MODEL_RSW, L>), dim3(row_blocks<L>(g)), dim3(Blk<L>::THREADS),
+                         row_lds_lines(MODEL_RSW) * lds_bytes<L>(), s, g, p, Mi, Mo, tw);
     else
-      hipLaunchKernelGGL((k_row<MODEL_QG2, L>), dim3(row_blocks<L>(g)), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, Mi, Mo, tw);
+      hipLaunchKernelGGL((k_row<MODEL_QG2, L>), dim3(row_blocks<L>(g)), dim3(Blk<L>::THREADS),
+                         row_lds_lines(MODEL_QG2) * lds_bytes<L>(), s, g, p, Mi, Mo, tw);
   }
 };
 template <int L>
