@@ -292,8 +292,23 @@ __device__ __forceinline__ void store_pair(const double2 (&v)[8], int t, const G
   });
 }
 
-// LDS line buffers per row of k_row (RSW transforms pairs of lines together)
-__host__ __device__ constexpr int row_lds_lines(int model) { return model == MODEL_RSW ? 2 : 1; }
+// LDS line buffers per row of k_row: RSW transforms pairs of lines together
+// where two buffers per row fit the 160 KB of LDS (nx <= 4096)
+template <int MODEL, int LOG2N>
+__host__ __device__ constexpr int row_lds_lines() {
+  return (MODEL == MODEL_RSW && 2 * Blk<LOG2N>::NB * FftPlan<LOG2N>::LDS * 16 <= 160 * 1024) ? 2 : 1;
+}
+// C = 2: both transforms per barrier; C = 1: one after the other
+template <int LOG2N, int DIR, int C>
+__device__ __forceinline__ void fft_pair(double2 (&w)[2][8], int t, const Twiddles<LOG2N>& tws,
+                                         double2* line, int stride) {
+  if constexpr (C == 2) {
+    fft_lines<LOG2N, DIR, 2>(w, t, tws, line, stride);
+  } else {
+    fft_line<LOG2N, DIR>(w[0], t, tws, line);
+    fft_line<LOG2N, DIR>(w[1], t, tws, line);
+  }
+}
 
 template <int MODEL, int LOG2N>
 __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, Blk<LOG2N>::THREADS >= 1024 ? 4 : SW_MINW_ROW)
@@ -303,7 +318,8 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, Blk<LOG2N>::THREADS >= 10
   extern __shared__ double2 smem[];
   const LineCtx c = line_ctx<LOG2N>();
   const int y = (Bk::NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * Bk::NB + c.ln;
-  double2* line = smem + c.ln * row_lds_lines(MODEL) * FftPlan<LOG2N>::LDS;
+  constexpr int CB = row_lds_lines<MODEL, LOG2N>();
+  double2* line = smem + c.ln * CB * FftPlan<LOG2N>::LDS;
   Twiddles<LOG2N> tws;
   tws.load(c.t, tw);
   const long long MF = g.mfield;
@@ -324,7 +340,7 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, Blk<LOG2N>::THREADS >= 10
     // u + i v and η + i ζ, transformed together (fft_lines leaves z[x = t + s*NT])
     load_pair<LOG2N>(w[0], c.t, g, U, V, y, false);
     load_eta_zeta<LOG2N>(w[1], c.t, g, H, V, Uy, y);
-    fft_lines<LOG2N, +1, 2>(w, c.t, tws, line, LS);
+    fft_pair<LOG2N, +1, CB>(w, c.t, tws, line, LS);
     double pc[8];
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
@@ -333,8 +349,8 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, Blk<LOG2N>::THREADS >= 10
       w[0][s] = make_double2(0.5 * (u * u + vv * vv), zeta * vv);  // K + i ζv
       w[1][s] = make_double2(zeta * u, u * eta);                   // ζu + i uη
     }
-    fft_lines<LOG2N, -1, 2>(w, c.t, tws, line, LS);
-    split_pairs<LOG2N, 2>(w, c.t, g, line, LS, [&](int cc, int k, double2 a, double2 b) {
+    fft_pair<LOG2N, -1, CB>(w, c.t, tws, line, LS);
+    auto emit = [&](int cc, int k, double2 a, double2 b) {
       const int o = midx(g, k, y);
       if (cc == 0) {
         Mo[o] = cadd(cmul_i(a, -(k * g.mk)), b);
@@ -343,7 +359,14 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, Blk<LOG2N>::THREADS >= 10
         Mo[2 * MF + o] = a;
         Mo[3 * MF + o] = cmul_i(b, -(k * g.mk));
       }
-    });
+    };
+    if constexpr (CB == 2) {
+      split_pairs<LOG2N, 2>(w, c.t, g, line, LS, emit);
+    } else {
+      split_pairs<LOG2N, 1>(reinterpret_cast<const double2(&)[1][8]>(w[0]), c.t, g, line, LS, emit);
+      split_pairs<LOG2N, 1>(reinterpret_cast<const double2(&)[1][8]>(w[1]), c.t, g, line, LS,
+                            [&](int, int k, double2 a, double2 b) { emit(1, k, a, b); });
+    }
     // vη (real input: the transform is the spectrum itself)
 #pragma unroll
     for (int s = 0; s < 8; ++s) v[s] = make_double2(pc[s], 0.0);
@@ -1193,12 +1216,14 @@ template <int L>
 struct RowL {
   static void run(int model, const Geom& g, const Phys& p, const double2* Mi, double2* Mo,
                   const double2* tw, hipStream_t s) {
+    constexpr size_t sh_rsw = row_lds_lines<MODEL_RSW, L>() * FftPlan<L>::LDS * Blk<L>::NB * sizeof(double2);
+    constexpr size_t sh_qg2 = row_lds_lines<MODEL_QG2, L>() * FftPlan<L>::LDS * Blk<L>::NB * sizeof(double2);
     if (model == MODEL_RSW)
-      hipLaunchKernelGGL((k_row<MODEL_RSW, L>), dim3(row_blocks<L>(g)), dim3(Blk<L>::THREADS),
-                         row_lds_lines(MODEL_RSW) * lds_bytes<L>(), s, g, p, Mi, Mo, tw);
+      hipLaunchKernelGGL((k_row<MODEL_RSW, L>), dim3(row_blocks<L>(g)), dim3(Blk<L>::THREADS), sh_rsw, s, g, p,
+                         Mi, Mo, tw);
     else
-      hipLaunchKernelGGL((k_row<MODEL_QG2, L>), dim3(row_blocks<L>(g)), dim3(Blk<L>::THREADS),
-                         row_lds_lines(MODEL_QG2) * lds_bytes<L>(), s, g, p, Mi, Mo, tw);
+      hipLaunchKernelGGL((k_row<MODEL_QG2, L>), dim3(row_blocks<L>(g)), dim3(Blk<L>::THREADS), sh_qg2, s, g, p,
+                         Mi, Mo, tw);
   }
 };
 template <int L>

@@ -456,8 +456,8 @@ class Problem:
     "IFMRK4"}, or "NOP" calcN for the linear-only check)."""
 
     def __init__(self, model, stepper, nx, dt, Lx=2 * np.pi, aliased_fraction=1 / 3,
-                 params=None, use_filter=False, calcN=None, **filter_kw):
-        self.grid = TwoDGrid(nx, Lx, aliased_fraction=aliased_fraction)
+                 params=None, use_filter=False, calcN=None, ny=None, Ly=None, **filter_kw):
+        self.grid = TwoDGrid(nx, Lx, ny=ny, Ly=Ly, aliased_fraction=aliased_fraction)
         self.params = params
         self.model = model
         if model == "rsw":

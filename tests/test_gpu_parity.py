@@ -198,3 +198,49 @@ def test_invalid_config_fails_loudly():
         RSW.Problem("gpu", nx=96)  # not a power of two
     with pytest.raises(LibSWError):
         RSW.Problem("gpu", nx=64, aliased_fraction=0.0)
+
+
+def _rect_problem(name, nx, ny):
+    """Oracle + libsw problems of one case on an nx x ny grid with a random
+    smooth dealiased IC (the reference's IC builders assume square grids)."""
+    from juliaraytracingsw_amd import rotating_shallow_water as RSW, two_layer_qg as QG2
+
+    p = sw_cases.case_params(name, 256)
+    dt = 2e-4
+    if p["model"] == "rsw":
+        params = O.RSWParams(1e-30, 4, p["f"], p["Cg"])
+    else:
+        params = O.QG2Params(p["U"], p["mu"], 1e-30, 4, F=p["F"])
+    fk = dict(order=p["order"]) if p["stepper"] == "FilteredAB3" else {}
+    pr = O.Problem(p["model"], p["stepper"], nx, dt, params=params, ny=ny, **fk)
+    g = pr.grid
+    rng = np.random.default_rng(7)
+    nf = 3 if p["model"] == "rsw" else 2
+    spec = g.rfft(rng.standard_normal((nf, ny, nx)))
+    spec *= np.exp(-g.Krsq / (0.05 * (g.kc ** 2 + (g.ny / 3) ** 2)))  # smooth: energy at low K
+    spec *= 0.2 / np.abs(g.irfft(spec)).max()
+    pr.set_solution(spec)
+    if p["model"] == "rsw":
+        prob = RSW.Problem("gpu", nx=nx, ny=ny, dt=dt, nu=1e-30, nnu=4, f=p["f"], Cg=p["Cg"],
+                           stepper=p["stepper"], **fk)
+    else:
+        prob = QG2.Problem("gpu", nx=nx, ny=ny, dt=dt, nu=1e-30, nnu=4, U=p["U"], mu=p["mu"], f0=p["f0"],
+                           Cg=p["Cg"], drhorho0=p["drhorho0"], stepper=p["stepper"], **fk)
+    prob.sol = pr.sol
+    return pr, prob
+
+
+@pytest.mark.parametrize("nx,ny", [(8192, 32), (32, 8192), (4096, 64), (64, 4096)])
+@pytest.mark.parametrize("name", ["rsw_fab3", "qg2_ifmab3", "rsw_ifmrk4"])
+def test_rectangular_long_lines(name, nx, ny):
+    """Every transform length up to 8192 (the 4096²/8192² configurations) on
+    cheap rectangular grids: x lines of 4096/8192 exercise the row pass, y
+    lines the column passes, at 1e-10 against the oracle."""
+    pr, prob = _rect_problem(name, nx, ny)
+    N_gpu = prob.calcN(pr.sol)
+    N_cpu = pr.calcN(pr.sol.copy(), pr.grid, pr.params)
+    assert _err(N_gpu, N_cpu, pr.grid) < RTOL
+    pr.stepforward(4)
+    prob.stepforward(4)
+    assert _err(prob.sol, pr.sol, pr.grid) < RTOL
+    prob.close()
