@@ -66,6 +66,11 @@ extern "C" {
 #define SW_DIAG_NAN   0  /* 1.0 if any NaN/Inf in the state              */
 #define SW_DIAG_KE    1  /* RSW: kinetic_energy; QG2: KE layer 1 + layer 2 */
 #define SW_DIAG_PE    2  /* potential_energy                              */
+#define SW_DIAG_CFL   3  /* clock.dt · max(max|u|/dx, max|v|/dy) of the physical
+                            velocities, both layers for QG2 (rsw/RSWDriver.jl:207-208,
+                            swqg/TwoLayerDriver.jl:100-101)                  */
+#define SW_DIAG_KE2   4  /* QG2: KE of layer 2 alone (the tuple's 2nd entry) */
+#define SW_DIAG_KE1   5  /* QG2: KE of layer 1 alone (the tuple's 1st entry) */
 
 /* Host-staged transport (optional, one slab per process).  When set, libsw
  * moves every inter-slab exchange through host memory and calls
@@ -160,6 +165,28 @@ int sw_get_physical(sw_ctx* ctx, int32_t field_id, double* out, size_t bytes);
 
 /* Scalar diagnostics of the current state (SW_DIAG_*). */
 int sw_diag(sw_ctx* ctx, int32_t diag_id, double* out);
+
+/* FF Diagnostic(kinetic_energy, prob; freq) + Diagnostic(potential_energy, …)
+ * recorded on the device while stepping (rsw/RSWDriver.jl:193-196,
+ * swqg/TwoLayerDriver.jl:86-89, FF increment! after each step): after every
+ * step with clock.step % freq == 0, libsw reduces the energies of the state
+ * the reference's functions read at that point — RSW: vars.uh/vh/ηh, i.e. the
+ * (dealiased) input of the step's last calcN (rsw/RotatingShallowWater.jl
+ * :147-149, 323-333); 2LQG: prob.sol after the step (swqg/TwoLayerQG.jl
+ * :230-252) — with no host synchronisation.  freq = 0 disables; at most
+ * `capacity` records are kept (later ones are dropped).  Resets the records. */
+typedef struct sw_energy_record {
+  int64_t step;            /* clock.step after the step                     */
+  double  t;               /* clock.t after the step                        */
+  double  ke;              /* RSW: kinetic energy; QG2: KE of layer 1       */
+  double  ke2;             /* QG2: KE of layer 2 (0 for RSW)                */
+  double  pe;              /* potential energy                              */
+} sw_energy_record;
+int sw_set_energy_diagnostics(sw_ctx* ctx, int64_t freq, int64_t capacity);
+/* Copies up to max_records records (oldest first); *n_records = the count.
+ * One slab per process: every rank must call it (it gathers the slabs). */
+int sw_get_energy_diagnostics(sw_ctx* ctx, sw_energy_record* out, int64_t max_records,
+                              int64_t* n_records);
 
 /* Per-kernel HIP-event timing of `nsteps` steps (the state advances).
  * Fills up to max_stats entries; *n_stats receives the count. */

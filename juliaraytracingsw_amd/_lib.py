@@ -15,7 +15,7 @@ SW_MODEL_RSW, SW_MODEL_QG2 = 0, 1
 SW_STEP_FILTERED_AB3, SW_STEP_IFMAB3, SW_STEP_IFMRK4 = 0, 1, 2
 SW_OK, SW_E_INVALID, SW_E_NOMEM, SW_E_HIP, SW_E_COMM, SW_E_NAN, SW_E_STATE = 0, -1, -2, -3, -4, -5, -6
 SW_PHYS_U, SW_PHYS_V, SW_PHYS_ETA, SW_PHYS_ZETA, SW_PHYS_Q, SW_PHYS_PSI = 0, 1, 2, 3, 4, 5
-SW_DIAG_NAN, SW_DIAG_KE, SW_DIAG_PE = 0, 1, 2
+SW_DIAG_NAN, SW_DIAG_KE, SW_DIAG_PE, SW_DIAG_CFL, SW_DIAG_KE2, SW_DIAG_KE1 = 0, 1, 2, 3, 4, 5
 
 STEPPERS = {"FilteredAB3": SW_STEP_FILTERED_AB3, "IFMAB3": SW_STEP_IFMAB3, "IFMRK4": SW_STEP_IFMRK4}
 
@@ -23,7 +23,8 @@ STEPPERS = {"FilteredAB3": SW_STEP_FILTERED_AB3, "IFMAB3": SW_STEP_IFMAB3, "IFMR
 EXPORTS = [
     "sw_config_default", "sw_create", "sw_destroy", "sw_last_error", "sw_get_dims",
     "sw_set_state", "sw_get_state", "sw_set_clock", "sw_get_clock", "sw_step", "sw_calcN",
-    "sw_get_physical", "sw_diag", "sw_profile_steps", "sw_step_alg_bytes", "sw_comm_unique_id",
+    "sw_get_physical", "sw_diag", "sw_set_energy_diagnostics", "sw_get_energy_diagnostics",
+    "sw_profile_steps", "sw_step_alg_bytes", "sw_comm_unique_id",
 ]
 
 
@@ -53,6 +54,11 @@ class SwConfig(C.Structure):
         ("comm_unique_id", C.c_void_p),
         ("exchange", EXCHANGE_FN), ("exchange_user", C.c_void_p),
     ]
+
+
+class SwEnergyRecord(C.Structure):
+    _fields_ = [("step", C.c_int64), ("t", C.c_double), ("ke", C.c_double), ("ke2", C.c_double),
+                ("pe", C.c_double)]
 
 
 class SwKernelStat(C.Structure):
@@ -91,6 +97,8 @@ def load(path: str | None = None):
         "sw_calcN": (C.c_int, [vp, vp, vp, sz]),
         "sw_get_physical": (C.c_int, [vp, i32, vp, sz]),
         "sw_diag": (C.c_int, [vp, i32, C.POINTER(dbl)]),
+        "sw_set_energy_diagnostics": (C.c_int, [vp, i64, i64]),
+        "sw_get_energy_diagnostics": (C.c_int, [vp, C.POINTER(SwEnergyRecord), i64, C.POINTER(i64)]),
         "sw_profile_steps": (C.c_int, [vp, i64, C.POINTER(SwKernelStat), i32, C.POINTER(i32)]),
         "sw_step_alg_bytes": (dbl, [vp]),
         "sw_comm_unique_id": (C.c_int, [vp]),
@@ -194,6 +202,21 @@ class Context:
         v = C.c_double()
         self._check(self.lib.sw_diag(self._h, int(diag_id), C.byref(v)), "sw_diag")
         return v.value
+
+    def set_energy_diagnostics(self, freq, capacity):
+        self._check(self.lib.sw_set_energy_diagnostics(self._h, int(freq), int(capacity)),
+                    "sw_set_energy_diagnostics")
+
+    def energy_diagnostics(self, max_records=None):
+        """[(step, t, ke, ke2, pe), …] recorded on the device while stepping."""
+        cap = 1 << 20 if max_records is None else int(max_records)
+        n = C.c_int64()
+        self._check(self.lib.sw_get_energy_diagnostics(self._h, None, 0, C.byref(n)),
+                    "sw_get_energy_diagnostics")
+        buf = (SwEnergyRecord * max(1, min(cap, n.value)))()
+        self._check(self.lib.sw_get_energy_diagnostics(self._h, buf, min(cap, n.value), C.byref(n)),
+                    "sw_get_energy_diagnostics")
+        return [(buf[i].step, buf[i].t, buf[i].ke, buf[i].ke2, buf[i].pe) for i in range(n.value)]
 
     def profile(self, nsteps):
         st = (SwKernelStat * 16)()

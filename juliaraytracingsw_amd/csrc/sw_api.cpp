@@ -62,7 +62,16 @@ struct sw_ctx {
   double2* stage = nullptr;                  // full (nkr,nl,nf) staging
   double2* gbuf = nullptr;                   // dist: all-gathered compact slabs
   double* dflt = nullptr;                    // physical staging / reductions
+  double* ecols = nullptr;                   // per-column energy sums [global column][3]
+  double* esum = nullptr;                    // energy sums / gathered maxima (sw_diag)
   int* flag = nullptr;
+  // FF Diagnostic(kinetic_energy / potential_energy; freq) recorded on the
+  // device during sw_step (sw_set_energy_diagnostics)
+  int64_t diag_freq = 0, diag_cap = 0, diag_n = 0;
+  double* erec = nullptr;                    // records: [rec][3] sums, or (one slab per
+                                             // process) [rec][kcl][3] column sums
+  std::vector<int64_t> diag_steps;
+  std::vector<double> diag_t;
   double t = 0.0;
   int64_t step = 0;
   std::string err;
@@ -389,8 +398,27 @@ int run_stage(sw_ctx* c, int op, int stage, double2* Slab::*X) {
   return 0;
 }
 
+// The state FF's energy diagnostics read after a step: RSW's
+// kinetic_energy(prob)/potential_energy(prob) read vars.uh/vh/ηh, which the
+// step's last calcN set from its (dealiased) input (rsw/RotatingShallowWater.jl
+// :147-149, 323-333): the pre-update state (FilteredAB3, IFMAB3) or the
+// stage-4 input (IFMRK4).  2LQG's recompute from prob.sol (swqg/TwoLayerQG.jl
+// :230-252), the post-update state.
+void record_energy(sw_ctx* c, double2* Slab::*X) {
+  if (c->dist) {  // this rank's column sums; added over ranks at retrieval
+    const Slab& s = c->sl[0];
+    sw::launch_energy_cols(c->cfg.model, s.g, c->p, s.*X, c->erec + (size_t)c->diag_n * s.g.kcl * 3, c->stream);
+    return;
+  }
+  for (Slab& s : c->sl) sw::launch_energy_cols(c->cfg.model, s.g, c->p, s.*X, c->ecols + 3 * s.g.kr0, c->stream);
+  sw::launch_energy_final(c->ecols, c->P * c->sl[0].g.kcl, c->erec + 3 * c->diag_n, c->stream);
+}
+
 int step_once(sw_ctx* c) {
   const int st = c->cfg.stepper;
+  const bool rec = c->diag_freq > 0 && (c->step + 1) % c->diag_freq == 0 && c->diag_n < c->diag_cap;
+  const bool rsw = c->cfg.model == SW_MODEL_RSW;
+  if (rec && rsw && st == SW_STEP_IFMAB3) record_energy(c, &Slab::sol);  // updated in place below
   if (st == SW_STEP_FILTERED_AB3 || st == SW_STEP_IFMAB3) {
     if (int rc = run_stage(c, st == SW_STEP_FILTERED_AB3 ? sw::OP_FAB3 : sw::OP_IFMAB3, 0, &Slab::sol))
       return rc;
@@ -403,6 +431,14 @@ int step_once(sw_ctx* c) {
   }
   c->t += c->cfg.dt;
   c->step += 1;
+  if (rec) {
+    if (rsw && st == SW_STEP_FILTERED_AB3) record_energy(c, &Slab::sol2);  // the pre-update buffer
+    else if (rsw && st == SW_STEP_IFMRK4) record_energy(c, &Slab::xs);    // stage-4 input
+    else if (!rsw) record_energy(c, &Slab::sol);
+    c->diag_steps.push_back(c->step);
+    c->diag_t.push_back(c->t);
+    c->diag_n += 1;
+  }
   return 0;
 }
 
@@ -468,11 +504,11 @@ int nan_flag(sw_ctx* c, int& h) {
   HIPCHK(c, hipMemsetAsync(c->flag, 0, sizeof(int), c->stream));
   for (Slab& s : c->sl) sw::launch_nan_check(c->nf, s.g, s.sol, c->flag, c->stream);
   HIPCHK(c, hipGetLastError());
-  int all[64] = {0};
+  std::vector<int> all(c->P + 1, 0);
   const int n = c->dist ? c->P : 1;
   if (c->dist)
     if (int rc = allgather(c, c->flag, c->flag + 1, sizeof(int))) return rc;
-  HIPCHK(c, hipMemcpyAsync(all, c->dist ? c->flag + 1 : c->flag, n * sizeof(int), hipMemcpyDeviceToHost,
+  HIPCHK(c, hipMemcpyAsync(all.data(), c->dist ? c->flag + 1 : c->flag, n * sizeof(int), hipMemcpyDeviceToHost,
                            c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   h = 0;
@@ -627,7 +663,9 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   const Geom& g = c->sl[0].g;
   if ((rc = alloc(c, (void**)&c->stage, full_bytes(c)))) return rc;
   if ((rc = alloc(c, (void**)&c->dflt, (size_t)g.nx * g.ny * sizeof(double)))) return rc;
-  if ((rc = alloc(c, (void**)&c->flag, 64 * sizeof(int)))) return rc;
+  if ((rc = alloc(c, (void**)&c->flag, 1024 * sizeof(int)))) return rc;
+  if ((rc = alloc(c, (void**)&c->ecols, 3 * (size_t)P * g.kcl * sizeof(double)))) return rc;
+  if ((rc = alloc(c, (void**)&c->esum, (3 + 2 * (size_t)P) * sizeof(double)))) return rc;
   if (c->dist) {
     const size_t gb = (size_t)P * c->nf * g.kcl * g.LrP * sizeof(double2);
     if ((rc = alloc(c, (void**)&c->gbuf, gb))) return rc;
@@ -659,7 +697,7 @@ void sw_destroy(sw_ctx* c) {
   if (!c) return;
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (Slab& s : c->sl) free_slab(s);
-  void* ptrs[] = {c->tw_x, c->tw_y, c->stage, c->gbuf, c->dflt, c->flag};
+  void* ptrs[] = {c->tw_x, c->tw_y, c->stage, c->gbuf, c->dflt, c->flag, c->ecols, c->esum, c->erec};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   if (c->comm) (void)ncclCommDestroy(c->comm);
@@ -754,18 +792,9 @@ int sw_calcN(sw_ctx* c, const void* sol, void* N, size_t bytes) {
   return SW_OK;
 }
 
-int sw_get_physical(sw_ctx* c, int32_t fid, double* out, size_t bytes) {
-  if (!ready(c)) return SW_E_STATE;
-  const Geom& g0 = c->sl[0].g;
-  if (!out || bytes != (size_t)g0.nx * g0.ny * sizeof(double))
-    return fail(c, SW_E_INVALID, "sw_get_physical: size mismatch");
-  const int id = fid & 7, layer = fid >> 3;
-  if (c->cfg.model == SW_MODEL_RSW) {
-    if (fid < 0 || fid > 3) return fail(c, SW_E_INVALID, "RSW physical ids are 0..3");
-  } else {
-    if (layer > 1 || id == SW_PHYS_ETA || id > 5) return fail(c, SW_E_INVALID, "bad QG2 physical id");
-  }
-  HIPCHK(c, hipSetDevice(c->cfg.device));
+// one physical field (updatevars!) of the current state into c->dflt: this
+// rank's rows (one slab per process) or every row (all slabs here)
+static int physical_to_dflt(sw_ctx* c, int32_t fid) {
   c->mixed_valid = false;  // mixed arrays are used as scratch
   for (Slab& s : c->sl) {
     sw::launch_make_spec(c->cfg.model, fid, s.g, c->p, s.sol, s.xs, c->stream);
@@ -774,6 +803,24 @@ int sw_get_physical(sw_ctx* c, int32_t fid, double* out, size_t bytes) {
   if (int rc = transpose(c, true, 1)) return rc;
   for (Slab& s : c->sl) sw::launch_row_c2r1(s.g, s.mir, c->dflt, c->tw_x, c->stream);
   HIPCHK(c, hipGetLastError());
+  return 0;
+}
+
+static bool valid_phys_id(const sw_ctx* c, int32_t fid) {
+  const int id = fid & 7, layer = fid >> 3;
+  if (c->cfg.model == SW_MODEL_RSW) return fid >= 0 && fid <= 3;
+  return fid >= 0 && layer <= 1 && id != SW_PHYS_ETA && id <= 5;
+}
+
+int sw_get_physical(sw_ctx* c, int32_t fid, double* out, size_t bytes) {
+  if (!ready(c)) return SW_E_STATE;
+  const Geom& g0 = c->sl[0].g;
+  if (!out || bytes != (size_t)g0.nx * g0.ny * sizeof(double))
+    return fail(c, SW_E_INVALID, "sw_get_physical: size mismatch");
+  if (!valid_phys_id(c, fid))
+    return fail(c, SW_E_INVALID, c->cfg.model == SW_MODEL_RSW ? "RSW physical ids are 0..3" : "bad QG2 physical id");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  if (int rc = physical_to_dflt(c, fid)) return rc;
   if (c->dist) {
     const size_t rows = (size_t)g0.nyl * g0.nx;
     if (int rc = allgather(c, c->dflt + (size_t)g0.y0 * g0.nx, c->dflt, rows * sizeof(double))) return rc;
@@ -781,6 +828,56 @@ int sw_get_physical(sw_ctx* c, int32_t fid, double* out, size_t bytes) {
   HIPCHK(c, hipMemcpyAsync(out, c->dflt, bytes, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return SW_OK;
+}
+
+// energy sums (k_energy_partial triples) -> (KE, KE2, PE)
+// (rsw/RotatingShallowWater.jl:323-333; swqg/TwoLayerQG.jl:230-250, KE per
+// layer), with the parsevalsum(2) normalisation
+static void energies_from_sums(const sw_ctx* c, const double a[3], double& ke, double& ke2, double& pe) {
+  const Geom& g = c->sl[0].g;
+  const double norm = g.Lx * g.Ly / ((double)g.nx * g.nx * (double)g.ny * g.ny);
+  if (c->cfg.model == SW_MODEL_RSW) {
+    ke = norm * a[0] / (2 * g.Lx * g.Ly);
+    ke2 = 0.0;
+    pe = 0.5 * c->p.Cg2 * norm * a[1] / (g.Lx * g.Ly);
+  } else {
+    ke = norm * a[0] / (g.Lx * g.Ly);
+    ke2 = norm * a[1] / (g.Lx * g.Ly);
+    pe = 1.0 / (2 * g.Lx * g.Ly) * c->p.F * norm * a[2];
+  }
+}
+
+// `nrec` energy records -> host sums [rec][3].  Single process: dev holds
+// the sums.  One slab per process: dev holds this rank's column sums
+// [rec][kcl][3]; they are gathered and added in global column order, so the
+// result is bitwise the same for any decomposition.
+static int gather_energy_sums(sw_ctx* c, const double* dev, int64_t nrec, std::vector<double>& out) {
+  out.assign((size_t)nrec * 3, 0.0);
+  if (nrec == 0) return 0;
+  if (!c->dist) {
+    HIPCHK(c, hipMemcpyAsync(out.data(), dev, out.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+  }
+  const size_t kcl = c->sl[0].g.kcl, per = (size_t)nrec * kcl * 3;
+  std::vector<double> all(per * c->P);
+  double* tmp = nullptr;
+  HIPCHK(c, hipMalloc((void**)&tmp, per * c->P * sizeof(double)));
+  int rc = allgather(c, dev, tmp, per * sizeof(double));
+  if (!rc && hipMemcpyAsync(all.data(), tmp, all.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream) !=
+                 hipSuccess)
+    rc = fail(c, SW_E_HIP, "energy gather copy failed");
+  (void)hipStreamSynchronize(c->stream);
+  (void)hipFree(tmp);
+  if (rc) return rc;
+  for (int64_t r = 0; r < nrec; ++r)
+    for (int k = 0; k < 3; ++k) {
+      double acc = 0.0;
+      for (int q = 0; q < c->P; ++q)
+        for (size_t col = 0; col < kcl; ++col) acc += all[q * per + ((size_t)r * kcl + col) * 3 + k];
+      out[(size_t)r * 3 + k] = acc;
+    }
+  return 0;
 }
 
 int sw_diag(sw_ctx* c, int32_t id, double* out) {
@@ -792,34 +889,98 @@ int sw_diag(sw_ctx* c, int32_t id, double* out) {
     *out = h ? 1.0 : 0.0;
     return SW_OK;
   }
-  if (id != SW_DIAG_KE && id != SW_DIAG_PE) return fail(c, SW_E_INVALID, "unknown diagnostic");
-  HIPCHK(c, hipMemsetAsync(c->dflt, 0, 2 * sizeof(double), c->stream));
-  for (Slab& s : c->sl) sw::launch_energy(c->cfg.model, s.g, c->p, s.sol, c->dflt, c->stream);
+  if (id == SW_DIAG_CFL) {
+    // rsw/RSWDriver.jl:207-208, swqg/TwoLayerDriver.jl:100-101:
+    // dt · max(maximum(|vars.u|)/dx, maximum(|vars.v|)/dy), both layers for 2LQG
+    const Geom& g0 = c->sl[0].g;
+    const int nlay = c->cfg.model == SW_MODEL_RSW ? 1 : 2;
+    unsigned long long* mx = reinterpret_cast<unsigned long long*>(c->flag + 512);  // [u, v] maxima
+    HIPCHK(c, hipMemsetAsync(mx, 0, 2 * sizeof(unsigned long long), c->stream));
+    const size_t off = c->dist ? (size_t)g0.y0 * g0.nx : 0;
+    const long long n = (long long)(c->dist ? g0.nyl : g0.ny) * g0.nx;
+    for (int layer = 0; layer < nlay; ++layer)
+      for (int comp = 0; comp < 2; ++comp) {
+        if (int rc = physical_to_dflt(c, layer * 8 + (comp == 0 ? SW_PHYS_U : SW_PHYS_V))) return rc;
+        sw::launch_absmax(c->dflt + off, n, mx + comp, c->stream);
+      }
+    HIPCHK(c, hipGetLastError());
+    double m[2] = {0.0, 0.0};
+    if (c->dist) {
+      std::vector<double> all(2 * (size_t)c->P);
+      if (int rc = allgather(c, mx, c->esum, 2 * sizeof(double))) return rc;
+      HIPCHK(c, hipMemcpyAsync(all.data(), c->esum, all.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      for (int q = 0; q < c->P; ++q) {
+        m[0] = std::max(m[0], all[2 * q]);
+        m[1] = std::max(m[1], all[2 * q + 1]);
+      }
+    } else {
+      HIPCHK(c, hipMemcpyAsync(m, mx, 2 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    *out = c->cfg.dt * std::max(m[0] / g0.dx, m[1] / g0.dy);
+    return SW_OK;
+  }
+  if (id != SW_DIAG_KE && id != SW_DIAG_PE && id != SW_DIAG_KE1 && id != SW_DIAG_KE2)
+    return fail(c, SW_E_INVALID, "unknown diagnostic");
+  for (Slab& s : c->sl) sw::launch_energy_cols(c->cfg.model, s.g, c->p, s.sol, c->ecols + 3 * s.g.kr0, c->stream);
+  if (c->dist) {
+    const Geom& g0 = c->sl[0].g;
+    if (int rc = allgather(c, c->ecols + 3 * g0.kr0, c->ecols, 3 * (size_t)g0.kcl * sizeof(double))) return rc;
+  }
+  sw::launch_energy_final(c->ecols, c->P * c->sl[0].g.kcl, c->esum, c->stream);
   HIPCHK(c, hipGetLastError());
-  // per-rank partial sums, added in rank order on every rank
-  std::vector<double> part(2 * (size_t)c->P, 0.0);
-  const int nparts = c->dist ? c->P : 1;
-  if (c->dist)
-    if (int rc = allgather(c, c->dflt, c->dflt + 2, 2 * sizeof(double))) return rc;
-  HIPCHK(c, hipMemcpyAsync(part.data(), c->dflt + (c->dist ? 2 : 0), 2 * nparts * sizeof(double),
-                           hipMemcpyDeviceToHost, c->stream));
+  std::vector<double> sums(3);
+  HIPCHK(c, hipMemcpyAsync(sums.data(), c->esum, 3 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  double acc[2] = {0, 0};
-  for (int i = 0; i < nparts; ++i) {
-    acc[0] += part[2 * i];
-    acc[1] += part[2 * i + 1];
+  double ke, ke2, pe;
+  energies_from_sums(c, sums.data(), ke, ke2, pe);
+  // RSW KE; 2LQG KE = KE_1 + KE_2 (the driver's tuple summed), KE2 = KE_2
+  if (id == SW_DIAG_KE) *out = ke + ke2;
+  else if (id == SW_DIAG_KE1) *out = ke;
+  else if (id == SW_DIAG_KE2) *out = ke2;
+  else *out = pe;
+  return SW_OK;
+}
+
+int sw_set_energy_diagnostics(sw_ctx* c, int64_t freq, int64_t capacity) {
+  if (!ready(c)) return SW_E_STATE;
+  if (freq < 0 || capacity < 0) return fail(c, SW_E_INVALID, "freq and capacity must be >= 0");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->erec) (void)hipFree(c->erec);
+  c->erec = nullptr;
+  c->diag_freq = freq;
+  c->diag_cap = freq > 0 ? capacity : 0;
+  c->diag_n = 0;
+  c->diag_steps.clear();
+  c->diag_t.clear();
+  if (c->diag_cap > 0) {
+    const size_t per = c->dist ? (size_t)c->sl[0].g.kcl * 3 : 3;
+    if (int rc = alloc(c, (void**)&c->erec, (size_t)c->diag_cap * per * sizeof(double))) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
   }
-  const Geom& g = c->sl[0].g;
-  const double norm = g.Lx * g.Ly / ((double)g.nx * g.nx * (double)g.ny * g.ny);  // parsevalsum2
-  if (c->cfg.model == SW_MODEL_RSW) {
-    // rsw/RotatingShallowWater.jl:323-331
-    if (id == SW_DIAG_KE) *out = norm * acc[0] / (2 * g.Lx * g.Ly);
-    else *out = 0.5 * c->p.Cg2 * norm * acc[1] / (g.Lx * g.Ly);
-  } else {
-    // swqg/TwoLayerQG.jl:230-250
-    if (id == SW_DIAG_KE) *out = norm * acc[0] / (g.Lx * g.Ly);
-    else *out = 1.0 / (2 * g.Lx * g.Ly) * c->p.F * norm * acc[1];
+  return SW_OK;
+}
+
+int sw_get_energy_diagnostics(sw_ctx* c, sw_energy_record* out, int64_t max_records, int64_t* n_records) {
+  if (!ready(c)) return SW_E_STATE;
+  if (max_records < 0 || (max_records > 0 && !out)) return fail(c, SW_E_INVALID, "bad record buffer");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  if (max_records == 0) {  // query: the number of records held
+    if (n_records) *n_records = c->diag_n;
+    return SW_OK;
   }
+  const int64_t n = std::min<int64_t>(c->diag_n, max_records);
+  std::vector<double> sums;
+  // one slab per process: every rank gathers every record (collective)
+  if (int rc = gather_energy_sums(c, c->erec, c->dist ? c->diag_n : n, sums)) return rc;
+  for (int64_t r = 0; r < n; ++r) {
+    out[r].step = c->diag_steps[r];
+    out[r].t = c->diag_t[r];
+    energies_from_sums(c, &sums[3 * r], out[r].ke, out[r].ke2, out[r].pe);
+  }
+  if (n_records) *n_records = n;
   return SW_OK;
 }
 

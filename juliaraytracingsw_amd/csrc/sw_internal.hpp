@@ -327,7 +327,12 @@ void launch_make_spec(int model, int field_id, const Geom& g, const Phys& p, con
                       double2* out, hipStream_t s);
 void launch_col_inv1(const Geom& g, const double2* X, double2* M, const double2* tw_y, hipStream_t s);
 void launch_row_c2r1(const Geom& g, const double2* M, double* out, const double2* tw_x, hipStream_t s);
-void launch_energy(int model, const Geom& g, const Phys& p, const double2* sol, double* acc,
-                   hipStream_t s);
+// energy sums of a compact state (sw_kernels.hip k_energy_cols): one triple
+// per local column into cols[3 krl + 0..2]; k_energy_final adds ncols
+// triples in order into out[0..2]
+void launch_energy_cols(int model, const Geom& g, const Phys& p, const double2* sol, double* cols,
+                        hipStream_t s);
+void launch_energy_final(const double* cols, int ncols, double* out, hipStream_t s);
+void launch_absmax(const double* f, long long n, unsigned long long* out, hipStream_t s);
 
 }  // namespace sw

@@ -1129,43 +1129,85 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
 }
 
 // Energies by Parseval over live modes (FF parsevalsum2 / parsevalsum:
-// weight 2 for 0 < kr < nx/2, 1 for kr = 0).  acc[0] = KE-sum, acc[1] = PE-sum.
-__global__ void k_energy(Geom g, Phys p, int model, const double2* __restrict__ sol, double* acc) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  int kr, j;
-  double ke = 0.0, pe = 0.0;
-  if (i < g.cfield && mode_of(g, i, kr, j)) {
+// weight 2 for 0 < kr < nx/2, 1 for kr = 0).  Three sums per state:
+//   RSW: 0 |u|²+|v|², 1 |η|², 2 unused
+//   QG2: 0 K²|ψ1|², 1 K²|ψ2|², 2 |ψ1-ψ2|²
+// Deterministic and independent of the slab decomposition: one block per
+// column reduces that column in a fixed order (k_energy_cols, padding
+// columns give 0), then the column sums are added in global column order
+// (k_energy_final).  No atomics: results repeat bitwise for any P.
+__device__ __forceinline__ double block_sum(double v, double* sh) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[w] = v;
+  __syncthreads();
+  double r = 0.0;
+  if (threadIdx.x == 0)
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) r += sh[i];
+  return r;
+}
+
+__global__ void __launch_bounds__(256) k_energy_cols(Geom g, Phys p, int model,
+                                                     const double2* __restrict__ sol,
+                                                     double* __restrict__ cols) {
+  __shared__ double sh[4];
+  const int krl = blockIdx.x;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+  if (krl < g.kcn) {
     const long long cf = g.cfield;
-    const double w = kr == 0 ? 1.0 : 2.0;
-    if (model == MODEL_RSW) {
-      const double2 u = sol[i], v = sol[cf + i], e = sol[2 * cf + i];
-      ke = w * (u.x * u.x + u.y * u.y + v.x * v.x + v.y * v.y);
-      pe = w * (e.x * e.x + e.y * e.y);
-    } else {
-      const double k = kr * g.mk, l = lwav(g, lrow_of(g, j));
-      const double K2 = k * k + l * l;
-      const double iK2 = K2 == 0.0 ? 0.0 : 1.0 / K2;
-      const double den = K2 + 2.0 * p.F;
-      const double2 q1 = sol[i], q2 = sol[cf + i];
-      const double2 qs = cadd(q1, q2);
-      double2 p1 = make_double2(-(K2 * q1.x + p.F * qs.x), -(K2 * q1.y + p.F * qs.y));
-      double2 p2 = make_double2(-(K2 * q2.x + p.F * qs.x), -(K2 * q2.y + p.F * qs.y));
-      p1 = make_double2((p1.x / den) * iK2, (p1.y / den) * iK2);
-      p2 = make_double2((p2.x / den) * iK2, (p2.y / den) * iK2);
-      ke = w * K2 * (p1.x * p1.x + p1.y * p1.y + p2.x * p2.x + p2.y * p2.y);
-      const double dx_ = p1.x - p2.x, dy_ = p1.y - p2.y;
-      pe = w * (dx_ * dx_ + dy_ * dy_);
+    const int kr = g.kr0 + krl;
+    const double w = kr == 0 ? 1.0 : 2.0, k = kr * g.mk;
+    for (int j = threadIdx.x; j < g.Lr; j += blockDim.x) {
+      const long long i = (long long)krl * g.LrP + j;
+      if (model == MODEL_RSW) {
+        const double2 u = sol[i], v = sol[cf + i], e = sol[2 * cf + i];
+        a0 += w * (u.x * u.x + u.y * u.y + v.x * v.x + v.y * v.y);
+        a1 += w * (e.x * e.x + e.y * e.y);
+      } else {
+        const double l = lwav(g, lrow_of(g, j));
+        const double K2 = k * k + l * l;
+        const double iK2 = K2 == 0.0 ? 0.0 : 1.0 / K2;
+        const double den = K2 + 2.0 * p.F;
+        const double2 q1 = sol[i], q2 = sol[cf + i];
+        const double2 qs = cadd(q1, q2);
+        double2 p1 = make_double2(-(K2 * q1.x + p.F * qs.x), -(K2 * q1.y + p.F * qs.y));
+        double2 p2 = make_double2(-(K2 * q2.x + p.F * qs.x), -(K2 * q2.y + p.F * qs.y));
+        p1 = make_double2((p1.x / den) * iK2, (p1.y / den) * iK2);
+        p2 = make_double2((p2.x / den) * iK2, (p2.y / den) * iK2);
+        a0 += w * K2 * (p1.x * p1.x + p1.y * p1.y);
+        a1 += w * K2 * (p2.x * p2.x + p2.y * p2.y);
+        const double dx_ = p1.x - p2.x, dy_ = p1.y - p2.y;
+        a2 += w * (dx_ * dx_ + dy_ * dy_);
+      }
     }
   }
-  // wave reduction
-  for (int off = 32; off > 0; off >>= 1) {
-    ke += __shfl_down(ke, off, 64);
-    pe += __shfl_down(pe, off, 64);
+  a0 = block_sum(a0, sh);
+  a1 = block_sum(a1, sh);
+  a2 = block_sum(a2, sh);
+  if (threadIdx.x == 0) {
+    cols[3 * krl] = a0;
+    cols[3 * krl + 1] = a1;
+    cols[3 * krl + 2] = a2;
   }
-  if ((threadIdx.x & 63) == 0) {
-    atomicAdd(acc, ke);
-    atomicAdd(acc + 1, pe);
+}
+
+__global__ void k_energy_final(const double* __restrict__ cols, int ncols, double* __restrict__ out) {
+  if (threadIdx.x < 3) {
+    double r = 0.0;
+    for (int b = 0; b < ncols; ++b) r += cols[3 * b + threadIdx.x];
+    out[threadIdx.x] = r;
   }
+}
+
+// max |f| over this slab's physical rows (non-negative doubles order like
+// their bit patterns, so an integer atomicMax is exact and order-free)
+__global__ void k_absmax(const double* __restrict__ f, long long n, unsigned long long* out) {
+  double m = 0.0;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    m = fmax(m, fabs(f[i]));
+  for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_down(m, off, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax(out, (unsigned long long)__double_as_longlong(m));
 }
 
 // ===========================================================================
@@ -1346,9 +1388,17 @@ void launch_row_c2r1(const Geom& g, const double2* M, double* out, const double2
   dispatch_log2<RowC2r1L>(g.log2nx, g, M, out, tw_x, s);
 }
 
-void launch_energy(int model, const Geom& g, const Phys& p, const double2* sol, double* acc,
-                   hipStream_t s) {
-  hipLaunchKernelGGL(k_energy, mode_grid(g), dim3(256), 0, s, g, p, model, sol, acc);
+void launch_energy_cols(int model, const Geom& g, const Phys& p, const double2* sol, double* cols,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(k_energy_cols, dim3(g.kcl), dim3(256), 0, s, g, p, model, sol, cols);
+}
+
+void launch_energy_final(const double* cols, int ncols, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_energy_final, dim3(1), dim3(64), 0, s, cols, ncols, out);
+}
+
+void launch_absmax(const double* f, long long n, unsigned long long* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_absmax, dim3(1024), dim3(256), 0, s, f, n, out);
 }
 
 }  // namespace sw

@@ -143,13 +143,21 @@ def qg2_problem(nx, stepper="IFMAB3", seed=1234, device=0, decomposition=None, *
     return prob, P
 
 
-def run_frames(prob, nframes, output_freq, on_frame=None, log_every=100):
-    """The drivers' frame loop (rsw/RSWDriver.jl:205-223): step output_freq,
-    NaN check (sw_step returns SW_E_NAN -> LibSWError), optional callback."""
+def run_frames(prob, nframes, output_freq, diags=(), on_frame=None, log_every=100):
+    """The drivers' frame loop (rsw/RSWDriver.jl:205-223, swqg/TwoLayerDriver.jl:98-117):
+    every log_every frames print step, t and the CFL number (device
+    reduction), then stepforward!(prob, diags, output_freq) with the energy
+    Diagnostics recorded on the device; a NaN makes sw_step return SW_E_NAN,
+    raised as LibSWError("Solution is NaN") (the reference's throw); then the
+    optional per-frame callback (updatevars!/output)."""
+    from . import problem
+
+    mod = RSW if prob.model == _lib.SW_MODEL_RSW else QG2
     t0 = time.time()
     for frame in range(nframes):
         if log_every and frame % log_every == 0:
-            print(f"step: {prob.clock.step:04d}, t: {prob.clock.t:.2f}, time: {(time.time() - t0) / 60:.2f} mins")
-        prob.stepforward(output_freq)
+            print(f"step: {prob.clock.step:04d}, t: {prob.clock.t:.2f}, cfl: {mod.cfl(prob):.2e}, "
+                  f"time: {(time.time() - t0) / 60:.2f} mins")
+        problem.stepforward(prob, list(diags), output_freq)
         if on_frame is not None:
             on_frame(prob, frame)

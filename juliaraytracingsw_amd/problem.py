@@ -7,6 +7,7 @@ reference's (``prob.sol``, ``prob.clock``, ``stepforward!(prob, n)`` …).
 from __future__ import annotations
 
 import ctypes as C
+import math
 
 import numpy as np
 
@@ -83,6 +84,7 @@ class Problem:
         self.grid = TwoDGrid(nx, Lx, ny, Ly, aliased_fraction)
         self.clock = Clock(self.ctx, dt)
         self.params = dict(params)
+        self._efreq = None  # energy-diagnostics frequency recorded on the device
 
     # FF prob.sol (a host copy; assignment uploads and dealiases)
     @property
@@ -104,7 +106,65 @@ class Problem:
     def close(self):
         self.ctx.close()
 
+    def _attach_energy_diagnostics(self, freq, ndata):
+        if self._efreq is None:
+            self.ctx.set_energy_diagnostics(freq, ndata)
+            self._efreq = freq
+        elif freq != self._efreq:
+            raise NotImplementedError("libsw records one energy-diagnostics frequency per problem")
 
-def stepforward(prob: Problem, nsteps: int = 1):
-    """``stepforward!(prob, nsteps)``."""
-    prob.stepforward(nsteps)
+
+class Diagnostic:
+    """FF ``Diagnostic(calc, prob; freq, nsteps, ndata)`` for the energy
+    diagnostics the drivers keep (rsw/RSWDriver.jl:193-196,
+    swqg/TwoLayerDriver.jl:86-89): ``calc`` is a module's ``kinetic_energy``
+    or ``potential_energy``.  Entry 0 is ``calc(prob)`` at construction; after
+    every step with ``clock.step % freq == 0`` libsw reduces the energies on
+    the device while stepping (sw_set_energy_diagnostics — no host round
+    trip per diagnostic), and ``stepforward(prob, diags, n)`` appends them.
+    Fields as FF's: ``data``, ``t``, ``steps``, ``value``, ``i`` (entries held),
+    ``freq``."""
+
+    def __init__(self, calc, prob, *, freq=1, nsteps=100, ndata=None):
+        field = getattr(calc, "_sw_energy", None)
+        if field is None:
+            raise ValueError("libsw records kinetic_energy / potential_energy diagnostics")
+        ndata = int(ndata or math.ceil((nsteps + 1) / freq))
+        prob._attach_energy_diagnostics(int(freq), ndata)
+        self.calc, self.prob, self.freq, self._field = calc, prob, int(freq), field
+        self.value = calc(prob)
+        self.data = [None] * ndata
+        self.t = np.zeros(ndata)
+        self.steps = np.zeros(ndata, np.int64)
+        self.data[0], self.t[0], self.steps[0] = self.value, prob.clock.t, prob.clock.step
+        self.i = 1
+        self._seen = 0  # device records consumed
+
+    def _take(self, records):
+        for step, t, ke, ke2, pe in records[self._seen:]:
+            if self.i >= len(self.data):
+                break
+            v = {"ke": ke, "pe": pe, "ke12": (ke, ke2)}[self._field]
+            self.data[self.i], self.t[self.i], self.steps[self.i] = v, t, step
+            self.value = v
+            self.i += 1
+        self._seen = len(records)
+
+
+def increment(diags):
+    """FF ``increment!(diags)``: pull the device-recorded energies."""
+    diags = [diags] if isinstance(diags, Diagnostic) else list(diags)
+    if diags:
+        recs = diags[0].prob.ctx.energy_diagnostics()
+        for d in diags:
+            d._take(recs)
+
+
+def stepforward(prob: Problem, diags_or_nsteps=1, nsteps=None):
+    """``stepforward!(prob, nsteps)`` or ``stepforward!(prob, diags, nsteps)``
+    (rsw/RSWDriver.jl:212, swqg/TwoLayerDriver.jl:105)."""
+    if nsteps is None:
+        prob.stepforward(int(diags_or_nsteps))
+        return
+    prob.stepforward(int(nsteps))
+    increment(diags_or_nsteps)

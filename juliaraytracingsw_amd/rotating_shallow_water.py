@@ -8,7 +8,7 @@ from __future__ import annotations
 import numpy as np
 
 from . import _lib
-from .problem import Problem as _Problem, stepforward  # noqa: F401
+from .problem import Diagnostic, Problem as _Problem, increment, stepforward  # noqa: F401
 
 
 def Problem(dev="gpu", *, nx=128, ny=None, Lx=2 * np.pi, Ly=None, nu=1.0e-16, nnu=4, f=1.0, Cg=1.0,
@@ -61,3 +61,13 @@ def potential_energy(prob):
 
 def energy(prob):
     return kinetic_energy(prob) + potential_energy(prob)
+
+
+def cfl(prob):
+    """The drivers' CFL number clock.dt · max(max|u|/dx, max|v|/dy)
+    (rsw/RSWDriver.jl:207-208), reduced on the device."""
+    return prob.ctx.diag(_lib.SW_DIAG_CFL)
+
+
+kinetic_energy._sw_energy = "ke"
+potential_energy._sw_energy = "pe"

@@ -9,7 +9,7 @@ from __future__ import annotations
 import numpy as np
 
 from . import _lib
-from .problem import Problem as _Problem, stepforward  # noqa: F401
+from .problem import Diagnostic, Problem as _Problem, increment, stepforward  # noqa: F401
 
 
 def Problem(dev="gpu", *, nx=128, ny=None, Lx=2 * np.pi, Ly=None, U=0.5, mu=1e-2, nu=1e-6, nnu=4,
@@ -52,10 +52,20 @@ def updatevars(prob):
 
 
 def kinetic_energy(prob):
-    """``kinetic_energy(prob)`` (:230-240), summed over both layers, of the dealiased state."""
-    return prob.ctx.diag(_lib.SW_DIAG_KE)
+    """``kinetic_energy(prob)`` (:230-240): the tuple (KE_1, KE_2) of the layers."""
+    return (prob.ctx.diag(_lib.SW_DIAG_KE1), prob.ctx.diag(_lib.SW_DIAG_KE2))
 
 
 def potential_energy(prob):
     """``potential_energy(prob)`` (:244-250)."""
     return prob.ctx.diag(_lib.SW_DIAG_PE)
+
+
+def cfl(prob):
+    """clock.dt · max(max|u|/dx, max|v|/dy) over both layers
+    (swqg/TwoLayerDriver.jl:100-101), reduced on the device."""
+    return prob.ctx.diag(_lib.SW_DIAG_CFL)
+
+
+kinetic_energy._sw_energy = "ke12"
+potential_energy._sw_energy = "pe"

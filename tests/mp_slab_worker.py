@@ -37,23 +37,28 @@ def main():
     prob = sw_cases.libsw_problem(p, decomposition=slab_comm.host_decomposition(rank, world))
     prob.sol = ic
     N = prob.calcN(ic)
+    prob.ctx.set_energy_diagnostics(2, 64)
     prob.stepforward(a.steps)
     sol = prob.sol
     phys = M.updatevars(prob)
-    ke, pe = M.kinetic_energy(prob), M.potential_energy(prob)
+    ke, pe = np.sum(M.kinetic_energy(prob)), M.potential_energy(prob)
+    recs, cfl = prob.ctx.energy_diagnostics(), M.cfl(prob)
     res = {}
     if rank == 0:
         ref = sw_cases.libsw_problem(p)
         ref.sol = ic
         Nr = ref.calcN(ic)
+        ref.ctx.set_energy_diagnostics(2, 64)
         ref.stepforward(a.steps)
         pr = M.updatevars(ref)
         res = dict(
             state_equal=bool(np.array_equal(sol, ref.sol)),
             calcN_equal=bool(np.array_equal(N, Nr)),
             physical_equal=bool(all(np.array_equal(phys[k], pr[k]) for k in pr)),
-            ke_rel=abs(ke / M.kinetic_energy(ref) - 1),
+            ke_rel=abs(ke / np.sum(M.kinetic_energy(ref)) - 1),
             pe_rel=abs(pe / M.potential_energy(ref) - 1),
+            records_equal=bool(recs == ref.ctx.energy_diagnostics() and len(recs) == a.steps // 2),
+            cfl_equal=bool(cfl == M.cfl(ref)),
             world=world,
         )
         ref.close()

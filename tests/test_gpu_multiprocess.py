@@ -1,7 +1,8 @@
 """One process per slab on the GPU box: torch.distributed.run starts `world`
 ranks, each with its own libsw context holding one slab, exchanging through
 the host-staged transport (gloo).  The gathered results must equal the
-undecomposed run bitwise (energies to rounding: per-rank partial sums)."""
+undecomposed run bitwise, the device-recorded energy diagnostics and the CFL
+reduction included."""
 import json
 import os
 import socket
@@ -33,4 +34,5 @@ def test_one_process_per_slab(case, world, tmp_path):
     res = json.loads(out.read_text())
     assert res["world"] == world
     assert res["state_equal"] and res["calcN_equal"] and res["physical_equal"], res
-    assert res["ke_rel"] < 1e-13 and res["pe_rel"] < 1e-13, res
+    assert res["ke_rel"] == 0 and res["pe_rel"] == 0, res
+    assert res["records_equal"] and res["cfl_equal"], res

@@ -172,7 +172,7 @@ def test_qg2_physical_and_energy():
     psi = pr.grid.irfft(psih)
     assert np.max(np.abs(got["psi"] - psi)) < 1e-12 * np.max(np.abs(psi))
     (KE1, KE2), PE = O.qg2_energies(pr.sol, pr.grid, pr.params)
-    assert abs(QG2.kinetic_energy(prob) / (KE1 + KE2) - 1) < 1e-12
+    assert abs(sum(QG2.kinetic_energy(prob)) / (KE1 + KE2) - 1) < 1e-12
     assert abs(QG2.potential_energy(prob) / PE - 1) < 1e-12
     prob.close()
 
@@ -243,4 +243,85 @@ def test_rectangular_long_lines(name, nx, ny):
     pr.stepforward(4)
     prob.stepforward(4)
     assert _err(prob.sol, pr.sol, pr.grid) < RTOL
+    prob.close()
+
+
+@pytest.mark.parametrize("name", sw_cases.CASES)
+def test_energy_diagnostics_recorded(name):
+    """FF Diagnostic(kinetic_energy / potential_energy; freq) as the drivers
+    keep them (rsw/RSWDriver.jl:193-196, swqg/TwoLayerDriver.jl:86-89),
+    recorded on the device while stepping.  Entry 0 is the value at
+    construction; then after every freq-th step RSW reads vars.uh/vh/ηh — the
+    input of the step's last calcN (rsw/RotatingShallowWater.jl:147-149) — and
+    2LQG the post-step sol (swqg/TwoLayerQG.jl:230-252).  libsw stores live
+    modes only, so its 2LQG energies are of the dealiased post-step sol; the
+    reference's also count the aliased modes the update has just written and
+    the next calcN discards (relative 1e-12 (IFMAB3) to 1e-8 (IFMRK4) of the
+    energy on this strongly nonlinear 64² case) — compared here against the
+    oracle's dealiased post-step state."""
+    from juliaraytracingsw_amd import rotating_shallow_water as RSW, two_layer_qg as QG2
+
+    rsw = name.startswith("rsw")
+    M = RSW if rsw else QG2
+    p = sw_cases.case_params(name, 64)
+    pr = sw_cases.oracle_problem(p)
+    pr.set_solution(sw_cases.initial_condition(p, pr.grid))
+    prob = sw_cases.libsw_problem(p)
+    prob.sol = pr.sol
+    freq, nsteps = 3, 10
+    KE = M.Diagnostic(M.kinetic_energy, prob, freq=freq, nsteps=nsteps)
+    PE = M.Diagnostic(M.potential_energy, prob, freq=freq, nsteps=nsteps)
+
+    def energies(st):
+        if rsw:
+            return O.rsw_energies(st, pr.grid, pr.params)
+        (k1, k2), pe = O.qg2_energies(st, pr.grid, pr.params)
+        return (k1, k2), pe
+
+    last = {}
+    calcN = pr.calcN
+
+    def spy(sol, grid, params):  # vars.uh etc. = the dealiased calcN input
+        last["x"] = grid.dealias(sol.copy())
+        return calcN(sol, grid, params)
+
+    pr.calcN = spy
+    expected = [(0, energies(pr.sol))]
+    for s in range(1, nsteps + 1):
+        pr.stepforward(1)
+        if s % freq == 0:
+            expected.append((s, energies(last["x"] if rsw else pr.grid.dealias(pr.sol.copy()))))
+    M.stepforward(prob, [KE, PE], nsteps)
+    assert KE.i == PE.i == len(expected) == 4
+    for i, (s, (ke, pe)) in enumerate(expected):
+        assert KE.steps[i] == s and PE.steps[i] == s
+        assert abs(KE.t[i] - s * p["dt"]) < 1e-12
+        assert np.allclose(np.atleast_1d(KE.data[i]), np.atleast_1d(ke), rtol=RTOL, atol=0), (i, KE.data[i], ke)
+        assert abs(PE.data[i] / pe - 1) < RTOL, (i, PE.data[i], pe)
+    prob.close()
+
+
+@pytest.mark.parametrize("name", ["rsw_fab3", "qg2_ifmab3"])
+def test_cfl_reduction(name):
+    """dt · max(max|u|/dx, max|v|/dy) (rsw/RSWDriver.jl:207-208), both layers
+    for 2LQG (swqg/TwoLayerDriver.jl:100-101), against the oracle's fields."""
+    from juliaraytracingsw_amd import rotating_shallow_water as RSW, two_layer_qg as QG2
+
+    p = sw_cases.case_params(name, 128)
+    pr = sw_cases.oracle_problem(p)
+    pr.set_solution(sw_cases.initial_condition(p, pr.grid))
+    prob = sw_cases.libsw_problem(p)
+    prob.sol = pr.sol
+    g = pr.grid
+    if name.startswith("rsw"):
+        ref = O.rsw_updatevars(pr.sol.copy(), g, pr.params)
+        u, v = ref["u"], ref["v"]
+        got = RSW.cfl(prob)
+    else:
+        psih = O.qg2_streamfunction(pr.sol, g, pr.params)
+        u = g.irfft(-1j * g.l[:, None] * psih)
+        v = g.irfft(1j * g.kr[None, :] * psih)
+        got = QG2.cfl(prob)
+    exp = p["dt"] * max(np.abs(u).max() / g.dx, np.abs(v).max() / g.dy)
+    assert abs(got / exp - 1) < 1e-12
     prob.close()
