@@ -33,7 +33,6 @@ struct Slab {
   double2* sol = nullptr;                    // compact state, nf fields
   double2* sol2 = nullptr;                   // FilteredAB3: the other state buffer (ping-pong)
   double2* hist[3] = {nullptr, nullptr, nullptr};  // FAB3 RHS ring / IFMAB3 N ring
-  double2 *E = nullptr, *E2 = nullptr;       // IF operators (E2 = exp(2Ldt) or exp(Ldt/2))
   double2* acc = nullptr;                    // IFMRK4 running stage combination
   double2* nbuf = nullptr;                   // unfused IFMRK4 / sw_calcN: calcN output
   double2* xs = nullptr;                     // stage input / scratch compact
@@ -196,13 +195,12 @@ const char* kname[K_NKERN] = {"col_inv", "row", "col_fwd", "update", "col_step",
 // state/history bytes of one stepper op per live mode, in live-field units
 // (reads + writes; AB3 steady state; IFMRK4 averaged over its four stages)
 double op_fields(const sw_ctx* c) {
+  // the integrating factors are evaluated per mode, never stored (sw_internal.hpp ExpOf)
   const int nf = c->nf, st = c->cfg.stepper;
-  if (st == SW_STEP_FILTERED_AB3) return 3 * nf + 2 * nf;          // sol,R-1,R-2 in; sol,RHS out
-  if (st == SW_STEP_IFMAB3) return 3 * nf + 2 * nf * nf + 2 * nf;  // sol,N-1,N-2,E,E2 in; sol,N out
-  // stages: 1 u,E,H in / acc out; 2 u,acc,H in / acc out; 3 u,acc,E,H in / acc out; 4 u,acc,E in / u out
-  const double s1 = nf + 2 * nf * nf + nf, s2 = 2 * nf + nf * nf + nf, s3 = 2 * nf + 2 * nf * nf + nf,
-               s4 = 2 * nf + nf * nf + nf;
-  return (s1 + s2 + s3 + s4) / 4;
+  if (st == SW_STEP_FILTERED_AB3) return 3 * nf + 2 * nf;  // sol,R-1,R-2 in; sol,RHS out
+  if (st == SW_STEP_IFMAB3) return 3 * nf + 2 * nf;        // sol,N-1,N-2 in; sol,N out
+  // stages: 1 u in / acc,x out; 2-3 u,acc in / acc,x out; 4 u,acc in / u out
+  return (3.0 * nf + 4.0 * nf + 4.0 * nf + 3.0 * nf) / 4;
 }
 
 double kernel_bytes(const sw_ctx* c, int kid) {
@@ -329,8 +327,11 @@ int calcN(sw_ctx* c, double2* Slab::*X, double2* Slab::*N) {
 // needs, so a primed step is row -> col_step (two launches).
 // The fused column pass is used where it wins (measured): RSW FilteredAB3,
 // whose update splits by field.  Other model/stepper pairs run the separate
-// col_inv / row / col_fwd / update kernels (the fused generic k_col_step keeps
-// all N fields live and spills on gfx950 at 2048²).
+// col_inv / row / col_fwd / update kernels: their update couples the fields
+// at a mode, and both one block per column holding every field (k_col_step,
+// SW_FUSE_ALL) and a per-(column, field group) update + inverse kernel that
+// re-evaluates the coupled update in every group measured slower at 2048²
+// than the separate kernels.
 bool use_fused(const sw_ctx* c) {
   if (c->cfg.unfused || c->cfg.nop_calcN) return false;
   if (c->fuse_all) return true;
@@ -342,8 +343,6 @@ sw::StepPtrs step_ptrs(const sw_ctx* c, const Slab& s) {
   sw::StepPtrs a{};
   a.sol = s.sol;
   a.sol_out = (st == SW_STEP_FILTERED_AB3) ? s.sol2 : s.sol;
-  a.E = s.E;
-  a.E2 = s.E2;
   a.xs = s.xs;
   a.euler = c->step < 3 ? 1 : 0;
   if (st == SW_STEP_IFMRK4) {
@@ -517,7 +516,7 @@ int nan_flag(sw_ctx* c, int& h) {
 }
 
 void free_slab(Slab& s) {
-  void* ptrs[] = {s.sol, s.sol2, s.hist[0], s.hist[1], s.hist[2], s.E, s.E2, s.acc, s.xs, s.mic, s.mfr};
+  void* ptrs[] = {s.sol, s.sol2, s.hist[0], s.hist[1], s.hist[2], s.acc, s.xs, s.mic, s.mfr};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   if (s.nbuf && s.nbuf != s.hist[0] && s.nbuf != s.hist[1] && s.nbuf != s.hist[2]) (void)hipFree(s.nbuf);
@@ -649,15 +648,6 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
     } else {
       for (int i = 0; i < 3; ++i)
         if ((rc = alloc(c, (void**)&s.hist[i], c->nf * cb))) return rc;
-    }
-    if (k.stepper != SW_STEP_FILTERED_AB3) {
-      const size_t eb = (size_t)c->nf * c->nf * cb;
-      if ((rc = alloc(c, (void**)&s.E, eb))) return rc;
-      if ((rc = alloc(c, (void**)&s.E2, eb))) return rc;
-      // IFMAB3: exp(L dt), exp(2 L dt) (utils/IFMAB3.jl:44-66); IFMRK4: exp(L dt), exp(L dt/2)
-      sw::launch_setup_expm(k.model, g, p, 1.0, s.E, c->stream);
-      sw::launch_setup_expm(k.model, g, p, k.stepper == SW_STEP_IFMAB3 ? 2.0 : 0.5, s.E2, c->stream);
-      HIPCHK(c, hipGetLastError());
     }
   }
   const Geom& g = c->sl[0].g;

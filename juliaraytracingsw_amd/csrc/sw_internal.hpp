@@ -191,102 +191,142 @@ __host__ __device__ inline void qg2_L(const Phys& p, double k, double l, cplx L[
 }
 
 // ---------------------------------------------------------------------------
-// Matrix exponential of a small complex matrix: Padé-13 scaling and squaring
-// (Higham 2005), the algorithm behind Julia's exp for matrices that
-// utils/IFMAB3.jl:26-41 calls per mode.
+// Per-mode integrating factors exp(τ L) (utils/IFMAB3.jl:26-41 computes them
+// with Julia's matrix exp per mode and stores E, E2 arrays).  libsw evaluates
+// them in closed form on the fly inside the stepper update instead — exact
+// up to rounding, like the reference's Padé-13 — so no (nf×nf) operator
+// planes are stored or streamed from HBM (36 F per RSW IFMAB3 step).
 // ---------------------------------------------------------------------------
-template <int n>
-__host__ __device__ inline void mm(const cplx A[n][n], const cplx B[n][n], cplx C[n][n]) {
-  for (int i = 0; i < n; ++i)
-    for (int j = 0; j < n; ++j) {
-      cplx s = cx(0.0);
-      for (int k = 0; k < n; ++k) s = s + A[i][k] * B[k][j];
-      C[i][j] = s;
-    }
+__host__ __device__ inline cplx cconj_(cplx a) { return cplx{a.re, -a.im}; }
+__host__ __device__ inline cplx cexp_(cplx z) {
+  const double e = exp(z.re);
+  return cplx{e * cos(z.im), e * sin(z.im)};
+}
+__host__ __device__ inline cplx csqrt_(cplx z) {
+  const double r = hypot(z.re, z.im);
+  if (r == 0.0) return cplx{0.0, 0.0};
+  double a = sqrt(0.5 * (r + fabs(z.re))), b = 0.5 * z.im / a;
+  if (z.re < 0.0) {
+    const double t = a;
+    a = fabs(b);
+    b = (z.im < 0.0 ? -t : t);
+  }
+  return cplx{a, b};
 }
 
-template <int n>
-__host__ __device__ inline void expm(const cplx Ain[n][n], cplx E[n][n]) {
-  const double b[14] = {64764752532480000.0, 32382376266240000.0, 7771770303897600.0,
-                        1187353796428800.0,  129060195264000.0,   10559470521600.0,
-                        670442572800.0,      33522128640.0,       1323241920.0,
-                        40840800.0,          960960.0,            16380.0,
-                        182.0,               1.0};
-  const double theta13 = 5.371920351148152;
-  double nrm = 0.0;  // 1-norm
-  for (int j = 0; j < n; ++j) {
-    double c = 0.0;
-    for (int i = 0; i < n; ++i) c += hypot(Ain[i][j].re, Ain[i][j].im);
-    nrm = c > nrm ? c : nrm;
+// RSW (rsw/RotatingShallowWater.jl:242-260): L = D I + A with the scalar
+// D = -ν K^(2nν) and A = [[0, f, -ik Cg²], [-f, 0, -il Cg²], [-ik, -il, 0]],
+// whose characteristic polynomial is λ³ + ω² λ (ω² = f² + Cg² K²), so
+//   exp(τ L) = e^(Dτ) (I + sin(ωτ)/ω A + 2 sin²(ωτ/2)/ω² A²).
+struct RswExp {
+  double k, l, e, s, c;
+};
+__host__ __device__ inline RswExp rsw_exp(const Phys& p, double k, double l, double tau) {
+#pragma clang fp contract(off)
+  const double K2 = k * k + l * l;
+  const double D = -(p.nu * ipow(K2, p.nnu));
+  const double w = sqrt(p.f * p.f + p.Cg2 * K2);
+  RswExp E;
+  E.k = k;
+  E.l = l;
+  E.e = exp(D * tau);
+  if (w * tau < 1e-8) {  // A ≈ 0 (f = 0, K = 0): series limits
+    E.s = tau;
+    E.c = 0.5 * tau * tau;
+  } else {
+    const double h = sin(0.5 * w * tau);
+    E.s = sin(w * tau) / w;
+    E.c = 2.0 * h * h / (w * w);
   }
-  int s = 0;
-  if (nrm > theta13) s = (int)ceil(log2(nrm / theta13));
-  const double sc = ldexp(1.0, -s);
-  cplx A[n][n], A2[n][n], A4[n][n], A6[n][n], T[n][n], Uo[n][n], V[n][n];
-  for (int i = 0; i < n; ++i)
-    for (int j = 0; j < n; ++j) A[i][j] = sc * Ain[i][j];
-  mm<n>(A, A, A2);
-  mm<n>(A2, A2, A4);
-  mm<n>(A4, A2, A6);
-  for (int i = 0; i < n; ++i)
-    for (int j = 0; j < n; ++j) T[i][j] = b[13] * A6[i][j] + b[11] * A4[i][j] + b[9] * A2[i][j];
-  mm<n>(A6, T, Uo);
-  for (int i = 0; i < n; ++i)
-    for (int j = 0; j < n; ++j) {
-      Uo[i][j] = Uo[i][j] + b[7] * A6[i][j] + b[5] * A4[i][j] + b[3] * A2[i][j];
-      if (i == j) Uo[i][j] = Uo[i][j] + cx(b[1]);
-    }
-  mm<n>(A, Uo, T);  // T = U
-  cplx W[n][n];
-  for (int i = 0; i < n; ++i)
-    for (int j = 0; j < n; ++j) W[i][j] = b[12] * A6[i][j] + b[10] * A4[i][j] + b[8] * A2[i][j];
-  mm<n>(A6, W, V);
-  for (int i = 0; i < n; ++i)
-    for (int j = 0; j < n; ++j) {
-      V[i][j] = V[i][j] + b[6] * A6[i][j] + b[4] * A4[i][j] + b[2] * A2[i][j];
-      if (i == j) V[i][j] = V[i][j] + cx(b[0]);
-    }
-  // solve (V - U) X = (V + U) by Gaussian elimination with partial pivoting
-  cplx P[n][n], Q[n][n];
-  for (int i = 0; i < n; ++i)
-    for (int j = 0; j < n; ++j) {
-      P[i][j] = V[i][j] - T[i][j];
-      Q[i][j] = V[i][j] + T[i][j];
-    }
-  for (int c = 0; c < n; ++c) {
-    int piv = c;
-    double best = hypot(P[c][c].re, P[c][c].im);
-    for (int r = c + 1; r < n; ++r) {
-      double v = hypot(P[r][c].re, P[r][c].im);
-      if (v > best) { best = v; piv = r; }
-    }
-    if (piv != c) {
-      for (int j = 0; j < n; ++j) {
-        cplx t1 = P[c][j]; P[c][j] = P[piv][j]; P[piv][j] = t1;
-        cplx t2 = Q[c][j]; Q[c][j] = Q[piv][j]; Q[piv][j] = t2;
-      }
-    }
-    for (int r = c + 1; r < n; ++r) {
-      cplx fct = cdiv(P[r][c], P[c][c]);
-      for (int j = c; j < n; ++j) P[r][j] = P[r][j] - fct * P[c][j];
-      for (int j = 0; j < n; ++j) Q[r][j] = Q[r][j] - fct * Q[c][j];
-    }
-  }
-  for (int c = n - 1; c >= 0; --c) {
-    for (int j = 0; j < n; ++j) {
-      cplx s2 = Q[c][j];
-      for (int k = c + 1; k < n; ++k) s2 = s2 - P[c][k] * Q[k][j];
-      Q[c][j] = cdiv(s2, P[c][c]);
-    }
-  }
-  for (int it = 0; it < s; ++it) {
-    mm<n>(Q, Q, T);
-    for (int i = 0; i < n; ++i)
-      for (int j = 0; j < n; ++j) Q[i][j] = T[i][j];
-  }
-  for (int i = 0; i < n; ++i)
-    for (int j = 0; j < n; ++j) E[i][j] = Q[i][j];
+  return E;
 }
+__host__ __device__ inline void rsw_A_mul(const Phys& p, double k, double l, const cplx x[3], cplx y[3]) {
+#pragma clang fp contract(off)
+  // y = A x (complex entries -ik Cg², -il Cg², -ik, -il applied as i·(real))
+  y[0] = cx(p.f * x[1].re + k * p.Cg2 * x[2].im, p.f * x[1].im - k * p.Cg2 * x[2].re);
+  y[1] = cx(-p.f * x[0].re + l * p.Cg2 * x[2].im, -p.f * x[0].im - l * p.Cg2 * x[2].re);
+  y[2] = cx(k * x[0].im + l * x[1].im, -(k * x[0].re) - l * x[1].re);
+}
+__host__ __device__ inline void exp_apply(const Phys& p, const RswExp& E, const cplx x[3], cplx y[3]) {
+#pragma clang fp contract(off)
+  cplx a[3], b[3];
+  rsw_A_mul(p, E.k, E.l, x, a);
+  rsw_A_mul(p, E.k, E.l, a, b);
+  for (int r = 0; r < 3; ++r) {
+    const cplx t = x[r] + E.s * a[r] + E.c * b[r];
+    y[r] = E.e * t;
+  }
+}
+
+// 2LQG (swqg/TwoLayerQG.jl:184-206, incl. the Float32 literals of qg2_L):
+// M = τL = m I + B with m = τ tr(L)/2, B traceless, B² = δ² I,
+//   exp(M) = e^m (cosh δ I + sinh(δ)/δ B).
+struct Qg2Exp {
+  cplx E[2][2];
+};
+__host__ __device__ inline cplx csinhc_(cplx z) {  // sinh(z)/z
+#pragma clang fp contract(off)
+  if (hypot(z.re, z.im) < 0.5) {  // Σ z^(2n)/(2n+1)!, n <= 10
+    const cplx z2 = z * z;
+    cplx r = cx(1.0), t = cx(1.0);
+    for (int n = 1; n <= 10; ++n) {
+      t = (1.0 / ((2.0 * n) * (2.0 * n + 1.0))) * (t * z2);
+      r = r + t;
+    }
+    return r;
+  }
+  const cplx sh = cx(sinh(z.re) * cos(z.im), cosh(z.re) * sin(z.im));
+  return cdiv(sh, z);
+}
+__host__ __device__ inline Qg2Exp qg2_exp(const Phys& p, double k, double l, double tau) {
+#pragma clang fp contract(off)
+  cplx L[2][2];
+  qg2_L(p, k, l, L);
+  const cplx m = (0.5 * tau) * (L[0][0] + L[1][1]);
+  const cplx b00 = (0.5 * tau) * (L[0][0] - L[1][1]);
+  const cplx b01 = tau * L[0][1], b10 = tau * L[1][0];
+  const cplx d = csqrt_(b00 * b00 + b01 * b10);
+  const cplx em = cexp_(m);
+  const cplx ch = cx(cosh(d.re) * cos(d.im), sinh(d.re) * sin(d.im));
+  const cplx sc = csinhc_(d);
+  Qg2Exp X;
+  X.E[0][0] = em * (ch + sc * b00);
+  X.E[1][1] = em * (ch - sc * b00);
+  X.E[0][1] = em * (sc * b01);
+  X.E[1][0] = em * (sc * b10);
+  return X;
+}
+__host__ __device__ inline void exp_apply(const Phys&, const Qg2Exp& X, const cplx x[2], cplx y[2]) {
+#pragma clang fp contract(off)
+  y[0] = X.E[0][0] * x[0] + X.E[0][1] * x[1];
+  y[1] = X.E[1][0] * x[0] + X.E[1][1] * x[1];
+}
+
+// exp(2τL) from exp(τL): RSW re-evaluates its cheap closed form; 2LQG squares
+// the 2×2 matrix (one evaluation of the complex transcendental form per mode)
+__host__ __device__ inline RswExp exp_double(const Phys& p, const RswExp& E, double tau) {
+  return rsw_exp(p, E.k, E.l, 2.0 * tau);
+}
+__host__ __device__ inline Qg2Exp exp_double(const Phys&, const Qg2Exp& X, double) {
+#pragma clang fp contract(off)
+  Qg2Exp Y;
+  for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 2; ++j) Y.E[i][j] = X.E[i][0] * X.E[0][j] + X.E[i][1] * X.E[1][j];
+  return Y;
+}
+
+template <int NF>
+struct ExpOf;
+template <>
+struct ExpOf<3> {
+  using T = RswExp;
+  __host__ __device__ static T make(const Phys& p, double k, double l, double tau) { return rsw_exp(p, k, l, tau); }
+};
+template <>
+struct ExpOf<2> {
+  using T = Qg2Exp;
+  __host__ __device__ static T make(const Phys& p, double k, double l, double tau) { return qg2_exp(p, k, l, tau); }
+};
 
 // ---------------------------------------------------------------------------
 // launchers (sw_kernels.hip)
@@ -306,8 +346,6 @@ struct StepPtrs {
   double2* h0;
   const double2* h1;
   const double2* h2;
-  const double2* E;
-  const double2* E2;
   double2* xs;        // IFMRK4 stages 1-3: the stage input written for the next calcN
   int euler;
   int stage;
@@ -317,8 +355,6 @@ void launch_col_step(int model, int op, const Geom& g, const Phys& p, const Step
                      const double2* Mf, double2* Minv, const double2* tw_y, hipStream_t s);
 void launch_step_elem(int nf, int op, const Geom& g, const Phys& p, const StepPtrs& a,
                       const double2* N, double2* xs, hipStream_t s);
-void launch_setup_expm(int model, const Geom& g, const Phys& p, double factor, double2* E,
-                       hipStream_t s);
 void launch_gather(int nf, const Geom& g, const double2* full, double2* compact, hipStream_t s);
 void launch_scatter(int nf, const Geom& g, int lo, int hi, const double2* compact, double2* full,
                     hipStream_t s);

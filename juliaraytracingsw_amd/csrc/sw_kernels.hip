@@ -507,18 +507,6 @@ __device__ __forceinline__ void model_L(const Phys& p, double k, double l, cplx 
 }
 
 template <int NF>
-__device__ __forceinline__ void load_mat(const double2* __restrict__ E, long long cf, long long i,
-                                         cplx M[NF][NF]) {
-#pragma unroll
-  for (int r = 0; r < NF; ++r)
-#pragma unroll
-    for (int cc = 0; cc < NF; ++cc) {
-      const double2 t = E[(r * NF + cc) * cf + i];
-      M[r][cc] = cx(t.x, t.y);
-    }
-}
-
-template <int NF>
 __device__ __forceinline__ void load_vec(const double2* __restrict__ X, long long cf, long long i,
                                          cplx x[NF]) {
 #pragma unroll
@@ -591,32 +579,32 @@ __device__ __forceinline__ void op_fab3(const Geom& g, const Phys& p, const Step
 }
 
 // utils/IFMAB3.jl:129-160: Euler for step < 3, else AB3 with E N₋₁, E2 N₋₂;
-// then sol = E·(…); filter.  N becomes history.
+// then sol = E·(…); filter.  N becomes history.  E = exp(dt L), E2 =
+// exp(2 dt L) evaluated per mode in closed form (sw_internal.hpp ExpOf).
 template <int NF>
 __device__ __forceinline__ void op_ifmab3(const Geom& g, const Phys& p, const StepPtrs& a, long long i,
                                           double k, double l, const cplx n[NF], cplx x[NF]) {
 #pragma clang fp contract(off)
   const long long cf = g.cfield;
-  cplx M[NF][NF], s[NF], y[NF];
-  load_mat<NF>(a.E, cf, i, M);
+  cplx s[NF], y[NF];
   load_vec<NF>(a.sol, cf, i, s);
   const double dt = p.dt;
+  const auto E = ExpOf<NF>::make(p, k, l, dt);
   if (a.euler) {
 #pragma unroll
     for (int f = 0; f < NF; ++f) y[f] = s[f] + dt * n[f];
   } else {
-    cplx r1[NF], r2[NF], e1[NF], e2[NF], M2[NF][NF];
+    cplx r1[NF], r2[NF], e1[NF], e2[NF];
     load_vec<NF>(a.h1, cf, i, r1);
     load_vec<NF>(a.h2, cf, i, r2);
-    load_mat<NF>(a.E2, cf, i, M2);
-    matvec<NF>(M, r1, e1);
-    matvec<NF>(M2, r2, e2);
+    exp_apply(p, E, r1, e1);
+    exp_apply(p, exp_double(p, E, dt), r2, e2);
 #pragma unroll
     for (int f = 0; f < NF; ++f)
       y[f] = s[f] + dt * cx(23.0 / 12 * n[f].re - 16.0 / 12 * e1[f].re + 5.0 / 12 * e2[f].re,
                             23.0 / 12 * n[f].im - 16.0 / 12 * e1[f].im + 5.0 / 12 * e2[f].im);
   }
-  matvec<NF>(M, y, x);
+  exp_apply(p, E, y, x);
   if (p.use_filter) {
     const double filt = filter_value(g, p, k, l);
 #pragma unroll
@@ -626,7 +614,8 @@ __device__ __forceinline__ void op_ifmab3(const Geom& g, const Phys& p, const St
   store_vec<NF>(a.sol_out, cf, i, x);
 }
 
-// Lawson IF-RK4, one calcN result per stage:
+// Lawson IF-RK4, one calcN result per stage, H = exp(dt L / 2)
+// in closed form, E = exp(dt L) from it (exp_double):
 //   1: k1 -> acc = E k1;          x = H (u + dt/2 k1)
 //   2: k2 -> acc += 2 H k2;       x = H u + dt/2 k2
 //   3: k3 -> acc += 2 H k3;       x = E u + dt H k3
@@ -637,38 +626,34 @@ __device__ __forceinline__ void op_rk4(const Geom& g, const Phys& p, const StepP
 #pragma clang fp contract(off)
   const long long cf = g.cfield;
   const double dt = p.dt;
-  cplx u[NF], M[NF][NF], t[NF], acc[NF];
+  cplx u[NF], t[NF], acc[NF];
   load_vec<NF>(a.sol, cf, i, u);
+  const auto H = ExpOf<NF>::make(p, k, l, 0.5 * dt);
   if (a.stage == 1) {
-    load_mat<NF>(a.E, cf, i, M);
-    matvec<NF>(M, n, acc);
-    load_mat<NF>(a.E2, cf, i, M);
+    exp_apply(p, exp_double(p, H, 0.5 * dt), n, acc);
 #pragma unroll
     for (int f = 0; f < NF; ++f) t[f] = u[f] + (0.5 * dt) * n[f];
-    matvec<NF>(M, t, x);
+    exp_apply(p, H, t, x);
     store_vec<NF>(a.h0, cf, i, acc);
   } else if (a.stage == 2 || a.stage == 3) {
     cplx hk[NF];
     load_vec<NF>(a.h0, cf, i, acc);
-    load_mat<NF>(a.E2, cf, i, M);
-    matvec<NF>(M, n, hk);
+    exp_apply(p, H, n, hk);
 #pragma unroll
     for (int f = 0; f < NF; ++f) acc[f] = acc[f] + 2.0 * hk[f];
     if (a.stage == 2) {
-      matvec<NF>(M, u, t);
+      exp_apply(p, H, u, t);
 #pragma unroll
       for (int f = 0; f < NF; ++f) x[f] = t[f] + (0.5 * dt) * n[f];
     } else {
-      load_mat<NF>(a.E, cf, i, M);
-      matvec<NF>(M, u, t);
+      exp_apply(p, exp_double(p, H, 0.5 * dt), u, t);
 #pragma unroll
       for (int f = 0; f < NF; ++f) x[f] = t[f] + dt * hk[f];
     }
     store_vec<NF>(a.h0, cf, i, acc);
   } else {
     load_vec<NF>(a.h0, cf, i, acc);
-    load_mat<NF>(a.E, cf, i, M);
-    matvec<NF>(M, u, t);
+    exp_apply(p, exp_double(p, H, 0.5 * dt), u, t);
     double filt = 1.0;
     if (p.use_filter) filt = filter_value(g, p, k, l);
 #pragma unroll
@@ -691,7 +676,7 @@ __device__ __forceinline__ void step_op(const Geom& g, const Phys& p, const Step
 // Elementwise (unfused) stepper kernel: N from memory; the stage input x is
 // written to xs (RK4 stages 1-3) for a separate col_inv.
 template <int NF, int OP>
-__global__ void k_step_elem(Geom g, Phys p, StepPtrs a, const double2* __restrict__ N,
+__global__ void __launch_bounds__(256) k_step_elem(Geom g, Phys p, StepPtrs a, const double2* __restrict__ N,
                             double2* __restrict__ xs) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   int kr, j;
@@ -969,27 +954,6 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     fft_line<LOG2N, +1>(v, c.t, tws, line);
     store(3);
   }
-}
-
-// per-mode exp(factor·dt·L) (utils/IFMAB3.jl:32-41), stored [r][c] planes
-template <int NF>
-__global__ void k_setup_expm(Geom g, Phys p, double factor, double2* __restrict__ E) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  int kr, j;
-  if (i >= g.cfield || !mode_of(g, i, kr, j)) return;
-  const double k = kr * g.mk, l = lwav(g, lrow_of(g, j));
-  cplx L[NF][NF], A[NF][NF], X[NF][NF];
-  model_L<NF>(p, k, l, L);
-  const double sdt = factor * p.dt;
-#pragma unroll
-  for (int r = 0; r < NF; ++r)
-#pragma unroll
-    for (int cc = 0; cc < NF; ++cc) A[r][cc] = sdt * L[r][cc];
-  expm<NF>(A, X);
-#pragma unroll
-  for (int r = 0; r < NF; ++r)
-#pragma unroll
-    for (int cc = 0; cc < NF; ++cc) E[(r * NF + cc) * g.cfield + i] = make_double2(X[r][cc].re, X[r][cc].im);
 }
 
 // ===========================================================================
@@ -1349,14 +1313,6 @@ void launch_step_elem(int nf, int op, const Geom& g, const Phys& p, const StepPt
     else SW_SE(2, OP_RK4);
   }
 #undef SW_SE
-}
-
-void launch_setup_expm(int model, const Geom& g, const Phys& p, double factor, double2* E,
-                       hipStream_t s) {
-  if (model == MODEL_RSW)
-    hipLaunchKernelGGL(k_setup_expm<3>, mode_grid(g), dim3(256), 0, s, g, p, factor, E);
-  else
-    hipLaunchKernelGGL(k_setup_expm<2>, mode_grid(g), dim3(256), 0, s, g, p, factor, E);
 }
 
 void launch_gather(int nf, const Geom& g, const double2* full, double2* cmp, hipStream_t s) {
