@@ -32,6 +32,10 @@ def b_alg(model, stepper, n):
     bT = 16 * Ns + 8 * Np
     if model == "rsw":
         return 13 * bT + (18 if stepper == "FilteredAB3" else 15) * 16 * Ns
+    if model == "ty":
+        # 4 calcN of 11 c2r + 13 r2c (thomasyamada/ThomasYamada.jl:129-262) and
+        # 4 ETDRK4 stages of (3.75·4 state + 4 N) fields + 1.25 coefficient planes
+        return 96 * bT + 4 * (4.75 * 4 + 1.25) * 16 * Ns
     if stepper == "IFMRK4":
         return 40 * bT + 30 * 16 * Ns
     return 10 * bT + 10 * 16 * Ns
@@ -46,10 +50,11 @@ def cpu_baseline(model, stepper, n, budget_s=20.0, max_steps=20):
 
     cores = min(16, len(os.sched_getaffinity(0)))
     O.set_fft_workers(cores)
-    p = sw_cases.case_params(f"{model}_{ {'FilteredAB3': 'fab3', 'IFMAB3': 'ifmab3', 'IFMRK4': 'ifmrk4'}[stepper]}", n)
+    short = {'FilteredAB3': 'fab3', 'IFMAB3': 'ifmab3', 'IFMRK4': 'ifmrk4', 'ETDRK4': 'etdrk4'}[stepper]
+    p = sw_cases.case_params(f"{model}_{short}", n)
     pr = sw_cases.oracle_problem(p)
     pr.set_solution(sw_cases.initial_condition(p, pr.grid))
-    pr.stepforward(3)  # the Euler start-up steps, untimed
+    pr.stepforward(3)  # the Euler start-up steps (AB3 steppers), untimed
     t0 = time.perf_counter()
     k = 0
     while k < max_steps and (time.perf_counter() - t0) < budget_s:
@@ -58,8 +63,8 @@ def cpu_baseline(model, stepper, n, budget_s=20.0, max_steps=20):
     dt = time.perf_counter() - t0
     O.set_fft_workers(None)
     return dict(value=k / dt, unit="timesteps/s", cores=cores, kind="port",
-                sample=f"{k} AB3 steps of the {n}² oracle restatement (numpy elementwise + scipy.fft "
-                       f"workers={cores}) after 3 untimed Euler steps")
+                sample=f"{k} {stepper} steps of the {n}² oracle restatement (numpy elementwise + scipy.fft "
+                       f"workers={cores}) after 3 untimed steps")
 
 
 def main():
@@ -68,8 +73,8 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--n", type=int, default=2048)
-    ap.add_argument("--model", default="rsw", choices=["rsw", "qg2"])
-    ap.add_argument("--stepper", default="FilteredAB3", choices=["FilteredAB3", "IFMAB3", "IFMRK4"])
+    ap.add_argument("--model", default="rsw", choices=["rsw", "qg2", "ty"])
+    ap.add_argument("--stepper", default="FilteredAB3", choices=["FilteredAB3", "IFMAB3", "IFMRK4", "ETDRK4"])
     ap.add_argument("--profile-steps", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", default="ensemble", choices=["ensemble", "slab"])
@@ -99,8 +104,12 @@ def main():
 
     slab = args.mode == "slab" and world > 1
     dec = slab_comm.rccl_decomposition(rank, world) if slab else None
+    if args.model == "ty":
+        args.stepper = "ETDRK4"  # the only Thomas-Yamada stepper
     if args.model == "rsw":
         prob, P = drivers.rsw_problem(args.n, args.stepper, device=local, decomposition=dec)
+    elif args.model == "ty":
+        prob, P = drivers.ty_problem(args.n, device=local, decomposition=dec)
     else:
         prob, P = drivers.qg2_problem(args.n, args.stepper, device=local, decomposition=dec)
 
@@ -158,8 +167,9 @@ def main():
         "scaling": "strong" if slab else "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic random-phase IC (set_shafer_initial_condition!, seeded)" if args.model == "rsw"
-                else "synthetic randn PV IC (set_seed_initial_condition!, seeded)",
+        "data": {"rsw": "synthetic random-phase IC (set_shafer_initial_condition!, seeded)",
+                 "qg2": "synthetic randn PV IC (set_seed_initial_condition!, seeded)",
+                 "ty": "synthetic random-phase IC (TYdriver set_initial_condition, seeded)"}[args.model],
         "config": {"workload": f"{args.model.upper()} {args.n}^2 {args.stepper} fp64 step, dt={P['dt']:.6g}",
                    "grid": args.n,
                    "parallelism": (f"slab{world}" if slab else f"ensemble{world}") if world > 1 else "single-gpu"},

@@ -32,16 +32,19 @@
 extern "C" {
 #endif
 
-#define SW_ABI_VERSION 2
+#define SW_ABI_VERSION 3
 
 /* models */
 #define SW_MODEL_RSW 0   /* rsw/RotatingShallowWater.jl: fields (u, v, η), 3×3 L   */
 #define SW_MODEL_QG2 1   /* swqg/TwoLayerQG.jl: fields (q1, q2), 2×2 L             */
+#define SW_MODEL_TY  2   /* thomasyamada/ThomasYamada.jl: fields (ζ_T, u_c, v_c, p_c),
+                            real diagonal L = -ν K^(2nν), stepper ETDRK4 */
 
 /* steppers */
 #define SW_STEP_FILTERED_AB3 0 /* FF FilteredAB3 with per-mode matvec L·sol */
 #define SW_STEP_IFMAB3       1 /* utils/IFMAB3.jl:68-169                               */
 #define SW_STEP_IFMRK4       2 /* Lawson IF-RK4, the build's definition of utils/IFMRK4.jl (A9) */
+#define SW_STEP_ETDRK4       3 /* FF ETDRK4TimeStepper (ThomasYamada.Problem default, :60) */
 
 /* error codes */
 #define SW_OK            0
@@ -54,7 +57,9 @@ extern "C" {
 
 /* physical-field ids for sw_get_physical (updatevars! equivalents)
  * RSW (rsw/RotatingShallowWater.jl:101-116): u, v, η, ζ=∂x v − ∂y u − f η
- * QG2 (swqg/TwoLayerQG.jl:113-129), per layer (layer = id / 8): q, ψ, ζ, u, v */
+ * QG2 (swqg/TwoLayerQG.jl:113-129), per layer (layer = id / 8): q, ψ, ζ, u, v
+ * TY  (thomasyamada/ThomasYamada.jl:67-92): 0 u_c, 1 v_c, 2 p_c, 3 ζ_T, 4 q_c,
+ *     5 ψ_T, 8 u_T, 9 v_T */
 #define SW_PHYS_U     0
 #define SW_PHYS_V     1
 #define SW_PHYS_ETA   2
@@ -71,6 +76,11 @@ extern "C" {
                             swqg/TwoLayerDriver.jl:100-101)                  */
 #define SW_DIAG_KE2   4  /* QG2: KE of layer 2 alone (the tuple's 2nd entry) */
 #define SW_DIAG_KE1   5  /* QG2: KE of layer 1 alone (the tuple's 1st entry) */
+/* TY (thomasyamada/ThomasYamada.jl:333-345): SW_DIAG_KE = baroclinic_energy[1]
+ * (|u_c|² + |v_c|²), SW_DIAG_PE = baroclinic_energy[2] (|p_c|²), SW_DIAG_BT =
+ * barotropic_energy; SW_DIAG_CFL = dt · max of maximum(u_c)/dx, maximum(v_c)/dy,
+ * maximum(u_T)/dx, maximum(v_T)/dy (signed maxima, thomasyamada/TYdriver.jl:150) */
+#define SW_DIAG_BT    6
 
 /* Host-staged transport (optional, one slab per process).  When set, libsw
  * moves every inter-slab exchange through host memory and calls
@@ -120,6 +130,8 @@ typedef struct sw_config {
   const void* comm_unique_id; /* ncclUniqueId bytes (128), from sw_comm_unique_id */
   sw_exchange_fn exchange;    /* optional host-staged transport instead of RCCL */
   void* exchange_user;
+  /* physics — TY Params (thomasyamada/ThomasYamada.jl:21-25)               */
+  double  Ro;               /* Rossby number                               */
 } sw_config;
 
 typedef struct sw_ctx sw_ctx;
@@ -178,9 +190,10 @@ int sw_diag(sw_ctx* ctx, int32_t diag_id, double* out);
 typedef struct sw_energy_record {
   int64_t step;            /* clock.step after the step                     */
   double  t;               /* clock.t after the step                        */
-  double  ke;              /* RSW: kinetic energy; QG2: KE of layer 1       */
-  double  ke2;             /* QG2: KE of layer 2 (0 for RSW)                */
-  double  pe;              /* potential energy                              */
+  double  ke;              /* RSW: kinetic energy; QG2: KE of layer 1;
+                              TY: baroclinic kinetic (|u_c|² + |v_c|²)      */
+  double  ke2;             /* QG2: KE of layer 2 (0 for RSW); TY: barotropic */
+  double  pe;              /* potential energy (TY: baroclinic |p_c|²)       */
 } sw_energy_record;
 int sw_set_energy_diagnostics(sw_ctx* ctx, int64_t freq, int64_t capacity);
 /* Copies up to max_records records (oldest first); *n_records = the count.

@@ -36,6 +36,8 @@ struct Slab {
   double2* acc = nullptr;                    // IFMRK4 running stage combination
   double2* nbuf = nullptr;                   // unfused IFMRK4 / sw_calcN: calcN output
   double2* xs = nullptr;                     // stage input / scratch compact
+  double2* xs2 = nullptr;                    // ETDRK4: second stage input s₂ (aliases hist[2])
+  double* etd = nullptr;                     // ETDRK4: per-mode coefficients [ETD_N][cfield]
   double2* mic = nullptr;                    // calcN inputs, column phase (col_inv / col_step out)
   double2* mir = nullptr;                    // calcN inputs, row phase (row in)
   double2* mfr = nullptr;                    // row outputs, row phase
@@ -197,6 +199,10 @@ const char* kname[K_NKERN] = {"col_inv", "row", "col_fwd", "update", "col_step",
 double op_fields(const sw_ctx* c) {
   // the integrating factors are evaluated per mode, never stored (sw_internal.hpp ExpOf)
   const int nf = c->nf, st = c->cfg.stepper;
+  // ETDRK4 stages: 1 u in / n1,acc,s1 out; 2 u in / n2,s2 out; 3 s1,acc,n1,n2
+  // in / acc,s2 out; 4 acc in / u out; plus the coefficient planes (real: half
+  // a field each) 4, 2, 3, 1
+  if (st == SW_STEP_ETDRK4) return (4.0 * nf + 3.0 * nf + 6.0 * nf + 2.0 * nf) / 4 + (2.0 + 1.0 + 1.5 + 0.5) / 4;
   if (st == SW_STEP_FILTERED_AB3) return 3 * nf + 2 * nf;  // sol,R-1,R-2 in; sol,RHS out
   if (st == SW_STEP_IFMAB3) return 3 * nf + 2 * nf;        // sol,N-1,N-2 in; sol,N out
   // stages: 1 u in / acc,x out; 2-3 u,acc in / acc,x out; 4 u,acc in / u out
@@ -317,7 +323,7 @@ int calcN(sw_ctx* c, double2* Slab::*X, double2* Slab::*N) {
   if (int rc = transpose(c, false, c->nfwd)) return rc;
   {
     Timer tm(c, K_COLFWD);
-    for (Slab& s : c->sl) sw::launch_col_fwd(model, s.g, c->p, s.mfc, s.*N, c->tw_y, c->stream);
+    for (Slab& s : c->sl) sw::launch_col_fwd(model, s.g, c->p, s.mfc, s.*N, s.*X, c->tw_y, c->stream);
   }
   return 0;
 }
@@ -333,7 +339,7 @@ int calcN(sw_ctx* c, double2* Slab::*X, double2* Slab::*N) {
 // re-evaluates the coupled update in every group measured slower at 2048²
 // than the separate kernels.
 bool use_fused(const sw_ctx* c) {
-  if (c->cfg.unfused || c->cfg.nop_calcN) return false;
+  if (c->cfg.unfused || c->cfg.nop_calcN || c->cfg.model == SW_MODEL_TY) return false;
   if (c->fuse_all) return true;
   return c->cfg.model == SW_MODEL_RSW && c->cfg.stepper == SW_STEP_FILTERED_AB3;
 }
@@ -347,6 +353,12 @@ sw::StepPtrs step_ptrs(const sw_ctx* c, const Slab& s) {
   a.euler = c->step < 3 ? 1 : 0;
   if (st == SW_STEP_IFMRK4) {
     a.h0 = s.acc;
+  } else if (st == SW_STEP_ETDRK4) {
+    a.h0 = s.acc;
+    a.n1 = s.hist[0];
+    a.n2 = s.hist[1];
+    a.xs2 = s.xs2;
+    a.etd = s.etd;
   } else {
     a.h0 = s.hist[c->head];
     a.h1 = s.hist[(c->head + 2) % 3];
@@ -383,7 +395,7 @@ int run_stage(sw_ctx* c, int op, int stage, double2* Slab::*X) {
   } else {
     // AB3 steppers: calcN writes straight into this step's history slot, which
     // the update then overwrites in place (N -> RHS or N); nbuf aliases it
-    if (op != sw::OP_RK4)
+    if (op != sw::OP_RK4 && op != sw::OP_ETDRK4)
       for (Slab& s : c->sl) s.nbuf = s.hist[c->head];
     if (int rc = calcN(c, X, &Slab::nbuf)) return rc;
     Timer tm(c, K_UPD);
@@ -424,6 +436,11 @@ int step_once(sw_ctx* c) {
     c->head = (c->head + 1) % 3;  // RHS₋₂ <- RHS₋₁ <- RHS by rotation (utils/IFMAB3.jl:165-166)
     if (st == SW_STEP_FILTERED_AB3)
       for (Slab& s : c->sl) std::swap(s.sol, s.sol2);
+  } else if (st == SW_STEP_ETDRK4) {  // FF ETDRK4substeps! + ETDRK4update!
+    for (int stage = 1; stage <= 4; ++stage)
+      if (int rc = run_stage(c, sw::OP_ETDRK4, stage,
+                             stage == 1 ? &Slab::sol : (stage == 2 ? &Slab::xs : &Slab::xs2)))
+        return rc;
   } else {  // IFMRK4
     for (int stage = 1; stage <= 4; ++stage)
       if (int rc = run_stage(c, sw::OP_RK4, stage, stage == 1 ? &Slab::sol : &Slab::xs)) return rc;
@@ -516,7 +533,7 @@ int nan_flag(sw_ctx* c, int& h) {
 }
 
 void free_slab(Slab& s) {
-  void* ptrs[] = {s.sol, s.sol2, s.hist[0], s.hist[1], s.hist[2], s.acc, s.xs, s.mic, s.mfr};
+  void* ptrs[] = {s.sol, s.sol2, s.hist[0], s.hist[1], s.hist[2], s.acc, s.xs, s.mic, s.mfr, s.etd};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   if (s.nbuf && s.nbuf != s.hist[0] && s.nbuf != s.hist[1] && s.nbuf != s.hist[2]) (void)hipFree(s.nbuf);
@@ -566,8 +583,11 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   c->cfg = *cfg;
   *out = c;
   const sw_config& k = c->cfg;
-  if (k.model != SW_MODEL_RSW && k.model != SW_MODEL_QG2) return fail(c, SW_E_INVALID, "unknown model");
-  if (k.stepper < 0 || k.stepper > 2) return fail(c, SW_E_INVALID, "unknown stepper");
+  if (k.model != SW_MODEL_RSW && k.model != SW_MODEL_QG2 && k.model != SW_MODEL_TY)
+    return fail(c, SW_E_INVALID, "unknown model");
+  if (k.stepper < 0 || k.stepper > 3) return fail(c, SW_E_INVALID, "unknown stepper");
+  if ((k.model == SW_MODEL_TY) != (k.stepper == SW_STEP_ETDRK4))
+    return fail(c, SW_E_INVALID, "ETDRK4 (diagonal L) is the Thomas-Yamada stepper and TY steps with ETDRK4 only");
   if (!pow2(k.nx) || !pow2(k.ny) || k.nx < 32 || k.ny < 32 || k.nx > 8192 || k.ny > 8192)
     return fail(c, SW_E_INVALID, "nx, ny must be powers of two in [32, 8192]");
   if (!(k.aliased_fraction > 0 && k.aliased_fraction < 1))
@@ -613,17 +633,19 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   p.U = k.U;
   p.mu = k.mu;
   p.F = k.F;
+  p.Ro = k.Ro;
   p.dt = k.dt;
   p.use_filter = (k.stepper == SW_STEP_FILTERED_AB3) ? 1 : (k.use_filter ? 1 : 0);
   p.forder = k.filter_order;
   p.innerK = k.filter_innerK;
   p.decay = -std::log(k.filter_tol) / std::pow(k.filter_outerK - k.filter_innerK, (double)k.filter_order);
 
-  c->nf = k.model == SW_MODEL_RSW ? 3 : 2;
+  c->nf = k.model == SW_MODEL_RSW ? 3 : (k.model == SW_MODEL_TY ? 4 : 2);
   // mixed fields per calcN: RSW U,V,H,Uy in / P,K,ζu,Q,vη out;
-  // QG2 Q,Ψ,Ψy per layer in / ψx q, ψy q per layer out
-  c->ninv = k.model == SW_MODEL_RSW ? 4 : 6;
-  c->nfwd = k.model == SW_MODEL_RSW ? 5 : 4;
+  // QG2 Q,Ψ,Ψy per layer in / ψx q, ψy q per layer out; TY ζ,ψ,ût,∂y ut,
+  // uc,∂y uc,vc,pc,∂y pc in / 7 combined product spectra out (k_row)
+  c->ninv = k.model == SW_MODEL_RSW ? 4 : (k.model == SW_MODEL_TY ? 9 : 6);
+  c->nfwd = k.model == SW_MODEL_RSW ? 5 : (k.model == SW_MODEL_TY ? 7 : 4);
 
   int rc;
   for (Slab& s : c->sl) {
@@ -642,10 +664,18 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
       if ((rc = alloc(c, (void**)&s.mir, c->ninv * mb))) return rc;
       if ((rc = alloc(c, (void**)&s.mfc, c->nfwd * mb))) return rc;
     }
-    if (k.stepper == SW_STEP_IFMRK4) {
+    if (k.stepper == SW_STEP_IFMRK4 || k.stepper == SW_STEP_ETDRK4) {
       if ((rc = alloc(c, (void**)&s.acc, c->nf * cb))) return rc;
       if ((rc = alloc(c, (void**)&s.nbuf, c->nf * cb))) return rc;
-    } else {
+    }
+    if (k.stepper == SW_STEP_ETDRK4) {  // N₁, N₂, s₂ and the coefficient table
+      for (int i = 0; i < 3; ++i)
+        if ((rc = alloc(c, (void**)&s.hist[i], c->nf * cb))) return rc;
+      s.xs2 = s.hist[2];
+      if ((rc = alloc(c, (void**)&s.etd, (size_t)sw::ETD_N * g.cfield * sizeof(double)))) return rc;
+      sw::launch_etd_coeffs(g, c->p, s.etd, c->stream);
+      HIPCHK(c, hipGetLastError());
+    } else if (k.stepper != SW_STEP_IFMRK4) {
       for (int i = 0; i < 3; ++i)
         if ((rc = alloc(c, (void**)&s.hist[i], c->nf * cb))) return rc;
     }
@@ -773,7 +803,7 @@ int sw_calcN(sw_ctx* c, const void* sol, void* N, size_t bytes) {
   for (Slab& s : c->sl) {
     sw::launch_gather(c->nf, s.g, c->stage, s.xs, c->stream);
     // scratch output: the ring slot that the next step overwrites anyway
-    if (c->cfg.stepper != SW_STEP_IFMRK4) s.nbuf = s.hist[c->head];
+    if (c->cfg.stepper != SW_STEP_IFMRK4 && c->cfg.stepper != SW_STEP_ETDRK4) s.nbuf = s.hist[c->head];
   }
   if (int rc = calcN(c, &Slab::xs, &Slab::nbuf)) return rc;
   if (int rc = collect_full(c, &Slab::nbuf)) return rc;
@@ -799,6 +829,7 @@ static int physical_to_dflt(sw_ctx* c, int32_t fid) {
 static bool valid_phys_id(const sw_ctx* c, int32_t fid) {
   const int id = fid & 7, layer = fid >> 3;
   if (c->cfg.model == SW_MODEL_RSW) return fid >= 0 && fid <= 3;
+  if (c->cfg.model == SW_MODEL_TY) return (fid >= 0 && fid <= 5) || fid == 8 || fid == 9;
   return fid >= 0 && layer <= 1 && id != SW_PHYS_ETA && id <= 5;
 }
 
@@ -808,7 +839,9 @@ int sw_get_physical(sw_ctx* c, int32_t fid, double* out, size_t bytes) {
   if (!out || bytes != (size_t)g0.nx * g0.ny * sizeof(double))
     return fail(c, SW_E_INVALID, "sw_get_physical: size mismatch");
   if (!valid_phys_id(c, fid))
-    return fail(c, SW_E_INVALID, c->cfg.model == SW_MODEL_RSW ? "RSW physical ids are 0..3" : "bad QG2 physical id");
+    return fail(c, SW_E_INVALID, c->cfg.model == SW_MODEL_RSW ? "RSW physical ids are 0..3"
+                                 : c->cfg.model == SW_MODEL_TY ? "TY physical ids are 0..5, 8, 9"
+                                                               : "bad QG2 physical id");
   HIPCHK(c, hipSetDevice(c->cfg.device));
   if (int rc = physical_to_dflt(c, fid)) return rc;
   if (c->dist) {
@@ -818,6 +851,14 @@ int sw_get_physical(sw_ctx* c, int32_t fid, double* out, size_t bytes) {
   HIPCHK(c, hipMemcpyAsync(out, c->dflt, bytes, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return SW_OK;
+}
+
+// k_absmax's order-preserving key -> the double
+static double key_double(unsigned long long k) {
+  const unsigned long long b = (k >> 63) ? (k & ~0x8000000000000000ull) : ~k;
+  double d;
+  std::memcpy(&d, &b, sizeof(d));
+  return d;
 }
 
 // energy sums (k_energy_partial triples) -> (KE, KE2, PE)
@@ -830,6 +871,11 @@ static void energies_from_sums(const sw_ctx* c, const double a[3], double& ke, d
     ke = norm * a[0] / (2 * g.Lx * g.Ly);
     ke2 = 0.0;
     pe = 0.5 * c->p.Cg2 * norm * a[1] / (g.Lx * g.Ly);
+  } else if (c->cfg.model == SW_MODEL_TY) {
+    // thomasyamada/ThomasYamada.jl:333-345: plain parsevalsum2 values
+    ke = norm * a[1];
+    ke2 = norm * a[0];
+    pe = norm * a[2];
   } else {
     ke = norm * a[0] / (g.Lx * g.Ly);
     ke2 = norm * a[1] / (g.Lx * g.Ly);
@@ -881,38 +927,44 @@ int sw_diag(sw_ctx* c, int32_t id, double* out) {
   }
   if (id == SW_DIAG_CFL) {
     // rsw/RSWDriver.jl:207-208, swqg/TwoLayerDriver.jl:100-101:
-    // dt · max(maximum(|vars.u|)/dx, maximum(|vars.v|)/dy), both layers for 2LQG
+    // dt · max(maximum(|vars.u|)/dx, maximum(|vars.v|)/dy), both layers for 2LQG;
+    // thomasyamada/TYdriver.jl:150: signed maxima of u_c, v_c, u_T, v_T
     const Geom& g0 = c->sl[0].g;
+    const bool ty = c->cfg.model == SW_MODEL_TY;
     const int nlay = c->cfg.model == SW_MODEL_RSW ? 1 : 2;
-    unsigned long long* mx = reinterpret_cast<unsigned long long*>(c->flag + 512);  // [u, v] maxima
+    unsigned long long* mx = reinterpret_cast<unsigned long long*>(c->flag + 512);  // [u, v] maxima keys
     HIPCHK(c, hipMemsetAsync(mx, 0, 2 * sizeof(unsigned long long), c->stream));
     const size_t off = c->dist ? (size_t)g0.y0 * g0.nx : 0;
     const long long n = (long long)(c->dist ? g0.nyl : g0.ny) * g0.nx;
     for (int layer = 0; layer < nlay; ++layer)
       for (int comp = 0; comp < 2; ++comp) {
         if (int rc = physical_to_dflt(c, layer * 8 + (comp == 0 ? SW_PHYS_U : SW_PHYS_V))) return rc;
-        sw::launch_absmax(c->dflt + off, n, mx + comp, c->stream);
+        sw::launch_absmax(c->dflt + off, n, mx + comp, ty ? 1 : 0, c->stream);
       }
     HIPCHK(c, hipGetLastError());
-    double m[2] = {0.0, 0.0};
+    unsigned long long kmax[2] = {0, 0};
     if (c->dist) {
-      std::vector<double> all(2 * (size_t)c->P);
-      if (int rc = allgather(c, mx, c->esum, 2 * sizeof(double))) return rc;
-      HIPCHK(c, hipMemcpyAsync(all.data(), c->esum, all.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+      std::vector<unsigned long long> all(2 * (size_t)c->P);
+      if (int rc = allgather(c, mx, c->esum, 2 * sizeof(unsigned long long))) return rc;
+      HIPCHK(c, hipMemcpyAsync(all.data(), c->esum, all.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                               c->stream));
       HIPCHK(c, hipStreamSynchronize(c->stream));
       for (int q = 0; q < c->P; ++q) {
-        m[0] = std::max(m[0], all[2 * q]);
-        m[1] = std::max(m[1], all[2 * q + 1]);
+        kmax[0] = std::max(kmax[0], all[2 * q]);
+        kmax[1] = std::max(kmax[1], all[2 * q + 1]);
       }
     } else {
-      HIPCHK(c, hipMemcpyAsync(m, mx, 2 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipMemcpyAsync(kmax, mx, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
       HIPCHK(c, hipStreamSynchronize(c->stream));
     }
-    *out = c->cfg.dt * std::max(m[0] / g0.dx, m[1] / g0.dy);
+    *out = c->cfg.dt * std::max(key_double(kmax[0]) / g0.dx, key_double(kmax[1]) / g0.dy);
     return SW_OK;
   }
-  if (id != SW_DIAG_KE && id != SW_DIAG_PE && id != SW_DIAG_KE1 && id != SW_DIAG_KE2)
+  if (id != SW_DIAG_KE && id != SW_DIAG_PE && id != SW_DIAG_KE1 && id != SW_DIAG_KE2 && id != SW_DIAG_BT)
     return fail(c, SW_E_INVALID, "unknown diagnostic");
+  if ((id == SW_DIAG_BT && c->cfg.model != SW_MODEL_TY) ||
+      ((id == SW_DIAG_KE1 || id == SW_DIAG_KE2) && c->cfg.model == SW_MODEL_TY))
+    return fail(c, SW_E_INVALID, "diagnostic not defined for this model");
   for (Slab& s : c->sl) sw::launch_energy_cols(c->cfg.model, s.g, c->p, s.sol, c->ecols + 3 * s.g.kr0, c->stream);
   if (c->dist) {
     const Geom& g0 = c->sl[0].g;
@@ -925,8 +977,10 @@ int sw_diag(sw_ctx* c, int32_t id, double* out) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   double ke, ke2, pe;
   energies_from_sums(c, sums.data(), ke, ke2, pe);
-  // RSW KE; 2LQG KE = KE_1 + KE_2 (the driver's tuple summed), KE2 = KE_2
-  if (id == SW_DIAG_KE) *out = ke + ke2;
+  // RSW KE; 2LQG KE = KE_1 + KE_2 (the driver's tuple summed), KE2 = KE_2;
+  // TY: KE, PE the baroclinic pair, BT barotropic
+  if (c->cfg.model == SW_MODEL_TY) *out = id == SW_DIAG_KE ? ke : (id == SW_DIAG_BT ? ke2 : pe);
+  else if (id == SW_DIAG_KE) *out = ke + ke2;
   else if (id == SW_DIAG_KE1) *out = ke;
   else if (id == SW_DIAG_KE2) *out = ke2;
   else *out = pe;

@@ -10,8 +10,8 @@
 
 namespace sw {
 
-enum { MODEL_RSW = 0, MODEL_QG2 = 1 };
-enum { ST_FAB3 = 0, ST_IFMAB3 = 1, ST_IFMRK4 = 2 };
+enum { MODEL_RSW = 0, MODEL_QG2 = 1, MODEL_TY = 2 };
+enum { ST_FAB3 = 0, ST_IFMAB3 = 1, ST_IFMRK4 = 2, ST_ETDRK4 = 3 };
 
 // Grid geometry of one slab in the layouts of DESIGN.md §2 and §6.
 // Slab s of P owns kr columns [kr0, kr0 + kcl) in the column passes and
@@ -43,6 +43,7 @@ struct Phys {
   double f, Cg2, nu;  // RSW
   int nnu;
   double U, mu, F;    // QG2
+  double Ro;          // TY Rossby number
   // filter (FF makefilter)
   int use_filter, forder;
   double innerK, decay;
@@ -337,8 +338,9 @@ void launch_col_inv(int model, const Geom& g, const Phys& p, const double2* X, d
                     const double2* tw_y, hipStream_t s);
 void launch_row(int model, const Geom& g, const Phys& p, const double2* Minv, double2* Mfwd,
                 const double2* tw_x, hipStream_t s);
+// X: the compact calcN input (TY adds its linear terms from it; unused otherwise)
 void launch_col_fwd(int model, const Geom& g, const Phys& p, const double2* Mfwd, double2* N,
-                    const double2* tw_y, hipStream_t s);
+                    const double2* X, const double2* tw_y, hipStream_t s);
 // Pointers of one stepper stage (see sw_kernels.hip).
 struct StepPtrs {
   const double2* sol;  // state in
@@ -349,8 +351,15 @@ struct StepPtrs {
   double2* xs;        // IFMRK4 stages 1-3: the stage input written for the next calcN
   int euler;
   int stage;
+  // ETDRK4 (FF ETDRK4TimeStepper): N₁, N₂, the second stage input s₂ and
+  // the per-mode coefficient table [E, E2, ζ, α, β, Γ][cfield]
+  double2* n1;
+  double2* n2;
+  double2* xs2;
+  const double* etd;
 };
-enum { OP_FAB3 = 0, OP_IFMAB3 = 1, OP_RK4 = 2 };
+enum { OP_FAB3 = 0, OP_IFMAB3 = 1, OP_RK4 = 2, OP_ETDRK4 = 3 };
+enum { ETD_E = 0, ETD_E2, ETD_ZETA, ETD_ALPHA, ETD_BETA, ETD_GAMMA, ETD_N };
 void launch_col_step(int model, int op, const Geom& g, const Phys& p, const StepPtrs& a,
                      const double2* Mf, double2* Minv, const double2* tw_y, hipStream_t s);
 void launch_step_elem(int nf, int op, const Geom& g, const Phys& p, const StepPtrs& a,
@@ -369,6 +378,9 @@ void launch_row_c2r1(const Geom& g, const double2* M, double* out, const double2
 void launch_energy_cols(int model, const Geom& g, const Phys& p, const double2* sol, double* cols,
                         hipStream_t s);
 void launch_energy_final(const double* cols, int ncols, double* out, hipStream_t s);
-void launch_absmax(const double* f, long long n, unsigned long long* out, hipStream_t s);
+// max |f| (sgn = 0) or max f (sgn = 1) as an order-preserving integer key
+void launch_absmax(const double* f, long long n, unsigned long long* out, int sgn, hipStream_t s);
+// ETDRK4 coefficient table of the real diagonal L = -ν K^(2nν) (FF getetdcoeffs)
+void launch_etd_coeffs(const Geom& g, const Phys& p, double* etd, hipStream_t s);
 
 }  // namespace sw

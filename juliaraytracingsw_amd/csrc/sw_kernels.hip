@@ -114,6 +114,68 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
       fft_line<LOG2N, +1>(v, c.t, tws, line);
       store(3);
     }
+  } else if constexpr (MODEL == MODEL_TY) {
+    // thomasyamada/ThomasYamada.jl:129-262.  Group → (input field, outputs):
+    //   0: ζ  → 0 ζ, 1 ψ = -ζ/K²        1: ζ  → 2 ût = -il ψ, 3 ∂y ut = l² ψ
+    //   2: uc → 4 uc, 5 il uc           3: vc → 6 vc
+    //   4: pc → 7 pc, 8 il pc
+    // (x-derivatives ik·… are formed in the row pass, where k is constant)
+    const int fin = grp <= 1 ? 0 : grp - 1;
+    const double2* Xf = X + (long long)fin * g.cfield + (long long)krc * g.LrP;
+    double2 x[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int m = c.t + s * NT;
+      const int j = compact_of(g, m);
+      const double2 t = Xf[j >= 0 ? j : 0];
+      x[s] = (live && j >= 0) ? t : zero2();
+      if (grp <= 1) {  // ψ = -ζ invKrsq (:125-127)
+        const double l = lwav(g, m);
+        const double K2 = k * k + l * l;
+        const double iK2 = K2 == 0.0 ? 0.0 : 1.0 / K2;
+        const double2 ps = make_double2(-x[s].x * iK2, -x[s].y * iK2);
+        if (grp == 1) x[s] = ps;
+        else v[s] = ps;
+      }
+    }
+    if (grp == 0) {
+      double2 psi[8];
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        psi[s] = v[s];
+        v[s] = cscale(x[s], scale);
+      }
+      fft_line<LOG2N, +1>(v, c.t, tws, line);
+      store(0);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) v[s] = cscale(psi[s], scale);
+      fft_line<LOG2N, +1>(v, c.t, tws, line);
+      store(1);
+    } else if (grp == 1) {  // x = ψ
+#pragma unroll
+      for (int s = 0; s < 8; ++s) v[s] = cmul_i(x[s], -lwav(g, c.t + s * NT) * scale);
+      fft_line<LOG2N, +1>(v, c.t, tws, line);
+      store(2);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const double l = lwav(g, c.t + s * NT);
+        v[s] = cscale(x[s], (l * l) * scale);
+      }
+      fft_line<LOG2N, +1>(v, c.t, tws, line);
+      store(3);
+    } else {
+      const int o = grp == 2 ? 4 : (grp == 3 ? 6 : 7);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) v[s] = cscale(x[s], scale);
+      fft_line<LOG2N, +1>(v, c.t, tws, line);
+      store(o);
+      if (grp != 3) {  // ∂y uc, ∂y pc
+#pragma unroll
+        for (int s = 0; s < 8; ++s) v[s] = cmul_i(x[s], lwav(g, c.t + s * NT) * scale);
+        fft_line<LOG2N, +1>(v, c.t, tws, line);
+        store(o + 1);
+      }
+    }
   } else {
     // streamfunctionfrompv! (swqg/TwoLayerQG.jl:101-111)
     const double2* X1 = X + (long long)krc * g.LrP;
@@ -182,6 +244,44 @@ __device__ __forceinline__ void load_pair(double2 (&v)[8], int t, const Geom& g,
       aa = cmul_i(aa, kw);
       bb = cmul_i(bb, kw);
     }
+    if (kk[s] == 0) {
+      aa.y = 0.0;
+      bb.y = 0.0;
+    }
+    if (m > half) {
+      aa = cconj(aa);
+      bb = cconj(bb);
+    }
+    const double2 z = make_double2(aa.x - bb.y, aa.y + bb.x);  // a + i b
+    v[s] = kk[s] < g.kc ? z : zero2();
+  }
+}
+
+// load_pair with a per-field x-multiplier m: 0 → 1, 1 → ik, 2 → (ik)² = -k²
+// (B may be null: b = 0)
+template <int LOG2N>
+__device__ __forceinline__ void load_pair_m(double2 (&v)[8], int t, const Geom& g,
+                                            const double2* __restrict__ A, int ma,
+                                            const double2* __restrict__ B, int mb, int y) {
+  constexpr int N = 1 << LOG2N, NT = N / 8, half = N / 2;
+  double2 a[8], b[8];
+  int kk[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const int m = t + s * NT;
+    kk[s] = m <= half ? m : N - m;
+    const int o = midx_i(g, kk[s] < g.kc ? kk[s] : 0, y);
+    a[s] = A[o];
+    b[s] = B ? B[o] : zero2();
+  }
+  auto mul = [](double2 x, int mm, double kw) {
+    return mm == 0 ? x : (mm == 1 ? cmul_i(x, kw) : cscale(x, -(kw * kw)));
+  };
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const int m = t + s * NT;
+    const double kw = kk[s] * g.mk;
+    double2 aa = mul(a[s], ma, kw), bb = mul(b[s], mb, kw);
     if (kk[s] == 0) {
       aa.y = 0.0;
       bb.y = 0.0;
@@ -377,6 +477,103 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, Blk<LOG2N>::THREADS >= 10
       const int k = c.t + s * Bk::NT;
       if (k < g.kc) Mo[4 * MF + midx(g, k, y)] = v[s];
     }
+  } else if constexpr (MODEL == MODEL_TY) {
+    // thomasyamada/ThomasYamada.jl:129-262.  Inputs (k_col_inv): 0 ζ, 1 ψ,
+    // 2 ût, 3 ∂y ut, 4 uc, 5 ∂y uc, 6 vc, 7 pc, 8 ∂y pc.  Physical fields in
+    // pairs through complex x-FFTs, products formed as soon as their factors
+    // exist, forward pairs split and combined on the x-spectral side:
+    //   p1 = vt ζ, p2 = ut ζ, p3 = uc vc, p4 = uc² - vc², p6 = ut uc,
+    //   p7 = vt vc, p8 = vt ∂y uc + vc ∂y ut, p9 = ut ∂x vc + uc ∂x vt,
+    //   p10 = ut ∂x pc + vt ∂y pc
+    // Outputs (×(-Ro); k_col_fwd applies the y-multiplier in brackets):
+    //   0 ik p̂2 - k² p̂3 [1]   1 i p̂1 + k p̂4 [l]   2 p̂3 [l²]   → N_ζ
+    //   3 ik p̂6 + p̂8 [1]                                      → N_uc
+    //   4 p̂7 [il]   5 p̂9 [1]                                   → N_vc
+    //   6 p̂10 [1]                                              → N_pc
+    const double2* F[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) F[i] = Mi + i * MF;
+    const double nRo = -p.Ro;
+    double zt[8], ut[8], vt[8], uc[8], vc[8], p6[8], p7[8], p8[8], p9[8], p10[8];
+    // ζ + i ut, vt + i uc
+    load_pair_m<LOG2N>(v, c.t, g, F[0], 0, F[2], 0, y);
+    fft_line<LOG2N, +1>(v, c.t, tws, line);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      zt[s] = v[s].x;
+      ut[s] = v[s].y;
+    }
+    load_pair_m<LOG2N>(v, c.t, g, F[1], 1, F[4], 0, y);
+    fft_line<LOG2N, +1>(v, c.t, tws, line);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      vt[s] = v[s].x;
+      uc[s] = v[s].y;
+      p6[s] = ut[s] * uc[s];
+    }
+    // vc + i ∂y uc
+    load_pair_m<LOG2N>(v, c.t, g, F[6], 0, F[5], 0, y);
+    fft_line<LOG2N, +1>(v, c.t, tws, line);
+    double2 w[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      vc[s] = v[s].x;
+      p7[s] = vt[s] * vc[s];
+      p8[s] = vt[s] * v[s].y;
+      w[s] = make_double2(ut[s] * zt[s], uc[s] * vc[s]);          // p2 + i p3
+      v[s] = make_double2(vt[s] * zt[s], uc[s] * uc[s] - vc[s] * vc[s]);  // p1 + i p4
+    }
+    fft_line<LOG2N, -1>(w, c.t, tws, line);
+    split_pair<LOG2N>(w, c.t, g, line, [&](int k, double2 a, double2 b) {
+      const double kw = k * g.mk;
+      const int o = midx(g, k, y);
+      Mo[o] = cscale(csub(cmul_i(a, kw), cscale(b, kw * kw)), nRo);
+      Mo[2 * MF + o] = cscale(b, nRo);
+    });
+    fft_line<LOG2N, -1>(v, c.t, tws, line);
+    split_pair<LOG2N>(v, c.t, g, line, [&](int k, double2 a, double2 b) {
+      const double kw = k * g.mk;
+      Mo[MF + midx(g, k, y)] = cscale(cadd(cmul_i(a, 1.0), cscale(b, kw)), nRo);
+    });
+    // ∂y ut + i ∂x vc
+    load_pair_m<LOG2N>(v, c.t, g, F[3], 0, F[6], 1, y);
+    fft_line<LOG2N, +1>(v, c.t, tws, line);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      p8[s] = p8[s] + vc[s] * v[s].x;
+      p9[s] = ut[s] * v[s].y;
+      v[s] = make_double2(p6[s], p8[s]);
+    }
+    fft_line<LOG2N, -1>(v, c.t, tws, line);
+    split_pair<LOG2N>(v, c.t, g, line, [&](int k, double2 a, double2 b) {
+      Mo[3 * MF + midx(g, k, y)] = cscale(cadd(cmul_i(a, k * g.mk), b), nRo);
+    });
+    // ∂x vt + i ∂x pc
+    load_pair_m<LOG2N>(v, c.t, g, F[1], 2, F[7], 1, y);
+    fft_line<LOG2N, +1>(v, c.t, tws, line);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      p9[s] = p9[s] + uc[s] * v[s].x;
+      p10[s] = ut[s] * v[s].y;
+      v[s] = make_double2(p7[s], p9[s]);
+    }
+    fft_line<LOG2N, -1>(v, c.t, tws, line);
+    split_pair<LOG2N>(v, c.t, g, line, [&](int k, double2 a, double2 b) {
+      const int o = midx(g, k, y);
+      Mo[4 * MF + o] = cscale(a, nRo);
+      Mo[5 * MF + o] = cscale(b, nRo);
+    });
+    // ∂y pc
+    load_pair_m<LOG2N>(v, c.t, g, F[8], 0, nullptr, 0, y);
+    fft_line<LOG2N, +1>(v, c.t, tws, line);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) v[s] = make_double2(p10[s] + vt[s] * v[s].x, 0.0);
+    fft_line<LOG2N, -1>(v, c.t, tws, line);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int k = c.t + s * Bk::NT;
+      if (k < g.kc) Mo[6 * MF + midx(g, k, y)] = cscale(v[s], nRo);
+    }
   } else {
     const double2 *Q1 = Mi, *Q2 = Mi + MF, *P1 = Mi + 2 * MF, *P2 = Mi + 3 * MF,
                   *Py1 = Mi + 4 * MF, *Py2 = Mi + 5 * MF;
@@ -411,18 +608,26 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, Blk<LOG2N>::THREADS >= 10
 //     N_u = F(P),  N_v = -il F(K̂) - F((ζu)^),  N_η = F(Q) - il F((vη)^)
 //   QG2 (swqg/TwoLayerQG.jl:171,179): N_l = -il F(A_l) + ik F(B_l)
 // ===========================================================================
-enum { MUL_ONE = 0, MUL_NEG, MUL_NIK, MUL_NIL, MUL_PIK };
+//   TY (thomasyamada/ThomasYamada.jl:166-262, k_row outputs):
+//     N_ζ = F(0) + l F(1) + l² F(2),  N_uc = F(3),  N_vc = il F(4) + F(5),
+//     N_pc = F(6);  plus the linear terms (:142-145) from the calcN input
+enum { MUL_ONE = 0, MUL_NEG, MUL_NIK, MUL_NIL, MUL_PIK, MUL_PIL, MUL_L, MUL_L2 };
 struct NTerms {
-  int fa, ma, fb, mb;  // fb < 0: one term
+  int fa, ma, fb, mb, fc, mc;  // fb < 0: one term; fc < 0: at most two
 };
 template <int MODEL>
 __device__ __forceinline__ NTerms nterms(int f) {
   if constexpr (MODEL == MODEL_RSW) {
-    if (f == 0) return NTerms{0, MUL_ONE, -1, MUL_ONE};
-    if (f == 1) return NTerms{1, MUL_NIL, 2, MUL_NEG};
-    return NTerms{3, MUL_ONE, 4, MUL_NIL};
+    if (f == 0) return NTerms{0, MUL_ONE, -1, MUL_ONE, -1, MUL_ONE};
+    if (f == 1) return NTerms{1, MUL_NIL, 2, MUL_NEG, -1, MUL_ONE};
+    return NTerms{3, MUL_ONE, 4, MUL_NIL, -1, MUL_ONE};
+  } else if constexpr (MODEL == MODEL_TY) {
+    if (f == 0) return NTerms{0, MUL_ONE, 1, MUL_L, 2, MUL_L2};
+    if (f == 1) return NTerms{3, MUL_ONE, -1, MUL_ONE, -1, MUL_ONE};
+    if (f == 2) return NTerms{4, MUL_PIL, 5, MUL_ONE, -1, MUL_ONE};
+    return NTerms{6, MUL_ONE, -1, MUL_ONE, -1, MUL_ONE};
   } else {
-    return NTerms{f, MUL_NIL, 2 + f, MUL_PIK};
+    return NTerms{f, MUL_NIL, 2 + f, MUL_PIK, -1, MUL_ONE};
   }
 }
 __device__ __forceinline__ double2 apply_mul(double2 a, int mul, double k, double l) {
@@ -431,14 +636,21 @@ __device__ __forceinline__ double2 apply_mul(double2 a, int mul, double k, doubl
     case MUL_NEG: return make_double2(-a.x, -a.y);
     case MUL_NIK: return cmul_i(a, -k);
     case MUL_NIL: return cmul_i(a, -l);
-    default: return cmul_i(a, k);
+    case MUL_PIK: return cmul_i(a, k);
+    case MUL_PIL: return cmul_i(a, l);
+    case MUL_L: return cscale(a, l);
+    default: return cscale(a, l * l);
   }
+}
+template <int MODEL>
+constexpr int model_nf() {
+  return MODEL == MODEL_RSW ? 3 : (MODEL == MODEL_TY ? 4 : 2);
 }
 
 template <int MODEL, int LOG2N>
 __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     k_col_fwd(Geom g, Phys p, const double2* __restrict__ Mf, double2* __restrict__ N,
-              const double2* __restrict__ tw) {
+              const double2* __restrict__ X, const double2* __restrict__ tw) {
   using B = Blk<LOG2N>;
   constexpr int NT = B::NT;
   extern __shared__ double2 smem[];
@@ -475,12 +687,35 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
 #pragma unroll
     for (int s = 0; s < 8; ++s) acc[s] = cadd(acc[s], apply_mul(v[s], nt.mb, k, lwav(g, c.t + s * NT)));
   }
+  if (MODEL == MODEL_TY && nt.fc >= 0) {
+    load_col(Mf + nt.fc * MF);
+    fft_line<LOG2N, -1>(v, c.t, tws, line);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) acc[s] = cadd(acc[s], apply_mul(v[s], nt.mc, k, lwav(g, c.t + s * NT)));
+  }
   if (live) {
     double2* Nf = N + (long long)grp * g.cfield + (long long)krl * g.LrP;
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       const int j = compact_of(g, c.t + s * NT);
-      if (j >= 0) Nf[j] = acc[s];
+      if (j >= 0) {
+        double2 r = acc[s];
+        if constexpr (MODEL == MODEL_TY) {
+          // linear terms (thomasyamada/ThomasYamada.jl:142-145), from the
+          // dealiased calcN input (ζ, uc, vc, pc)
+          const long long i = (long long)krl * g.LrP + j;
+          const double l = lwav(g, c.t + s * NT);
+          if (grp == 1) {  // vc - ik pc
+            r = cadd(csub(X[2 * g.cfield + i], cmul_i(X[3 * g.cfield + i], k)), r);
+          } else if (grp == 2) {  // -uc - il pc
+            const double2 u = X[g.cfield + i];
+            r = cadd(csub(make_double2(-u.x, -u.y), cmul_i(X[3 * g.cfield + i], l)), r);
+          } else if (grp == 3) {  // -ik uc - il vc
+            r = cadd(csub(cmul_i(X[g.cfield + i], -k), cmul_i(X[2 * g.cfield + i], l)), r);
+          }
+        }
+        Nf[j] = r;
+      }
     }
   }
 }
@@ -665,12 +900,113 @@ __device__ __forceinline__ void op_rk4(const Geom& g, const Phys& p, const StepP
   }
 }
 
+// FF ETDRK4TimeStepper (ETDRK4substeps!/ETDRK4update!) for a real diagonal
+// L shared by every field; coefficients per mode from the table a.etd
+// (k_etd_coeffs).  One calcN result per stage:
+//   1: N1 -> n1 = N1; acc = E u + α N1;           x = s1 = E2 u + ζ N1
+//   2: N2 -> n2 = N2;                             x = s2 = E2 u + ζ N2
+//   3: N3 -> acc = acc + 2β (n2 + N3);            x = s2 = E2 s1 + ζ (2 N3 - n1)
+//   4: N4 -> u = acc + Γ N4
+// acc accumulates FF's left-to-right sum E u + α N1 + 2β (N2 + N3) + Γ N4
+// term by term, so the rounding sequence is FF's.
+template <int NF>
+__device__ __forceinline__ void op_etdrk4(const Geom& g, const Phys& p, const StepPtrs& a, long long i,
+                                          const cplx n[NF], cplx x[NF]) {
+#pragma clang fp contract(off)
+  const long long cf = g.cfield;
+  const double* T = a.etd + i;
+  if (a.stage == 1) {
+    const double E = T[ETD_E * cf], E2 = T[ETD_E2 * cf], z = T[ETD_ZETA * cf], al = T[ETD_ALPHA * cf];
+    cplx u[NF], acc[NF];
+    load_vec<NF>(a.sol, cf, i, u);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      acc[f] = E * u[f] + al * n[f];
+      x[f] = E2 * u[f] + z * n[f];
+    }
+    store_vec<NF>(a.n1, cf, i, n);
+    store_vec<NF>(a.h0, cf, i, acc);
+    store_vec<NF>(a.xs, cf, i, x);
+  } else if (a.stage == 2) {
+    const double E2 = T[ETD_E2 * cf], z = T[ETD_ZETA * cf];
+    cplx u[NF];
+    load_vec<NF>(a.sol, cf, i, u);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) x[f] = E2 * u[f] + z * n[f];
+    store_vec<NF>(a.n2, cf, i, n);
+    store_vec<NF>(a.xs2, cf, i, x);
+  } else if (a.stage == 3) {
+    const double E2 = T[ETD_E2 * cf], z = T[ETD_ZETA * cf], b2 = 2.0 * T[ETD_BETA * cf];
+    cplx s1[NF], acc[NF], N1[NF], N2[NF];
+    load_vec<NF>(a.xs, cf, i, s1);
+    load_vec<NF>(a.h0, cf, i, acc);
+    load_vec<NF>(a.n1, cf, i, N1);
+    load_vec<NF>(a.n2, cf, i, N2);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      acc[f] = acc[f] + b2 * (N2[f] + n[f]);
+      x[f] = E2 * s1[f] + z * (2.0 * n[f] - N1[f]);
+    }
+    store_vec<NF>(a.h0, cf, i, acc);
+    store_vec<NF>(a.xs2, cf, i, x);
+  } else {
+    const double G = T[ETD_GAMMA * cf];
+    cplx acc[NF];
+    load_vec<NF>(a.h0, cf, i, acc);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) x[f] = acc[f] + G * n[f];
+    store_vec<NF>(a.sol_out, cf, i, x);
+  }
+}
+
 template <int NF, int OP>
 __device__ __forceinline__ void step_op(const Geom& g, const Phys& p, const StepPtrs& a, long long i,
                                         double k, double l, const cplx n[NF], cplx x[NF]) {
   if constexpr (OP == OP_FAB3) op_fab3<NF>(g, p, a, i, k, l, n, x);
   else if constexpr (OP == OP_IFMAB3) op_ifmab3<NF>(g, p, a, i, k, l, n, x);
+  else if constexpr (OP == OP_ETDRK4) op_etdrk4<NF>(g, p, a, i, n, x);
   else op_rk4<NF>(g, p, a, i, k, l, n, x);
+}
+
+// FF getetdcoeffs(dt, L; ncirc = 32, rcirc = 1) per live mode for the real
+// diagonal L = -ν K^(2nν) (thomasyamada/ThomasYamada.jl:265-277): the mean
+// over 32 points z = dt L + e^{2πi (j + 1/2)/32} of the Cox–Matthews
+// functions, times dt, real part; plus e^{dt L}, e^{dt L / 2}.
+__device__ __forceinline__ cplx cexp_d(cplx z) {
+  const double e = exp(z.re);
+  return cplx{e * cos(z.im), e * sin(z.im)};
+}
+__global__ void __launch_bounds__(256) k_etd_coeffs(Geom g, Phys p, double* __restrict__ etd) {
+#pragma clang fp contract(off)
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= g.cfield) return;
+  int kr, j;
+  const long long cf = g.cfield;
+  if (!mode_of(g, i, kr, j)) {
+    for (int c = 0; c < ETD_N; ++c) etd[c * cf + i] = 0.0;
+    return;
+  }
+  const double k = kr * g.mk, l = lwav(g, lrow_of(g, j));
+  const double L = -(p.nu * ipow(k * k + l * l, p.nnu));
+  const double dt = p.dt;
+  const double zr = dt * L;
+  cplx sz = cx(0.0), sa = cx(0.0), sb = cx(0.0), sg = cx(0.0);
+  for (int m = 0; m < 32; ++m) {
+    const double th = 2.0 * 3.14159265358979323846 / 32.0 * (m + 0.5);
+    const cplx z = cx(zr + cos(th), sin(th));
+    const cplx ez = cexp_d(z), ez2 = cexp_d(0.5 * z);
+    const cplx z2 = z * z, z3 = z2 * z;
+    sz = sz + cdiv(ez2 - cx(1.0), z);
+    sa = sa + cdiv(cx(-4.0) - z + ez * (cx(4.0) - 3.0 * z + z2), z3);
+    sb = sb + cdiv(cx(2.0) + z + ez * (cx(-2.0) + z), z3);
+    sg = sg + cdiv(cx(-4.0) - 3.0 * z - z2 + ez * (cx(4.0) - z), z3);
+  }
+  etd[ETD_E * cf + i] = exp(dt * L);
+  etd[ETD_E2 * cf + i] = exp(dt * L / 2);
+  etd[ETD_ZETA * cf + i] = dt * (sz.re / 32.0);
+  etd[ETD_ALPHA * cf + i] = dt * (sa.re / 32.0);
+  etd[ETD_BETA * cf + i] = dt * (sb.re / 32.0);
+  etd[ETD_GAMMA * cf + i] = dt * (sg.re / 32.0);
 }
 
 // Elementwise (unfused) stepper kernel: N from memory; the stage input x is
@@ -1013,7 +1349,20 @@ __global__ void k_make_spec(Geom g, Phys p, int model, int fid, const double2* _
   const long long cf = g.cfield;
   const double k = kr * g.mk, l = lwav(g, lrow_of(g, j));
   double2 r = zero2();
-  if (model == MODEL_RSW) {
+  if (model == MODEL_TY) {
+    // thomasyamada/ThomasYamada.jl:67-92: 0 uc, 1 vc, 2 pc, 3 ζt, 4 qc =
+    // ik vc - il uc - pc, 5 ψt = -ζt/K², 8 ut = -il ψt, 9 vt = ik ψt
+    const double K2 = k * k + l * l;
+    const double iK2 = K2 == 0.0 ? 0.0 : 1.0 / K2;
+    const double2 z = sol[i];
+    const double2 ps = make_double2(-z.x * iK2, -z.y * iK2);
+    if (fid <= 2) r = sol[(fid + 1) * cf + i];
+    else if (fid == 3) r = z;
+    else if (fid == 4) r = csub(csub(cmul_i(sol[2 * cf + i], k), cmul_i(sol[cf + i], l)), sol[3 * cf + i]);
+    else if (fid == 5) r = ps;
+    else if (fid == 8) r = cmul_i(ps, -l);
+    else if (fid == 9) r = cmul_i(ps, k);
+  } else if (model == MODEL_RSW) {
     if (fid <= 2) {
       r = sol[fid * cf + i];
     } else {
@@ -1128,6 +1477,16 @@ __global__ void __launch_bounds__(256) k_energy_cols(Geom g, Phys p, int model,
         const double2 u = sol[i], v = sol[cf + i], e = sol[2 * cf + i];
         a0 += w * (u.x * u.x + u.y * u.y + v.x * v.x + v.y * v.y);
         a1 += w * (e.x * e.x + e.y * e.y);
+      } else if (model == MODEL_TY) {
+        // barotropic |K⁻¹ ζ|², baroclinic |uc|² + |vc|², |pc|²
+        const double l = lwav(g, lrow_of(g, j));
+        const double K2 = k * k + l * l;
+        const double r = sqrt(K2 == 0.0 ? 0.0 : 1.0 / K2);
+        const double2 z = sol[i], u = sol[cf + i], v = sol[2 * cf + i], q = sol[3 * cf + i];
+        const double zx = r * z.x, zy = r * z.y;
+        a0 += w * (zx * zx + zy * zy);
+        a1 += w * (u.x * u.x + u.y * u.y + v.x * v.x + v.y * v.y);
+        a2 += w * (q.x * q.x + q.y * q.y);
       } else {
         const double l = lwav(g, lrow_of(g, j));
         const double K2 = k * k + l * l;
@@ -1164,14 +1523,19 @@ __global__ void k_energy_final(const double* __restrict__ cols, int ncols, doubl
   }
 }
 
-// max |f| over this slab's physical rows (non-negative doubles order like
-// their bit patterns, so an integer atomicMax is exact and order-free)
-__global__ void k_absmax(const double* __restrict__ f, long long n, unsigned long long* out) {
-  double m = 0.0;
+// max |f| (sgn = 0) or max f (sgn = 1) over this slab's physical rows, as an
+// order-preserving integer key (dkey) so that an integer atomicMax is exact
+// and order-free; the host decodes it (key_double in sw_api.cpp)
+__device__ __forceinline__ unsigned long long dkey(double d) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(d);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__global__ void k_absmax(const double* __restrict__ f, long long n, unsigned long long* out, int sgn) {
+  double m = sgn ? -INFINITY : 0.0;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
-    m = fmax(m, fabs(f[i]));
+    m = fmax(m, sgn ? f[i] : fabs(f[i]));
   for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_down(m, off, 64));
-  if ((threadIdx.x & 63) == 0) atomicMax(out, (unsigned long long)__double_as_longlong(m));
+  if ((threadIdx.x & 63) == 0) atomicMax(out, dkey(m));
 }
 
 // ===========================================================================
@@ -1211,9 +1575,11 @@ template <int L>
 struct ColInvL {
   static void run(int model, const Geom& g, const Phys& p, const double2* X, double2* M,
                   const double2* tw, hipStream_t s) {
-    const dim3 grid(col_blocks<L>(g), model == MODEL_RSW ? 3 : 2);
+    const dim3 grid(col_blocks<L>(g), model == MODEL_RSW ? 3 : (model == MODEL_TY ? 5 : 2));
     if (model == MODEL_RSW)
       hipLaunchKernelGGL((k_col_inv<MODEL_RSW, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw);
+    else if (model == MODEL_TY)
+      hipLaunchKernelGGL((k_col_inv<MODEL_TY, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw);
     else
       hipLaunchKernelGGL((k_col_inv<MODEL_QG2, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw);
   }
@@ -1227,6 +1593,9 @@ struct RowL {
     if (model == MODEL_RSW)
       hipLaunchKernelGGL((k_row<MODEL_RSW, L>), dim3(row_blocks<L>(g)), dim3(Blk<L>::THREADS), sh_rsw, s, g, p,
                          Mi, Mo, tw);
+    else if (model == MODEL_TY)
+      hipLaunchKernelGGL((k_row<MODEL_TY, L>), dim3(row_blocks<L>(g)), dim3(Blk<L>::THREADS), sh_qg2, s, g, p,
+                         Mi, Mo, tw);
     else
       hipLaunchKernelGGL((k_row<MODEL_QG2, L>), dim3(row_blocks<L>(g)), dim3(Blk<L>::THREADS), sh_qg2, s, g, p,
                          Mi, Mo, tw);
@@ -1234,13 +1603,18 @@ struct RowL {
 };
 template <int L>
 struct ColFwdL {
-  static void run(int model, const Geom& g, const Phys& p, const double2* Mf, double2* N,
+  static void run(int model, const Geom& g, const Phys& p, const double2* Mf, double2* N, const double2* X,
                   const double2* tw, hipStream_t s) {
-    const dim3 grid(col_blocks<L>(g), model == MODEL_RSW ? 3 : 2);
+    const dim3 grid(col_blocks<L>(g), model == MODEL_RSW ? 3 : (model == MODEL_TY ? 4 : 2));
     if (model == MODEL_RSW)
-      hipLaunchKernelGGL((k_col_fwd<MODEL_RSW, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, Mf, N, tw);
+      hipLaunchKernelGGL((k_col_fwd<MODEL_RSW, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, Mf, N, X,
+                         tw);
+    else if (model == MODEL_TY)
+      hipLaunchKernelGGL((k_col_fwd<MODEL_TY, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, Mf, N, X,
+                         tw);
     else
-      hipLaunchKernelGGL((k_col_fwd<MODEL_QG2, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, Mf, N, tw);
+      hipLaunchKernelGGL((k_col_fwd<MODEL_QG2, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, Mf, N, X,
+                         tw);
   }
 };
 template <int L>
@@ -1265,8 +1639,8 @@ void launch_row(int model, const Geom& g, const Phys& p, const double2* Minv, do
   dispatch_log2<RowL>(g.log2nx, model, g, p, Minv, Mfwd, tw_x, s);
 }
 void launch_col_fwd(int model, const Geom& g, const Phys& p, const double2* Mfwd, double2* N,
-                    const double2* tw_y, hipStream_t s) {
-  dispatch_log2<ColFwdL>(g.log2ny, model, g, p, Mfwd, N, tw_y, s);
+                    const double2* X, const double2* tw_y, hipStream_t s) {
+  dispatch_log2<ColFwdL>(g.log2ny, model, g, p, Mfwd, N, X, tw_y, s);
 }
 
 static inline dim3 mode_grid(const Geom& g) { return dim3((unsigned)((g.cfield + 255) / 256)); }
@@ -1303,7 +1677,9 @@ void launch_col_step(int model, int op, const Geom& g, const Phys& p, const Step
 void launch_step_elem(int nf, int op, const Geom& g, const Phys& p, const StepPtrs& a,
                       const double2* N, double2* xs, hipStream_t s) {
 #define SW_SE(F, O) hipLaunchKernelGGL((k_step_elem<F, O>), mode_grid(g), dim3(256), 0, s, g, p, a, N, xs)
-  if (nf == 3) {
+  if (nf == 4) {
+    SW_SE(4, OP_ETDRK4);
+  } else if (nf == 3) {
     if (op == OP_FAB3) SW_SE(3, OP_FAB3);
     else if (op == OP_IFMAB3) SW_SE(3, OP_IFMAB3);
     else SW_SE(3, OP_RK4);
@@ -1353,8 +1729,12 @@ void launch_energy_final(const double* cols, int ncols, double* out, hipStream_t
   hipLaunchKernelGGL(k_energy_final, dim3(1), dim3(64), 0, s, cols, ncols, out);
 }
 
-void launch_absmax(const double* f, long long n, unsigned long long* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_absmax, dim3(1024), dim3(256), 0, s, f, n, out);
+void launch_absmax(const double* f, long long n, unsigned long long* out, int sgn, hipStream_t s) {
+  hipLaunchKernelGGL(k_absmax, dim3(1024), dim3(256), 0, s, f, n, out, sgn);
+}
+
+void launch_etd_coeffs(const Geom& g, const Phys& p, double* etd, hipStream_t s) {
+  hipLaunchKernelGGL(k_etd_coeffs, mode_grid(g), dim3(256), 0, s, g, p, etd);
 }
 
 }  // namespace sw

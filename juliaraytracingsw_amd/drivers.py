@@ -1,5 +1,5 @@
-"""Driver-side setup mirroring rsw/RSWDriver.jl and swqg/TwoLayerDriver.jl
-(SURVEY A12): parameter formulas, synthetic random-phase initial conditions
+"""Driver-side setup mirroring rsw/RSWDriver.jl, swqg/TwoLayerDriver.jl and
+thomasyamada/TYdriver.jl: parameter formulas, synthetic random-phase initial conditions
 and the frame loop.  Setup only — the per-step work is libsw's.
 """
 from __future__ import annotations
@@ -11,6 +11,7 @@ import numpy as np
 
 from . import _lib
 from . import rotating_shallow_water as RSW
+from . import thomas_yamada as TY
 from . import two_layer_qg as QG2
 from .grid import TwoDGrid
 
@@ -21,6 +22,20 @@ RSW_PARAMETERS = dict(L=2 * np.pi, f=3.0, Cg=1.0, nnu=4, nutune=20.0, cfltune=0.
 QG2_PARAMETERS = dict(L=2 * np.pi, background_Cg=1.0, f=3.0, deformation_radius=1 / 6,
                       intervortex_radius=1.0, nnu=4, nutune=40.0, cfltune=0.025,
                       aliased_fraction=1 / 3, ug=0.025)
+
+
+# thomasyamada/cpu-setup/Parameters.jl (the first of the three setups)
+TY_PARAMETERS = dict(Lx=6 * np.pi, nx=512, Ro=1.0, nnu=8, startup_dt=3e-2, dt=5e-3, stepper="ETDRK4",
+                     k0w_range=(0.0, 5 / 3), k0g_range=(10 / 3, 13 / 3), at=0.0, ag=0.3, aw=0.1)
+
+
+def ty_parameters(nx=None, **over):
+    """thomasyamada/cpu-setup/Parameters.jl: ν = 5e-34 (Lx/2π)^16, nν = 8."""
+    P = dict(TY_PARAMETERS, **over)
+    if nx is not None:
+        P["nx"] = nx
+    P.setdefault("nu", 5.0e-34 * (P["Lx"] / (2 * np.pi)) ** 16)
+    return P
 
 
 def rsw_parameters(nx, **over):
@@ -118,6 +133,47 @@ def set_seed_initial_condition(prob, rng):
     QG2.set_solution(prob, np.fft.rfft2(q0, axes=(-2, -1)))
 
 
+def set_ty_initial_condition(prob, rng, k0w_range=(0, 1), k0g_range=(0, 1), at=0.0, ag=0.0, aw=0.0):
+    """thomasyamada/TYdriver.jl:36-87 (set_initial_condition): phases
+    θ, θ₀, θ₊, θ₋ = U[0,1) over (nkr, nl) column-major from the seeded ``rng``
+    (Julia's stream is not reproducible), projected on the TYUtils bases
+    inside the annuli, each part scaled by its physical max — taken with
+    libsw's own c2r."""
+    g = prob.grid
+    K2 = g.kr[None, :] ** 2 + g.l[:, None] ** 2
+    wf = (k0w_range[0] ** 2 <= K2) & (K2 <= k0w_range[1] ** 2)
+    gf = (k0g_range[0] ** 2 <= K2) & (K2 <= k0g_range[1] ** 2)
+    th = [rng.random((g.nkr, g.nl)).T for _ in range(4)]
+    ph, ph0, php, phm = [np.exp(2 * np.pi * 1j * t) for t in th]
+    P0, Pp, Pm = TY._bases(g)
+    psith = ph * gf
+    gh = [P0[i] * ph0 * gf for i in range(3)]
+    wh = [(Pp[i] * php + Pm[i] * phm) * wf for i in range(3)]
+    z = np.zeros_like(psith)
+
+    def absmax(f):  # max |c2r(f)| through field ζ_T (physical id 3)
+        TY.set_solution(prob, f, z, z, z)
+        return float(np.max(np.abs(prob.ctx.physical(3, g.ny, g.nx))))
+
+    mt, mg, mw = absmax(psith), absmax(gh[0]), absmax(wh[0])
+    psith = psith * (at / mt) if mt > 0 else z
+    gh = [x * (ag / mg) for x in gh] if mg > 0 else [z] * 3
+    wh = [x * (aw / mw) for x in wh] if mw > 0 else [z] * 3
+    TY.set_solution(prob, -K2 * psith, wh[0] + gh[0], wh[1] + gh[1], wh[2] + gh[2])
+
+
+def ty_problem(nx=512, seed=5678, device=0, decomposition=None, **over):
+    """TYdriver.start! set-up (:119-149): Problem with the Parameters.jl
+    values and the seeded random-phase IC, fp64 on the GPU."""
+    P = ty_parameters(nx, **over)
+    prob = TY.Problem("gpu", nx=P["nx"], Lx=P["Lx"], nu=P["nu"], nnu=P["nnu"], Ro=P["Ro"], dt=P["dt"],
+                      device=device, decomposition=decomposition)
+    rng = np.random.default_rng(seed)
+    set_ty_initial_condition(prob, rng, k0w_range=P["k0w_range"], k0g_range=P["k0g_range"], at=P["at"],
+                             ag=P["ag"], aw=P["aw"])
+    return prob, P
+
+
 def rsw_problem(nx, stepper="FilteredAB3", seed=20261015, device=0, decomposition=None, **over):
     """RSWDriver.initialize_problem (:134-176) on the GPU in fp64 with the named
     stepper and the shafer random-phase IC."""
@@ -152,7 +208,7 @@ def run_frames(prob, nframes, output_freq, diags=(), on_frame=None, log_every=10
     optional per-frame callback (updatevars!/output)."""
     from . import problem
 
-    mod = RSW if prob.model == _lib.SW_MODEL_RSW else QG2
+    mod = {_lib.SW_MODEL_RSW: RSW, _lib.SW_MODEL_QG2: QG2, _lib.SW_MODEL_TY: TY}[prob.model]
     t0 = time.time()
     for frame in range(nframes):
         if log_every and frame % log_every == 0:

@@ -128,7 +128,8 @@ class Diagnostic:
     def __init__(self, calc, prob, *, freq=1, nsteps=100, ndata=None):
         field = getattr(calc, "_sw_energy", None)
         if field is None:
-            raise ValueError("libsw records kinetic_energy / potential_energy diagnostics")
+            raise ValueError("libsw records the models' energy diagnostics (kinetic_energy, "
+                             "potential_energy, baroclinic_energy, barotropic_energy)")
         ndata = int(ndata or math.ceil((nsteps + 1) / freq))
         prob._attach_energy_diagnostics(int(freq), ndata)
         self.calc, self.prob, self.freq, self._field = calc, prob, int(freq), field
@@ -144,7 +145,7 @@ class Diagnostic:
         for step, t, ke, ke2, pe in records[self._seen:]:
             if self.i >= len(self.data):
                 break
-            v = {"ke": ke, "pe": pe, "ke12": (ke, ke2)}[self._field]
+            v = {"ke": ke, "pe": pe, "ke12": (ke, ke2), "bc": (ke, pe), "bt": ke2}[self._field]
             self.data[self.i], self.t[self.i], self.steps[self.i] = v, t, step
             self.value = v
             self.i += 1

@@ -1,0 +1,122 @@
+"""``ThomasYamada`` module mirror (thomasyamada/ThomasYamada.jl).
+
+Same names, argument meaning and defaults as the reference's ``Problem``
+(:55-74): fields (ζ_T, u_c, v_c, p_c), a real diagonal L = -ν K^(2nν) on all
+four fields (:265-277), stepped by FourierFlows' ``ETDRK4`` (the default
+``stepper``).  calcN (:129-262), the ETDRK4 coefficient table and every stage
+run in libsw on the GPU.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+from .problem import Diagnostic, Problem as _Problem, increment, stepforward  # noqa: F401
+
+
+def Problem(dev="gpu", *, nx=128, ny=None, Lx=2 * np.pi, Ly=None, nu=3.5e-25, nnu=8, Ro=0.2,
+            stepper="ETDRK4", dt=5e-2, aliased_fraction=1 / 3, T=np.float64, device=0,
+            check_nan=True, unfused=False, decomposition=None):
+    """``ThomasYamada.Problem(dev; nx, ny, Lx, Ly, ν, nν, Ro, stepper, dt,
+    aliased_fraction, T)`` (:55-74).  ``stepper`` must be "ETDRK4" (the only
+    stepper the reference runs this model with, cpu-setup/Parameters.jl:12)."""
+    if dev not in ("gpu", "GPU", "GPU()"):
+        raise _lib.LibSWError("libsw runs on the GPU only (dev='gpu')")
+    if stepper != "ETDRK4":
+        raise _lib.LibSWError("the Thomas-Yamada model is stepped with ETDRK4")
+    ny = nx if ny is None else ny
+    Ly = Lx if Ly is None else Ly
+    params = dict(nu=float(nu), nnu=int(nnu), Ro=float(Ro))
+    return _Problem(_lib.SW_MODEL_TY, nx=nx, ny=ny, Lx=Lx, Ly=Ly, dt=dt,
+                    aliased_fraction=aliased_fraction, stepper=stepper, params=params,
+                    device=device, check_nan=check_nan, T=T, unfused=unfused,
+                    **(decomposition or {}))
+
+
+def set_solution(prob, zeta0h, u0h, v0h, p0h):
+    """``set_solution!(prob, ζ0h, u0h, v0h, p0h)`` (:279-306): upload + dealias."""
+    prob.sol = np.stack([np.asarray(zeta0h), np.asarray(u0h), np.asarray(v0h), np.asarray(p0h)])
+
+
+def updatevars(prob):
+    """``updatevars!(prob)`` (:67-92): physical ζ_T, u_c, v_c, p_c, u_T, v_T,
+    q_c (and ψ_T) of the dealiased state, each [ny][nx]."""
+    g = prob.grid
+    ids = (("zt", 3), ("uc", 0), ("vc", 1), ("pc", 2), ("ut", 8), ("vt", 9), ("qc", 4), ("psit", 5))
+    return {name: prob.ctx.physical(fid, g.ny, g.nx) for name, fid in ids}
+
+
+def enforce_reality_condition(prob):
+    """``enforce_reality_condition!(prob)`` (:94-117): each field through
+    c2r then r2c.  On a dealiased state that is the projection onto
+    Hermitian-consistent spectra: the kr = 0 column becomes
+    (X(0, l) + conj X(0, -l)) / 2 (numpy's c2r rule); every other
+    live mode is unchanged."""
+    s = prob.sol
+    c0 = s[:, :, 0]
+    mirror = np.conj(np.roll(c0[:, ::-1], 1, axis=1))  # X(0, -l)
+    s[:, :, 0] = 0.5 * (c0 + mirror)
+    prob.sol = s
+
+
+def baroclinic_energy(prob):
+    """``baroclinic_energy(prob)`` (:333-342): (|u_c|² + |v_c|², |p_c|²) by
+    parsevalsum2, reduced on the device."""
+    return (prob.ctx.diag(_lib.SW_DIAG_KE), prob.ctx.diag(_lib.SW_DIAG_PE))
+
+
+def barotropic_energy(prob):
+    """``barotropic_energy(prob)`` (:344-351): parsevalsum2(K⁻¹ ζ_T)."""
+    return prob.ctx.diag(_lib.SW_DIAG_BT)
+
+
+def _parsevalsum2(uh, grid):
+    U = np.abs(uh) ** 2
+    s = 2 * U.sum() - U[:, 0].sum()
+    if grid.nx % 2 == 0:
+        s -= U[:, -1].sum()
+    return grid.Lx * grid.Ly / (grid.nx ** 2 * grid.ny ** 2) * s
+
+
+def _bases(grid):
+    """thomasyamada/TYUtils.jl:10-38: Φ₀, Φ₊, Φ₋ per mode, each [3][nl][nkr]."""
+    kr = grid.kr[None, :]
+    l = grid.l[:, None]
+    K2 = kr ** 2 + l ** 2
+    om = np.sqrt(1 + K2)
+    with np.errstate(divide="ignore"):
+        iK2 = np.where(K2 == 0, 0.0, 1.0 / K2)
+    s = np.sqrt(iK2 / 2) / om
+    one = np.ones_like(K2)
+    P0 = np.stack([1j * l / om * one, -1j * kr / om * one, -1 / om + 0j])
+    Pp = np.stack([(om * kr + 1j * l) * s, (om * l - 1j * kr) * s, (om ** 2 - 1) * s + 0j])
+    Pm = np.stack([(-om * kr + 1j * l) * s, (-om * l - 1j * kr) * s, (om ** 2 - 1) * s + 0j])
+    P0[:, 0, 0] = [0, 0, 1]
+    Pp[:, 0, 0] = np.array([1j, 1, 0]) / np.sqrt(2)
+    Pm[:, 0, 0] = np.array([1j, -1, 0]) / np.sqrt(2)
+    return P0, Pp, Pm
+
+
+def wave_geostrophic_energy(prob):
+    """``wave_geostrophic_energy(prob)`` (:353-367) via
+    ``decompose_balanced_wave`` (thomasyamada/TYUtils.jl:40-51): ((wave KE,
+    wave PE), (geostrophic KE, geostrophic PE)).  A per-frame driver
+    diagnostic, evaluated on the host from the downloaded state."""
+    g = prob.grid
+    b = prob.sol[1:4]
+    P0, Pp, Pm = _bases(g)
+    G = (b * np.conj(P0)).sum(0)[None] * P0
+    W = (b * np.conj(Pp)).sum(0)[None] * Pp + (b * np.conj(Pm)).sum(0)[None] * Pm
+    ps = lambda f: _parsevalsum2(f, g)  # noqa: E731
+    return ((ps(W[0]) + ps(W[1]), ps(W[2])), (ps(G[0]) + ps(G[1]), ps(G[2])))
+
+
+def cfl(prob):
+    """clock.dt · max(maximum(u_c)/dx, maximum(v_c)/dy, maximum(u_T)/dx,
+    maximum(v_T)/dy) (thomasyamada/TYdriver.jl:150-151: signed maxima),
+    reduced on the device."""
+    return prob.ctx.diag(_lib.SW_DIAG_CFL)
+
+
+baroclinic_energy._sw_energy = "bc"
+barotropic_energy._sw_energy = "bt"

@@ -350,6 +350,156 @@ def qg2_energies(sol, grid, p):
 
 
 # --------------------------------------------------------------------------
+# Thomas–Yamada barotropic/baroclinic model (thomasyamada/ThomasYamada.jl)
+# --------------------------------------------------------------------------
+class TYParams:
+    """thomasyamada/ThomasYamada.jl:21-25 (ν, nν, Ro)."""
+
+    def __init__(self, nu, nnu, Ro):
+        self.nu, self.nnu, self.Ro = float(nu), int(nnu), float(Ro)
+
+
+def ty_L(grid: TwoDGrid, p: TYParams):
+    """thomasyamada/ThomasYamada.jl:265-277: real diagonal L = D on all four
+    fields, shape [4, nl, nkr]."""
+    D = -p.nu * grid.Krsq ** p.nnu
+    return np.stack([D, D, D, D])
+
+
+def ty_calcN(sol, grid: TwoDGrid, p: TYParams):
+    """thomasyamada/ThomasYamada.jl:129-262 (calcN! + calcN_vorticity!,
+    calcN_baroclinic!, calcN_pressure!) op for op; ``sol`` = (ζ_T, u_c, v_c,
+    p_c) is dealiased IN PLACE (line 130)."""
+    grid.dealias(sol)
+    kr = grid.kr[None, :]
+    l = grid.l[:, None]
+    Ro = p.Ro
+    zth, uch, vch, pch = sol[0].copy(), sol[1].copy(), sol[2].copy(), sol[3].copy()
+    psith = -zth * grid.invKrsq                           # :125-127
+    uth = -1j * l * psith                                 # :138
+    vth = 1j * kr * psith                                 # :139
+    N = np.empty_like(sol)
+    N[0] = 0.0                                            # :142
+    N[1] = vch - 1j * kr * pch                            # :143
+    N[2] = -uch - 1j * l * pch                            # :144
+    N[3] = -1j * kr * uch - 1j * l * vch                  # :145
+    zt = grid.irfft(zth)                                  # :148-149
+    ut = grid.irfft(uth)                                  # :150-152
+    vt = grid.irfft(vth)                                  # :153
+    uc = grid.irfft(uch)                                  # :154-156
+    vc = grid.irfft(vch)                                  # :157
+    # calcN_vorticity! (:166-202)
+    vzh = grid.rfft(vt * zt)                              # :174-177
+    uzh = grid.rfft(ut * zt)                              # :179-182
+    N[0] += -Ro * (1j * l * vzh + 1j * kr * uzh)          # :183
+    uvh = grid.rfft(uc * vc)                              # :186-189
+    N[0] += -Ro * (-kr ** 2 + l ** 2) * uvh               # :190
+    v2h = grid.rfft(vc * vc)                              # :192-199
+    u2h = grid.rfft(uc * uc)
+    N[0] += -Ro * (-kr * l * v2h + kr * l * u2h)          # :201
+    # calcN_baroclinic! (:204-243)
+    ucuth = grid.rfft(ut * uc)                            # :212-217
+    vcvth = grid.rfft(vt * vc)
+    N[1] += -Ro * (1j * kr * ucuth)                       # :218
+    N[2] += -Ro * (1j * l * vcvth)                        # :219
+    vtucy = grid.irfft(1j * l * uch) * vt                 # :225-231
+    vcuty = grid.irfft(1j * l * uth) * vc
+    N[1] += -Ro * (grid.rfft(vtucy) + grid.rfft(vcuty))   # :232-234
+    utvcx = grid.irfft(1j * kr * vch) * ut                # :240-246
+    ucvtx = grid.irfft(1j * kr * vth) * uc
+    N[2] += -Ro * (grid.rfft(utvcx) + grid.rfft(ucvtx))   # :247-249
+    # calcN_pressure! (:251-262), pch restored from sol at :161
+    utpcx = grid.irfft(1j * kr * pch) * ut                # :257-264
+    vtpcy = grid.irfft(1j * l * pch) * vt
+    N[3] += -Ro * (grid.rfft(utpcx) + grid.rfft(vtpcy))   # :265-266
+    return N
+
+
+def ty_updatevars(sol, grid: TwoDGrid, p: TYParams):
+    """thomasyamada/ThomasYamada.jl:67-92 -> dict of physical fields."""
+    grid.dealias(sol)
+    kr = grid.kr[None, :]
+    l = grid.l[:, None]
+    psith = -sol[0] * grid.invKrsq
+    qch = 1j * kr * sol[2] - 1j * l * sol[1] - sol[3]
+    return {"zt": grid.irfft(sol[0]), "uc": grid.irfft(sol[1]), "vc": grid.irfft(sol[2]),
+            "pc": grid.irfft(sol[3]), "ut": grid.irfft(-1j * l * psith),
+            "vt": grid.irfft(1j * kr * psith), "qc": grid.irfft(qch)}
+
+
+def ty_balanced_basis(grid: TwoDGrid):
+    """thomasyamada/TYUtils.jl:10-20 (Φ₀), shape [3, nl, nkr]."""
+    kr = np.broadcast_to(grid.kr[None, :], grid.Krsq.shape)
+    l = np.broadcast_to(grid.l[:, None], grid.Krsq.shape)
+    om = np.sqrt(1 + kr ** 2 + l ** 2)
+    P = np.stack([1j * l / om, -1j * kr / om, -1 / om + 0j])
+    P[:, 0, 0] = [0, 0, 1]
+    return P
+
+
+def ty_wave_bases(grid: TwoDGrid):
+    """thomasyamada/TYUtils.jl:22-38 (Φ₊, Φ₋), each [3, nl, nkr]."""
+    kr = np.broadcast_to(grid.kr[None, :], grid.Krsq.shape)
+    l = np.broadcast_to(grid.l[:, None], grid.Krsq.shape)
+    om = np.sqrt(1 + kr ** 2 + l ** 2)
+    s = np.sqrt(grid.invKrsq / 2) / om
+    Pp = np.stack([(om * kr + 1j * l) * s, (om * l - 1j * kr) * s, (om ** 2 - 1) * s + 0j])
+    Pm = np.stack([(-om * kr + 1j * l) * s, (-om * l - 1j * kr) * s, (om ** 2 - 1) * s + 0j])
+    Pp[:, 0, 0] = np.array([1j, 1, 0]) / np.sqrt(2)
+    Pm[:, 0, 0] = np.array([1j, -1, 0]) / np.sqrt(2)
+    return Pp, Pm
+
+
+def ty_decompose(sol, grid: TwoDGrid):
+    """thomasyamada/TYUtils.jl:40-51: balanced (G) and wave (W) parts of
+    (u_c, v_c, p_c)."""
+    b = sol[1:4]
+    P0 = ty_balanced_basis(grid)
+    Pp, Pm = ty_wave_bases(grid)
+    G = (b * np.conj(P0)).sum(0)[None] * P0
+    W = (b * np.conj(Pp)).sum(0)[None] * Pp + (b * np.conj(Pm)).sum(0)[None] * Pm
+    return G, W
+
+
+def ty_energies(sol, grid: TwoDGrid):
+    """barotropic_energy, baroclinic_energy, wave_geostrophic_energy
+    (thomasyamada/ThomasYamada.jl:333-367) of ``sol`` as is."""
+    bt = parsevalsum2(np.sqrt(grid.invKrsq) * sol[0], grid)
+    bc = (parsevalsum2(sol[1], grid) + parsevalsum2(sol[2], grid), parsevalsum2(sol[3], grid))
+    G, W = ty_decompose(sol, grid)
+    wg = ((parsevalsum2(W[0], grid) + parsevalsum2(W[1], grid), parsevalsum2(W[2], grid)),
+          (parsevalsum2(G[0], grid) + parsevalsum2(G[1], grid), parsevalsum2(G[2], grid)))
+    return bt, bc, wg
+
+
+def ty_initial_condition(grid: TwoDGrid, rng, k0w_range=(0.0, 5 / 3), k0g_range=(10 / 3, 13 / 3),
+                         at=0.0, ag=0.3, aw=0.1):
+    """thomasyamada/TYdriver.jl:36-87 (set_initial_condition): random phases
+    on the wave / geostrophic annuli projected on the TYUtils bases, each part
+    scaled by its physical max.  Julia's RNG stream is not reproducible here:
+    ``rng`` is a seeded numpy Generator drawing θ, θ₀, θ₊, θ₋ over (nkr, nl)
+    in Julia column-major order.  Returns sol (4, nl, nkr)."""
+    K2 = grid.Krsq
+    wf = (k0w_range[0] ** 2 <= K2) & (K2 <= k0w_range[1] ** 2)
+    gf = (k0g_range[0] ** 2 <= K2) & (K2 <= k0g_range[1] ** 2)
+    th = [rng.random((grid.nkr, grid.nl)).T for _ in range(4)]
+    ph, ph0, php, phm = [np.exp(2 * np.pi * 1j * t) for t in th]
+    P0 = ty_balanced_basis(grid)
+    Pp, Pm = ty_wave_bases(grid)
+    psith = ph * gf
+    g = [P0[i] * ph0 * gf for i in range(3)]
+    w = [(Pp[i] * php + Pm[i] * phm) * wf for i in range(3)]
+    mt = np.max(np.abs(grid.irfft(psith)))
+    mg = np.max(np.abs(grid.irfft(g[0])))
+    mw = np.max(np.abs(grid.irfft(w[0])))
+    psith = psith * at / mt if mt > 0 else psith * 0
+    g = [x * ag / mg for x in g] if mg > 0 else [x * 0 for x in g]
+    w = [x * aw / mw for x in w] if mw > 0 else [x * 0 for x in w]
+    zh = -K2 * psith
+    return np.stack([zh, w[0] + g[0], w[1] + g[1], w[2] + g[2]])
+
+
+# --------------------------------------------------------------------------
 # Time steppers
 # --------------------------------------------------------------------------
 class Clock:
@@ -447,6 +597,53 @@ class IFMRK4:
         clock.step += 1
 
 
+def etdrk4_coeffs(dt, L, ncirc=32, rcirc=1.0):
+    """FF ``getetdcoeffs(dt, L; ncirc=32, rcirc=1)`` for a real diagonal L
+    (FourierFlows.jl timesteppers; not vendored in the reference — restated
+    from its published Cox–Matthews / Kassam–Trefethen contour form): the
+    mean over ``ncirc`` points z = dt L + r e^{2πi (j+1/2)/ncirc} of
+      ζ = (e^{z/2} - 1)/z,  α = (-4 - z + e^z (4 - 3z + z²))/z³,
+      β = (2 + z + e^z (z - 2))/z³,  Γ = (-4 - 3z - z² + e^z (4 - z))/z³,
+    each times dt, real part (L real)."""
+    circ = rcirc * np.exp(2j * np.pi / ncirc * (np.arange(ncirc) + 0.5))
+    zc = dt * L[..., None] + circ
+    ez = np.exp(zc)
+    z3 = zc ** 3
+    zeta = (np.exp(zc / 2) - 1) / zc
+    alpha = (-4 - zc + ez * (4 - 3 * zc + zc ** 2)) / z3
+    beta = (2 + zc + ez * (-2 + zc)) / z3
+    gamma = (-4 - 3 * zc - zc ** 2 + ez * (4 - zc)) / z3
+    return tuple(dt * np.real(c.mean(axis=-1)) for c in (zeta, alpha, beta, gamma))
+
+
+class ETDRK4:
+    """FF ``ETDRK4TimeStepper`` (the stepper ThomasYamada.Problem defaults to,
+    thomasyamada/ThomasYamada.jl:60, cpu-setup/Parameters.jl:12): with
+    E = e^{dt L}, E2 = e^{dt L/2} and the contour coefficients
+      N1 = N(u);        s1 = E2 u + ζ N1
+      N2 = N(s1);       s2 = E2 u + ζ N2
+      N3 = N(s2);       s2 = E2 s1 + ζ (2 N3 - N1)
+      N4 = N(s2);       u  = E u + α N1 + 2β (N2 + N3) + Γ N4."""
+
+    def __init__(self, L, dt, grid, nf):
+        self.expLdt = np.exp(dt * L)
+        self.expLdt2 = np.exp(dt * L / 2)
+        self.zeta, self.alpha, self.beta, self.gamma = etdrk4_coeffs(dt, L)
+
+    def stepforward(self, sol, clock, calcN, grid, params):
+        E, E2, z = self.expLdt, self.expLdt2, self.zeta
+        N1 = calcN(sol, grid, params)
+        s1 = E2 * sol + z * N1
+        N2 = calcN(s1, grid, params)
+        s2 = E2 * sol + z * N2
+        N3 = calcN(s2, grid, params)
+        s2 = E2 * s1 + z * (2 * N3 - N1)
+        N4 = calcN(s2, grid, params)
+        sol[...] = E * sol + self.alpha * N1 + 2 * self.beta * (N2 + N3) + self.gamma * N4
+        clock.t += clock.dt
+        clock.step += 1
+
+
 # --------------------------------------------------------------------------
 # Problems and driver formulas
 # --------------------------------------------------------------------------
@@ -457,6 +654,7 @@ class Problem:
 
     def __init__(self, model, stepper, nx, dt, Lx=2 * np.pi, aliased_fraction=1 / 3,
                  params=None, use_filter=False, calcN=None, ny=None, Ly=None, **filter_kw):
+        # model "ty" (thomasyamada/ThomasYamada.jl:55-74) takes stepper "ETDRK4"
         self.grid = TwoDGrid(nx, Lx, ny=ny, Ly=Ly, aliased_fraction=aliased_fraction)
         self.params = params
         self.model = model
@@ -468,10 +666,20 @@ class Problem:
             self.nf = 2
             self.L = qg2_L(self.grid, params)
             self.calcN = qg2_calcN if calcN is None else calcN
+        elif model == "ty":
+            self.nf = 4
+            self.L = ty_L(self.grid, params)
+            self.calcN = ty_calcN if calcN is None else calcN
+            if stepper != "ETDRK4":
+                raise ValueError("the Thomas-Yamada model is stepped with ETDRK4")
         else:
             raise ValueError(model)
         self.clock = Clock(dt)
-        if stepper == "FilteredAB3":
+        if stepper == "ETDRK4":
+            if model != "ty":
+                raise ValueError("ETDRK4 needs a diagonal L (Thomas-Yamada)")
+            self.ts = ETDRK4(self.L, dt, self.grid, self.nf)
+        elif stepper == "FilteredAB3":
             self.ts = FilteredAB3(self.L, self.grid, self.nf, **filter_kw)
         elif stepper == "IFMAB3":
             self.ts = IFMAB3(self.L, dt, self.grid, self.nf, use_filter=use_filter, **filter_kw)

@@ -39,6 +39,9 @@ def make(name, n, steps):
 
 
 if __name__ == "__main__":
-    for name in sw_cases.CASES:
+    only = sys.argv[1:]  # optional case names
+    for name in sw_cases.ALL_CASES:
+        if only and name not in only:
+            continue
         print(make(name, 32, [1, 10, 100]))
         print(make(name, 64, [10]))

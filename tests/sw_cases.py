@@ -12,11 +12,24 @@ import numpy as np
 import sw_oracle as O
 
 CASES = ["rsw_fab3", "rsw_ifmab3", "rsw_ifmrk4", "qg2_ifmab3", "qg2_ifmrk4", "qg2_fab3"]
+# Thomas–Yamada (thomasyamada/ThomasYamada.jl) stepped by FF ETDRK4
+TY_CASES = ["ty_etdrk4"]
+ALL_CASES = CASES + TY_CASES
 
 
 def case_params(name, n):
     model, st = name.split("_", 1)
-    stepper = {"fab3": "FilteredAB3", "ifmab3": "IFMAB3", "ifmrk4": "IFMRK4"}[st]
+    stepper = {"fab3": "FilteredAB3", "ifmab3": "IFMAB3", "ifmrk4": "IFMRK4", "etdrk4": "ETDRK4"}[st]
+    if model == "ty":
+        # thomasyamada/cpu-setup/Parameters.jl: Lx = 6π, ν = 5e-34 (Lx/2π)^16,
+        # nν = 8, Ro = 1, dt = 5e-3; annuli k0g = (10/3, 13/3), k0w = (0, 5/3).
+        # Small grids: larger dt and (32²) annuli inside the live band; a
+        # small barotropic amplitude so every term of calcN is active at once.
+        Lx = 6 * np.pi
+        kg, kw = ((4 / 3, 2.0), (0.0, 1.0)) if n <= 32 else ((10 / 3, 13 / 3), (0.0, 5 / 3))
+        return dict(model="ty", stepper=stepper, n=n, Lx=Lx, dt=2e-2 if n <= 256 else 5e-3,
+                    nu=5.0e-34 * (Lx / (2 * np.pi)) ** 16, nnu=8, Ro=1.0, k0g=kg, k0w=kw,
+                    at=0.1, ag=0.3, aw=0.1, seed=5678)
     if model == "rsw":
         cfl = 0.05 if n <= 256 else 0.01
         nut = 20.0
@@ -38,6 +51,9 @@ def case_params(name, n):
 
 
 def oracle_problem(p):
+    if p["model"] == "ty":
+        return O.Problem("ty", "ETDRK4", p["n"], p["dt"], Lx=p["Lx"],
+                         params=O.TYParams(p["nu"], p["nnu"], p["Ro"]))
     if p["model"] == "rsw":
         params = O.RSWParams(p["nu"], p["nnu"], p["f"], p["Cg"])
     else:
@@ -48,6 +64,9 @@ def oracle_problem(p):
 
 def initial_condition(p, grid):
     rng = np.random.default_rng(p["seed"])
+    if p["model"] == "ty":
+        return O.ty_initial_condition(grid, rng, k0w_range=p["k0w"], k0g_range=p["k0g"],
+                                      at=p["at"], ag=p["ag"], aw=p["aw"])
     if p["model"] == "rsw":
         return O.shafer_ic(grid, p["Kg"], p["Kw"], p["ag"], p["aw"], p["f"], p["Cg"] ** 2, rng)
     q0 = p["amp"] * rng.standard_normal((2, grid.ny, grid.nx))
@@ -56,8 +75,10 @@ def initial_condition(p, grid):
 
 def libsw_problem(p, **kw):
     """The GPU problem for the same case, through the package's public mirror."""
-    from juliaraytracingsw_amd import rotating_shallow_water as RSW, two_layer_qg as QG2
+    from juliaraytracingsw_amd import rotating_shallow_water as RSW, thomas_yamada as TY, two_layer_qg as QG2
 
+    if p["model"] == "ty":
+        return TY.Problem("gpu", nx=p["n"], Lx=p["Lx"], dt=p["dt"], nu=p["nu"], nnu=p["nnu"], Ro=p["Ro"], **kw)
     fk = dict(order=p["order"]) if p["stepper"] == "FilteredAB3" else {}
     if p["model"] == "rsw":
         return RSW.Problem("gpu", nx=p["n"], dt=p["dt"], nu=p["nu"], nnu=p["nnu"], f=p["f"], Cg=p["Cg"],

@@ -185,12 +185,94 @@ def test_kr0_column_hermitian_part_preserved():
     assert np.max(np.abs((col - herm)[:, live])) < 1e-12 * np.max(np.abs(col))
 
 
+# --- Thomas–Yamada + ETDRK4 ------------------------------------------------------
+def test_ty_decomposition_known_answers():
+    """thomasyamada/Notebooks/TestDecomposition.ipynb cells 2-3 and 7: a
+    purely geostrophic IC has no wave part (max|Wh| ~ 1e-13 there), and the
+    balanced + wave parts rebuild (u_c, v_c, p_c) (max|Gh + Wh - sol| ~ 5e-13)
+    — the TYUtils bases are orthonormal per mode."""
+    g = O.TwoDGrid(64, 6 * np.pi)
+    rng = np.random.default_rng(5678)
+    ic = O.ty_initial_condition(g, rng, at=0.5, ag=0.5, aw=0.0)
+    G, W = O.ty_decompose(ic, g)
+    assert np.max(np.abs(W)) < 1e-13 * np.max(np.abs(ic))
+    assert O.parsevalsum2(W[0], g) + O.parsevalsum2(W[1], g) + O.parsevalsum2(W[2], g) < 1e-24
+    rng = np.random.default_rng(1)
+    b = rng.standard_normal((4, g.nl, g.nkr)) + 1j * rng.standard_normal((4, g.nl, g.nkr))
+    G, W = O.ty_decompose(b, g)
+    assert np.max(np.abs(G + W - b[1:4])) < 1e-13 * np.max(np.abs(b))
+
+
+def test_ty_linear_modes():
+    """The TYUtils bases are the eigenvectors of the linear part of calcN!
+    (thomasyamada/ThomasYamada.jl:142-145): Φ₀ is balanced (eigenvalue 0)
+    and Φ± oscillate at ∓iω, ω = sqrt(1 + K²)."""
+    g = O.TwoDGrid(32, 6 * np.pi)
+    p = O.TYParams(0.0, 8, 0.0)  # Ro = 0: calcN is the linear part alone
+    P0 = O.ty_balanced_basis(g)
+    Pp, Pm = O.ty_wave_bases(g)
+    om = np.sqrt(1 + g.Krsq)
+    m = g.live.copy()
+    m[0, 0] = False
+    for P, lam in ((P0, 0 * om), (Pp, -1j * om), (Pm, 1j * om)):
+        sol = np.concatenate([np.zeros((1,) + P.shape[1:], complex), P])
+        N = O.ty_calcN(sol, g, p)
+        assert np.max(np.abs(N[1:4] - lam * g.dealias(P.copy()))[:, m]) < 1e-12 * np.max(om[m])
+        assert np.max(np.abs(N[0])) == 0
+
+
+def test_etdrk4_coefficients():
+    """getetdcoeffs' contour means equal the Cox–Matthews functions: the
+    z → 0 limits (ζ, α, β, Γ)/dt → (1/2, 1/6, 1/6, 1/6) and the closed forms
+    at moderate and stiff z (where the contour avoids their cancellation)."""
+    dt = 0.1
+    z = np.array([0.0, -1e-8, -0.5, -3.0, -40.0, -900.0])
+    ze, al, be, ga = O.etdrk4_coeffs(dt, z / dt)
+    np.testing.assert_allclose([ze[0] / dt, al[0] / dt, be[0] / dt, ga[0] / dt], [0.5, 1 / 6, 1 / 6, 1 / 6],
+                               rtol=1e-14)
+    zz = z[2:]
+    ez = np.exp(zz)
+    np.testing.assert_allclose(ze[2:], dt * (np.exp(zz / 2) - 1) / zz, rtol=1e-12)
+    np.testing.assert_allclose(al[2:], dt * (-4 - zz + ez * (4 - 3 * zz + zz ** 2)) / zz ** 3, rtol=1e-12)
+    np.testing.assert_allclose(be[2:], dt * (2 + zz + ez * (-2 + zz)) / zz ** 3, rtol=1e-12)
+    np.testing.assert_allclose(ga[2:], dt * (-4 - 3 * zz - zz ** 2 + ez * (4 - zz)) / zz ** 3, rtol=1e-12)
+
+
+def test_etdrk4_linear_exactness():
+    """With N ≡ 0, ETDRK4 is exp(L t)·sol0 exactly (E = e^{dt L} per mode)."""
+    g = O.TwoDGrid(32, 6 * np.pi)
+    p = O.TYParams(1e-4, 2, 1.0)
+    pr = O.Problem("ty", "ETDRK4", 32, 0.05, Lx=6 * np.pi, params=p, calcN=lambda s, g, p: np.zeros_like(s))
+    rng = np.random.default_rng(3)
+    pr.set_solution(rng.standard_normal(pr.sol.shape) + 1j * rng.standard_normal(pr.sol.shape))
+    s0 = pr.sol.copy()
+    pr.stepforward(6)
+    assert O.parity_error(pr.sol, np.exp(6 * 0.05 * O.ty_L(g, p)) * s0, g) < 1e-14
+
+
+def test_etdrk4_fourth_order():
+    """ETDRK4 converges at fourth order on the nonlinear TY step, also with a
+    stiff hyperviscosity (ν K⁴ up to ≈ 320, dt·L down to ≈ -26)."""
+    for nu in (0.0, 1.0):
+        p = dict(sw_cases.case_params("ty_etdrk4", 32), nu=nu, nnu=2)
+        sols = {}
+        for dt in (0.08, 0.04, 0.01):
+            p2 = dict(p, dt=dt)
+            pr = sw_cases.oracle_problem(p2)
+            pr.set_solution(sw_cases.initial_condition(p2, pr.grid))
+            pr.stepforward(int(round(1.6 / dt)))
+            sols[dt] = pr.grid.dealias(pr.sol.copy())
+        e1 = np.max(np.abs(sols[0.08] - sols[0.01]))
+        e2 = np.max(np.abs(sols[0.04] - sols[0.01]))
+        assert e1 / e2 > 12, (nu, e1 / e2)
+
+
 # --- golden fixtures -----------------------------------------------------------
 GOLDEN_FILES = sorted(glob.glob(os.path.join(GOLDEN, "*.npz")))
 
 
 def test_golden_present():
-    assert len(GOLDEN_FILES) == 2 * len(sw_cases.CASES)
+    assert len(GOLDEN_FILES) == 2 * len(sw_cases.ALL_CASES)
 
 
 @pytest.mark.parametrize("fn", GOLDEN_FILES, ids=[os.path.basename(f) for f in GOLDEN_FILES])
