@@ -51,10 +51,16 @@ struct sw_ctx {
   int P = 1;                                 // slabs in the decomposition
   bool dist = false;                         // one slab per process (P > 1)
   bool hostx = false;                        // dist with the host-staged exchange hook
-  ncclComm_t comm = nullptr;                 // dist without the hook: RCCL
+  ncclComm_t nccl = nullptr;                 // dist without the hook: RCCL
   char *hsend = nullptr, *hrecv = nullptr;   // pinned staging of the host-staged exchange
   size_t hbytes = 0;
   hipStream_t stream = nullptr;
+  // pipelined slab exchange: transposes on a side stream,
+  // ordered against the compute stream by events
+  hipStream_t comm = nullptr;
+  hipEvent_t ev_row = nullptr, ev_join = nullptr;
+  hipEvent_t ev_fwd[8] = {}, ev_col[8] = {};
+  bool overlap = false;                      // pipelined exchange (default: RCCL; SW_OVERLAP=0/1)
   double2 *tw_x = nullptr, *tw_y = nullptr;
   std::vector<Slab> sl;                      // slabs held by this process
   int head = 0;
@@ -250,21 +256,23 @@ struct Timer {
 // The transpose between the column and the row passes: block q
 // of every source slab p goes to block p of slab q.  inv: column-phase calcN
 // inputs -> row phase; fwd: row outputs -> column phase.  The blocks are
-// contiguous in both layouts, so no pack/unpack kernels exist.
-int transpose(sw_ctx* c, bool inv, int nfields) {
-  if (c->P == 1) return 0;
-  Timer tm(c, K_XCHG);
+// contiguous in both layouts, so no pack/unpack kernels exist.  Moves the
+// listed fields on stream `st` (RCCL: one group of sends/receives).
+int transpose_fields(sw_ctx* c, bool inv, const int* fields, int nfl, hipStream_t st) {
+  if (c->P == 1 || nfl == 0) return 0;
   const Geom& g0 = c->sl[0].g;
   const size_t blk = (size_t)g0.kcl * g0.nyl;  // elements per (slab pair, field)
   const long long MF = g0.mfield;
   if (!c->dist) {
-    for (int o = 0; o < nfields; ++o)
+    for (int i = 0; i < nfl; ++i) {
+      const int o = fields[i];
       for (int p = 0; p < c->P; ++p)
         for (int q = 0; q < c->P; ++q) {
           const double2* src = (inv ? c->sl[p].mic : c->sl[p].mfr) + o * MF + q * blk;
           double2* dst = (inv ? c->sl[q].mir : c->sl[q].mfc) + o * MF + p * blk;
-          HIPCHK(c, hipMemcpyAsync(dst, src, blk * sizeof(double2), hipMemcpyDeviceToDevice, c->stream));
+          HIPCHK(c, hipMemcpyAsync(dst, src, blk * sizeof(double2), hipMemcpyDeviceToDevice, st));
         }
+    }
     return 0;
   }
   const Slab& s = c->sl[0];
@@ -272,34 +280,112 @@ int transpose(sw_ctx* c, bool inv, int nfields) {
   if (c->hostx) {
     // stage [q][field][block] so block q of every field is one contiguous
     // message for rank q (one 2-D copy per field each way)
-    const size_t fb = blk * sizeof(double2), rowb = nfields * fb;
+    const size_t fb = blk * sizeof(double2), rowb = nfl * fb;
     if (rowb * c->P > c->hbytes) return fail(c, SW_E_INVALID, "exchange staging too small");
-    for (int o = 0; o < nfields; ++o)
-      HIPCHK(c, hipMemcpy2DAsync(c->hsend + o * fb, rowb, (inv ? s.mic : s.mfr) + o * MF, fb, fb, c->P,
-                                 hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (int i = 0; i < nfl; ++i)
+      HIPCHK(c, hipMemcpy2DAsync(c->hsend + i * fb, rowb, (inv ? s.mic : s.mfr) + fields[i] * MF, fb, fb, c->P,
+                                 hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
     if (c->cfg.exchange(c->cfg.exchange_user, c->hsend, c->hrecv, rowb, c->P) != 0)
       return fail(c, SW_E_COMM, "exchange hook failed");
-    for (int o = 0; o < nfields; ++o)
-      HIPCHK(c, hipMemcpy2DAsync((inv ? s.mir : s.mfc) + o * MF, fb, c->hrecv + o * fb, rowb, fb, c->P,
-                                 hipMemcpyHostToDevice, c->stream));
+    for (int i = 0; i < nfl; ++i)
+      HIPCHK(c, hipMemcpy2DAsync((inv ? s.mir : s.mfc) + fields[i] * MF, fb, c->hrecv + i * fb, rowb, fb, c->P,
+                                 hipMemcpyHostToDevice, st));
     return 0;
   }
   NCCLCHK(c, ncclGroupStart());
-  for (int o = 0; o < nfields; ++o) {
-    const double2* src = (inv ? s.mic : s.mfr) + o * MF;
-    double2* dst = (inv ? s.mir : s.mfc) + o * MF;
+  for (int i = 0; i < nfl; ++i) {
+    const double2* src = (inv ? s.mic : s.mfr) + fields[i] * MF;
+    double2* dst = (inv ? s.mir : s.mfc) + fields[i] * MF;
     for (int q = 0; q < c->P; ++q) {
       if (q == me) {
         HIPCHK(c, hipMemcpyAsync(dst + me * blk, src + me * blk, blk * sizeof(double2),
-                                 hipMemcpyDeviceToDevice, c->stream));
+                                 hipMemcpyDeviceToDevice, st));
       } else {
-        NCCLCHK(c, ncclSend(src + q * blk, 2 * blk, ncclDouble, q, c->comm, c->stream));
-        NCCLCHK(c, ncclRecv(dst + q * blk, 2 * blk, ncclDouble, q, c->comm, c->stream));
+        NCCLCHK(c, ncclSend(src + q * blk, 2 * blk, ncclDouble, q, c->nccl, st));
+        NCCLCHK(c, ncclRecv(dst + q * blk, 2 * blk, ncclDouble, q, c->nccl, st));
       }
     }
   }
   NCCLCHK(c, ncclGroupEnd());
+  return 0;
+}
+
+// fields [0, nfields) on the compute stream (the sequential schedule)
+int transpose(sw_ctx* c, bool inv, int nfields) {
+  if (c->P == 1) return 0;
+  Timer tm(c, K_XCHG);
+  int f[16];
+  for (int i = 0; i < nfields; ++i) f[i] = i;
+  return transpose_fields(c, inv, f, nfields, c->stream);
+}
+
+// --- pipelined exchange (P > 1, RCCL or in-process copies) ------------------
+// The column pass is launched per field group; each group's transpose runs on
+// the side stream while the compute stream transforms the next group:
+//  * forward: the row outputs go over in the order the column pass consumes
+//    them (fwd_need[f] = the row outputs column field f reads, nterms), and
+//    column field f starts as soon as its inputs have arrived;
+//  * inverse: the outputs of column group g (inv_out[g]) go over while group
+//    g+1 is computed; the row pass waits for the last of them.
+// Same kernels, same data, same results as the sequential schedule (tested
+// bitwise); only the order of independent work changes.
+struct PipeSpec {
+  int ninvg, nfc;          // inverse-producing column groups, column fields
+  int inv_out[5][3];       // per group: output fields (-1 = none)
+  int fwd_need[4][3];      // per column field: forward inputs (-1 = none)
+};
+const PipeSpec& pipe_spec(int model) {
+  // RSW: col_inv/col_step group f -> U,Uy | V | H; N_u <- P, N_v <- K,ζu,
+  //      N_η <- Q,vη (k_col_fwd nterms)
+  static const PipeSpec rsw = {3, 3, {{0, 3, -1}, {1, -1, -1}, {2, -1, -1}},
+                               {{0, -1, -1}, {1, 2, -1}, {3, 4, -1}}};
+  // QG2: layer l -> Q_l, Ψ_l, Ψy_l; N_l <- ψx q_l, ψy q_l
+  static const PipeSpec qg2 = {2, 2, {{0, 2, 4}, {1, 3, 5}}, {{0, 2, -1}, {1, 3, -1}}};
+  // TY: k_col_inv groups and k_col_fwd nterms
+  static const PipeSpec ty = {5, 4, {{0, 1, -1}, {2, 3, -1}, {4, 5, -1}, {6, -1, -1}, {7, 8, -1}},
+                              {{0, 1, 2}, {3, -1, -1}, {4, 5, -1}, {6, -1, -1}}};
+  return model == SW_MODEL_RSW ? rsw : (model == SW_MODEL_TY ? ty : qg2);
+}
+
+bool pipelined(const sw_ctx* c) { return c->P > 1 && !c->hostx && c->overlap && !c->prof; }
+
+// after the compute stream has launched the producer of inverse group g
+int inv_group_async(sw_ctx* c, int g) {
+  const PipeSpec& ps = pipe_spec(c->cfg.model);
+  HIPCHK(c, hipEventRecord(c->ev_col[g], c->stream));
+  HIPCHK(c, hipStreamWaitEvent(c->comm, c->ev_col[g], 0));
+  int f[3], n = 0;
+  for (int x : ps.inv_out[g])
+    if (x >= 0) f[n++] = x;
+  return transpose_fields(c, true, f, n, c->comm);
+}
+
+// the compute stream waits for everything queued on the side stream
+int join_comm(sw_ctx* c) {
+  if (!c->comm) return 0;
+  HIPCHK(c, hipEventRecord(c->ev_join, c->comm));
+  HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
+  return 0;
+}
+
+// after the compute stream has launched the row pass: forward transposes in
+// column-field order, ev_fwd[f] = inputs of column field f have arrived
+int fwd_async(sw_ctx* c) {
+  const PipeSpec& ps = pipe_spec(c->cfg.model);
+  HIPCHK(c, hipEventRecord(c->ev_row, c->stream));
+  HIPCHK(c, hipStreamWaitEvent(c->comm, c->ev_row, 0));
+  bool sent[16] = {};
+  for (int fc = 0; fc < ps.nfc; ++fc) {
+    int f[3], n = 0;
+    for (int x : ps.fwd_need[fc])
+      if (x >= 0 && !sent[x]) {
+        f[n++] = x;
+        sent[x] = true;
+      }
+    if (int rc = transpose_fields(c, false, f, n, c->comm)) return rc;
+    HIPCHK(c, hipEventRecord(c->ev_fwd[fc], c->comm));
+  }
   return 0;
 }
 
@@ -309,6 +395,21 @@ int calcN(sw_ctx* c, double2* Slab::*X, double2* Slab::*N) {
   if (c->cfg.nop_calcN) {  // NOPcalcN!: N .= 0
     for (Slab& s : c->sl)
       HIPCHK(c, hipMemsetAsync(s.*N, 0, (size_t)c->nf * s.g.cfield * sizeof(double2), c->stream));
+    return 0;
+  }
+  if (pipelined(c)) {
+    const PipeSpec& ps = pipe_spec(model);
+    for (int g = 0; g < ps.ninvg; ++g) {
+      for (Slab& s : c->sl) sw::launch_col_inv(model, s.g, c->p, s.*X, s.mic, c->tw_y, c->stream, g, 1);
+      if (int rc = inv_group_async(c, g)) return rc;
+    }
+    if (int rc = join_comm(c)) return rc;
+    for (Slab& s : c->sl) sw::launch_row(model, s.g, c->p, s.mir, s.mfr, c->tw_x, c->stream);
+    if (int rc = fwd_async(c)) return rc;
+    for (int f = 0; f < ps.nfc; ++f) {
+      HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_fwd[f], 0));
+      for (Slab& s : c->sl) sw::launch_col_fwd(model, s.g, c->p, s.mfc, s.*N, s.*X, c->tw_y, c->stream, f, 1);
+    }
     return 0;
   }
   {
@@ -369,6 +470,29 @@ sw::StepPtrs step_ptrs(const sw_ctx* c, const Slab& s) {
 
 int run_stage(sw_ctx* c, int op, int stage, double2* Slab::*X) {
   const int model = c->cfg.model;
+  if (use_fused(c) && pipelined(c) && model == SW_MODEL_RSW && op == sw::OP_FAB3) {
+    const PipeSpec& ps = pipe_spec(model);
+    if (!c->mixed_valid) {
+      for (int g = 0; g < ps.ninvg; ++g) {
+        for (Slab& s : c->sl) sw::launch_col_inv(model, s.g, c->p, s.*X, s.mic, c->tw_y, c->stream, g, 1);
+        if (int rc = inv_group_async(c, g)) return rc;
+      }
+    }
+    if (int rc = join_comm(c)) return rc;
+    for (Slab& s : c->sl) sw::launch_row(model, s.g, c->p, s.mir, s.mfr, c->tw_x, c->stream);
+    if (int rc = fwd_async(c)) return rc;
+    for (int f = 0; f < ps.nfc; ++f) {  // column field f -> inverse group f
+      HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_fwd[f], 0));
+      for (Slab& s : c->sl) {
+        sw::StepPtrs a = step_ptrs(c, s);
+        a.stage = stage;
+        sw::launch_col_step(model, op, s.g, c->p, a, s.mfc, s.mic, c->tw_y, c->stream, f, 1);
+      }
+      if (int rc = inv_group_async(c, f)) return rc;
+    }
+    c->mixed_valid = true;  // mir receives the next stage's inverse transforms (joined before use)
+    return 0;
+  }
   if (use_fused(c)) {
     if (!c->mixed_valid) {
       {
@@ -473,7 +597,7 @@ void scatter_cols(const Geom& g, int& lo, int& hi) {
 // (in place allowed: mine == dst + rank * bytes)
 int allgather(sw_ctx* c, const void* mine, void* dst, size_t bytes) {
   if (!c->hostx) {
-    NCCLCHK(c, ncclAllGather(mine, dst, bytes, ncclUint8, c->comm, c->stream));
+    NCCLCHK(c, ncclAllGather(mine, dst, bytes, ncclUint8, c->nccl, c->stream));
     return 0;
   }
   if (bytes * c->P > c->hbytes) return fail(c, SW_E_INVALID, "exchange staging too small");
@@ -612,10 +736,26 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   HIPCHK(c, hipEventCreate(&c->ev0));
   HIPCHK(c, hipEventCreate(&c->ev1));
+  if (P > 1) {
+    HIPCHK(c, hipStreamCreateWithFlags(&c->comm, hipStreamNonBlocking));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_row, hipEventDisableTiming));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+    for (int i = 0; i < 8; ++i) {
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_fwd[i], hipEventDisableTiming));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_col[i], hipEventDisableTiming));
+    }
+    // Pipelined by default across GPUs (RCCL over xGMI runs beside the column
+    // kernels).  With every slab in this process the "transposes" are copies
+    // through the same HBM the kernels stream, and splitting the column pass
+    // into per-field launches only costs (tools/overlap_check.py, DESIGN.md
+    // §6): sequential by default there.
+    c->overlap = c->dist && !c->hostx;
+    if (const char* e = std::getenv("SW_OVERLAP")) c->overlap = e[0] == '1';
+  }
   if (c->dist && !c->hostx) {
     ncclUniqueId id;
     std::memcpy(&id, k.comm_unique_id, sizeof(id));
-    NCCLCHK(c, ncclCommInitRank(&c->comm, P, id, k.rank));
+    NCCLCHK(c, ncclCommInitRank(&c->nccl, P, id, k.rank));
   }
 
   c->sl.resize(nlocal);
@@ -720,7 +860,14 @@ void sw_destroy(sw_ctx* c) {
   void* ptrs[] = {c->tw_x, c->tw_y, c->stage, c->gbuf, c->dflt, c->flag, c->ecols, c->esum, c->erec};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
-  if (c->comm) (void)ncclCommDestroy(c->comm);
+  if (c->nccl) (void)ncclCommDestroy(c->nccl);
+  for (hipEvent_t e : {c->ev_row, c->ev_join})
+    if (e) (void)hipEventDestroy(e);
+  for (int i = 0; i < 8; ++i) {
+    if (c->ev_fwd[i]) (void)hipEventDestroy(c->ev_fwd[i]);
+    if (c->ev_col[i]) (void)hipEventDestroy(c->ev_col[i]);
+  }
+  if (c->comm) (void)hipStreamDestroy(c->comm);
   if (c->hsend) (void)hipHostFree(c->hsend);
   if (c->hrecv) (void)hipHostFree(c->hrecv);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -783,6 +930,7 @@ int sw_step(sw_ctx* c, int64_t nsteps) {
   HIPCHK(c, hipSetDevice(c->cfg.device));
   for (int64_t i = 0; i < nsteps; ++i)
     if (int rc = step_once(c)) return rc;
+  if (int rc = join_comm(c)) return rc;  // primed inverse transposes still on the side stream
   HIPCHK(c, hipGetLastError());
   if (c->cfg.check_nan && nsteps > 0) {
     int h = 0;
@@ -1035,6 +1183,7 @@ int sw_profile_steps(sw_ctx* c, int64_t nsteps, sw_kernel_stat* out, int32_t max
     s.launches = 0;
     s.ms = 0.0;
   }
+  if (int rc = join_comm(c)) return rc;
   c->prof = true;
   int rc = 0;
   for (int64_t i = 0; i < nsteps && !rc; ++i) rc = step_once(c);

@@ -334,13 +334,17 @@ struct ExpOf<2> {
 // ---------------------------------------------------------------------------
 struct Bufs;  // fwd
 
+// column-pass launches over a range of groups (col_inv: output groups, see
+// k_col_inv; col_fwd / col_step: fields); n < 0 = from the first to the last
+int col_inv_groups(int model);
+int col_fields(int model);
 void launch_col_inv(int model, const Geom& g, const Phys& p, const double2* X, double2* Minv,
-                    const double2* tw_y, hipStream_t s);
+                    const double2* tw_y, hipStream_t s, int g0 = 0, int ng = -1);
 void launch_row(int model, const Geom& g, const Phys& p, const double2* Minv, double2* Mfwd,
                 const double2* tw_x, hipStream_t s);
 // X: the compact calcN input (TY adds its linear terms from it; unused otherwise)
 void launch_col_fwd(int model, const Geom& g, const Phys& p, const double2* Mfwd, double2* N,
-                    const double2* X, const double2* tw_y, hipStream_t s);
+                    const double2* X, const double2* tw_y, hipStream_t s, int f0 = 0, int nfl = -1);
 // Pointers of one stepper stage (see sw_kernels.hip).
 struct StepPtrs {
   const double2* sol;  // state in
@@ -361,7 +365,8 @@ struct StepPtrs {
 enum { OP_FAB3 = 0, OP_IFMAB3 = 1, OP_RK4 = 2, OP_ETDRK4 = 3 };
 enum { ETD_E = 0, ETD_E2, ETD_ZETA, ETD_ALPHA, ETD_BETA, ETD_GAMMA, ETD_N };
 void launch_col_step(int model, int op, const Geom& g, const Phys& p, const StepPtrs& a,
-                     const double2* Mf, double2* Minv, const double2* tw_y, hipStream_t s);
+                     const double2* Mf, double2* Minv, const double2* tw_y, hipStream_t s, int f0 = 0,
+                     int nfl = -1);
 void launch_step_elem(int nf, int op, const Geom& g, const Phys& p, const StepPtrs& a,
                       const double2* N, double2* xs, hipStream_t s);
 void launch_gather(int nf, const Geom& g, const double2* full, double2* compact, hipStream_t s);

@@ -68,13 +68,13 @@ __device__ __forceinline__ double2 zero2() { return make_double2(0.0, 0.0); }
 template <int MODEL, int LOG2N>
 __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     k_col_inv(Geom g, Phys p, const double2* __restrict__ X, double2* __restrict__ M,
-              const double2* __restrict__ tw) {
+              const double2* __restrict__ tw, int gbase) {
   using B = Blk<LOG2N>;
   constexpr int NT = B::NT;
   extern __shared__ double2 smem[];
   const LineCtx c = line_ctx<LOG2N>();
   const int krl = (B::NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * B::NB + c.ln;
-  const int grp = blockIdx.y;
+  const int grp = gbase + blockIdx.y;
   const bool live = krl < g.kcn;
   if (B::NB == 1 && !live) return;  // padding column: nobody reads it
   double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
@@ -650,13 +650,13 @@ constexpr int model_nf() {
 template <int MODEL, int LOG2N>
 __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     k_col_fwd(Geom g, Phys p, const double2* __restrict__ Mf, double2* __restrict__ N,
-              const double2* __restrict__ X, const double2* __restrict__ tw) {
+              const double2* __restrict__ X, const double2* __restrict__ tw, int gbase) {
   using B = Blk<LOG2N>;
   constexpr int NT = B::NT;
   extern __shared__ double2 smem[];
   const LineCtx c = line_ctx<LOG2N>();
   const int krl = (B::NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * B::NB + c.ln;
-  const int grp = blockIdx.y;
+  const int grp = gbase + blockIdx.y;
   const bool live = krl < g.kcn;
   if (B::NB == 1 && !live) return;
   const int krA = krl < g.kcl ? krl : g.kcl - 1;  // in-bounds address
@@ -1204,14 +1204,14 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
 template <int LOG2N>
 __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     k_col_step_fab3_rsw(Geom g, Phys p, StepPtrs a, const double2* __restrict__ Mf,
-                        double2* __restrict__ Minv, const double2* __restrict__ tw) {
+                        double2* __restrict__ Minv, const double2* __restrict__ tw, int fbase) {
   using B = Blk<LOG2N>;
   constexpr int NT = B::NT;
   extern __shared__ double2 smem[];
   const LineCtx c = line_ctx<LOG2N>();
   int krl, f;
-  if (B::NB == 1 && gridDim.y == 1) {
-    // 1-D grid of 3*kcl blocks (kcl a multiple of 64).  The 3 fields of the 8
+  if (fbase < 0) {
+    // all fields, 1-D grid of 3*kcl blocks (NB == 1, kcl a multiple of 64).  The 3 fields of the 8
     // columns that share each 128-B chunk of the mixed layout (24 blocks) sit
     // on one XCD label (b % 8) within 192 consecutive block ids: they meet in
     // one L2, where the other fields' reads of the old state and the chunk
@@ -1221,7 +1221,7 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     krl = q * 64 + x * 8 + jj / 3;
   } else {
     krl = blockIdx.x * B::NB + c.ln;
-    f = blockIdx.y;
+    f = fbase + blockIdx.y;
   }
   const bool live = krl < g.kcn;
   if (B::NB == 1 && !live) return;
@@ -1574,14 +1574,14 @@ static size_t lds_bytes() {
 template <int L>
 struct ColInvL {
   static void run(int model, const Geom& g, const Phys& p, const double2* X, double2* M,
-                  const double2* tw, hipStream_t s) {
-    const dim3 grid(col_blocks<L>(g), model == MODEL_RSW ? 3 : (model == MODEL_TY ? 5 : 2));
+                  const double2* tw, hipStream_t s, int g0, int ng) {
+    const dim3 grid(col_blocks<L>(g), ng);
     if (model == MODEL_RSW)
-      hipLaunchKernelGGL((k_col_inv<MODEL_RSW, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw);
+      hipLaunchKernelGGL((k_col_inv<MODEL_RSW, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
     else if (model == MODEL_TY)
-      hipLaunchKernelGGL((k_col_inv<MODEL_TY, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw);
+      hipLaunchKernelGGL((k_col_inv<MODEL_TY, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
     else
-      hipLaunchKernelGGL((k_col_inv<MODEL_QG2, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw);
+      hipLaunchKernelGGL((k_col_inv<MODEL_QG2, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
   }
 };
 template <int L>
@@ -1604,17 +1604,17 @@ struct RowL {
 template <int L>
 struct ColFwdL {
   static void run(int model, const Geom& g, const Phys& p, const double2* Mf, double2* N, const double2* X,
-                  const double2* tw, hipStream_t s) {
-    const dim3 grid(col_blocks<L>(g), model == MODEL_RSW ? 3 : (model == MODEL_TY ? 4 : 2));
+                  const double2* tw, hipStream_t s, int f0, int nfl) {
+    const dim3 grid(col_blocks<L>(g), nfl);
     if (model == MODEL_RSW)
       hipLaunchKernelGGL((k_col_fwd<MODEL_RSW, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, Mf, N, X,
-                         tw);
+                         tw, f0);
     else if (model == MODEL_TY)
       hipLaunchKernelGGL((k_col_fwd<MODEL_TY, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, Mf, N, X,
-                         tw);
+                         tw, f0);
     else
       hipLaunchKernelGGL((k_col_fwd<MODEL_QG2, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, Mf, N, X,
-                         tw);
+                         tw, f0);
   }
 };
 template <int L>
@@ -1630,17 +1630,23 @@ struct RowC2r1L {
   }
 };
 
+// number of column-pass groups per launch unit: col_inv groups, col_fwd fields
+int col_inv_groups(int model) { return model == MODEL_RSW ? 3 : (model == MODEL_TY ? 5 : 2); }
+int col_fields(int model) { return model == MODEL_RSW ? 3 : (model == MODEL_TY ? 4 : 2); }
+
 void launch_col_inv(int model, const Geom& g, const Phys& p, const double2* X, double2* Minv,
-                    const double2* tw_y, hipStream_t s) {
-  dispatch_log2<ColInvL>(g.log2ny, model, g, p, X, Minv, tw_y, s);
+                    const double2* tw_y, hipStream_t s, int g0, int ng) {
+  if (ng < 0) ng = col_inv_groups(model) - g0;
+  dispatch_log2<ColInvL>(g.log2ny, model, g, p, X, Minv, tw_y, s, g0, ng);
 }
 void launch_row(int model, const Geom& g, const Phys& p, const double2* Minv, double2* Mfwd,
                 const double2* tw_x, hipStream_t s) {
   dispatch_log2<RowL>(g.log2nx, model, g, p, Minv, Mfwd, tw_x, s);
 }
 void launch_col_fwd(int model, const Geom& g, const Phys& p, const double2* Mfwd, double2* N,
-                    const double2* X, const double2* tw_y, hipStream_t s) {
-  dispatch_log2<ColFwdL>(g.log2ny, model, g, p, Mfwd, N, X, tw_y, s);
+                    const double2* X, const double2* tw_y, hipStream_t s, int f0, int nfl) {
+  if (nfl < 0) nfl = col_fields(model) - f0;
+  dispatch_log2<ColFwdL>(g.log2ny, model, g, p, Mfwd, N, X, tw_y, s, f0, nfl);
 }
 
 static inline dim3 mode_grid(const Geom& g) { return dim3((unsigned)((g.cfield + 255) / 256)); }
@@ -1648,17 +1654,21 @@ static inline dim3 mode_grid(const Geom& g) { return dim3((unsigned)((g.cfield +
 template <int L>
 struct ColStepL {
   static void run(int model, int op, const Geom& g, const Phys& p, const StepPtrs& a,
-                  const double2* Mf, double2* Minv, const double2* tw, hipStream_t s) {
+                  const double2* Mf, double2* Minv, const double2* tw, hipStream_t s, int f0, int nfl) {
     const dim3 grid(col_blocks<L>(g)), blk(Blk<L>::THREADS);
     const size_t sh = lds_bytes<L>();
 #define SW_CS(M, O) hipLaunchKernelGGL((k_col_step<M, L, O>), grid, blk, sh, s, g, p, a, Mf, Minv, tw)
     if (model == MODEL_RSW) {
-      if (op == OP_FAB3)
-        hipLaunchKernelGGL((k_col_step_fab3_rsw<L>),
-                           (Blk<L>::NB == 1 && g.kcl % 64 == 0) ? dim3(3 * g.kcl) : dim3(col_blocks<L>(g), 3),
-                           blk, sh,
-                           s, g, p, a, Mf, Minv, tw);
-      else if (op == OP_IFMAB3) SW_CS(MODEL_RSW, OP_IFMAB3);
+      // all three fields: the XCD-interleaved 1-D grid where it applies; a
+      // field range (pipelined slab exchange): one grid row per field
+      const bool all = f0 == 0 && nfl == 3;
+      if (op == OP_FAB3) {
+        if (all && Blk<L>::NB == 1 && g.kcl % 64 == 0)
+          hipLaunchKernelGGL((k_col_step_fab3_rsw<L>), dim3(3 * g.kcl), blk, sh, s, g, p, a, Mf, Minv, tw, -1);
+        else
+          hipLaunchKernelGGL((k_col_step_fab3_rsw<L>), dim3(col_blocks<L>(g), nfl), blk, sh, s, g, p, a, Mf, Minv,
+                             tw, f0);
+      } else if (op == OP_IFMAB3) SW_CS(MODEL_RSW, OP_IFMAB3);
       else SW_CS(MODEL_RSW, OP_RK4);
     } else {
       if (op == OP_FAB3) SW_CS(MODEL_QG2, OP_FAB3);
@@ -1670,8 +1680,9 @@ struct ColStepL {
 };
 
 void launch_col_step(int model, int op, const Geom& g, const Phys& p, const StepPtrs& a,
-                     const double2* Mf, double2* Minv, const double2* tw_y, hipStream_t s) {
-  dispatch_log2<ColStepL>(g.log2ny, model, op, g, p, a, Mf, Minv, tw_y, s);
+                     const double2* Mf, double2* Minv, const double2* tw_y, hipStream_t s, int f0, int nfl) {
+  if (nfl < 0) nfl = col_fields(model) - f0;
+  dispatch_log2<ColStepL>(g.log2ny, model, op, g, p, a, Mf, Minv, tw_y, s, f0, nfl);
 }
 
 void launch_step_elem(int nf, int op, const Geom& g, const Phys& p, const StepPtrs& a,

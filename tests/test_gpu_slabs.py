@@ -20,15 +20,21 @@ def _slabbed(p, P, **kw):
     return sw_cases.libsw_problem(p, decomposition=dict(nranks=P, local_slabs=P), **kw)
 
 
+@pytest.mark.parametrize("overlap", [True, False])
 @pytest.mark.parametrize("unfused", [False, True])
 @pytest.mark.parametrize("P", [2, 4])
-@pytest.mark.parametrize("name", sw_cases.CASES)
-def test_slabs_bitwise(name, P, unfused):
+@pytest.mark.parametrize("name", sw_cases.ALL_CASES)
+def test_slabs_bitwise(name, P, unfused, overlap, monkeypatch):
+    """overlap: the pipelined schedule (column groups launched one by one,
+    their transposes on the side stream, events between the streams); else
+    the sequential schedule (SW_OVERLAP=0).  Both bitwise equal P = 1."""
     p = sw_cases.case_params(name, 128)
     pr = sw_cases.oracle_problem(p)
     ic = sw_cases.initial_condition(p, pr.grid)
     a = sw_cases.libsw_problem(p, unfused=unfused)
+    monkeypatch.setenv("SW_OVERLAP", "1" if overlap else "0")
     b = _slabbed(p, P, unfused=unfused)
+    monkeypatch.delenv("SW_OVERLAP", raising=False)
     a.sol = ic
     b.sol = ic
     assert np.array_equal(a.sol, b.sol)
@@ -41,13 +47,17 @@ def test_slabs_bitwise(name, P, unfused):
     b.close()
 
 
+@pytest.mark.parametrize("overlap", [True, False])
 @pytest.mark.parametrize("P", [2, 8])
-def test_slabs_bitwise_2048(P):
-    """The metric configuration (RSW 2048² FilteredAB3) split 2 and 8 ways."""
+def test_slabs_bitwise_2048(P, overlap, monkeypatch):
+    """The metric configuration (RSW 2048² FilteredAB3) split 2 and 8 ways,
+    pipelined (the RCCL default) and sequential."""
     from juliaraytracingsw_amd import drivers
 
     a, _ = drivers.rsw_problem(2048, "FilteredAB3")
+    monkeypatch.setenv("SW_OVERLAP", "1" if overlap else "0")
     b, _ = drivers.rsw_problem(2048, "FilteredAB3", decomposition=dict(nranks=P, local_slabs=P))
+    monkeypatch.delenv("SW_OVERLAP", raising=False)
     a.stepforward(5)
     b.stepforward(5)
     assert np.array_equal(a.sol, b.sol)

@@ -151,3 +151,23 @@ def test_ty_invalid_combinations():
         TY.Problem("gpu", nx=64, stepper="IFMAB3")
     with pytest.raises(LibSWError):
         RSW.Problem("gpu", nx=64, stepper="ETDRK4")
+
+
+def test_ty_snapshot_restart(tmp_path):
+    """Output/saveoutput of prob.sol then a restart from the file (state and
+    clock): the single-step ETDRK4 continues bitwise."""
+    from juliaraytracingsw_amd import output
+
+    p, pr, a = _pair(64)
+    fn = str(tmp_path / "ty.jld2")
+    out = output.Output(a, fn)
+    output.saveproblem(out)
+    a.stepforward(4)
+    output.saveoutput(out)
+    a.stepforward(3)
+    b = sw_cases.libsw_problem(p)
+    assert output.restart(b, fn) == 4
+    b.stepforward(3)
+    assert np.array_equal(a.sol, b.sol) and b.clock.step == 7
+    a.close()
+    b.close()
