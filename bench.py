@@ -32,6 +32,10 @@ def b_alg(model, stepper, n):
     bT = 16 * Ns + 8 * Np
     if model == "rsw":
         return 13 * bT + (18 if stepper == "FilteredAB3" else 15) * 16 * Ns
+    if model == "mlqg":
+        # 4 calcN of 2-layer batched 3 c2r + 2 r2c (GF calcN_advection!) and
+        # 4 FilteredRK4 stages of 4.25·2 state + 2 N fields
+        return 4 * 10 * bT + 4 * (4.25 * 2 + 2) * 16 * Ns
     if model == "ty":
         # 4 calcN of 11 c2r + 13 r2c (thomasyamada/ThomasYamada.jl:129-262) and
         # 4 ETDRK4 stages of (3.75·4 state + 4 N) fields + 1.25 coefficient planes
@@ -50,7 +54,8 @@ def cpu_baseline(model, stepper, n, budget_s=20.0, max_steps=20):
 
     cores = min(16, len(os.sched_getaffinity(0)))
     O.set_fft_workers(cores)
-    short = {'FilteredAB3': 'fab3', 'IFMAB3': 'ifmab3', 'IFMRK4': 'ifmrk4', 'ETDRK4': 'etdrk4'}[stepper]
+    short = {'FilteredAB3': 'fab3', 'IFMAB3': 'ifmab3', 'IFMRK4': 'ifmrk4', 'ETDRK4': 'etdrk4',
+             'FilteredRK4': 'frk4'}[stepper]
     p = sw_cases.case_params(f"{model}_{short}", n)
     pr = sw_cases.oracle_problem(p)
     pr.set_solution(sw_cases.initial_condition(p, pr.grid))
@@ -73,8 +78,9 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--n", type=int, default=2048)
-    ap.add_argument("--model", default="rsw", choices=["rsw", "qg2", "ty"])
-    ap.add_argument("--stepper", default="FilteredAB3", choices=["FilteredAB3", "IFMAB3", "IFMRK4", "ETDRK4"])
+    ap.add_argument("--model", default="rsw", choices=["rsw", "qg2", "ty", "mlqg"])
+    ap.add_argument("--stepper", default="FilteredAB3",
+                    choices=["FilteredAB3", "IFMAB3", "IFMRK4", "ETDRK4", "FilteredRK4"])
     ap.add_argument("--profile-steps", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", default="ensemble", choices=["ensemble", "slab"])
@@ -106,10 +112,14 @@ def main():
     dec = slab_comm.rccl_decomposition(rank, world) if slab else None
     if args.model == "ty":
         args.stepper = "ETDRK4"  # the only Thomas-Yamada stepper
+    if args.model == "mlqg":
+        args.stepper = "FilteredRK4"  # TwoLayerSimulation's stepper
     if args.model == "rsw":
         prob, P = drivers.rsw_problem(args.n, args.stepper, device=local, decomposition=dec)
     elif args.model == "ty":
         prob, P = drivers.ty_problem(args.n, device=local, decomposition=dec)
+    elif args.model == "mlqg":
+        prob, P = drivers.mlqg_problem(args.n, device=local, decomposition=dec)
     else:
         prob, P = drivers.qg2_problem(args.n, args.stepper, device=local, decomposition=dec)
 
@@ -169,7 +179,8 @@ def main():
         "dtype": "f64",
         "data": {"rsw": "synthetic random-phase IC (set_shafer_initial_condition!, seeded)",
                  "qg2": "synthetic randn PV IC (set_seed_initial_condition!, seeded)",
-                 "ty": "synthetic random-phase IC (TYdriver set_initial_condition, seeded)"}[args.model],
+                 "ty": "synthetic random-phase IC (TYdriver set_initial_condition, seeded)",
+                 "mlqg": "synthetic filtered randn PV IC (TwoLayerSimulation, seeded)"}[args.model],
         "config": {"workload": f"{args.model.upper()} {args.n}^2 {args.stepper} fp64 step, dt={P['dt']:.6g}",
                    "grid": args.n,
                    "parallelism": (f"slab{world}" if slab else f"ensemble{world}") if world > 1 else "single-gpu"},

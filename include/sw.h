@@ -32,19 +32,23 @@
 extern "C" {
 #endif
 
-#define SW_ABI_VERSION 3
+#define SW_ABI_VERSION 4
 
 /* models */
 #define SW_MODEL_RSW 0   /* rsw/RotatingShallowWater.jl: fields (u, v, η), 3×3 L   */
 #define SW_MODEL_QG2 1   /* swqg/TwoLayerQG.jl: fields (q1, q2), 2×2 L             */
 #define SW_MODEL_TY  2   /* thomasyamada/ThomasYamada.jl: fields (ζ_T, u_c, v_c, p_c),
                             real diagonal L = -ν K^(2nν), stepper ETDRK4 */
+#define SW_MODEL_MLQG 3  /* GeophysicalFlows MultiLayerQG, nlayers = 2, as
+                            simulation/TwoLayerSimulation.jl:37-47 builds it: fields
+                            (q1, q2); aliased_fraction may be 0 (the reference's) */
 
 /* steppers */
 #define SW_STEP_FILTERED_AB3 0 /* FF FilteredAB3 with per-mode matvec L·sol */
 #define SW_STEP_IFMAB3       1 /* utils/IFMAB3.jl:68-169                               */
 #define SW_STEP_IFMRK4       2 /* Lawson IF-RK4, the build's definition of utils/IFMRK4.jl (A9) */
 #define SW_STEP_ETDRK4       3 /* FF ETDRK4TimeStepper (ThomasYamada.Problem default, :60) */
+#define SW_STEP_FILTERED_RK4 4 /* FF FilteredRK4 (simulation/Parameters.jl:25), RSW/QG2/MLQG */
 
 /* error codes */
 #define SW_OK            0
@@ -132,6 +136,11 @@ typedef struct sw_config {
   void* exchange_user;
   /* physics — TY Params (thomasyamada/ThomasYamada.jl:21-25)               */
   double  Ro;               /* Rossby number                               */
+  /* physics — MLQG (GeophysicalFlows MultiLayerQG.Problem keywords, 2 layers;
+   * μ, ν, nν above): f₀, β, rest depths H, buoyancies b (g′ = b₁ − b₂) and
+   * imposed zonal flows U per layer                                        */
+  double  f0, beta;
+  double  H[2], b[2], Ulayer[2];
 } sw_config;
 
 typedef struct sw_ctx sw_ctx;

@@ -8,6 +8,8 @@ mirror of the reference's module interfaces:
 * ``rotating_shallow_water`` — rsw/RotatingShallowWater.jl
 * ``two_layer_qg``           — swqg/TwoLayerQG.jl
 * ``thomas_yamada``          — thomasyamada/ThomasYamada.jl (ETDRK4)
+* ``multilayer_qg``          — GeophysicalFlows MultiLayerQG (FilteredRK4), simulation/TwoLayerSimulation.jl
+* ``output``                 — snapshot output / restart (FF Output, utils/SequencedOutputs.jl)
 * ``drivers``                — rsw/RSWDriver.jl, swqg/TwoLayerDriver.jl setup
 """
 from ._lib import LibSWError, load, LIB_PATH  # noqa: F401

@@ -10,15 +10,15 @@ import os
 
 import numpy as np
 
-SW_ABI_VERSION = 3
-SW_MODEL_RSW, SW_MODEL_QG2, SW_MODEL_TY = 0, 1, 2
-SW_STEP_FILTERED_AB3, SW_STEP_IFMAB3, SW_STEP_IFMRK4, SW_STEP_ETDRK4 = 0, 1, 2, 3
+SW_ABI_VERSION = 4
+SW_MODEL_RSW, SW_MODEL_QG2, SW_MODEL_TY, SW_MODEL_MLQG = 0, 1, 2, 3
+SW_STEP_FILTERED_AB3, SW_STEP_IFMAB3, SW_STEP_IFMRK4, SW_STEP_ETDRK4, SW_STEP_FILTERED_RK4 = 0, 1, 2, 3, 4
 SW_OK, SW_E_INVALID, SW_E_NOMEM, SW_E_HIP, SW_E_COMM, SW_E_NAN, SW_E_STATE = 0, -1, -2, -3, -4, -5, -6
 SW_PHYS_U, SW_PHYS_V, SW_PHYS_ETA, SW_PHYS_ZETA, SW_PHYS_Q, SW_PHYS_PSI = 0, 1, 2, 3, 4, 5
 SW_DIAG_NAN, SW_DIAG_KE, SW_DIAG_PE, SW_DIAG_CFL, SW_DIAG_KE2, SW_DIAG_KE1, SW_DIAG_BT = 0, 1, 2, 3, 4, 5, 6
 
 STEPPERS = {"FilteredAB3": SW_STEP_FILTERED_AB3, "IFMAB3": SW_STEP_IFMAB3, "IFMRK4": SW_STEP_IFMRK4,
-            "ETDRK4": SW_STEP_ETDRK4}
+            "ETDRK4": SW_STEP_ETDRK4, "FilteredRK4": SW_STEP_FILTERED_RK4}
 
 # every symbol include/sw.h declares (checked by tests/test_abi.py)
 EXPORTS = [
@@ -55,6 +55,8 @@ class SwConfig(C.Structure):
         ("comm_unique_id", C.c_void_p),
         ("exchange", EXCHANGE_FN), ("exchange_user", C.c_void_p),
         ("Ro", C.c_double),
+        ("f0", C.c_double), ("beta", C.c_double),
+        ("H", C.c_double * 2), ("b", C.c_double * 2), ("Ulayer", C.c_double * 2),
     ]
 
 

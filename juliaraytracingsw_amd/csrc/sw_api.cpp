@@ -48,6 +48,7 @@ struct sw_ctx {
   sw_config cfg{};
   Phys p{};
   int nf = 0, ninv = 0, nfwd = 0;
+  int kmodel = 0;                            // kernel family (MLQG -> QG2)
   int P = 1;                                 // slabs in the decomposition
   bool dist = false;                         // one slab per process (P > 1)
   bool hostx = false;                        // dist with the host-staged exchange hook
@@ -145,6 +146,12 @@ Geom make_geom(const sw_config& k, int P, int s) {
   g.kc = iLx - 1;
   g.lc = iLy - 1;
   g.lr2 = iRy;
+  if (k.aliased_fraction == 0) {
+    // FF with aliased_fraction = 0 zeroes only the Nyquist column kr = nx/2
+    // (kc = nx/2 above) and the Nyquist row l = -ny/2
+    g.lc = k.ny / 2;
+    g.lr2 = k.ny / 2 + 1;
+  }
   g.Lr = g.lc + (k.ny - g.lr2);
   g.LrP = (g.Lr + 7) / 8 * 8;
   g.Lx = k.Lx;
@@ -208,6 +215,9 @@ double op_fields(const sw_ctx* c) {
   // ETDRK4 stages: 1 u in / n1,acc,s1 out; 2 u in / n2,s2 out; 3 s1,acc,n1,n2
   // in / acc,s2 out; 4 acc in / u out; plus the coefficient planes (real: half
   // a field each) 4, 2, 3, 1
+  // FilteredRK4 stages: 1 sol in / acc,x out; 2-3 x,sol,acc in / acc,x out;
+  // 4 x,sol,acc in / sol out
+  if (st == SW_STEP_FILTERED_RK4) return (3.0 * nf + 5.0 * nf + 5.0 * nf + 4.0 * nf) / 4;
   if (st == SW_STEP_ETDRK4) return (4.0 * nf + 3.0 * nf + 6.0 * nf + 2.0 * nf) / 4 + (2.0 + 1.0 + 1.5 + 0.5) / 4;
   if (st == SW_STEP_FILTERED_AB3) return 3 * nf + 2 * nf;  // sol,R-1,R-2 in; sol,RHS out
   if (st == SW_STEP_IFMAB3) return 3 * nf + 2 * nf;        // sol,N-1,N-2 in; sol,N out
@@ -352,7 +362,7 @@ bool pipelined(const sw_ctx* c) { return c->P > 1 && !c->hostx && c->overlap && 
 
 // after the compute stream has launched the producer of inverse group g
 int inv_group_async(sw_ctx* c, int g) {
-  const PipeSpec& ps = pipe_spec(c->cfg.model);
+  const PipeSpec& ps = pipe_spec(c->kmodel);
   HIPCHK(c, hipEventRecord(c->ev_col[g], c->stream));
   HIPCHK(c, hipStreamWaitEvent(c->comm, c->ev_col[g], 0));
   int f[3], n = 0;
@@ -372,7 +382,7 @@ int join_comm(sw_ctx* c) {
 // after the compute stream has launched the row pass: forward transposes in
 // column-field order, ev_fwd[f] = inputs of column field f have arrived
 int fwd_async(sw_ctx* c) {
-  const PipeSpec& ps = pipe_spec(c->cfg.model);
+  const PipeSpec& ps = pipe_spec(c->kmodel);
   HIPCHK(c, hipEventRecord(c->ev_row, c->stream));
   HIPCHK(c, hipStreamWaitEvent(c->comm, c->ev_row, 0));
   bool sent[16] = {};
@@ -391,7 +401,7 @@ int fwd_async(sw_ctx* c) {
 
 // equation.calcN!(N, X, …): col_inv -> transpose -> row -> transpose -> col_fwd
 int calcN(sw_ctx* c, double2* Slab::*X, double2* Slab::*N) {
-  const int model = c->cfg.model;
+  const int model = c->kmodel;
   if (c->cfg.nop_calcN) {  // NOPcalcN!: N .= 0
     for (Slab& s : c->sl)
       HIPCHK(c, hipMemsetAsync(s.*N, 0, (size_t)c->nf * s.g.cfield * sizeof(double2), c->stream));
@@ -440,7 +450,9 @@ int calcN(sw_ctx* c, double2* Slab::*X, double2* Slab::*N) {
 // re-evaluates the coupled update in every group measured slower at 2048²
 // than the separate kernels.
 bool use_fused(const sw_ctx* c) {
-  if (c->cfg.unfused || c->cfg.nop_calcN || c->cfg.model == SW_MODEL_TY) return false;
+  if (c->cfg.unfused || c->cfg.nop_calcN || c->cfg.model == SW_MODEL_TY || c->cfg.model == SW_MODEL_MLQG ||
+      c->cfg.stepper == SW_STEP_FILTERED_RK4)
+    return false;
   if (c->fuse_all) return true;
   return c->cfg.model == SW_MODEL_RSW && c->cfg.stepper == SW_STEP_FILTERED_AB3;
 }
@@ -452,7 +464,7 @@ sw::StepPtrs step_ptrs(const sw_ctx* c, const Slab& s) {
   a.sol_out = (st == SW_STEP_FILTERED_AB3) ? s.sol2 : s.sol;
   a.xs = s.xs;
   a.euler = c->step < 3 ? 1 : 0;
-  if (st == SW_STEP_IFMRK4) {
+  if (st == SW_STEP_IFMRK4 || st == SW_STEP_FILTERED_RK4) {
     a.h0 = s.acc;
   } else if (st == SW_STEP_ETDRK4) {
     a.h0 = s.acc;
@@ -469,7 +481,7 @@ sw::StepPtrs step_ptrs(const sw_ctx* c, const Slab& s) {
 }
 
 int run_stage(sw_ctx* c, int op, int stage, double2* Slab::*X) {
-  const int model = c->cfg.model;
+  const int model = c->kmodel;
   if (use_fused(c) && pipelined(c) && model == SW_MODEL_RSW && op == sw::OP_FAB3) {
     const PipeSpec& ps = pipe_spec(model);
     if (!c->mixed_valid) {
@@ -519,7 +531,7 @@ int run_stage(sw_ctx* c, int op, int stage, double2* Slab::*X) {
   } else {
     // AB3 steppers: calcN writes straight into this step's history slot, which
     // the update then overwrites in place (N -> RHS or N); nbuf aliases it
-    if (op != sw::OP_RK4 && op != sw::OP_ETDRK4)
+    if (op != sw::OP_RK4 && op != sw::OP_ETDRK4 && op != sw::OP_FRK4)
       for (Slab& s : c->sl) s.nbuf = s.hist[c->head];
     if (int rc = calcN(c, X, &Slab::nbuf)) return rc;
     Timer tm(c, K_UPD);
@@ -560,6 +572,9 @@ int step_once(sw_ctx* c) {
     c->head = (c->head + 1) % 3;  // RHS₋₂ <- RHS₋₁ <- RHS by rotation (utils/IFMAB3.jl:165-166)
     if (st == SW_STEP_FILTERED_AB3)
       for (Slab& s : c->sl) std::swap(s.sol, s.sol2);
+  } else if (st == SW_STEP_FILTERED_RK4) {  // FF RK4substeps! + RK4update! + filter
+    for (int stage = 1; stage <= 4; ++stage)
+      if (int rc = run_stage(c, sw::OP_FRK4, stage, stage == 1 ? &Slab::sol : &Slab::xs)) return rc;
   } else if (st == SW_STEP_ETDRK4) {  // FF ETDRK4substeps! + ETDRK4update!
     for (int stage = 1; stage <= 4; ++stage)
       if (int rc = run_stage(c, sw::OP_ETDRK4, stage,
@@ -573,7 +588,8 @@ int step_once(sw_ctx* c) {
   c->step += 1;
   if (rec) {
     if (rsw && st == SW_STEP_FILTERED_AB3) record_energy(c, &Slab::sol2);  // the pre-update buffer
-    else if (rsw && st == SW_STEP_IFMRK4) record_energy(c, &Slab::xs);    // stage-4 input
+    else if (rsw && (st == SW_STEP_IFMRK4 || st == SW_STEP_FILTERED_RK4))
+      record_energy(c, &Slab::xs);  // stage-4 input
     else if (!rsw) record_energy(c, &Slab::sol);
     c->diag_steps.push_back(c->step);
     c->diag_t.push_back(c->t);
@@ -707,15 +723,20 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   c->cfg = *cfg;
   *out = c;
   const sw_config& k = c->cfg;
-  if (k.model != SW_MODEL_RSW && k.model != SW_MODEL_QG2 && k.model != SW_MODEL_TY)
-    return fail(c, SW_E_INVALID, "unknown model");
-  if (k.stepper < 0 || k.stepper > 3) return fail(c, SW_E_INVALID, "unknown stepper");
+  if (k.model < SW_MODEL_RSW || k.model > SW_MODEL_MLQG) return fail(c, SW_E_INVALID, "unknown model");
+  if (k.stepper < 0 || k.stepper > 4) return fail(c, SW_E_INVALID, "unknown stepper");
+  if (k.model == SW_MODEL_MLQG && k.stepper != SW_STEP_FILTERED_RK4 && k.stepper != SW_STEP_FILTERED_AB3)
+    return fail(c, SW_E_INVALID, "MultiLayerQG steps with FilteredRK4 (or FilteredAB3): its L is the hyperviscosity alone");
+  if (k.model == SW_MODEL_MLQG && (!(k.H[0] > 0) || !(k.H[1] > 0) || k.b[0] == k.b[1]))
+    return fail(c, SW_E_INVALID, "MultiLayerQG needs H > 0 and b[0] != b[1]");
   if ((k.model == SW_MODEL_TY) != (k.stepper == SW_STEP_ETDRK4))
     return fail(c, SW_E_INVALID, "ETDRK4 (diagonal L) is the Thomas-Yamada stepper and TY steps with ETDRK4 only");
   if (!pow2(k.nx) || !pow2(k.ny) || k.nx < 32 || k.ny < 32 || k.nx > 8192 || k.ny > 8192)
     return fail(c, SW_E_INVALID, "nx, ny must be powers of two in [32, 8192]");
-  if (!(k.aliased_fraction > 0 && k.aliased_fraction < 1))
-    return fail(c, SW_E_INVALID, "aliased_fraction must be in (0,1)");
+  if (!(k.aliased_fraction >= 0 && k.aliased_fraction < 1))
+    return fail(c, SW_E_INVALID, "aliased_fraction must be in [0,1)");
+  if (k.aliased_fraction == 0 && k.model == SW_MODEL_RSW)
+    return fail(c, SW_E_INVALID, "RSW needs aliased_fraction > 0 (its calcN uses the dealiased vorticity form)");
   if (k.filter_order < 0) return fail(c, SW_E_INVALID, "filter_order must be >= 0");
   const int P = k.nranks;
   if (!pow2(P) || k.ny / P < 32)
@@ -774,13 +795,24 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   p.mu = k.mu;
   p.F = k.F;
   p.Ro = k.Ro;
+  p.model = k.model;
+  if (k.model == SW_MODEL_MLQG) {  // MultiLayerQG.Params, 2 layers, no topography
+    const double gp = k.b[0] - k.b[1];
+    p.F = k.f0 * k.f0 / (gp * k.H[0]);
+    p.F2 = k.f0 * k.f0 / (gp * k.H[1]);
+    p.U1 = k.Ulayer[0];
+    p.U2 = k.Ulayer[1];
+    p.Qy1 = k.beta - p.F * (k.Ulayer[1] - k.Ulayer[0]);
+    p.Qy2 = k.beta - p.F2 * (k.Ulayer[0] - k.Ulayer[1]);
+  }
   p.dt = k.dt;
-  p.use_filter = (k.stepper == SW_STEP_FILTERED_AB3) ? 1 : (k.use_filter ? 1 : 0);
+  p.use_filter = (k.stepper == SW_STEP_FILTERED_AB3 || k.stepper == SW_STEP_FILTERED_RK4) ? 1 : (k.use_filter ? 1 : 0);
   p.forder = k.filter_order;
   p.innerK = k.filter_innerK;
   p.decay = -std::log(k.filter_tol) / std::pow(k.filter_outerK - k.filter_innerK, (double)k.filter_order);
 
   c->nf = k.model == SW_MODEL_RSW ? 3 : (k.model == SW_MODEL_TY ? 4 : 2);
+  c->kmodel = k.model == SW_MODEL_MLQG ? SW_MODEL_QG2 : k.model;  // MLQG runs the 2LQG kernels
   // mixed fields per calcN: RSW U,V,H,Uy in / P,K,ζu,Q,vη out;
   // QG2 Q,Ψ,Ψy per layer in / ψx q, ψy q per layer out; TY ζ,ψ,ût,∂y ut,
   // uc,∂y uc,vc,pc,∂y pc in / 7 combined product spectra out (k_row)
@@ -804,7 +836,7 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
       if ((rc = alloc(c, (void**)&s.mir, c->ninv * mb))) return rc;
       if ((rc = alloc(c, (void**)&s.mfc, c->nfwd * mb))) return rc;
     }
-    if (k.stepper == SW_STEP_IFMRK4 || k.stepper == SW_STEP_ETDRK4) {
+    if (k.stepper == SW_STEP_IFMRK4 || k.stepper == SW_STEP_ETDRK4 || k.stepper == SW_STEP_FILTERED_RK4) {
       if ((rc = alloc(c, (void**)&s.acc, c->nf * cb))) return rc;
       if ((rc = alloc(c, (void**)&s.nbuf, c->nf * cb))) return rc;
     }
@@ -815,7 +847,7 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
       if ((rc = alloc(c, (void**)&s.etd, (size_t)sw::ETD_N * g.cfield * sizeof(double)))) return rc;
       sw::launch_etd_coeffs(g, c->p, s.etd, c->stream);
       HIPCHK(c, hipGetLastError());
-    } else if (k.stepper != SW_STEP_IFMRK4) {
+    } else if (k.stepper != SW_STEP_IFMRK4 && k.stepper != SW_STEP_FILTERED_RK4) {
       for (int i = 0; i < 3; ++i)
         if ((rc = alloc(c, (void**)&s.hist[i], c->nf * cb))) return rc;
     }
@@ -951,7 +983,9 @@ int sw_calcN(sw_ctx* c, const void* sol, void* N, size_t bytes) {
   for (Slab& s : c->sl) {
     sw::launch_gather(c->nf, s.g, c->stage, s.xs, c->stream);
     // scratch output: the ring slot that the next step overwrites anyway
-    if (c->cfg.stepper != SW_STEP_IFMRK4 && c->cfg.stepper != SW_STEP_ETDRK4) s.nbuf = s.hist[c->head];
+    if (c->cfg.stepper != SW_STEP_IFMRK4 && c->cfg.stepper != SW_STEP_ETDRK4 &&
+        c->cfg.stepper != SW_STEP_FILTERED_RK4)
+      s.nbuf = s.hist[c->head];
   }
   if (int rc = calcN(c, &Slab::xs, &Slab::nbuf)) return rc;
   if (int rc = collect_full(c, &Slab::nbuf)) return rc;
@@ -1019,6 +1053,14 @@ static void energies_from_sums(const sw_ctx* c, const double a[3], double& ke, d
     ke = norm * a[0] / (2 * g.Lx * g.Ly);
     ke2 = 0.0;
     pe = 0.5 * c->p.Cg2 * norm * a[1] / (g.Lx * g.Ly);
+  } else if (c->cfg.model == SW_MODEL_MLQG) {
+    // MultiLayerQG.energies: KE_j = parsevalsum(K²|ψ_j|²)/(2 Lx Ly) H_j/H,
+    // PE = parsevalsum(|ψ₂ - ψ₁|²)/(2 Lx Ly) f₀²/g′/H
+    const sw_config& k = c->cfg;
+    const double Ht = k.H[0] + k.H[1];
+    ke = norm * a[0] / (2 * g.Lx * g.Ly) * k.H[0] / Ht;
+    ke2 = norm * a[1] / (2 * g.Lx * g.Ly) * k.H[1] / Ht;
+    pe = norm * a[2] / (2 * g.Lx * g.Ly) * k.f0 * k.f0 / (k.b[0] - k.b[1]) / Ht;
   } else if (c->cfg.model == SW_MODEL_TY) {
     // thomasyamada/ThomasYamada.jl:333-345: plain parsevalsum2 values
     ke = norm * a[1];
@@ -1078,7 +1120,8 @@ int sw_diag(sw_ctx* c, int32_t id, double* out) {
     // dt · max(maximum(|vars.u|)/dx, maximum(|vars.v|)/dy), both layers for 2LQG;
     // thomasyamada/TYdriver.jl:150: signed maxima of u_c, v_c, u_T, v_T
     const Geom& g0 = c->sl[0].g;
-    const bool ty = c->cfg.model == SW_MODEL_TY;
+    // signed maxima: thomasyamada/TYdriver.jl:150, simulation/TwoLayerSimulation.jl:124
+    const bool ty = c->cfg.model == SW_MODEL_TY || c->cfg.model == SW_MODEL_MLQG;
     const int nlay = c->cfg.model == SW_MODEL_RSW ? 1 : 2;
     unsigned long long* mx = reinterpret_cast<unsigned long long*>(c->flag + 512);  // [u, v] maxima keys
     HIPCHK(c, hipMemsetAsync(mx, 0, 2 * sizeof(unsigned long long), c->stream));

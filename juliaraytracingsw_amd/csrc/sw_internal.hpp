@@ -10,8 +10,10 @@
 
 namespace sw {
 
-enum { MODEL_RSW = 0, MODEL_QG2 = 1, MODEL_TY = 2 };
-enum { ST_FAB3 = 0, ST_IFMAB3 = 1, ST_IFMRK4 = 2, ST_ETDRK4 = 3 };
+// MODEL_MLQG (GeophysicalFlows MultiLayerQG, 2 layers) runs the MODEL_QG2
+// kernels; Phys::model selects its streamfunction and linear terms at run time
+enum { MODEL_RSW = 0, MODEL_QG2 = 1, MODEL_TY = 2, MODEL_MLQG = 3 };
+enum { ST_FAB3 = 0, ST_IFMAB3 = 1, ST_IFMRK4 = 2, ST_ETDRK4 = 3, ST_FRK4 = 4 };
 
 // Grid geometry of one slab in the layouts of DESIGN.md §2 and §6.
 // Slab s of P owns kr columns [kr0, kr0 + kcl) in the column passes and
@@ -44,6 +46,9 @@ struct Phys {
   int nnu;
   double U, mu, F;    // QG2
   double Ro;          // TY Rossby number
+  int model;          // MODEL_* of the problem (MLQG shares the QG2 kernels)
+  // MLQG: F1 = F (above), F2, per-layer mean flow and background PV gradient
+  double F2, U1, U2, Qy1, Qy2;
   // filter (FF makefilter)
   int use_filter, forder;
   double innerK, decay;
@@ -189,6 +194,31 @@ __host__ __device__ inline void qg2_L(const Phys& p, double k, double l, cplx L[
   const double D = -(p.nu * ipow(K2, p.nnu));
   L[0][0] = cx(L[0][0].re + D, L[0][0].im + (-k * p.U));
   L[1][1] = cx(L[1][1].re + D, L[1][1].im + (k * p.U));
+}
+
+// Streamfunction of layer `layer` from the PV pair at K² (0 at K = 0):
+//  2LQG streamfunctionfrompv! (swqg/TwoLayerQG.jl:101-111, its op order);
+//  MLQG ψ̂ = S⁻¹ q̂, S⁻¹ = [[-(K²+F₂), -F₁], [-F₂, -(K²+F₁)]] / (K²(K²+F₁+F₂))
+__host__ __device__ inline void qg_psi(const Phys& p, double K2, double q1r, double q1i, double q2r, double q2i,
+                                       int layer, double& pr, double& pi) {
+#pragma clang fp contract(off)
+  if (p.model == MODEL_MLQG) {
+    const double inv = K2 == 0.0 ? 0.0 : 1.0 / (K2 * (K2 + p.F + p.F2));
+    if (layer == 0) {
+      pr = (-(K2 + p.F2) * q1r - p.F * q2r) * inv;
+      pi = (-(K2 + p.F2) * q1i - p.F * q2i) * inv;
+    } else {
+      pr = (-p.F2 * q1r - (K2 + p.F) * q2r) * inv;
+      pi = (-p.F2 * q1i - (K2 + p.F) * q2i) * inv;
+    }
+    return;
+  }
+  const double iK2 = K2 == 0.0 ? 0.0 : 1.0 / K2;
+  const double den = K2 + 2.0 * p.F;
+  const double qsr = q1r + q2r, qsi = q1i + q2i;
+  const double qgr = layer ? q2r : q1r, qgi = layer ? q2i : q1i;
+  pr = (-(K2 * qgr + p.F * qsr) / den) * iK2;
+  pi = (-(K2 * qgi + p.F * qsi) / den) * iK2;
 }
 
 // ---------------------------------------------------------------------------
@@ -362,7 +392,7 @@ struct StepPtrs {
   double2* xs2;
   const double* etd;
 };
-enum { OP_FAB3 = 0, OP_IFMAB3 = 1, OP_RK4 = 2, OP_ETDRK4 = 3 };
+enum { OP_FAB3 = 0, OP_IFMAB3 = 1, OP_RK4 = 2, OP_ETDRK4 = 3, OP_FRK4 = 4 };
 enum { ETD_E = 0, ETD_E2, ETD_ZETA, ETD_ALPHA, ETD_BETA, ETD_GAMMA, ETD_N };
 void launch_col_step(int model, int op, const Geom& g, const Phys& p, const StepPtrs& a,
                      const double2* Mf, double2* Minv, const double2* tw_y, hipStream_t s, int f0 = 0,

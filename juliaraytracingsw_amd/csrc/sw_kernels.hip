@@ -193,12 +193,8 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
       }
       const double l = lwav(g, m);
       const double K2 = k * k + l * l;
-      const double iK2 = K2 == 0.0 ? 0.0 : 1.0 / K2;
-      const double den = K2 + 2.0 * p.F;
-      const double2 qs = cadd(q1, q2);
       const double2 qg = grp == 0 ? q1 : q2;
-      double2 ps = make_double2(-(K2 * qg.x + p.F * qs.x), -(K2 * qg.y + p.F * qs.y));
-      psi[s] = make_double2((ps.x / den) * iK2, (ps.y / den) * iK2);
+      qg_psi(p, K2, q1.x, q1.y, q2.x, q2.y, grp, psi[s].x, psi[s].y);
       v[s] = cscale(qg, scale);
     }
     fft_line<LOG2N, +1>(v, c.t, tws, line);
@@ -700,6 +696,22 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
       const int j = compact_of(g, c.t + s * NT);
       if (j >= 0) {
         double2 r = acc[s];
+        if constexpr (MODEL == MODEL_QG2) {
+          if (p.model == MODEL_MLQG) {
+            // MultiLayerQG calcN!: the mean flow and background-gradient
+            // terms -ik U_j q_j - ik Qy_j ψ_j, and the bottom drag μ K² ψ_2
+            // on the lower layer, from the calcN input
+            const long long i = (long long)krl * g.LrP + j;
+            const double l = lwav(g, c.t + s * NT);
+            const double K2 = k * k + l * l;
+            const double2 q1 = X[i], q2 = X[g.cfield + i];
+            double2 ps;
+            qg_psi(p, K2, q1.x, q1.y, q2.x, q2.y, grp, ps.x, ps.y);
+            const double2 qg = grp ? q2 : q1;
+            r = csub(csub(r, cmul_i(qg, k * (grp ? p.U2 : p.U1))), cmul_i(ps, k * (grp ? p.Qy2 : p.Qy1)));
+            if (grp == 1) r = cadd(r, cscale(ps, p.mu * K2));
+          }
+        }
         if constexpr (MODEL == MODEL_TY) {
           // linear terms (thomasyamada/ThomasYamada.jl:142-145), from the
           // dealiased calcN input (ζ, uc, vc, pc)
@@ -737,7 +749,15 @@ __device__ __forceinline__ void model_L(const Phys& p, double k, double l, cplx 
   if constexpr (NF == 3) {
     rsw_L(p, k, l, L);
   } else {
-    qg2_L(p, k, l, L);
+    if (p.model == MODEL_MLQG) {  // MultiLayerQG Equation: L = -ν K^(2nν) per layer
+      const double D = -(p.nu * ipow(k * k + l * l, p.nnu));
+      L[0][0] = cx(D);
+      L[0][1] = cx(0.0);
+      L[1][0] = cx(0.0);
+      L[1][1] = cx(D);
+    } else {
+      qg2_L(p, k, l, L);
+    }
   }
 }
 
@@ -959,12 +979,61 @@ __device__ __forceinline__ void op_etdrk4(const Geom& g, const Phys& p, const St
   }
 }
 
+// FF FilteredRK4 (simulation/Parameters.jl:25; RK4substeps!/RK4update!):
+// RHS_s = N(X_s) + L·X_s for the stage input X_s (a.sol at stage 1, a.xs
+// after), then
+//   1: acc = RHS/6;        x = sol + dt/2 RHS
+//   2: acc = acc + RHS/3;  x = sol + dt/2 RHS
+//   3: acc = acc + RHS/3;  x = sol + dt RHS
+//   4: sol = (sol + dt (acc + RHS/6)) · filter
+// acc follows FF's left-to-right sum RHS₁/6 + RHS₂/3 + RHS₃/3 + RHS₄/6.
+template <int NF>
+__device__ __forceinline__ void op_frk4(const Geom& g, const Phys& p, const StepPtrs& a, long long i,
+                                        double k, double l, const cplx n[NF], cplx x[NF]) {
+#pragma clang fp contract(off)
+  const long long cf = g.cfield;
+  const double dt = p.dt;
+  cplx L[NF][NF], X[NF], u[NF], rhs[NF], acc[NF];
+  model_L<NF>(p, k, l, L);
+  load_vec<NF>(a.stage == 1 ? a.sol : a.xs, cf, i, X);
+  if (a.stage == 1) {
+#pragma unroll
+    for (int f = 0; f < NF; ++f) u[f] = X[f];
+  } else {
+    load_vec<NF>(a.sol, cf, i, u);
+  }
+  matvec<NF>(L, X, rhs);
+#pragma unroll
+  for (int f = 0; f < NF; ++f) rhs[f] = n[f] + rhs[f];
+  if (a.stage > 1) load_vec<NF>(a.h0, cf, i, acc);
+  if (a.stage < 4) {
+    const double h = a.stage == 3 ? dt : dt / 2;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const cplx r = a.stage == 1 ? cx(rhs[f].re / 6, rhs[f].im / 6) : cx(rhs[f].re / 3, rhs[f].im / 3);
+      acc[f] = a.stage == 1 ? r : acc[f] + r;
+      x[f] = u[f] + h * rhs[f];
+    }
+    store_vec<NF>(a.h0, cf, i, acc);
+    store_vec<NF>(a.xs, cf, i, x);
+  } else {
+    const double filt = filter_value(g, p, k, l);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const cplx r = u[f] + dt * (acc[f] + cx(rhs[f].re / 6, rhs[f].im / 6));
+      x[f] = cx(r.re * filt, r.im * filt);
+    }
+    store_vec<NF>(a.sol_out, cf, i, x);
+  }
+}
+
 template <int NF, int OP>
 __device__ __forceinline__ void step_op(const Geom& g, const Phys& p, const StepPtrs& a, long long i,
                                         double k, double l, const cplx n[NF], cplx x[NF]) {
   if constexpr (OP == OP_FAB3) op_fab3<NF>(g, p, a, i, k, l, n, x);
   else if constexpr (OP == OP_IFMAB3) op_ifmab3<NF>(g, p, a, i, k, l, n, x);
   else if constexpr (OP == OP_ETDRK4) op_etdrk4<NF>(g, p, a, i, n, x);
+  else if constexpr (OP == OP_FRK4) op_frk4<NF>(g, p, a, i, k, l, n, x);
   else op_rk4<NF>(g, p, a, i, k, l, n, x);
 }
 
@@ -1174,12 +1243,7 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
       for (int s = 0; s < 8; ++s) {  // streamfunctionfrompv! (swqg/TwoLayerQG.jl:101-111)
         const double l = lwav(g, c.t + s * NT);
         const double K2 = k * k + l * l;
-        const double iK2 = K2 == 0.0 ? 0.0 : 1.0 / K2;
-        const double den = K2 + 2.0 * p.F;
-        const double2 qs = cadd(q1[s], q2[s]);
-        const double2 qg = f ? q2[s] : q1[s];
-        const double2 ps = make_double2(-(K2 * qg.x + p.F * qs.x), -(K2 * qg.y + p.F * qs.y));
-        psi[s] = make_double2((ps.x / den) * iK2, (ps.y / den) * iK2);
+        qg_psi(p, K2, q1[s].x, q1[s].y, q2[s].x, q2[s].y, f, psi[s].x, psi[s].y);
         v[s] = cscale(psi[s], scale);
       }
       fft_line<LOG2N, +1>(v, c.t, tws, line);
@@ -1378,11 +1442,8 @@ __global__ void k_make_spec(Geom g, Phys p, int model, int fid, const double2* _
       r = qg;
     } else {
       const double K2 = k * k + l * l;
-      const double iK2 = K2 == 0.0 ? 0.0 : 1.0 / K2;
-      const double den = K2 + 2.0 * p.F;
-      const double2 qs = cadd(q1, q2);
-      double2 ps = make_double2(-(K2 * qg.x + p.F * qs.x), -(K2 * qg.y + p.F * qs.y));
-      ps = make_double2((ps.x / den) * iK2, (ps.y / den) * iK2);
+      double2 ps;
+      qg_psi(p, K2, q1.x, q1.y, q2.x, q2.y, layer, ps.x, ps.y);
       if (id == 5) r = ps;
       else if (id == 3) r = make_double2(-K2 * ps.x, -K2 * ps.y);
       else if (id == 0) r = cmul_i(ps, -l);
@@ -1490,14 +1551,10 @@ __global__ void __launch_bounds__(256) k_energy_cols(Geom g, Phys p, int model,
       } else {
         const double l = lwav(g, lrow_of(g, j));
         const double K2 = k * k + l * l;
-        const double iK2 = K2 == 0.0 ? 0.0 : 1.0 / K2;
-        const double den = K2 + 2.0 * p.F;
         const double2 q1 = sol[i], q2 = sol[cf + i];
-        const double2 qs = cadd(q1, q2);
-        double2 p1 = make_double2(-(K2 * q1.x + p.F * qs.x), -(K2 * q1.y + p.F * qs.y));
-        double2 p2 = make_double2(-(K2 * q2.x + p.F * qs.x), -(K2 * q2.y + p.F * qs.y));
-        p1 = make_double2((p1.x / den) * iK2, (p1.y / den) * iK2);
-        p2 = make_double2((p2.x / den) * iK2, (p2.y / den) * iK2);
+        double2 p1, p2;
+        qg_psi(p, K2, q1.x, q1.y, q2.x, q2.y, 0, p1.x, p1.y);
+        qg_psi(p, K2, q1.x, q1.y, q2.x, q2.y, 1, p2.x, p2.y);
         a0 += w * K2 * (p1.x * p1.x + p1.y * p1.y);
         a1 += w * K2 * (p2.x * p2.x + p2.y * p2.y);
         const double dx_ = p1.x - p2.x, dy_ = p1.y - p2.y;
@@ -1691,11 +1748,13 @@ void launch_step_elem(int nf, int op, const Geom& g, const Phys& p, const StepPt
   if (nf == 4) {
     SW_SE(4, OP_ETDRK4);
   } else if (nf == 3) {
-    if (op == OP_FAB3) SW_SE(3, OP_FAB3);
+    if (op == OP_FRK4) SW_SE(3, OP_FRK4);
+    else if (op == OP_FAB3) SW_SE(3, OP_FAB3);
     else if (op == OP_IFMAB3) SW_SE(3, OP_IFMAB3);
     else SW_SE(3, OP_RK4);
   } else {
-    if (op == OP_FAB3) SW_SE(2, OP_FAB3);
+    if (op == OP_FRK4) SW_SE(2, OP_FRK4);
+    else if (op == OP_FAB3) SW_SE(2, OP_FAB3);
     else if (op == OP_IFMAB3) SW_SE(2, OP_IFMAB3);
     else SW_SE(2, OP_RK4);
   }

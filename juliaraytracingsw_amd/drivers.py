@@ -10,6 +10,7 @@ import time
 import numpy as np
 
 from . import _lib
+from . import multilayer_qg as MLQG
 from . import rotating_shallow_water as RSW
 from . import thomas_yamada as TY
 from . import two_layer_qg as QG2
@@ -36,6 +37,53 @@ def ty_parameters(nx=None, **over):
         P["nx"] = nx
     P.setdefault("nu", 5.0e-34 * (P["Lx"] / (2 * np.pi)) ** 16)
     return P
+
+
+# simulation/Parameters.jl (TwoLayerSimulation with GeophysicalFlows MultiLayerQG)
+MLQG_PARAMETERS = dict(Lx=2 * np.pi, nx=512, f=1.0, deformation_radius=1 / 15, intervortex_radius=1 / 2,
+                       avg_U=0.1, H0=1.0, nnu=8, nu=0.0, stepper="FilteredRK4", b2=1.0, beta=0.0)
+
+
+def mlqg_parameters(nx=None, **over):
+    """simulation/Parameters.jl: compute_parameters (μ, b₁, shear), dt = 0.02 dx/avg_U,
+    U = [s, -s], b = [b₁, b₂], H = [H0/2, H0/2], q0_amplitude = 1e-2 avg_U."""
+    P = dict(MLQG_PARAMETERS, **over)
+    if nx is not None:
+        P["nx"] = nx
+    c1, c2 = 3.2, 0.36
+    l_star = P["intervortex_radius"] / P["deformation_radius"]
+    kappa_star = c2 / math.log(l_star / c1)
+    s = P["avg_U"] / l_star
+    mu = 2 * s * kappa_star / P["deformation_radius"]
+    b1 = 4 * P["f"] ** 2 * P["deformation_radius"] ** 2 / P["H0"] + P["b2"]
+    dx = P["Lx"] / P["nx"]
+    return dict(P, mu=mu, U=[s, -s], b=[b1, P["b2"]], H=[P["H0"] / 2, P["H0"] / 2], dt=0.02 * dx / P["avg_U"],
+                q0_amplitude=1e-2 * P["avg_U"])
+
+
+def _ff_filter(grid, order=4, innerK=0.65, outerK=1.0, tol=1e-15):
+    """FF makefilter values on the host (set-up only; libsw's stepper evaluates
+    the same formula per mode)."""
+    K = np.sqrt((grid.kr[None, :] * grid.dx / np.pi) ** 2 + (grid.l[:, None] * grid.dy / np.pi) ** 2)
+    decay = -np.log(tol) / (outerK - innerK) ** order
+    return np.where(K < innerK, 1.0, np.exp(-decay * (K - innerK) ** order))
+
+
+def mlqg_problem(nx=512, seed=1234, device=0, decomposition=None, **over):
+    """TwoLayerSimulation.start! set-up (simulation/TwoLayerSimulation.jl:13-53):
+    MultiLayerQG.Problem(2, dev; nx, Lx, f₀, H, b, U, μ, β, dt, stepper,
+    aliased_fraction = 0), q₀ = q0_amplitude·randn (seeded numpy stream),
+    q̂₀ = filter·rfft(q₀), set_q!."""
+    P = mlqg_parameters(nx, **over)
+    prob = MLQG.Problem(2, "gpu", nx=P["nx"], Lx=P["Lx"], f0=P["f"], H=P["H"], b=P["b"], U=P["U"], mu=P["mu"],
+                        beta=P["beta"], nu=P["nu"], nnu=P["nnu"], dt=P["dt"], stepper=P["stepper"],
+                        aliased_fraction=0, device=device, decomposition=decomposition)
+    rng = np.random.default_rng(seed)
+    g = prob.grid
+    q0 = P["q0_amplitude"] * rng.standard_normal((2, g.ny, g.nx))
+    q0h = _ff_filter(g)[None] * np.fft.rfft2(q0, axes=(-2, -1))
+    prob.sol = q0h  # set_q!(prob, irfft(q̂₀)) = upload of q̂₀ (dealiased)
+    return prob, P
 
 
 def rsw_parameters(nx, **over):
@@ -208,7 +256,8 @@ def run_frames(prob, nframes, output_freq, diags=(), on_frame=None, log_every=10
     optional per-frame callback (updatevars!/output)."""
     from . import problem
 
-    mod = {_lib.SW_MODEL_RSW: RSW, _lib.SW_MODEL_QG2: QG2, _lib.SW_MODEL_TY: TY}[prob.model]
+    mod = {_lib.SW_MODEL_RSW: RSW, _lib.SW_MODEL_QG2: QG2, _lib.SW_MODEL_TY: TY,
+           _lib.SW_MODEL_MLQG: MLQG}[prob.model]
     t0 = time.time()
     for frame in range(nframes):
         if log_every and frame % log_every == 0:

@@ -57,7 +57,10 @@ class Problem:
         cfg.aliased_fraction = float(aliased_fraction)
         cfg.dt = float(dt)
         for k, v in params.items():
-            setattr(cfg, k, v)
+            if k in ("H", "b", "Ulayer"):
+                getattr(cfg, k)[:] = [float(x) for x in v]
+            else:
+                setattr(cfg, k, v)
         cfg.use_filter = 1 if use_filter else 0
         cfg.filter_order = int(fk["order"])
         cfg.filter_innerK = float(fk["innerK"])
@@ -145,7 +148,8 @@ class Diagnostic:
         for step, t, ke, ke2, pe in records[self._seen:]:
             if self.i >= len(self.data):
                 break
-            v = {"ke": ke, "pe": pe, "ke12": (ke, ke2), "bc": (ke, pe), "bt": ke2}[self._field]
+            v = {"ke": ke, "pe": pe, "ke12": (ke, ke2), "bc": (ke, pe), "bt": ke2,
+                 "mlqg": ((ke, ke2), (pe,))}[self._field]
             self.data[self.i], self.t[self.i], self.steps[self.i] = v, t, step
             self.value = v
             self.i += 1

@@ -17,8 +17,15 @@ to mirror the reference op sequence one broadcast / one transform at a time:
 * ``utils/IFMAB3.jl`` (9-11, 26-30, 125-169) and FF ``FilteredAB3`` (A7, with
   ``addlinearterm!`` generalised to the per-mode matvec).
 * ``utils/IFMRK4.jl`` structure (13-22, 157-163) -> Lawson IF-RK4.
+* ``thomasyamada/ThomasYamada.jl`` calcN! (129-262), L (265-277),
+  ``thomasyamada/TYUtils.jl`` bases, ``TYdriver.jl:36-87`` IC, and FF
+  ``ETDRK4``/``getetdcoeffs`` (restated: FF not vendored).
+* GeophysicalFlows ``MultiLayerQG`` (2 layers) + FF ``FilteredRK4`` as
+  ``simulation/TwoLayerSimulation.jl`` runs it (GF not vendored: restated from
+  its published equations, PARITY UNPINNED against GF; pinned by the
+  analytic Phillips baroclinic growth rate).
 * Driver parameter formulas and initial conditions: ``rsw/RSWDriver.jl:88-176``,
-  ``swqg/TwoLayerDriver.jl:10-68``.
+  ``swqg/TwoLayerDriver.jl:10-68``, ``simulation/Parameters.jl``.
 
 Parity pinning.  The reference cannot run here (no Julia / FourierFlows /
 FFTW).  This restatement is pinned by every known answer the
@@ -85,8 +92,8 @@ def aliased_index_range(n: int, aliased_fraction: float):
     L = (1-af)/2, R = (1+af)/2, iL = floor(L n) + 1, iR = ceil(R n)
     (SURVEY A1).  kralias = iL:nkr, lalias = iL:iR (1-based, inclusive).
     """
-    if not (0.0 < aliased_fraction < 1.0):
-        raise ValueError("aliased_fraction must be in (0, 1)")
+    if not (0.0 <= aliased_fraction < 1.0):
+        raise ValueError("aliased_fraction must be in [0, 1)")
     L = (1 - aliased_fraction) / 2
     R = (1 + aliased_fraction) / 2
     iL = math.floor(L * n) + 1
@@ -127,6 +134,11 @@ class TwoDGrid:
         iLy, iRy = aliased_index_range(self.ny, self.aliased_fraction)
         self.kralias = (iLx - 1, self.nkr)        # zeroed kr columns
         self.lalias = (iLy - 1, iRy)              # zeroed l rows [a, b)
+        if self.aliased_fraction == 0:
+            # FF getaliasedwavenumbers with aliased_fraction = 0: only the
+            # Nyquist column kr = nx/2 and row l = -ny/2 are zeroed
+            self.kralias = (self.nkr - 1, self.nkr)
+            self.lalias = (self.ny // 2, self.ny // 2 + 1)
         mask = np.ones((self.nl, self.nkr), dtype=bool)
         mask[:, self.kralias[0]:self.kralias[1]] = False
         mask[self.lalias[0]:self.lalias[1], :] = False
@@ -500,6 +512,130 @@ def ty_initial_condition(grid: TwoDGrid, rng, k0w_range=(0.0, 5 / 3), k0g_range=
 
 
 # --------------------------------------------------------------------------
+# GeophysicalFlows MultiLayerQG, nlayers = 2 (simulation/TwoLayerSimulation.jl)
+# --------------------------------------------------------------------------
+# GeophysicalFlows.jl is not vendored in the reference (no Manifest; SURVEY
+# §8c): its MultiLayerQG is restated here from the package's published
+# equations and call sequence (GF ≥ 0.15 keyword set: f₀, H, b, U, μ, β, ν,
+# nν).  PARITY UNPINNED against GF itself; pinned instead by the analytic
+# baroclinic-instability growth rate of the two-layer (Phillips) problem and
+# by the shared J(ψ, q) term of TwoLayerQG (tests/test_oracle.py).
+class MLQGParams:
+    """MultiLayerQG.Params for 2 layers: g′ = b₁ − b₂, F_j = f₀²/(g′ H_j),
+    background PV gradients Qy₁ = β − F₁(U₂ − U₁), Qy₂ = β − F₂(U₁ − U₂)
+    (no topography: Qx = 0)."""
+
+    def __init__(self, f0, H, b, U, mu, beta=0.0, nu=0.0, nnu=1):
+        self.f0, self.mu, self.beta, self.nu, self.nnu = float(f0), float(mu), float(beta), float(nu), int(nnu)
+        self.H = [float(h) for h in H]
+        self.b = [float(x) for x in b]
+        self.U = [float(u) for u in U]
+        self.gp = self.b[0] - self.b[1]
+        self.F1 = self.f0 ** 2 / (self.gp * self.H[0])
+        self.F2 = self.f0 ** 2 / (self.gp * self.H[1])
+        self.Qy = [self.beta - self.F1 * (self.U[1] - self.U[0]), self.beta - self.F2 * (self.U[0] - self.U[1])]
+
+
+def mlqg_streamfunction(qh, grid: TwoDGrid, p: MLQGParams):
+    """streamfunctionfrompv!: ψ̂ = S⁻¹ q̂ per mode, S = [[-K²-F₁, F₁],
+    [F₂, -K²-F₂]]; S⁻¹ = [[-(K²+F₂), -F₁], [-F₂, -(K²+F₁)]] / (K²(K²+F₁+F₂)),
+    0 at K = 0."""
+    K2 = grid.Krsq
+    den = K2 * (K2 + p.F1 + p.F2)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        inv = np.where(K2 == 0, 0.0, 1.0 / den)
+    q1, q2 = qh[0], qh[1]
+    return np.stack([(-(K2 + p.F2) * q1 - p.F1 * q2) * inv, (-p.F2 * q1 - (K2 + p.F1) * q2) * inv])
+
+
+def mlqg_pvfromstreamfunction(psih, grid: TwoDGrid, p: MLQGParams):
+    """pvfromstreamfunction!: q̂ = S ψ̂ (simulation / raytracing set-up)."""
+    K2 = grid.Krsq
+    return np.stack([(-K2 - p.F1) * psih[0] + p.F1 * psih[1], p.F2 * psih[0] + (-K2 - p.F2) * psih[1]])
+
+
+def mlqg_calcN(sol, grid: TwoDGrid, p: MLQGParams):
+    """MultiLayerQG calcN! (calcN_advection! + bottom drag), op sequence of GF:
+    N = -(U+u)·Qx^ - (v Qy)^ - ik((U+u) q)^ - il(v q)^, then
+    N_n += μ K² ψ̂_n.  ``sol`` dealiased in place (aliased_fraction = 0 zeroes
+    only the Nyquist row and column)."""
+    grid.dealias(sol)
+    kr = grid.kr[None, :]
+    l = grid.l[:, None]
+    qh = sol.copy()
+    psih = mlqg_streamfunction(qh, grid, p)
+    u = grid.irfft(-1j * l * psih) + np.array(p.U)[:, None, None]
+    v = grid.irfft(1j * kr * psih)
+    N = -grid.rfft(v * np.array(p.Qy)[:, None, None])
+    q = grid.irfft(qh)
+    N -= 1j * kr * grid.rfft(u * q) + 1j * l * grid.rfft(v * q)
+    N[1] += p.mu * grid.Krsq * psih[1]
+    return N
+
+
+def mlqg_L(grid: TwoDGrid, p: MLQGParams):
+    """MultiLayerQG Equation: L = -ν K^(2nν) on each layer (the mean-flow,
+    background-gradient and drag terms are in calcN), as [2, nl, nkr]."""
+    D = -p.nu * grid.Krsq ** p.nnu
+    return np.stack([D, D])
+
+
+def mlqg_linear_operator(grid: TwoDGrid, p: MLQGParams):
+    """The full per-mode linearisation of MultiLayerQG about rest (L plus the
+    linear part of calcN), [nl, nkr, 2, 2] acting on q̂ — what libsw applies
+    as its matvec (the nonlinear J(ψ, q) alone goes through the transforms)."""
+    K2 = grid.Krsq
+    k = np.broadcast_to(grid.kr[None, :], K2.shape)
+    den = K2 * (K2 + p.F1 + p.F2)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        inv = np.where(K2 == 0, 0.0, 1.0 / den)
+    Si = np.zeros(K2.shape + (2, 2))
+    Si[..., 0, 0] = -(K2 + p.F2) * inv
+    Si[..., 0, 1] = -p.F1 * inv
+    Si[..., 1, 0] = -p.F2 * inv
+    Si[..., 1, 1] = -(K2 + p.F1) * inv
+    A = np.zeros(K2.shape + (2, 2), np.complex128)
+    D = -p.nu * K2 ** p.nnu
+    for j in range(2):
+        A[..., j, j] += D - 1j * k * p.U[j]
+        A[..., j, :] += -1j * k[..., None] * p.Qy[j] * Si[..., j, :]
+    A[..., 1, :] += p.mu * K2[..., None] * Si[..., 1, :]
+    return A
+
+
+def mlqg_energies(sol, grid: TwoDGrid, p: MLQGParams):
+    """MultiLayerQG.energies: KE_j = 1/(2 Lx Ly) parsevalsum(K²|ψ̂_j|²) H_j/H,
+    PE = 1/(2 Lx Ly) f₀²/g′ parsevalsum(|ψ̂₂ − ψ̂₁|²)/H."""
+    psih = mlqg_streamfunction(sol, grid, p)
+    Ht = sum(p.H)
+
+    def parsevalsum(fh):
+        s = 2 * fh.sum() - fh[:, 0].sum()
+        if grid.nx % 2 == 0:
+            s -= fh[:, -1].sum()
+        return (grid.Lx * grid.Ly / (grid.nx ** 2 * grid.ny ** 2)) * s.real
+
+    KE = [1 / (2 * grid.Lx * grid.Ly) * parsevalsum(grid.Krsq * np.abs(psih[j]) ** 2) * p.H[j] / Ht
+          for j in range(2)]
+    PE = 1 / (2 * grid.Lx * grid.Ly) * p.f0 ** 2 / p.gp * parsevalsum(np.abs(psih[1] - psih[0]) ** 2) / Ht
+    return KE, PE
+
+
+def mlqg_simulation_params(nx, Lx=2 * np.pi, f=1.0, rd=1 / 15, lv=1 / 2, avg_U=0.1, H0=1.0, nnu=8, nu=0.0):
+    """simulation/Parameters.jl compute_parameters and the derived values."""
+    c1, c2 = 3.2, 0.36
+    l_star = lv / rd
+    b2 = 1.0
+    kappa_star = c2 / np.log(l_star / c1)
+    U = avg_U / l_star
+    mu = 2 * U * kappa_star / rd
+    b1 = 4 * f ** 2 * rd ** 2 / H0 + b2
+    dx = Lx / nx
+    return dict(f0=f, H=[H0 / 2, H0 / 2], b=[b1, b2], U=[U, -U], mu=mu, beta=0.0, nu=nu, nnu=nnu,
+                dt=0.02 * dx / avg_U, q0_amplitude=1e-2 * avg_U)
+
+
+# --------------------------------------------------------------------------
 # Time steppers
 # --------------------------------------------------------------------------
 class Clock:
@@ -531,6 +667,35 @@ class FilteredAB3:
         clock.step += 1
         self.RHSm2 = self.RHSm1.copy()
         self.RHSm1 = self.RHS.copy()
+
+
+class FilteredRK4:
+    """FF ``FilteredRK4TimeStepper`` (TwoLayerSimulation's stepper,
+    simulation/Parameters.jl:25): RHS = calcN + L·sol (``addlinearterm!``,
+    a per-mode matvec for matrix L), RK4 substeps with sol₁ = sol + dt/2 RHS₁,
+    sol + dt/2 RHS₂, sol + dt RHS₃, then
+    sol += dt (RHS₁/6 + RHS₂/3 + RHS₃/3 + RHS₄/6); sol .*= filter."""
+
+    def __init__(self, L, grid, nf, order=4, innerK=0.65, outerK=1.0, tol=1e-15):
+        self.L = L
+        self.filter = makefilter(grid, order=order, innerK=innerK, outerK=outerK, tol=tol)[None]
+
+    def _rhs(self, x, calcN, grid, params):
+        N = calcN(x, grid, params)
+        if self.L.ndim == 4:
+            return N + mvmul(self.L, x)
+        return N + self.L * x
+
+    def stepforward(self, sol, clock, calcN, grid, params):
+        dt = clock.dt
+        R1 = self._rhs(sol, calcN, grid, params)
+        R2 = self._rhs(sol + dt / 2 * R1, calcN, grid, params)
+        R3 = self._rhs(sol + dt / 2 * R2, calcN, grid, params)
+        R4 = self._rhs(sol + dt * R3, calcN, grid, params)
+        sol += dt * (R1 / 6 + R2 / 3 + R3 / 3 + R4 / 6)
+        sol *= self.filter
+        clock.t += dt
+        clock.step += 1
 
 
 class IFMAB3:
@@ -672,6 +837,10 @@ class Problem:
             self.calcN = ty_calcN if calcN is None else calcN
             if stepper != "ETDRK4":
                 raise ValueError("the Thomas-Yamada model is stepped with ETDRK4")
+        elif model == "mlqg":
+            self.nf = 2
+            self.L = mlqg_L(self.grid, params)
+            self.calcN = mlqg_calcN if calcN is None else calcN
         else:
             raise ValueError(model)
         self.clock = Clock(dt)
@@ -681,6 +850,8 @@ class Problem:
             self.ts = ETDRK4(self.L, dt, self.grid, self.nf)
         elif stepper == "FilteredAB3":
             self.ts = FilteredAB3(self.L, self.grid, self.nf, **filter_kw)
+        elif stepper == "FilteredRK4":
+            self.ts = FilteredRK4(self.L, self.grid, self.nf, **filter_kw)
         elif stepper == "IFMAB3":
             self.ts = IFMAB3(self.L, dt, self.grid, self.nf, use_filter=use_filter, **filter_kw)
         elif stepper == "IFMRK4":

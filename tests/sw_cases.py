@@ -14,12 +14,24 @@ import sw_oracle as O
 CASES = ["rsw_fab3", "rsw_ifmab3", "rsw_ifmrk4", "qg2_ifmab3", "qg2_ifmrk4", "qg2_fab3"]
 # Thomas–Yamada (thomasyamada/ThomasYamada.jl) stepped by FF ETDRK4
 TY_CASES = ["ty_etdrk4"]
-ALL_CASES = CASES + TY_CASES
+# GeophysicalFlows MultiLayerQG (2 layers, aliased_fraction = 0) stepped by
+# FF FilteredRK4, as simulation/TwoLayerSimulation.jl runs it
+MLQG_CASES = ["mlqg_frk4"]
+ALL_CASES = CASES + TY_CASES + MLQG_CASES
 
 
 def case_params(name, n):
     model, st = name.split("_", 1)
-    stepper = {"fab3": "FilteredAB3", "ifmab3": "IFMAB3", "ifmrk4": "IFMRK4", "etdrk4": "ETDRK4"}[st]
+    stepper = {"fab3": "FilteredAB3", "ifmab3": "IFMAB3", "ifmrk4": "IFMRK4", "etdrk4": "ETDRK4",
+               "frk4": "FilteredRK4"}[st]
+    if model == "mlqg":
+        # simulation/Parameters.jl (f = 1, rd = 1/15, ℓ = 1/2, avg_U = 0.1, H =
+        # [1/2, 1/2], nν = 8, ν = 0, dt = 0.02 dx/avg_U), aliased_fraction = 0;
+        # small grids: a larger PV amplitude so J(ψ, q) matters within steps
+        P = O.mlqg_simulation_params(n)
+        return dict(model="mlqg", stepper=stepper, n=n, af=0.0, dt=P["dt"], f0=P["f0"], H=P["H"], b=P["b"],
+                    U=P["U"], mu=P["mu"], beta=P["beta"], nu=P["nu"], nnu=P["nnu"],
+                    amp=0.5 if n <= 256 else P["q0_amplitude"], seed=1234)
     if model == "ty":
         # thomasyamada/cpu-setup/Parameters.jl: Lx = 6π, ν = 5e-34 (Lx/2π)^16,
         # nν = 8, Ro = 1, dt = 5e-3; annuli k0g = (10/3, 13/3), k0w = (0, 5/3).
@@ -51,6 +63,9 @@ def case_params(name, n):
 
 
 def oracle_problem(p):
+    if p["model"] == "mlqg":
+        params = O.MLQGParams(p["f0"], p["H"], p["b"], p["U"], p["mu"], p["beta"], p["nu"], p["nnu"])
+        return O.Problem("mlqg", p["stepper"], p["n"], p["dt"], aliased_fraction=p["af"], params=params)
     if p["model"] == "ty":
         return O.Problem("ty", "ETDRK4", p["n"], p["dt"], Lx=p["Lx"],
                          params=O.TYParams(p["nu"], p["nnu"], p["Ro"]))
@@ -64,6 +79,10 @@ def oracle_problem(p):
 
 def initial_condition(p, grid):
     rng = np.random.default_rng(p["seed"])
+    if p["model"] == "mlqg":
+        # simulation/TwoLayerSimulation.jl:50-53: q₀ = a·randn, q̂₀ = filter·rfft(q₀)
+        q0 = p["amp"] * rng.standard_normal((2, grid.ny, grid.nx))
+        return O.makefilter(grid)[None] * grid.rfft(q0)
     if p["model"] == "ty":
         return O.ty_initial_condition(grid, rng, k0w_range=p["k0w"], k0g_range=p["k0g"],
                                       at=p["at"], ag=p["ag"], aw=p["aw"])
@@ -77,6 +96,12 @@ def libsw_problem(p, **kw):
     """The GPU problem for the same case, through the package's public mirror."""
     from juliaraytracingsw_amd import rotating_shallow_water as RSW, thomas_yamada as TY, two_layer_qg as QG2
 
+    if p["model"] == "mlqg":
+        from juliaraytracingsw_amd import multilayer_qg as MLQG
+
+        return MLQG.Problem(2, "gpu", nx=p["n"], f0=p["f0"], H=p["H"], b=p["b"], U=p["U"], mu=p["mu"],
+                            beta=p["beta"], nu=p["nu"], nnu=p["nnu"], dt=p["dt"], stepper=p["stepper"],
+                            aliased_fraction=p["af"], **kw)
     if p["model"] == "ty":
         return TY.Problem("gpu", nx=p["n"], Lx=p["Lx"], dt=p["dt"], nu=p["nu"], nnu=p["nnu"], Ro=p["Ro"], **kw)
     fk = dict(order=p["order"]) if p["stepper"] == "FilteredAB3" else {}

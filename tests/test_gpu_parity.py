@@ -32,7 +32,7 @@ def test_golden(fn):
     d = np.load(fn)
     p = json.loads(str(d["params"]))
     prob = sw_cases.libsw_problem(p)
-    g = O.TwoDGrid(p["n"])
+    g = O.TwoDGrid(p["n"], aliased_fraction=p.get("af", 1 / 3))
     N0 = prob.calcN(d["ic"])
     assert _err(N0, d["N0"], g) < RTOL
     prob.sol = d["ic"]

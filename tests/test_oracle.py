@@ -267,6 +267,85 @@ def test_etdrk4_fourth_order():
         assert e1 / e2 > 12, (nu, e1 / e2)
 
 
+# --- GeophysicalFlows MultiLayerQG + FilteredRK4 ---------------------------------
+def _mlqg_params(**over):
+    P = O.mlqg_simulation_params(64)
+    P.update(over)
+    return O.MLQGParams(P["f0"], P["H"], P["b"], P["U"], P["mu"], P["beta"], P["nu"], P["nnu"])
+
+
+def test_mlqg_phillips_growth_rate():
+    """Analytic known answer pinning the restated MultiLayerQG (parity unpinned
+    against GeophysicalFlows itself): the two-layer Phillips problem (β = 0,
+    μ = 0, ν = 0, equal depths, U₁ = -U₂ = U) grows at
+    σ = k U sqrt((2F − K²)/(2F + K²)) for K² < 2F and is neutral otherwise —
+    the largest real part of the eigenvalues of the per-mode linear operator
+    (L plus the linear part of calcN!)."""
+    g = O.TwoDGrid(64, aliased_fraction=0)
+    p = _mlqg_params(mu=0.0)
+    assert p.F1 == p.F2
+    A = O.mlqg_linear_operator(g, p)
+    got = np.linalg.eigvals(A).real.max(-1)
+    k = g.kr[None, :] * np.ones_like(g.Krsq)
+    F, U, K2 = p.F1, p.U[0], g.Krsq
+    exp = np.where(K2 < 2 * F, k * U * np.sqrt(np.clip((2 * F - K2) / (2 * F + K2), 0, None)), 0.0)
+    m = g.live & (np.abs(K2 - 2 * F) > 1.0)  # away from the double root at K² = 2F
+    assert np.max(np.abs(got - exp)[m]) < 1e-12
+    assert exp[m].max() > 0.05  # unstable band resolved
+
+
+def test_mlqg_calcN_linear_part():
+    """calcN!'s linear part (mean flow, background PV gradient, bottom drag)
+    is the linear operator minus L: calcN(ε q)/ε → (A − L) q as ε → 0."""
+    g = O.TwoDGrid(32, aliased_fraction=0)
+    p = _mlqg_params(nu=1e-3, nnu=2, beta=0.7)
+    rng = np.random.default_rng(2)
+    q = g.dealias(rng.standard_normal((2, 32, 17)) + 1j * rng.standard_normal((2, 32, 17)))
+    eps = 1e-7
+    lin = O.mlqg_calcN(eps * q, g, p) / eps
+    exp = O.mvmul(O.mlqg_linear_operator(g, p), q) - O.mlqg_L(g, p) * q
+    assert O.parity_error(lin, exp, g) < 1e-6
+
+
+def test_mlqg_energies_and_inversion():
+    """pvfromstreamfunction! ∘ streamfunctionfrompv! is the identity (K ≠ 0),
+    and the energies are positive quadratic forms of ψ."""
+    g = O.TwoDGrid(32, aliased_fraction=0)
+    p = _mlqg_params()
+    rng = np.random.default_rng(4)
+    q = g.dealias(rng.standard_normal((2, 32, 17)) + 1j * rng.standard_normal((2, 32, 17)))
+    q[:, 0, 0] = 0
+    back = O.mlqg_pvfromstreamfunction(O.mlqg_streamfunction(q, g, p), g, p)
+    assert O.parity_error(back, q, g) < 1e-13
+    (k1, k2), pe = O.mlqg_energies(q, g, p)
+    assert k1 > 0 and k2 > 0 and pe > 0
+
+
+def test_filtered_rk4_fourth_order():
+    """FF FilteredRK4 converges at fourth order (filter ≡ 1 here, innerK > 1)
+    on the nonlinear MultiLayerQG step."""
+    p = sw_cases.case_params("mlqg_frk4", 32)
+    sols = {}
+    for dt in (0.04, 0.02, 0.005):
+        params = O.MLQGParams(p["f0"], p["H"], p["b"], p["U"], p["mu"], p["beta"], p["nu"], p["nnu"])
+        pr = O.Problem("mlqg", "FilteredRK4", 32, dt, aliased_fraction=0, params=params, innerK=10.0, outerK=11.0)
+        pr.set_solution(sw_cases.initial_condition(p, pr.grid))
+        pr.stepforward(int(round(2.0 / dt)))
+        sols[dt] = pr.grid.dealias(pr.sol.copy())
+    e1 = np.max(np.abs(sols[0.04] - sols[0.005]))
+    e2 = np.max(np.abs(sols[0.02] - sols[0.005]))
+    assert e1 / e2 > 12, e1 / e2
+
+
+def test_aliased_fraction_zero_grid():
+    """FF TwoDGrid(aliased_fraction = 0): dealias! zeroes only the Nyquist
+    column and row (the reference's MultiLayerQG set-up,
+    simulation/TwoLayerSimulation.jl:38)."""
+    g = O.TwoDGrid(64, aliased_fraction=0)
+    assert g.kc == 32 and g.kralias == (32, 33) and g.lalias == (32, 33)
+    assert g.live.sum() == 32 * 63
+
+
 # --- golden fixtures -----------------------------------------------------------
 GOLDEN_FILES = sorted(glob.glob(os.path.join(GOLDEN, "*.npz")))
 

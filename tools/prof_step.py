@@ -15,8 +15,13 @@ ap.add_argument("--n", type=int, default=2048)
 ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--warmup", type=int, default=5)
 a = ap.parse_args()
-mk = drivers.rsw_problem if a.model == "rsw" else drivers.qg2_problem
-prob, _ = mk(a.n, a.stepper)
+if a.model == "ty":
+    prob, _ = drivers.ty_problem(a.n)
+elif a.model == "mlqg":
+    prob, _ = drivers.mlqg_problem(a.n)
+else:
+    mk = drivers.rsw_problem if a.model == "rsw" else drivers.qg2_problem
+    prob, _ = mk(a.n, a.stepper)
 prob.stepforward(a.warmup)
 prob.stepforward(a.steps)
 print("done", prob.clock.step)
