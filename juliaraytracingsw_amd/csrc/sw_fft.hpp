@@ -101,17 +101,35 @@ struct FftPlan {
 };
 
 // W^(k_i << (LOG2N - lNs_i - 3)) for every twiddled stage i (forward sign).
+// Lines of 8192 points run 1024 threads per block, which caps a thread at
+// 128 VGPRs: there the stage twiddles are read from the (L1-resident) table
+// at each stage instead of being held in registers for the whole kernel.
 template <int LOG2N>
 struct Twiddles {
-  double2 w[FftPlan<LOG2N>::NTW > 0 ? FftPlan<LOG2N>::NTW : 1];
+  static constexpr bool kPreload = LOG2N < 13;
+  double2 w[(kPreload && FftPlan<LOG2N>::NTW > 0) ? FftPlan<LOG2N>::NTW : 1];
+  const double2* tab = nullptr;
+  int t0 = 0;
   __device__ __forceinline__ void load(int t, const double2* __restrict__ tw) {
     using P = FftPlan<LOG2N>;
+    if constexpr (kPreload) {
 #pragma unroll
-    for (int i = 0; i < P::NTW; ++i) {
-      const int lNs = P::FIRST8 + 3 * i;
-      const int k = t & ((1 << lNs) - 1);
-      w[i] = tw[k << (LOG2N - lNs - 3)];
+      for (int i = 0; i < P::NTW; ++i) w[i] = tw[index(t, i)];
+    } else {
+      tab = tw;
+      t0 = t;
     }
+  }
+  __device__ __forceinline__ static int index(int t, int i) {
+    using P = FftPlan<LOG2N>;
+    const int lNs = P::FIRST8 + 3 * i;
+    const int k = t & ((1 << lNs) - 1);
+    return k << (LOG2N - lNs - 3);
+  }
+  // W^k of twiddled stage i for this thread
+  __device__ __forceinline__ double2 get(int i) const {
+    if constexpr (kPreload) return w[i];
+    else return tab[index(t0, i)];
   }
 };
 
@@ -135,10 +153,12 @@ __device__ __forceinline__ void fft_lines(double2 (&v)[C][8], int t, const Twidd
   // derived powers w2..w7 across the several transforms of one kernel, which
   // would pin 28 VGPRs per stage for the kernel's whole lifetime.
   double2 tw1[P::NTW > 0 ? P::NTW : 1];
+  if constexpr (Twiddles<LOG2N>::kPreload) {
 #pragma unroll
-  for (int i = 0; i < P::NTW; ++i) {
-    tw1[i] = tws.w[i];
-    asm volatile("" : "+v"(tw1[i].x), "+v"(tw1[i].y));
+    for (int i = 0; i < P::NTW; ++i) {
+      tw1[i] = tws.w[i];
+      asm volatile("" : "+v"(tw1[i].x), "+v"(tw1[i].y));
+    }
   }
   if constexpr (P::REM == 2) {  // radix-4, Ns = 1: butterflies j = t, t + NT
 #pragma unroll
@@ -185,7 +205,8 @@ __device__ __forceinline__ void fft_lines(double2 (&v)[C][8], int t, const Twidd
     const int Ns = 1 << lNs;
     const int k = t & (Ns - 1);
     if (lNs > 0) {
-      const double2 w1 = DIR < 0 ? tw1[ti] : cconj(tw1[ti]);
+      const double2 wt = Twiddles<LOG2N>::kPreload ? tw1[ti] : tws.get(ti);
+      const double2 w1 = DIR < 0 ? wt : cconj(wt);
       const double2 w2 = cmul(w1, w1), w3 = cmul(w2, w1), w4 = cmul(w2, w2);
       const double2 w5 = cmul(w4, w1), w6 = cmul(w3, w3), w7 = cmul(w4, w3);
 #pragma unroll
