@@ -207,17 +207,28 @@ __device__ __forceinline__ void fft_lines(double2 (&v)[C][8], int t, const Twidd
     if (lNs > 0) {
       const double2 wt = Twiddles<LOG2N>::kPreload ? tw1[ti] : tws.get(ti);
       const double2 w1 = DIR < 0 ? wt : cconj(wt);
-      const double2 w2 = cmul(w1, w1), w3 = cmul(w2, w1), w4 = cmul(w2, w2);
-      const double2 w5 = cmul(w4, w1), w6 = cmul(w3, w3), w7 = cmul(w4, w3);
+      if constexpr (Twiddles<LOG2N>::kPreload) {
+        const double2 w2 = cmul(w1, w1), w3 = cmul(w2, w1), w4 = cmul(w2, w2);
+        const double2 w5 = cmul(w4, w1), w6 = cmul(w3, w3), w7 = cmul(w4, w3);
 #pragma unroll
-      for (int c = 0; c < C; ++c) {
-        v[c][1] = cmul(v[c][1], w1);
-        v[c][2] = cmul(v[c][2], w2);
-        v[c][3] = cmul(v[c][3], w3);
-        v[c][4] = cmul(v[c][4], w4);
-        v[c][5] = cmul(v[c][5], w5);
-        v[c][6] = cmul(v[c][6], w6);
-        v[c][7] = cmul(v[c][7], w7);
+        for (int c = 0; c < C; ++c) {
+          v[c][1] = cmul(v[c][1], w1);
+          v[c][2] = cmul(v[c][2], w2);
+          v[c][3] = cmul(v[c][3], w3);
+          v[c][4] = cmul(v[c][4], w4);
+          v[c][5] = cmul(v[c][5], w5);
+          v[c][6] = cmul(v[c][6], w6);
+          v[c][7] = cmul(v[c][7], w7);
+        }
+      } else {
+        // 128-VGPR budget (8192): powers formed as a chain, two live at a time
+        double2 wp = w1;
+#pragma unroll
+        for (int r = 1; r < 8; ++r) {
+#pragma unroll
+          for (int c = 0; c < C; ++c) v[c][r] = cmul(v[c][r], wp);
+          if (r < 7) wp = cmul(wp, w1);
+        }
       }
     }
 #pragma unroll

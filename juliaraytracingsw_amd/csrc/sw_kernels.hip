@@ -434,9 +434,18 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, Blk<LOG2N>::THREADS >= 10
     constexpr int LS = FftPlan<LOG2N>::LDS;  // two line buffers per row
     double2 w[2][8];
     // u + i v and η + i ζ, transformed together (fft_lines leaves z[x = t + s*NT])
-    load_pair<LOG2N>(w[0], c.t, g, U, V, y, false);
-    load_eta_zeta<LOG2N>(w[1], c.t, g, H, V, Uy, y);
-    fft_pair<LOG2N, +1, CB>(w, c.t, tws, line, LS);
+    if constexpr (CB == 2) {
+      load_pair<LOG2N>(w[0], c.t, g, U, V, y, false);
+      load_eta_zeta<LOG2N>(w[1], c.t, g, H, V, Uy, y);
+      fft_pair<LOG2N, +1, CB>(w, c.t, tws, line, LS);
+    } else {
+      // nx = 8192 (128 VGPRs per thread): one pair at a time, the second
+      // pair's loads issued after the first transform
+      load_pair<LOG2N>(w[0], c.t, g, U, V, y, false);
+      fft_line<LOG2N, +1>(w[0], c.t, tws, line);
+      load_eta_zeta<LOG2N>(w[1], c.t, g, H, V, Uy, y);
+      fft_line<LOG2N, +1>(w[1], c.t, tws, line);
+    }
     double pc[8];
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
@@ -1599,7 +1608,11 @@ __global__ void k_absmax(const double* __restrict__ f, long long n, unsigned lon
 // launchers
 // ===========================================================================
 // host-side: dispatch the LOG2N instantiation (N = 32 … 8192)
+#ifdef SW_ONLY_LOG2  // register/spill experiments: instantiate one length only
+#define SW_LOG2_CASES(X) X(SW_ONLY_LOG2)
+#else
 #define SW_LOG2_CASES(X) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13)
+#endif
 
 template <template <int> class F, typename... Args>
 static void dispatch_log2(int log2n, Args&&... args) {
