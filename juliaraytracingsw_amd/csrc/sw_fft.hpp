@@ -104,9 +104,12 @@ struct FftPlan {
 // Lines of 8192 points run 1024 threads per block, which caps a thread at
 // 128 VGPRs: there the stage twiddles are read from the (L1-resident) table
 // at each stage instead of being held in registers for the whole kernel.
+#ifndef SW_TWFLY_LOG2
+#define SW_TWFLY_LOG2 13  // lines of at least 2^this read their stage twiddles per stage
+#endif
 template <int LOG2N>
 struct Twiddles {
-  static constexpr bool kPreload = LOG2N < 13;
+  static constexpr bool kPreload = LOG2N < SW_TWFLY_LOG2;
   double2 w[(kPreload && FftPlan<LOG2N>::NTW > 0) ? FftPlan<LOG2N>::NTW : 1];
   const double2* tab = nullptr;
   int t0 = 0;

@@ -392,7 +392,11 @@ __device__ __forceinline__ void store_pair(const double2 (&v)[8], int t, const G
 // where two buffers per row fit the 160 KB of LDS (nx <= 4096)
 template <int MODEL, int LOG2N>
 __host__ __device__ constexpr int row_lds_lines() {
+#ifdef SW_ROW_CB1  // sweep knob: one line buffer per row
+  return 1;
+#else
   return (MODEL == MODEL_RSW && 2 * Blk<LOG2N>::NB * FftPlan<LOG2N>::LDS * 16 <= 160 * 1024) ? 2 : 1;
+#endif
 }
 // C = 2: both transforms per barrier; C = 1: one after the other
 template <int LOG2N, int DIR, int C>
