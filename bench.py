@@ -165,8 +165,14 @@ def main():
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.model, args.stepper, args.n)
+    metric = f"timesteps/sec, {args.model.upper()} {args.n}^2 {args.stepper} fp64"
+    if (args.model, args.n, args.stepper) == ("rsw", 2048, "FilteredAB3"):
+        try:  # the BASELINE.json metric this default configuration measures
+            metric = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+        except Exception:
+            pass
     out = {
-        "metric": f"timesteps/sec, {args.model.upper()} {args.n}^2 {args.stepper} fp64 (BASELINE.json metric)",
+        "metric": metric,
         "value": value,
         "unit": "timesteps/s",
         "n_gpus": world,
