@@ -107,6 +107,41 @@ def test_mlqg_physical_energy_cfl_diagnostics():
     prob.close()
 
 
+@pytest.mark.parametrize("nx,ny", [(256, 64), (64, 256)])
+@pytest.mark.parametrize("model", ["mlqg", "ty"])
+def test_rectangular_ty_mlqg(model, nx, ny):
+    """Rectangular grids (Lx ≠ Ly too) for the Thomas–Yamada and MultiLayerQG
+    paths: separate x and y wavenumber spacings everywhere (k_row's ik,
+    k_col_inv's il, the per-mode linear terms, the ETDRK4 table, the filter)."""
+    from juliaraytracingsw_amd import multilayer_qg as MLQG, thomas_yamada as TY
+
+    rng = np.random.default_rng(11)
+    Lx, Ly = 2 * np.pi * nx / 128, 2 * np.pi * ny / 128
+    if model == "mlqg":
+        P = O.mlqg_simulation_params(128)
+        params = O.MLQGParams(P["f0"], P["H"], P["b"], P["U"], P["mu"], 0.5, 1e-14, 4)
+        pr = O.Problem("mlqg", "FilteredRK4", nx, 0.01, Lx=Lx, ny=ny, Ly=Ly, aliased_fraction=0, params=params)
+        prob = MLQG.Problem(2, "gpu", nx=nx, ny=ny, Lx=Lx, Ly=Ly, f0=P["f0"], H=P["H"], b=P["b"], U=P["U"],
+                            mu=P["mu"], beta=0.5, nu=1e-14, nnu=4, dt=0.01, aliased_fraction=0)
+        nf = 2
+    else:
+        params = O.TYParams(1e-12, 4, 1.0)
+        pr = O.Problem("ty", "ETDRK4", nx, 0.02, Lx=Lx, ny=ny, Ly=Ly, params=params)
+        prob = TY.Problem("gpu", nx=nx, ny=ny, Lx=Lx, Ly=Ly, nu=1e-12, nnu=4, Ro=1.0, dt=0.02)
+        nf = 4
+    g = pr.grid
+    spec = g.rfft(rng.standard_normal((nf, ny, nx)))
+    spec *= np.exp(-g.Krsq / (0.02 * (g.kc ** 2 + (g.ny / 3) ** 2)))
+    spec *= 0.3 / np.abs(g.irfft(spec)).max()
+    pr.set_solution(spec)
+    prob.sol = pr.sol
+    assert O.parity_error(prob.calcN(pr.sol), pr.calcN(pr.sol.copy(), g, pr.params), g) < RTOL
+    pr.stepforward(3)
+    prob.stepforward(3)
+    assert O.parity_error(prob.sol, pr.sol, g) < RTOL
+    prob.close()
+
+
 def test_mlqg_driver_setup():
     """TwoLayerSimulation set-up: parameters and the filtered randn IC."""
     from juliaraytracingsw_amd import drivers
