@@ -128,7 +128,7 @@ void alias_range(int n, double af, int& iL, int& iR) {
 // lines per block of the column kernels (Blk<log2ny>::NB in sw_kernels.hip)
 int col_lines_per_block(int ny) {
   const int NT = ny / 8;
-  return NT >= 256 ? 1 : std::min(256 / NT, 32);
+  return NT >= SW_BLK_THREADS ? 1 : std::min(SW_BLK_THREADS / NT, 32);
 }
 
 // geometry of slab s of P

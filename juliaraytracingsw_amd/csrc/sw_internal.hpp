@@ -8,6 +8,14 @@
 // in every kernel (and on the host), so kernel fusion never changes results.
 #pragma clang fp contract(off)
 
+// Short lines (N/8 threads each) are packed into blocks of up to this many
+// threads (kernels and host geometry must agree).  64: one
+// line per block from N = 512 up, the most blocks on small grids (measured,
+// sw_kernels.hip row_tgt)
+#ifndef SW_BLK_THREADS
+#define SW_BLK_THREADS 64
+#endif
+
 namespace sw {
 
 // MODEL_MLQG (GeophysicalFlows MultiLayerQG, 2 layers) runs the MODEL_QG2

@@ -34,12 +34,12 @@ __device__ __forceinline__ int col_of_block(int b, int nb) {
 
 // threads per block: one line of NT = N/8 threads, or several short lines
 // packed into 256 threads
-template <int LOG2N>
+template <int LOG2N, int TGT = SW_BLK_THREADS>
 struct Blk {
   static constexpr int NT = FftPlan<LOG2N>::NT;
   // at most 32 lines, so that NB divides the local rows (>= 32) and the local
   // columns (a multiple of NB)
-  static constexpr int NB = NT >= 256 ? 1 : (256 / NT > 32 ? 32 : 256 / NT);
+  static constexpr int NB = NT >= TGT ? 1 : (TGT / NT > 32 ? 32 : TGT / NT);
   static constexpr int THREADS = NB * NT;
 };
 
@@ -390,12 +390,25 @@ __device__ __forceinline__ void store_pair(const double2 (&v)[8], int t, const G
 
 // LDS line buffers per row of k_row: RSW transforms pairs of lines together
 // where two buffers per row fit the 160 KB of LDS (nx <= 4096)
+// Threads per block of the row pass.  Measured (tools/sweep_sizes.sh): the
+// RSW row (two line buffers) runs best with up to 256 threads per block
+// (1024²: 29 vs 36 µs at 128), every other kernel with one line per block
+// down to 64 threads (512² TY / MultiLayerQG steps +11-14 %, 1024² RSW
+// col_step 31 -> 28 µs) — more, smaller blocks spread a small grid over the
+// 256 CUs.
+template <int MODEL>
+__host__ __device__ constexpr int row_tgt() {
+  return MODEL == MODEL_RSW ? 256 : SW_BLK_THREADS;
+}
+template <int MODEL, int LOG2N>
+using BlkRow = Blk<LOG2N, row_tgt<MODEL>()>;
+
 template <int MODEL, int LOG2N>
 __host__ __device__ constexpr int row_lds_lines() {
 #ifdef SW_ROW_CB1  // sweep knob: one line buffer per row
   return 1;
 #else
-  return (MODEL == MODEL_RSW && 2 * Blk<LOG2N>::NB * FftPlan<LOG2N>::LDS * 16 <= 160 * 1024) ? 2 : 1;
+  return (MODEL == MODEL_RSW && 2 * BlkRow<MODEL, LOG2N>::NB * FftPlan<LOG2N>::LDS * 16 <= 160 * 1024) ? 2 : 1;
 #endif
 }
 // C = 2: both transforms per barrier; C = 1: one after the other
@@ -411,10 +424,10 @@ __device__ __forceinline__ void fft_pair(double2 (&w)[2][8], int t, const Twiddl
 }
 
 template <int MODEL, int LOG2N>
-__global__ void __launch_bounds__(Blk<LOG2N>::THREADS, Blk<LOG2N>::THREADS >= 1024 ? 4 : SW_MINW_ROW)
+__global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS), (BlkRow<MODEL, LOG2N>::THREADS >= 1024 ? 4 : SW_MINW_ROW))
     k_row(Geom g, Phys p, const double2* __restrict__ Mi, double2* __restrict__ Mo,
           const double2* __restrict__ tw) {
-  using Bk = Blk<LOG2N>;
+  using Bk = BlkRow<MODEL, LOG2N>;
   extern __shared__ double2 smem[];
   const LineCtx c = line_ctx<LOG2N>();
   const int y = (Bk::NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * Bk::NB + c.ln;
@@ -1662,17 +1675,18 @@ template <int L>
 struct RowL {
   static void run(int model, const Geom& g, const Phys& p, const double2* Mi, double2* Mo,
                   const double2* tw, hipStream_t s) {
-    constexpr size_t sh_rsw = row_lds_lines<MODEL_RSW, L>() * FftPlan<L>::LDS * Blk<L>::NB * sizeof(double2);
-    constexpr size_t sh_qg2 = row_lds_lines<MODEL_QG2, L>() * FftPlan<L>::LDS * Blk<L>::NB * sizeof(double2);
+    using BR = BlkRow<MODEL_RSW, L>;
+    using BQ = BlkRow<MODEL_QG2, L>;
+    using BT = BlkRow<MODEL_TY, L>;
+    constexpr size_t sh_rsw = row_lds_lines<MODEL_RSW, L>() * FftPlan<L>::LDS * BR::NB * sizeof(double2);
+    constexpr size_t sh_qg2 = FftPlan<L>::LDS * BQ::NB * sizeof(double2);
+    constexpr size_t sh_ty = FftPlan<L>::LDS * BT::NB * sizeof(double2);
     if (model == MODEL_RSW)
-      hipLaunchKernelGGL((k_row<MODEL_RSW, L>), dim3(row_blocks<L>(g)), dim3(Blk<L>::THREADS), sh_rsw, s, g, p,
-                         Mi, Mo, tw);
+      hipLaunchKernelGGL((k_row<MODEL_RSW, L>), dim3(g.nyl / BR::NB), dim3(BR::THREADS), sh_rsw, s, g, p, Mi, Mo, tw);
     else if (model == MODEL_TY)
-      hipLaunchKernelGGL((k_row<MODEL_TY, L>), dim3(row_blocks<L>(g)), dim3(Blk<L>::THREADS), sh_qg2, s, g, p,
-                         Mi, Mo, tw);
+      hipLaunchKernelGGL((k_row<MODEL_TY, L>), dim3(g.nyl / BT::NB), dim3(BT::THREADS), sh_ty, s, g, p, Mi, Mo, tw);
     else
-      hipLaunchKernelGGL((k_row<MODEL_QG2, L>), dim3(row_blocks<L>(g)), dim3(Blk<L>::THREADS), sh_qg2, s, g, p,
-                         Mi, Mo, tw);
+      hipLaunchKernelGGL((k_row<MODEL_QG2, L>), dim3(g.nyl / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p, Mi, Mo, tw);
   }
 };
 template <int L>
