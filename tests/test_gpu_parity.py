@@ -191,6 +191,19 @@ def test_nan_detection():
     prob.close()
 
 
+def test_config1_driver_params_blow_up_like_the_reference():
+    """BASELINE config 1 (RSWDriver 128², FilteredAB3, driver νtune) is
+    linearly unstable (tests/test_oracle.py); libsw reports it the way the
+    driver does (rsw/RSWDriver.jl:213-218): SW_E_NAN, "Solution is NaN"."""
+    from juliaraytracingsw_amd import LibSWError, drivers
+
+    prob, _ = drivers.rsw_problem(128, "FilteredAB3")
+    with pytest.raises(LibSWError) as ei:
+        prob.stepforward(200)
+    assert ei.value.code == -5
+    prob.close()
+
+
 def test_invalid_config_fails_loudly():
     from juliaraytracingsw_amd import LibSWError, rotating_shallow_water as RSW
 

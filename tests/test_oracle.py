@@ -346,6 +346,22 @@ def test_aliased_fraction_zero_grid():
     assert g.live.sum() == 32 * 63
 
 
+def test_config1_fab3_at_driver_nutune_is_unstable():
+    """BASELINE config 1 (RSWDriver at 128², FilteredAB3) with the driver's own
+    νtune = 20: the explicit hyperviscous rate at kmax is dt·ν·kmax⁸ = νtune·dx
+    ≈ 0.98, outside AB3's real-axis stability interval (6/11), so the run
+    blows up within 50 steps — as the reference's FilteredAB3 would.  The
+    parity cases therefore scale νtune with the grid (tests/sw_cases.py)."""
+    n = 128
+    dt, nu = O.rsw_driver_params(n)
+    assert abs(dt * nu * ((n / 2 - 1) * (2 / 3)) ** 8 - 20 * 2 * np.pi / n) < 1e-12
+    pr = O.Problem("rsw", "FilteredAB3", n, dt, params=O.RSWParams(nu, 4, 3.0, 1.0), order=8)
+    pr.set_solution(O.shafer_ic(pr.grid, (10, 13), (0, 5), 0.2, 0.1, 3.0, 1.0, np.random.default_rng(1)))
+    with np.errstate(all="ignore"):
+        pr.stepforward(60)
+    assert not np.isfinite(pr.sol).all() or np.abs(pr.sol).max() > 1e6
+
+
 # --- golden fixtures -----------------------------------------------------------
 GOLDEN_FILES = sorted(glob.glob(os.path.join(GOLDEN, "*.npz")))
 
