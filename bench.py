@@ -94,11 +94,20 @@ def main():
     import torch
 
     dist = None
+    # SW_BENCH_BACKEND=gloo: rehearse the N-rank ensemble path with several
+    # ranks sharing the box's GPUs (RCCL refuses two ranks on one GPU); the
+    # driver's multi-GPU runs use the default, RCCL ("nccl"), one GPU per rank
+    backend = os.environ.get("SW_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         import torch.distributed as dist
 
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     def barrier_sync():
         torch.cuda.synchronize()
@@ -130,7 +139,7 @@ def main():
     barrier_sync()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if backend == "gloo" else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
