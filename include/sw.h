@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SW_ABI_VERSION 4
+#define SW_ABI_VERSION 5
 
 /* models */
 #define SW_MODEL_RSW 0   /* rsw/RotatingShallowWater.jl: fields (u, v, η), 3×3 L   */
@@ -85,6 +85,13 @@ extern "C" {
  * barotropic_energy; SW_DIAG_CFL = dt · max of maximum(u_c)/dx, maximum(v_c)/dy,
  * maximum(u_T)/dx, maximum(v_T)/dy (signed maxima, thomasyamada/TYdriver.jl:150) */
 #define SW_DIAG_BT    6
+/* TY wave_geostrophic_energy (thomasyamada/ThomasYamada.jl:353-367, the
+ * TYUtils.jl:40-51 balanced/wave split of (u_c, v_c, p_c)), reduced on the
+ * device: ((WAVE_KE, WAVE_PE), (GEO_KE, GEO_PE)) */
+#define SW_DIAG_WAVE_KE 7
+#define SW_DIAG_WAVE_PE 8
+#define SW_DIAG_GEO_KE  9
+#define SW_DIAG_GEO_PE  10
 
 /* Host-staged transport (optional, one slab per process).  When set, libsw
  * moves every inter-slab exchange through host memory and calls
@@ -203,6 +210,8 @@ typedef struct sw_energy_record {
                               TY: baroclinic kinetic (|u_c|² + |v_c|²)      */
   double  ke2;             /* QG2: KE of layer 2 (0 for RSW); TY: barotropic */
   double  pe;              /* potential energy (TY: baroclinic |p_c|²)       */
+  double  wg[4];           /* TY: wave KE, wave PE, geostrophic KE,
+                              geostrophic PE (SW_DIAG_WAVE_KE..GEO_PE); else 0 */
 } sw_energy_record;
 int sw_set_energy_diagnostics(sw_ctx* ctx, int64_t freq, int64_t capacity);
 /* Copies up to max_records records (oldest first); *n_records = the count.

@@ -10,12 +10,13 @@ import os
 
 import numpy as np
 
-SW_ABI_VERSION = 4
+SW_ABI_VERSION = 5
 SW_MODEL_RSW, SW_MODEL_QG2, SW_MODEL_TY, SW_MODEL_MLQG = 0, 1, 2, 3
 SW_STEP_FILTERED_AB3, SW_STEP_IFMAB3, SW_STEP_IFMRK4, SW_STEP_ETDRK4, SW_STEP_FILTERED_RK4 = 0, 1, 2, 3, 4
 SW_OK, SW_E_INVALID, SW_E_NOMEM, SW_E_HIP, SW_E_COMM, SW_E_NAN, SW_E_STATE = 0, -1, -2, -3, -4, -5, -6
 SW_PHYS_U, SW_PHYS_V, SW_PHYS_ETA, SW_PHYS_ZETA, SW_PHYS_Q, SW_PHYS_PSI = 0, 1, 2, 3, 4, 5
 SW_DIAG_NAN, SW_DIAG_KE, SW_DIAG_PE, SW_DIAG_CFL, SW_DIAG_KE2, SW_DIAG_KE1, SW_DIAG_BT = 0, 1, 2, 3, 4, 5, 6
+SW_DIAG_WAVE_KE, SW_DIAG_WAVE_PE, SW_DIAG_GEO_KE, SW_DIAG_GEO_PE = 7, 8, 9, 10
 
 STEPPERS = {"FilteredAB3": SW_STEP_FILTERED_AB3, "IFMAB3": SW_STEP_IFMAB3, "IFMRK4": SW_STEP_IFMRK4,
             "ETDRK4": SW_STEP_ETDRK4, "FilteredRK4": SW_STEP_FILTERED_RK4}
@@ -62,7 +63,7 @@ class SwConfig(C.Structure):
 
 class SwEnergyRecord(C.Structure):
     _fields_ = [("step", C.c_int64), ("t", C.c_double), ("ke", C.c_double), ("ke2", C.c_double),
-                ("pe", C.c_double)]
+                ("pe", C.c_double), ("wg", C.c_double * 4)]
 
 
 class SwKernelStat(C.Structure):
@@ -212,7 +213,8 @@ class Context:
                     "sw_set_energy_diagnostics")
 
     def energy_diagnostics(self, max_records=None):
-        """[(step, t, ke, ke2, pe), …] recorded on the device while stepping."""
+        """[(step, t, ke, ke2, pe, wg), …] recorded on the device while stepping
+        (wg: TY's (wave KE, wave PE, geostrophic KE, geostrophic PE))."""
         cap = 1 << 20 if max_records is None else int(max_records)
         n = C.c_int64()
         self._check(self.lib.sw_get_energy_diagnostics(self._h, None, 0, C.byref(n)),
@@ -220,7 +222,7 @@ class Context:
         buf = (SwEnergyRecord * max(1, min(cap, n.value)))()
         self._check(self.lib.sw_get_energy_diagnostics(self._h, buf, min(cap, n.value), C.byref(n)),
                     "sw_get_energy_diagnostics")
-        return [(buf[i].step, buf[i].t, buf[i].ke, buf[i].ke2, buf[i].pe) for i in range(n.value)]
+        return [(buf[i].step, buf[i].t, buf[i].ke, buf[i].ke2, buf[i].pe, tuple(buf[i].wg)) for i in range(n.value)]
 
     def profile(self, nsteps):
         st = (SwKernelStat * 16)()

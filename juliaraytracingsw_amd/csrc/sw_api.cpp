@@ -70,14 +70,14 @@ struct sw_ctx {
   double2* stage = nullptr;                  // full (nkr,nl,nf) staging
   double2* gbuf = nullptr;                   // dist: all-gathered compact slabs
   double* dflt = nullptr;                    // physical staging / reductions
-  double* ecols = nullptr;                   // per-column energy sums [global column][3]
+  double* ecols = nullptr;                   // per-column energy sums [global column][SW_NSUM]
   double* esum = nullptr;                    // energy sums / gathered maxima (sw_diag)
   int* flag = nullptr;
   // FF Diagnostic(kinetic_energy / potential_energy; freq) recorded on the
   // device during sw_step (sw_set_energy_diagnostics)
   int64_t diag_freq = 0, diag_cap = 0, diag_n = 0;
-  double* erec = nullptr;                    // records: [rec][3] sums, or (one slab per
-                                             // process) [rec][kcl][3] column sums
+  double* erec = nullptr;                    // records: [rec][SW_NSUM] sums, or (one slab per
+                                             // process) [rec][kcl][SW_NSUM] column sums
   std::vector<int64_t> diag_steps;
   std::vector<double> diag_t;
   double t = 0.0;
@@ -554,11 +554,11 @@ int run_stage(sw_ctx* c, int op, int stage, double2* Slab::*X) {
 void record_energy(sw_ctx* c, double2* Slab::*X) {
   if (c->dist) {  // this rank's column sums; added over ranks at retrieval
     const Slab& s = c->sl[0];
-    sw::launch_energy_cols(c->cfg.model, s.g, c->p, s.*X, c->erec + (size_t)c->diag_n * s.g.kcl * 3, c->stream);
+    sw::launch_energy_cols(c->cfg.model, s.g, c->p, s.*X, c->erec + (size_t)c->diag_n * s.g.kcl * SW_NSUM, c->stream);
     return;
   }
-  for (Slab& s : c->sl) sw::launch_energy_cols(c->cfg.model, s.g, c->p, s.*X, c->ecols + 3 * s.g.kr0, c->stream);
-  sw::launch_energy_final(c->ecols, c->P * c->sl[0].g.kcl, c->erec + 3 * c->diag_n, c->stream);
+  for (Slab& s : c->sl) sw::launch_energy_cols(c->cfg.model, s.g, c->p, s.*X, c->ecols + SW_NSUM * s.g.kr0, c->stream);
+  sw::launch_energy_final(c->ecols, c->P * c->sl[0].g.kcl, c->erec + SW_NSUM * c->diag_n, c->stream);
 }
 
 int step_once(sw_ctx* c) {
@@ -856,8 +856,8 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   if ((rc = alloc(c, (void**)&c->stage, full_bytes(c)))) return rc;
   if ((rc = alloc(c, (void**)&c->dflt, (size_t)g.nx * g.ny * sizeof(double)))) return rc;
   if ((rc = alloc(c, (void**)&c->flag, 1024 * sizeof(int)))) return rc;
-  if ((rc = alloc(c, (void**)&c->ecols, 3 * (size_t)P * g.kcl * sizeof(double)))) return rc;
-  if ((rc = alloc(c, (void**)&c->esum, (3 + 2 * (size_t)P) * sizeof(double)))) return rc;
+  if ((rc = alloc(c, (void**)&c->ecols, SW_NSUM * (size_t)P * g.kcl * sizeof(double)))) return rc;
+  if ((rc = alloc(c, (void**)&c->esum, (SW_NSUM + 2 * (size_t)P) * sizeof(double)))) return rc;
   if (c->dist) {
     const size_t gb = (size_t)P * c->nf * g.kcl * g.LrP * sizeof(double2);
     if ((rc = alloc(c, (void**)&c->gbuf, gb))) return rc;
@@ -1046,9 +1046,13 @@ static double key_double(unsigned long long k) {
 // energy sums (k_energy_partial triples) -> (KE, KE2, PE)
 // (rsw/RotatingShallowWater.jl:323-333; swqg/TwoLayerQG.jl:230-250, KE per
 // layer), with the parsevalsum(2) normalisation
-static void energies_from_sums(const sw_ctx* c, const double a[3], double& ke, double& ke2, double& pe) {
+static void energies_from_sums(const sw_ctx* c, const double a[SW_NSUM], double& ke, double& ke2, double& pe,
+                               double* wg = nullptr) {
   const Geom& g = c->sl[0].g;
   const double norm = g.Lx * g.Ly / ((double)g.nx * g.nx * (double)g.ny * g.ny);
+  // TY wave_geostrophic_energy (:353-367): (wave KE, wave PE, geo KE, geo PE)
+  if (wg)
+    for (int i = 0; i < 4; ++i) wg[i] = c->cfg.model == SW_MODEL_TY ? norm * a[3 + i] : 0.0;
   if (c->cfg.model == SW_MODEL_RSW) {
     ke = norm * a[0] / (2 * g.Lx * g.Ly);
     ke2 = 0.0;
@@ -1073,19 +1077,19 @@ static void energies_from_sums(const sw_ctx* c, const double a[3], double& ke, d
   }
 }
 
-// `nrec` energy records -> host sums [rec][3].  Single process: dev holds
+// `nrec` energy records -> host sums [rec][SW_NSUM].  Single process: dev holds
 // the sums.  One slab per process: dev holds this rank's column sums
 // [rec][kcl][3]; they are gathered and added in global column order, so the
 // result is bitwise the same for any decomposition.
 static int gather_energy_sums(sw_ctx* c, const double* dev, int64_t nrec, std::vector<double>& out) {
-  out.assign((size_t)nrec * 3, 0.0);
+  out.assign((size_t)nrec * SW_NSUM, 0.0);
   if (nrec == 0) return 0;
   if (!c->dist) {
     HIPCHK(c, hipMemcpyAsync(out.data(), dev, out.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return 0;
   }
-  const size_t kcl = c->sl[0].g.kcl, per = (size_t)nrec * kcl * 3;
+  const size_t kcl = c->sl[0].g.kcl, per = (size_t)nrec * kcl * SW_NSUM;
   std::vector<double> all(per * c->P);
   double* tmp = nullptr;
   HIPCHK(c, hipMalloc((void**)&tmp, per * c->P * sizeof(double)));
@@ -1097,11 +1101,11 @@ static int gather_energy_sums(sw_ctx* c, const double* dev, int64_t nrec, std::v
   (void)hipFree(tmp);
   if (rc) return rc;
   for (int64_t r = 0; r < nrec; ++r)
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < SW_NSUM; ++k) {
       double acc = 0.0;
       for (int q = 0; q < c->P; ++q)
-        for (size_t col = 0; col < kcl; ++col) acc += all[q * per + ((size_t)r * kcl + col) * 3 + k];
-      out[(size_t)r * 3 + k] = acc;
+        for (size_t col = 0; col < kcl; ++col) acc += all[q * per + ((size_t)r * kcl + col) * SW_NSUM + k];
+      out[(size_t)r * SW_NSUM + k] = acc;
     }
   return 0;
 }
@@ -1151,23 +1155,28 @@ int sw_diag(sw_ctx* c, int32_t id, double* out) {
     *out = c->cfg.dt * std::max(key_double(kmax[0]) / g0.dx, key_double(kmax[1]) / g0.dy);
     return SW_OK;
   }
-  if (id != SW_DIAG_KE && id != SW_DIAG_PE && id != SW_DIAG_KE1 && id != SW_DIAG_KE2 && id != SW_DIAG_BT)
+  const bool wgid = id >= SW_DIAG_WAVE_KE && id <= SW_DIAG_GEO_PE;
+  if (id != SW_DIAG_KE && id != SW_DIAG_PE && id != SW_DIAG_KE1 && id != SW_DIAG_KE2 && id != SW_DIAG_BT && !wgid)
     return fail(c, SW_E_INVALID, "unknown diagnostic");
-  if ((id == SW_DIAG_BT && c->cfg.model != SW_MODEL_TY) ||
+  if (((id == SW_DIAG_BT || wgid) && c->cfg.model != SW_MODEL_TY) ||
       ((id == SW_DIAG_KE1 || id == SW_DIAG_KE2) && c->cfg.model == SW_MODEL_TY))
     return fail(c, SW_E_INVALID, "diagnostic not defined for this model");
-  for (Slab& s : c->sl) sw::launch_energy_cols(c->cfg.model, s.g, c->p, s.sol, c->ecols + 3 * s.g.kr0, c->stream);
+  for (Slab& s : c->sl) sw::launch_energy_cols(c->cfg.model, s.g, c->p, s.sol, c->ecols + SW_NSUM * s.g.kr0, c->stream);
   if (c->dist) {
     const Geom& g0 = c->sl[0].g;
-    if (int rc = allgather(c, c->ecols + 3 * g0.kr0, c->ecols, 3 * (size_t)g0.kcl * sizeof(double))) return rc;
+    if (int rc = allgather(c, c->ecols + SW_NSUM * g0.kr0, c->ecols, SW_NSUM * (size_t)g0.kcl * sizeof(double))) return rc;
   }
   sw::launch_energy_final(c->ecols, c->P * c->sl[0].g.kcl, c->esum, c->stream);
   HIPCHK(c, hipGetLastError());
-  std::vector<double> sums(3);
-  HIPCHK(c, hipMemcpyAsync(sums.data(), c->esum, 3 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  std::vector<double> sums(SW_NSUM);
+  HIPCHK(c, hipMemcpyAsync(sums.data(), c->esum, SW_NSUM * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  double ke, ke2, pe;
-  energies_from_sums(c, sums.data(), ke, ke2, pe);
+  double ke, ke2, pe, wg[4];
+  energies_from_sums(c, sums.data(), ke, ke2, pe, wg);
+  if (wgid) {
+    *out = wg[id - SW_DIAG_WAVE_KE];
+    return SW_OK;
+  }
   // RSW KE; 2LQG KE = KE_1 + KE_2 (the driver's tuple summed), KE2 = KE_2;
   // TY: KE, PE the baroclinic pair, BT barotropic
   if (c->cfg.model == SW_MODEL_TY) *out = id == SW_DIAG_KE ? ke : (id == SW_DIAG_BT ? ke2 : pe);
@@ -1191,7 +1200,7 @@ int sw_set_energy_diagnostics(sw_ctx* c, int64_t freq, int64_t capacity) {
   c->diag_steps.clear();
   c->diag_t.clear();
   if (c->diag_cap > 0) {
-    const size_t per = c->dist ? (size_t)c->sl[0].g.kcl * 3 : 3;
+    const size_t per = c->dist ? (size_t)c->sl[0].g.kcl * SW_NSUM : SW_NSUM;
     if (int rc = alloc(c, (void**)&c->erec, (size_t)c->diag_cap * per * sizeof(double))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
   }
@@ -1213,7 +1222,7 @@ int sw_get_energy_diagnostics(sw_ctx* c, sw_energy_record* out, int64_t max_reco
   for (int64_t r = 0; r < n; ++r) {
     out[r].step = c->diag_steps[r];
     out[r].t = c->diag_t[r];
-    energies_from_sums(c, &sums[3 * r], out[r].ke, out[r].ke2, out[r].pe);
+    energies_from_sums(c, &sums[(size_t)SW_NSUM * r], out[r].ke, out[r].ke2, out[r].pe, out[r].wg);
   }
   if (n_records) *n_records = n;
   return SW_OK;

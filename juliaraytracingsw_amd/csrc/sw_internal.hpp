@@ -16,6 +16,10 @@
 #define SW_BLK_THREADS 64
 #endif
 
+// Parseval sums per energy evaluation (k_energy_cols; 3 for RSW/QG2/MLQG,
+// 7 for TY with its wave/balanced split)
+#define SW_NSUM 7
+
 namespace sw {
 
 // MODEL_MLQG (GeophysicalFlows MultiLayerQG, 2 layers) runs the MODEL_QG2

@@ -1529,13 +1529,54 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
 }
 
 // Energies by Parseval over live modes (FF parsevalsum2 / parsevalsum:
-// weight 2 for 0 < kr < nx/2, 1 for kr = 0).  Three sums per state:
-//   RSW: 0 |u|²+|v|², 1 |η|², 2 unused
-//   QG2: 0 K²|ψ1|², 1 K²|ψ2|², 2 |ψ1-ψ2|²
+// weight 2 for 0 < kr < nx/2, 1 for kr = 0).  SW_NSUM sums per state:
+//   RSW: 0 |u|²+|v|², 1 |η|², 2.. unused
+//   QG2/MLQG: 0 K²|ψ1|², 1 K²|ψ2|², 2 |ψ1-ψ2|², 3.. unused
+//   TY: 0 |K⁻¹ζ|², 1 |u_c|²+|v_c|², 2 |p_c|², then the wave/balanced split
+//       (ty_split): 3 |W_u|²+|W_v|², 4 |W_p|², 5 |G_u|²+|G_v|², 6 |G_p|²
 // Deterministic and independent of the slab decomposition: one block per
 // column reduces that column in a fixed order (k_energy_cols, padding
 // columns give 0), then the column sums are added in global column order
 // (k_energy_final).  No atomics: results repeat bitwise for any P.
+// thomasyamada/TYUtils.jl:10-51 (decompose_balanced_wave) at one mode (k, l):
+// G = (b·Φ₀*)Φ₀, W = (b·Φ₊*)Φ₊ + (b·Φ₋*)Φ₋ of b = (u_c, v_c, p_c), with
+// ω = √(1+K²), Φ₀ = (il, −ik, −1)/ω, Φ± = (±ωk + il, ±ωl − ik, ω²−1)·s,
+// s = √(1/(2K²))/ω; at K = 0, Φ₀ = (0, 0, 1) and Φ± = (i, ±1, 0)/√2.
+// Adds w·(|W_u|²+|W_v|², |W_p|², |G_u|²+|G_v|², |G_p|²) to a[0..3].
+__device__ __forceinline__ double2 cdotc(double2 u, double2 v, double2 q, double2 P0, double2 P1, double2 P2) {
+  return cadd(cadd(cmul(u, cconj(P0)), cmul(v, cconj(P1))), cmul(q, cconj(P2)));
+}
+__device__ void ty_split(double k, double l, double2 u, double2 v, double2 q, double w, double* a) {
+  double2 Z[3], Pp[3], Pm[3];
+  const double K2 = k * k + l * l;
+  if (K2 == 0.0) {
+    const double r = sqrt(0.5);
+    Z[0] = make_double2(0.0, 0.0), Z[1] = make_double2(0.0, 0.0), Z[2] = make_double2(1.0, 0.0);
+    Pp[0] = make_double2(0.0, r), Pp[1] = make_double2(r, 0.0), Pp[2] = make_double2(0.0, 0.0);
+    Pm[0] = make_double2(0.0, r), Pm[1] = make_double2(-r, 0.0), Pm[2] = make_double2(0.0, 0.0);
+  } else {
+    const double om = sqrt(1.0 + K2), io = 1.0 / om;
+    const double sc = sqrt(1.0 / K2 / 2.0) / om;
+    Z[0] = make_double2(0.0, l * io), Z[1] = make_double2(0.0, -k * io), Z[2] = make_double2(-io, 0.0);
+    Pp[0] = make_double2(om * k * sc, l * sc), Pp[1] = make_double2(om * l * sc, -k * sc);
+    Pm[0] = make_double2(-om * k * sc, l * sc), Pm[1] = make_double2(-om * l * sc, -k * sc);
+    Pp[2] = Pm[2] = make_double2((om * om - 1.0) * sc, 0.0);
+  }
+  const double2 c0 = cdotc(u, v, q, Z[0], Z[1], Z[2]);
+  const double2 cp = cdotc(u, v, q, Pp[0], Pp[1], Pp[2]);
+  const double2 cm = cdotc(u, v, q, Pm[0], Pm[1], Pm[2]);
+  double2 W[3], G[3];
+  for (int j = 0; j < 3; ++j) {
+    W[j] = cadd(cmul(cp, Pp[j]), cmul(cm, Pm[j]));
+    G[j] = cmul(c0, Z[j]);
+  }
+  auto n2 = [](double2 z) { return z.x * z.x + z.y * z.y; };
+  a[0] += w * (n2(W[0]) + n2(W[1]));
+  a[1] += w * n2(W[2]);
+  a[2] += w * (n2(G[0]) + n2(G[1]));
+  a[3] += w * n2(G[2]);
+}
+
 __device__ __forceinline__ double block_sum(double v, double* sh) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
   const int w = threadIdx.x >> 6;
@@ -1553,7 +1594,7 @@ __global__ void __launch_bounds__(256) k_energy_cols(Geom g, Phys p, int model,
                                                      double* __restrict__ cols) {
   __shared__ double sh[4];
   const int krl = blockIdx.x;
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, ws[4] = {0.0, 0.0, 0.0, 0.0};
   if (krl < g.kcn) {
     const long long cf = g.cfield;
     const int kr = g.kr0 + krl;
@@ -1574,6 +1615,7 @@ __global__ void __launch_bounds__(256) k_energy_cols(Geom g, Phys p, int model,
         a0 += w * (zx * zx + zy * zy);
         a1 += w * (u.x * u.x + u.y * u.y + v.x * v.x + v.y * v.y);
         a2 += w * (q.x * q.x + q.y * q.y);
+        ty_split(k, l, u, v, q, w, ws);
       } else {
         const double l = lwav(g, lrow_of(g, j));
         const double K2 = k * k + l * l;
@@ -1591,17 +1633,19 @@ __global__ void __launch_bounds__(256) k_energy_cols(Geom g, Phys p, int model,
   a0 = block_sum(a0, sh);
   a1 = block_sum(a1, sh);
   a2 = block_sum(a2, sh);
+  if (model == MODEL_TY)
+    for (int i = 0; i < 4; ++i) ws[i] = block_sum(ws[i], sh);
   if (threadIdx.x == 0) {
-    cols[3 * krl] = a0;
-    cols[3 * krl + 1] = a1;
-    cols[3 * krl + 2] = a2;
+    double* o = cols + SW_NSUM * krl;
+    o[0] = a0, o[1] = a1, o[2] = a2;
+    for (int i = 0; i < 4; ++i) o[3 + i] = ws[i];
   }
 }
 
 __global__ void k_energy_final(const double* __restrict__ cols, int ncols, double* __restrict__ out) {
-  if (threadIdx.x < 3) {
+  if (threadIdx.x < SW_NSUM) {
     double r = 0.0;
-    for (int b = 0; b < ncols; ++b) r += cols[3 * b + threadIdx.x];
+    for (int b = 0; b < ncols; ++b) r += cols[SW_NSUM * b + threadIdx.x];
     out[threadIdx.x] = r;
   }
 }

@@ -132,7 +132,8 @@ class Diagnostic:
         field = getattr(calc, "_sw_energy", None)
         if field is None:
             raise ValueError("libsw records the models' energy diagnostics (kinetic_energy, "
-                             "potential_energy, baroclinic_energy, barotropic_energy)")
+                             "potential_energy, baroclinic_energy, barotropic_energy, "
+                             "wave_geostrophic_energy, energies)")
         ndata = int(ndata or math.ceil((nsteps + 1) / freq))
         prob._attach_energy_diagnostics(int(freq), ndata)
         self.calc, self.prob, self.freq, self._field = calc, prob, int(freq), field
@@ -145,11 +146,11 @@ class Diagnostic:
         self._seen = 0  # device records consumed
 
     def _take(self, records):
-        for step, t, ke, ke2, pe in records[self._seen:]:
+        for step, t, ke, ke2, pe, wg in records[self._seen:]:
             if self.i >= len(self.data):
                 break
             v = {"ke": ke, "pe": pe, "ke12": (ke, ke2), "bc": (ke, pe), "bt": ke2,
-                 "mlqg": ((ke, ke2), (pe,))}[self._field]
+                 "mlqg": ((ke, ke2), (pe,)), "wg": ((wg[0], wg[1]), (wg[2], wg[3]))}[self._field]
             self.data[self.i], self.t[self.i], self.steps[self.i] = v, t, step
             self.value = v
             self.i += 1

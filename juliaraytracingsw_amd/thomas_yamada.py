@@ -70,16 +70,9 @@ def barotropic_energy(prob):
     return prob.ctx.diag(_lib.SW_DIAG_BT)
 
 
-def _parsevalsum2(uh, grid):
-    U = np.abs(uh) ** 2
-    s = 2 * U.sum() - U[:, 0].sum()
-    if grid.nx % 2 == 0:
-        s -= U[:, -1].sum()
-    return grid.Lx * grid.Ly / (grid.nx ** 2 * grid.ny ** 2) * s
-
-
 def _bases(grid):
-    """thomasyamada/TYUtils.jl:10-38: Φ₀, Φ₊, Φ₋ per mode, each [3][nl][nkr]."""
+    """thomasyamada/TYUtils.jl:10-38: Φ₀, Φ₊, Φ₋ per mode, each [3][nl][nkr]
+    (host set-up of the driver's initial condition)."""
     kr = grid.kr[None, :]
     l = grid.l[:, None]
     K2 = kr ** 2 + l ** 2
@@ -100,15 +93,11 @@ def _bases(grid):
 def wave_geostrophic_energy(prob):
     """``wave_geostrophic_energy(prob)`` (:353-367) via
     ``decompose_balanced_wave`` (thomasyamada/TYUtils.jl:40-51): ((wave KE,
-    wave PE), (geostrophic KE, geostrophic PE)).  A per-frame driver
-    diagnostic, evaluated on the host from the downloaded state."""
-    g = prob.grid
-    b = prob.sol[1:4]
-    P0, Pp, Pm = _bases(g)
-    G = (b * np.conj(P0)).sum(0)[None] * P0
-    W = (b * np.conj(Pp)).sum(0)[None] * Pp + (b * np.conj(Pm)).sum(0)[None] * Pm
-    ps = lambda f: _parsevalsum2(f, g)  # noqa: E731
-    return ((ps(W[0]) + ps(W[1]), ps(W[2])), (ps(G[0]) + ps(G[1]), ps(G[2])))
+    wave PE), (geostrophic KE, geostrophic PE)), the per-mode projection on
+    Φ₀, Φ₊, Φ₋ and its Parseval sums reduced on the device (k_energy_cols)."""
+    d = prob.ctx.diag
+    return ((d(_lib.SW_DIAG_WAVE_KE), d(_lib.SW_DIAG_WAVE_PE)),
+            (d(_lib.SW_DIAG_GEO_KE), d(_lib.SW_DIAG_GEO_PE)))
 
 
 def cfl(prob):
@@ -120,3 +109,4 @@ def cfl(prob):
 
 baroclinic_energy._sw_energy = "bc"
 barotropic_energy._sw_energy = "bt"
+wave_geostrophic_energy._sw_energy = "wg"

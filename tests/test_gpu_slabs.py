@@ -89,6 +89,26 @@ def test_slabs_physical_and_energy(name):
     b.close()
 
 
+def test_slabs_ty_energies():
+    """TY's seven Parseval sums (barotropic, baroclinic, wave/geostrophic)
+    repeat bitwise for any slab decomposition."""
+    from juliaraytracingsw_amd import thomas_yamada as TY
+
+    p = sw_cases.case_params("ty_etdrk4", 128)
+    pr = sw_cases.oracle_problem(p)
+    ic = sw_cases.initial_condition(p, pr.grid)
+    a = sw_cases.libsw_problem(p)
+    b = _slabbed(p, 4)
+    a.sol = ic
+    b.sol = ic
+    a.stepforward(2)
+    b.stepforward(2)
+    for f in (TY.barotropic_energy, TY.baroclinic_energy, TY.wave_geostrophic_energy):
+        assert f(a) == f(b), f.__name__
+    a.close()
+    b.close()
+
+
 def test_slab_config_errors():
     from juliaraytracingsw_amd import LibSWError, rotating_shallow_water as RSW
 

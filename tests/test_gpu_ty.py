@@ -101,6 +101,14 @@ def test_ty_physical_energy_cfl():
     assert abs(k2 / bk - 1) < 1e-10 and abs(p2 / bp - 1) < 1e-10
     (a, b), (c, d) = TY.wave_geostrophic_energy(prob)
     np.testing.assert_allclose([a, b, c, d], [wk, wp, gk, gp], rtol=1e-10)
+    # the K = 0 mode's special bases (TYUtils.jl:18, 35-36): a mean flow and
+    # a mean p_c only
+    s0 = np.zeros_like(sol)
+    s0[1:4, 0, 0] = [3.0 + 1.0j, -2.0 + 0.5j, 0.7]
+    prob.sol = s0
+    (a, b), (c, d) = TY.wave_geostrophic_energy(prob)
+    _, _, ((wk, wp), (gk, gp)) = O.ty_energies(s0, pr.grid)
+    np.testing.assert_allclose([a, b, c, d], [wk, wp, gk, gp], rtol=1e-12, atol=1e-300)
     g = pr.grid
     exp = p["dt"] * max(ref["uc"].max() / g.dx, ref["vc"].max() / g.dy, ref["ut"].max() / g.dx,
                         ref["vt"].max() / g.dy)
@@ -118,17 +126,19 @@ def test_ty_energy_diagnostics_recorded():
     freq, nsteps = 2, 6
     BT = TY.Diagnostic(TY.barotropic_energy, prob, freq=freq, nsteps=nsteps)
     BC = TY.Diagnostic(TY.baroclinic_energy, prob, freq=freq, nsteps=nsteps)
+    WG = TY.Diagnostic(TY.wave_geostrophic_energy, prob, freq=freq, nsteps=nsteps)
     expected = [(0, O.ty_energies(pr.sol, pr.grid))]
     for s in range(1, nsteps + 1):
         pr.stepforward(1)
         if s % freq == 0:
             expected.append((s, O.ty_energies(pr.grid.dealias(pr.sol.copy()), pr.grid)))
-    TY.stepforward(prob, [BT, BC], nsteps)
-    assert BT.i == BC.i == len(expected) == 4
-    for i, (s, (bt, bc, _)) in enumerate(expected):
+    TY.stepforward(prob, [BT, BC, WG], nsteps)
+    assert BT.i == BC.i == WG.i == len(expected) == 4
+    for i, (s, (bt, bc, wg)) in enumerate(expected):
         assert BT.steps[i] == s
         assert abs(BT.data[i] / bt - 1) < RTOL
         np.testing.assert_allclose(BC.data[i], bc, rtol=RTOL)
+        np.testing.assert_allclose(np.ravel(WG.data[i]), np.ravel(wg), rtol=RTOL)
     prob.close()
 
 
