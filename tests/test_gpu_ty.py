@@ -101,6 +101,10 @@ def test_ty_physical_energy_cfl():
     assert abs(k2 / bk - 1) < 1e-10 and abs(p2 / bp - 1) < 1e-10
     (a, b), (c, d) = TY.wave_geostrophic_energy(prob)
     np.testing.assert_allclose([a, b, c, d], [wk, wp, gk, gp], rtol=1e-10)
+    g = pr.grid
+    exp = p["dt"] * max(ref["uc"].max() / g.dx, ref["vc"].max() / g.dy, ref["ut"].max() / g.dx,
+                        ref["vt"].max() / g.dy)
+    assert abs(TY.cfl(prob) / exp - 1) < 1e-10
     # the K = 0 mode's special bases (TYUtils.jl:18, 35-36): a mean flow and
     # a mean p_c only
     s0 = np.zeros_like(sol)
@@ -109,10 +113,6 @@ def test_ty_physical_energy_cfl():
     (a, b), (c, d) = TY.wave_geostrophic_energy(prob)
     _, _, ((wk, wp), (gk, gp)) = O.ty_energies(s0, pr.grid)
     np.testing.assert_allclose([a, b, c, d], [wk, wp, gk, gp], rtol=1e-12, atol=1e-300)
-    g = pr.grid
-    exp = p["dt"] * max(ref["uc"].max() / g.dx, ref["vc"].max() / g.dy, ref["ut"].max() / g.dx,
-                        ref["vt"].max() / g.dy)
-    assert abs(TY.cfl(prob) / exp - 1) < 1e-10
     prob.close()
 
 
