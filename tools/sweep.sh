@@ -1,11 +1,11 @@
 #!/bin/bash
-# On the GPU box: short bench of every build/var/*.so (per-kernel HIP-event times).
+# On the GPU box: short bench of every sweep_var/*.so (per-kernel HIP-event times).
 # usage: bash tools/sweep.sh [--check] [extra bench args]
 #   --check: first run the RSW FilteredAB3 parity/slab GPU tests against each variant
 mkdir -p gpurun_out/sweep
 CHECK=0
 if [ "$1" = "--check" ]; then CHECK=1; shift; fi
-for so in build/var/*.so; do
+for so in sweep_var/*.so; do
   n=$(basename $so .so)
   if [ $CHECK = 1 ]; then
     LIBSW_PATH=$PWD/$so timeout -k 10 300 python -m pytest tests/test_gpu_parity.py tests/test_gpu_slabs.py -q -x -k "rsw_fab3" \

@@ -1,9 +1,9 @@
 #!/bin/bash
-# On the GPU box: per-kernel times of every build/var/*.so at the large
+# On the GPU box: per-kernel times of every sweep_var/*.so at the large
 # configurations.  usage: bash tools/sweep_sizes.sh "model stepper n steps" ...
 mkdir -p gpurun_out/sizes
 CFGS=("$@")
-for so in build/var/*.so; do
+for so in sweep_var/*.so; do
   v=$(basename $so .so)
   for cfg in "${CFGS[@]}"; do
     read -r m st n k <<< "$cfg"
