@@ -83,6 +83,25 @@ def test_oracle_parity_large(name, n, steps):
     prob.close()
 
 
+@pytest.mark.parametrize("name,n", [(c, 128 if c.startswith(("ty", "mlqg")) else 256) for c in sw_cases.ALL_CASES] +
+                         [("rsw_fab3", 1024), ("qg2_ifmab3", 1024)])
+def test_oracle_parity_100_steps(name, n):
+    """SURVEY §8c parity metric: ≤ 1e-10 after 100 steps (checked every 25),
+    every model × stepper, and at BASELINE config 2's 1024²."""
+    p = sw_cases.case_params(name, n)
+    pr = sw_cases.oracle_problem(p)
+    pr.set_solution(sw_cases.initial_condition(p, pr.grid))
+    prob = sw_cases.libsw_problem(p)
+    prob.sol = pr.sol
+    for done in (25, 50, 75, 100):
+        pr.stepforward(25)
+        prob.stepforward(25)
+        e = _err(prob.sol, pr.sol, pr.grid)
+        assert e < RTOL, (done, e)
+    assert prob.clock.step == 100
+    prob.close()
+
+
 def test_nop_calcN_linear_exactness():
     """NOPcalcN! (rsw/RotatingShallowWater.jl:135-138): IFMAB3 with N ≡ 0 gives
     exp(L t)·sol0; this also checks the device Padé-13 expm against scipy."""
