@@ -146,6 +146,17 @@ def main():
     # roofline: per-kernel HIP-event durations on libsw's stream
     stats = prob.ctx.profile(args.profile_steps)
     step_alg = prob.ctx.step_alg_bytes()
+    # the boundary's host-buffer cost: one state download and
+    # upload through the C ABI, i.e. over PCIe (after the timed region)
+    tg, tu = [], []
+    st = prob.ctx.get_state()  # the caller's prob.sol buffer, reused per frame
+    for _ in range(3):
+        t0 = time.perf_counter()
+        prob.ctx.get_state(out=st)
+        tg.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        prob.ctx.set_state(st)
+        tu.append(time.perf_counter() - t0)
     prob.close()
 
     if rank != 0:
@@ -209,6 +220,12 @@ def main():
         "kernels": [{"name": s["name"], "avg_us": s["avg_ms"] * 1e3, "per_step": s["launches"] / args.profile_steps,
                      "alg_bytes": s["alg_bytes"]} for s in stats],
         "cpu_baseline": cpu,
+        # RSWDriver saves a frame every output_freq = floor(output_dt/dt) steps
+        # (rsw/RSWDriver.jl:152, output_dt = 0.025/f): 81 steps at 2048²
+        "host_boundary": {"state_bytes": int(st.nbytes), "get_state_ms": min(tg) * 1e3,
+                          "set_state_ms": min(tu) * 1e3,
+                          "steps_per_s_with_state_download_every_81_steps":
+                              81 / (81 * ms_per_step * 1e-3 + min(tg))},
     }
     print(json.dumps(out))
     if dist is not None:

@@ -175,8 +175,15 @@ class Context:
             raise ValueError(f"state shape {a.shape} != {self.state_shape}")
         self._check(self.lib.sw_set_state(self._h, a.ctypes.data, a.nbytes), "sw_set_state")
 
-    def get_state(self):
-        a = np.empty(self.state_shape, np.complex128)
+    def get_state(self, out=None):
+        """The state as Julia's (nkr, nl, nf) array; ``out`` (C-contiguous
+        complex128 of that shape) is filled in place, as FF's ``prob.sol``."""
+        if out is None:
+            a = np.empty(self.state_shape, np.complex128)
+        else:
+            a = out
+            if a.shape != self.state_shape or a.dtype != np.complex128 or not a.flags.c_contiguous:
+                raise ValueError("get_state: out must be C-contiguous complex128 of the state shape")
         self._check(self.lib.sw_get_state(self._h, a.ctypes.data, a.nbytes), "sw_get_state")
         return a
 
