@@ -75,8 +75,8 @@ def cpu_baseline(model, stepper, n, budget_s=20.0, max_steps=20):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--n", type=int, default=2048)
     ap.add_argument("--model", default="rsw", choices=["rsw", "qg2", "ty", "mlqg"])
     ap.add_argument("--stepper", default="FilteredAB3",
