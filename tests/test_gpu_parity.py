@@ -10,6 +10,7 @@ import pytest
 
 import sw_cases
 import sw_oracle as O
+from juliaraytracingsw_amd import _lib
 
 pytestmark = pytest.mark.gpu
 
@@ -230,6 +231,24 @@ def test_invalid_config_fails_loudly():
         RSW.Problem("gpu", nx=96)  # not a power of two
     with pytest.raises(LibSWError):
         RSW.Problem("gpu", nx=64, aliased_fraction=0.0)
+    for bad in (dict(nx=16384), dict(nx=16), dict(nx=64, ny=24), dict(nx=64, aliased_fraction=1.0)):
+        with pytest.raises(LibSWError):  # outside [32, 8192], not a power of two, no live modes
+            RSW.Problem("gpu", **bad)
+    prob = RSW.Problem("gpu", nx=64)
+    with pytest.raises(LibSWError) as e:
+        prob.ctx.step(-1)
+    assert e.value.code == _lib.SW_E_INVALID and "nsteps" in str(e.value)
+    with pytest.raises(LibSWError):
+        prob.ctx.diag(99)
+    with pytest.raises(LibSWError):  # TY-only diagnostic on an RSW problem
+        prob.ctx.diag(_lib.SW_DIAG_WAVE_KE)
+    with pytest.raises(ValueError):  # wrong state shape never reaches the device
+        prob.ctx.set_state(np.zeros((3, 64, 32), complex))
+    rc = prob.ctx.lib.sw_set_state(prob.ctx._h, None, 0)  # raw ABI: null buffer
+    assert rc == _lib.SW_E_INVALID
+    prob.stepforward(2)  # the context stays usable after rejected calls
+    assert prob.clock.step == 2
+    prob.close()
 
 
 def _rect_problem(name, nx, ny):
