@@ -90,6 +90,21 @@ __device__ __forceinline__ void lds_barrier() {
 #endif
 }
 
+// Opaque thread index on lines of at least 2^SW_OPAQUE_LOG2 points (1024
+// threads, 128 VGPRs): the addresses a helper derives from t (LDS offsets of
+// every FFT stage, mirror indices, tile offsets) are recomputed per call (a
+// few integer ops) instead of being shared across the kernel's many calls and
+// spilled for its whole life.  8192²: RSW row 2892 → 2278 µs (spills 67 →
+// 23), 2LQG row 2308 → 2158 µs (20 → 0); shorter lines measured neutral to
+// slower (TY 512² col_inv +23 %), so they keep the shared addresses.
+#ifndef SW_OPAQUE_LOG2
+#define SW_OPAQUE_LOG2 13
+#endif
+#define SW_OPAQUE_T(t)                                                  \
+  do {                                                                  \
+    if constexpr (LOG2N >= SW_OPAQUE_LOG2) asm volatile("" : "+v"(t)); \
+  } while (0)
+
 template <int LOG2N>
 struct FftPlan {
   static constexpr int N = 1 << LOG2N;
@@ -152,6 +167,7 @@ __device__ __forceinline__ void fft_lines(double2 (&v)[C][8], int t, const Twidd
                                           double2* __restrict__ line, int stride) {
   using P = FftPlan<LOG2N>;
   constexpr int NT = P::NT;
+  SW_OPAQUE_T(t);
   // Opaque copy of the stage twiddles: keeps the compiler from sharing the
   // derived powers w2..w7 across the several transforms of one kernel, which
   // would pin 28 VGPRs per stage for the kernel's whole lifetime.

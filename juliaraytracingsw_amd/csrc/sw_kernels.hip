@@ -220,6 +220,7 @@ template <int LOG2N>
 __device__ __forceinline__ void load_pair(double2 (&v)[8], int t, const Geom& g,
                                           const double2* __restrict__ A,
                                           const double2* __restrict__ B, int y, bool deriv) {
+  SW_OPAQUE_T(t);
   constexpr int N = 1 << LOG2N, NT = N / 8, half = N / 2;
   double2 a[8], b[8];
   int kk[8];
@@ -259,6 +260,7 @@ template <int LOG2N>
 __device__ __forceinline__ void load_pair_m(double2 (&v)[8], int t, const Geom& g,
                                             const double2* __restrict__ A, int ma,
                                             const double2* __restrict__ B, int mb, int y) {
+  SW_OPAQUE_T(t);
   constexpr int N = 1 << LOG2N, NT = N / 8, half = N / 2;
   double2 a[8], b[8];
   int kk[8];
@@ -297,11 +299,16 @@ __device__ __forceinline__ void load_eta_zeta(double2 (&v)[8], int t, const Geom
                                               const double2* __restrict__ H,
                                               const double2* __restrict__ V,
                                               const double2* __restrict__ Uy, int y) {
+  SW_OPAQUE_T(t);
   constexpr int N = 1 << LOG2N, NT = N / 8, half = N / 2;
+  // 8192-point lines (128 VGPRs, the first pair live): four points at a time
+  constexpr int CH = LOG2N >= 13 ? 4 : 8;
+#pragma unroll
+  for (int s0 = 0; s0 < 8; s0 += CH) {
   double2 h[8], vv[8], uy[8];
   int kk[8];
 #pragma unroll
-  for (int s = 0; s < 8; ++s) {
+  for (int s = s0; s < s0 + CH; ++s) {
     const int m = t + s * NT;
     kk[s] = m <= half ? m : N - m;
     const int o = midx_i(g, kk[s] < g.kc ? kk[s] : 0, y);
@@ -310,7 +317,7 @@ __device__ __forceinline__ void load_eta_zeta(double2 (&v)[8], int t, const Geom
     uy[s] = Uy[o];
   }
 #pragma unroll
-  for (int s = 0; s < 8; ++s) {
+  for (int s = s0; s < s0 + CH; ++s) {
     const int m = t + s * NT;
     double2 aa = h[s], bb = csub(cmul_i(vv[s], kk[s] * g.mk), uy[s]);
     if (kk[s] == 0) {
@@ -324,6 +331,8 @@ __device__ __forceinline__ void load_eta_zeta(double2 (&v)[8], int t, const Geom
     const double2 z = make_double2(aa.x - bb.y, aa.y + bb.x);
     v[s] = kk[s] < g.kc ? z : zero2();
   }
+  if constexpr (CH < 8) __builtin_amdgcn_sched_barrier(0);
+  }
 }
 
 // After a forward FFT of z = a + i b (Z[t + s*NT] in v), hand Â[k], B̂[k] for
@@ -332,6 +341,7 @@ __device__ __forceinline__ void load_eta_zeta(double2 (&v)[8], int t, const Geom
 template <int LOG2N, typename Emit>
 __device__ __forceinline__ void split_pair(const double2 (&v)[8], int t, const Geom& g,
                                            double2* line, Emit emit) {
+  SW_OPAQUE_T(t);
   constexpr int N = 1 << LOG2N, NT = N / 8;
   lds_barrier();  // previous LDS readers are done
 #pragma unroll
@@ -355,6 +365,7 @@ __device__ __forceinline__ void split_pair(const double2 (&v)[8], int t, const G
 template <int LOG2N, int C, typename Emit>
 __device__ __forceinline__ void split_pairs(const double2 (&v)[C][8], int t, const Geom& g,
                                             double2* line, int stride, Emit emit) {
+  SW_OPAQUE_T(t);
   constexpr int N = 1 << LOG2N, NT = N / 8;
   lds_barrier();
 #pragma unroll
