@@ -301,14 +301,10 @@ __device__ __forceinline__ void load_eta_zeta(double2 (&v)[8], int t, const Geom
                                               const double2* __restrict__ Uy, int y) {
   SW_OPAQUE_T(t);
   constexpr int N = 1 << LOG2N, NT = N / 8, half = N / 2;
-  // 8192-point lines (128 VGPRs, the first pair live): four points at a time
-  constexpr int CH = LOG2N >= 13 ? 4 : 8;
-#pragma unroll
-  for (int s0 = 0; s0 < 8; s0 += CH) {
   double2 h[8], vv[8], uy[8];
   int kk[8];
 #pragma unroll
-  for (int s = s0; s < s0 + CH; ++s) {
+  for (int s = 0; s < 8; ++s) {
     const int m = t + s * NT;
     kk[s] = m <= half ? m : N - m;
     const int o = midx_i(g, kk[s] < g.kc ? kk[s] : 0, y);
@@ -317,7 +313,7 @@ __device__ __forceinline__ void load_eta_zeta(double2 (&v)[8], int t, const Geom
     uy[s] = Uy[o];
   }
 #pragma unroll
-  for (int s = s0; s < s0 + CH; ++s) {
+  for (int s = 0; s < 8; ++s) {
     const int m = t + s * NT;
     double2 aa = h[s], bb = csub(cmul_i(vv[s], kk[s] * g.mk), uy[s]);
     if (kk[s] == 0) {
@@ -330,8 +326,6 @@ __device__ __forceinline__ void load_eta_zeta(double2 (&v)[8], int t, const Geom
     }
     const double2 z = make_double2(aa.x - bb.y, aa.y + bb.x);
     v[s] = kk[s] < g.kc ? z : zero2();
-  }
-  if constexpr (CH < 8) __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -468,11 +462,12 @@ __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS), (BlkRow<MODEL
       fft_pair<LOG2N, +1, CB>(w, c.t, tws, line, LS);
     } else {
       // nx = 8192 (128 VGPRs per thread): one pair at a time, the second
-      // pair's loads issued after the first transform
-      load_pair<LOG2N>(w[0], c.t, g, U, V, y, false);
-      fft_line<LOG2N, +1>(w[0], c.t, tws, line);
+      // pair's loads issued after the first transform; η + iζ (three loads)
+      // first, while nothing else is live
       load_eta_zeta<LOG2N>(w[1], c.t, g, H, V, Uy, y);
       fft_line<LOG2N, +1>(w[1], c.t, tws, line);
+      load_pair<LOG2N>(w[0], c.t, g, U, V, y, false);
+      fft_line<LOG2N, +1>(w[0], c.t, tws, line);
     }
     double pc[8];
 #pragma unroll
