@@ -67,3 +67,22 @@ def test_gfx950_code_object(lib_path):
     """The fat binary carries a gfx950 code object (hipcc --offload-arch=gfx950)."""
     data = open(lib_path, "rb").read()
     assert b"gfx950" in data
+
+
+def test_integration_bindings_track_the_header():
+    """INTEGRATION.md's Julia SWConfig and the ctypes mirror carry the header's
+    ABI version and the header's config fields, in order."""
+    from juliaraytracingsw_amd import _lib
+
+    hdr = open(HEADER).read()
+    abi = int(re.search(r"#define SW_ABI_VERSION (\d+)", hdr).group(1))
+    assert _lib.SW_ABI_VERSION == abi
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    assert int(re.search(r"abi_version::Int32 = (\d+)", doc).group(1)) == abi
+    body = re.search(r"typedef struct sw_config \{(.*?)\} sw_config;", hdr, flags=re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    hfields = re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*(?:\[\d+\])?\s*[;,]", body)
+    julia = re.search(r"Base\.@kwdef mutable struct SWConfig(.*?)\nend", doc, flags=re.S).group(1)
+    jfields = re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)::", julia)
+    assert jfields == hfields
+    assert [f[0] for f in _lib.SwConfig._fields_] == hfields
