@@ -5,6 +5,11 @@ baseline (the oracle restatement, scipy.fft on the host cores).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--mode ensemble|slab]
 
+Defaults: 200 untimed + 2000 timed steps (state resident in HBM).  Also
+reported, never in `value`: `host_boundary` (one state download/upload
+through the C ABI, over PCIe, and the rate with the driver's per-frame
+download).
+
 N > 1 is launched by torch.distributed.run, one process per GPU.
   --mode ensemble (default): every rank steps its own independent 2048²
       problem (an ensemble of seeded runs, the reference's job-array usage);
