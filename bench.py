@@ -3,26 +3,33 @@
 metric) on N MI355X, plus the roofline of the dominant kernel and the CPU
 baseline (the oracle restatement, scipy.fft on the host cores).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode ensemble|slab]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode slab|ensemble]
 
-Defaults: 200 untimed + 2000 timed steps (state resident in HBM).  Also
-reported, never in `value`: `host_boundary` (one state download/upload
-through the C ABI, over PCIe, and the rate with the driver's per-frame
-download).
+Defaults: 200 untimed + 2000 timed steps (state resident in HBM).
 
-N > 1 is launched by torch.distributed.run, one process per GPU.
-  --mode ensemble (default): every rank steps its own independent 2048²
-      problem (an ensemble of seeded runs, the reference's job-array usage);
-      no collective on the data path; value = all ranks' steps / max-over-ranks
-      time; scaling "weak".
-  --mode slab: ONE problem slab-decomposed over the N GPUs, transposes as RCCL
-      all-to-alls; value = that problem's steps / time; scaling
-      "strong".  Meant for the large configurations (4096², 8192²): at 2048²
-      the transposes cost more than the step.
+N > 1: one process per GPU.  Started as `python bench.py --gpus N` (no
+WORLD_SIZE in the environment) the script launches `torch.distributed.run
+--nproc-per-node N` on itself as a child process, before any GPU call, and
+exits with its status; the driver's own torch.distributed.run launch lands
+directly in the rank code.
+  --mode slab (default): ONE problem slab-decomposed over the N GPUs, the
+      transposes as RCCL all-to-alls over xGMI; value = that
+      problem's steps / max-over-ranks time; scaling "strong".
+  --mode ensemble: every rank steps its own independent problem (the
+      reference's job-array usage); value = all ranks' steps / time; "weak".
+Extra keys on the same JSON line (never `value`):
+  `ensemble` — the ensemble throughput of the same configuration on the N GPUs;
+  `config5` — BASELINE config 5 (TwoLayerQG 8192² IFMRK4) decomposed over the
+      N GPUs (one GPU at N = 1), steps/s (--no-config5 to skip);
+  `host_boundary` — one state download/upload through the C ABI over PCIe,
+      and the rate with the driver's per-frame download;
+  `cpu_baseline` — rank 0 at N = 1 only.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -30,6 +37,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+SHORT = {'FilteredAB3': 'fab3', 'IFMAB3': 'ifmab3', 'IFMRK4': 'ifmrk4', 'ETDRK4': 'etdrk4',
+         'FilteredRK4': 'frk4'}
+
 
 # SURVEY §8(d) B_alg model (fp64): b_T = 16 Ns + 8 Np per logical 2D transform
 def b_alg(model, stepper, n):
@@ -50,31 +60,88 @@ def b_alg(model, stepper, n):
     return 10 * bT + 10 * 16 * Ns
 
 
-def cpu_baseline(model, stepper, n, budget_s=20.0, max_steps=20):
-    """Time the oracle (fp64 numpy/scipy restatement) on the host cores."""
+def _cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(model, stepper, n, grids=(128, 1024, 2048), budget_s=24.0, samples=5):
+    """The oracle (fp64 numpy/scipy restatement of the reference op sequence)
+    on the host cores: at each grid, 3 untimed start-up steps, then the median
+    of `samples` timed samples of k steps, k sized so the whole baseline is
+    about `budget_s` of CPU work (BASELINE.md §3's protocol, bounded)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import statistics
+
     import sw_cases
     import sw_oracle as O
 
-    cores = min(16, len(os.sched_getaffinity(0)))
+    affinity = len(os.sched_getaffinity(0))
+    # the box's CPU share: the harness sets OMP_NUM_THREADS to it (16 per GPU);
+    # sched_getaffinity shows the whole machine there
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    cores = min(affinity, share) if share > 0 else affinity
     O.set_fft_workers(cores)
-    short = {'FilteredAB3': 'fab3', 'IFMAB3': 'ifmab3', 'IFMRK4': 'ifmrk4', 'ETDRK4': 'etdrk4',
-             'FilteredRK4': 'frk4'}[stepper]
-    p = sw_cases.case_params(f"{model}_{short}", n)
-    pr = sw_cases.oracle_problem(p)
-    pr.set_solution(sw_cases.initial_condition(p, pr.grid))
-    pr.stepforward(3)  # the Euler start-up steps (AB3 steppers), untimed
-    t0 = time.perf_counter()
-    k = 0
-    while k < max_steps and (time.perf_counter() - t0) < budget_s:
-        pr.stepforward(1)
-        k += 1
-    dt = time.perf_counter() - t0
+    grids = sorted(set(grids) | {n})
+    per = budget_s / len(grids)
+    by_grid = {}
+    for g in grids:
+        p = sw_cases.case_params(f"{model}_{SHORT[stepper]}", g)
+        pr = sw_cases.oracle_problem(p)
+        pr.set_solution(sw_cases.initial_condition(p, pr.grid))
+        t0 = time.perf_counter()
+        pr.stepforward(3)  # the Euler start-up steps (AB3 steppers), untimed; also sizes k
+        k = max(1, int(per / samples / max((time.perf_counter() - t0) / 3, 1e-6)))
+        rates = []
+        for _ in range(samples):
+            t0 = time.perf_counter()
+            pr.stepforward(k)
+            rates.append(k / (time.perf_counter() - t0))
+        by_grid[str(g)] = {"steps_per_s": statistics.median(rates), "steps_per_sample": k,
+                           "samples": samples, "min": min(rates), "max": max(rates)}
     O.set_fft_workers(None)
-    return dict(value=k / dt, unit="timesteps/s", cores=cores, kind="port",
-                sample=f"{k} {stepper} steps of the {n}² oracle restatement (numpy elementwise + scipy.fft "
-                       f"workers={cores}) after 3 untimed steps")
+    return dict(value=by_grid[str(n)]["steps_per_s"], unit="timesteps/s", cores=cores, kind="port",
+                nproc=os.cpu_count(), affinity_cores=affinity, cpu_model=_cpu_model(), by_grid=by_grid,
+                sample=f"{stepper} steps of the {model.upper()} oracle restatement (numpy elementwise + "
+                       f"scipy.fft workers={cores}) at {', '.join(f'{g}²' for g in grids)}: 3 untimed steps, "
+                       f"then the median of {samples} samples of k steps per grid (k in by_grid); value = "
+                       f"the {n}² median")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` without a launcher: start torch.distributed.run on
+    this script as a child (no exec, no GPU touched here) and return its code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__),
+           *sys.argv[1:]]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.call(cmd, env=env)
+
+
+def make_problem(model, n, stepper, local, dec):
+    from juliaraytracingsw_amd import drivers
+
+    if model == "rsw":
+        return drivers.rsw_problem(n, stepper, device=local, decomposition=dec)
+    if model == "ty":
+        return drivers.ty_problem(n, device=local, decomposition=dec)
+    if model == "mlqg":
+        return drivers.mlqg_problem(n, device=local, decomposition=dec)
+    return drivers.qg2_problem(n, stepper, device=local, decomposition=dec)
 
 
 def main():
@@ -88,20 +155,36 @@ def main():
                     choices=["FilteredAB3", "IFMAB3", "IFMRK4", "ETDRK4", "FilteredRK4"])
     ap.add_argument("--profile-steps", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", default="ensemble", choices=["ensemble", "slab"])
+    ap.add_argument("--no-config5", action="store_true")
+    ap.add_argument("--config5-steps", type=int, default=20)
+    ap.add_argument("--mode", default="slab", choices=["ensemble", "slab"])
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_rsw2048_fab3.json"))
+    ap.add_argument("--dry-run", action="store_true",
+                    help="print the rank plan (n_gpus, parallelism, scaling) and exit, touching no GPU")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE {world}; n_gpus = {world}", file=sys.stderr)
+    slab = args.mode == "slab" and world > 1
+    parallelism = (f"slab{world}" if slab else f"ensemble{world}") if world > 1 else "single-gpu"
+    if args.dry_run:
+        if rank == 0:
+            print(json.dumps({"n_gpus": world, "parallelism": parallelism,
+                              "scaling": "strong" if slab else "weak", "rank0_of": world}))
+        return
 
     import torch
 
     dist = None
-    # SW_BENCH_BACKEND=gloo: rehearse the N-rank ensemble path with several
-    # ranks sharing the box's GPUs (RCCL refuses two ranks on one GPU); the
-    # driver's multi-GPU runs use the default, RCCL ("nccl"), one GPU per rank
+    # SW_BENCH_BACKEND=gloo: rehearse the N-rank path with several ranks
+    # sharing the box's GPU and the host-staged slab transport (RCCL refuses
+    # two ranks on one GPU); the driver's multi-GPU runs use the default,
+    # RCCL ("nccl"), one GPU per rank
     backend = os.environ.get("SW_BENCH_BACKEND", "nccl")
     if backend == "gloo":
         local = local % max(1, torch.cuda.device_count())
@@ -120,33 +203,39 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    from juliaraytracingsw_amd import drivers, slab_comm
+    def max_over_ranks(x):
+        if dist is None:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device="cpu" if backend == "gloo" else "cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
 
-    slab = args.mode == "slab" and world > 1
-    dec = slab_comm.rccl_decomposition(rank, world) if slab else None
+    from juliaraytracingsw_amd import slab_comm
+
+    def decomposition():
+        if world == 1:
+            return None
+        if backend == "gloo":
+            return slab_comm.host_decomposition(rank, world)
+        return slab_comm.rccl_decomposition(rank, world)
+
+    def timed(prob, warmup, steps):
+        prob.stepforward(warmup)
+        barrier_sync()
+        t0 = time.perf_counter()
+        prob.stepforward(steps)  # sw_step returns when its stream is drained
+        barrier_sync()
+        return max_over_ranks(time.perf_counter() - t0)
+
     if args.model == "ty":
         args.stepper = "ETDRK4"  # the only Thomas-Yamada stepper
     if args.model == "mlqg":
         args.stepper = "FilteredRK4"  # TwoLayerSimulation's stepper
-    if args.model == "rsw":
-        prob, P = drivers.rsw_problem(args.n, args.stepper, device=local, decomposition=dec)
-    elif args.model == "ty":
-        prob, P = drivers.ty_problem(args.n, device=local, decomposition=dec)
-    elif args.model == "mlqg":
-        prob, P = drivers.mlqg_problem(args.n, device=local, decomposition=dec)
-    else:
-        prob, P = drivers.qg2_problem(args.n, args.stepper, device=local, decomposition=dec)
 
-    prob.stepforward(args.warmup)
-    barrier_sync()
-    t0 = time.perf_counter()
-    prob.stepforward(args.steps)  # sw_step returns when its stream is drained
-    barrier_sync()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if backend == "gloo" else "cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    # headline: the configured problem, slab-decomposed over the N GPUs
+    # (or one independent problem per GPU with --mode ensemble)
+    prob, P = make_problem(args.model, args.n, args.stepper, local, decomposition() if slab else None)
+    elapsed = timed(prob, args.warmup, args.steps)
 
     # roofline: per-kernel HIP-event durations on libsw's stream
     stats = prob.ctx.profile(args.profile_steps)
@@ -163,18 +252,48 @@ def main():
         prob.ctx.set_state(st)
         tu.append(time.perf_counter() - t0)
     prob.close()
+    del prob
+
+    # extra: the ensemble throughput of the same configuration (N > 1)
+    ensemble = None
+    if slab:
+        e, _ = make_problem(args.model, args.n, args.stepper, local, None)
+        k = max(1, args.steps // 4)
+        te = timed(e, min(args.warmup, 50), k)
+        ensemble = {"value": world * k / te, "unit": "timesteps/s", "steps_per_rank": k,
+                    "scaling": "weak", "workload": f"{world} independent {args.model.upper()} {args.n}^2 "
+                                                  f"{args.stepper} problems, one per GPU"}
+        e.close()
+        del e
+
+    # extra: BASELINE config 5, TwoLayerQG 8192² IFMRK4 over the N GPUs
+    config5 = None
+    if not args.no_config5 and (args.model, args.n, args.stepper) == ("rsw", 2048, "FilteredAB3"):
+        c5, _ = make_problem("qg2", 8192, "IFMRK4", local, decomposition())
+        t5 = timed(c5, 3, args.config5_steps)
+        s5 = c5.ctx.profile(3)
+        c5.close()
+        del c5
+        config5 = {"value": args.config5_steps / t5, "unit": "timesteps/s", "n_gpus": world,
+                   "steps": args.config5_steps, "ms_per_step": t5 / args.config5_steps * 1e3,
+                   "scaling": "strong" if world > 1 else None,
+                   "workload": "TwoLayerQG 8192^2 IFMRK4 fp64 (BASELINE config 5), "
+                               + (f"slab{world}" if world > 1 else "single-gpu"),
+                   "kernels": [{"name": s["name"], "avg_us": s["avg_ms"] * 1e3, "per_step": s["launches"] / 3}
+                               for s in s5]}
 
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
         return
 
-    dom = max(stats, key=lambda s: s["avg_ms"] * s["launches"])
+    kern = [s for s in stats if s["name"] != "transpose"]
+    dom = max(kern, key=lambda s: s["avg_ms"] * s["launches"])
     achieved = dom["alg_bytes"] / (dom["avg_ms"] * 1e-3) / 1e9
     traffic = None
     try:
         tj = json.load(open(args.traffic_json))
-        if tj.get("config") == f"{args.model}{args.n}_{args.stepper}":
+        if tj.get("config") == f"{args.model}{args.n}_{args.stepper}" and world == 1:
             traffic = tj["kernels"].get(dom["name"])
     except Exception:
         traffic = None
@@ -196,6 +315,7 @@ def main():
             metric = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
         except Exception:
             pass
+    per_gpu_rate = value / world if slab else args.steps / elapsed
     out = {
         "metric": metric,
         "value": value,
@@ -214,16 +334,22 @@ def main():
                  "mlqg": "synthetic filtered randn PV IC (TwoLayerSimulation, seeded)"}[args.model],
         "config": {"workload": f"{args.model.upper()} {args.n}^2 {args.stepper} fp64 step, dt={P['dt']:.6g}",
                    "grid": args.n,
-                   "parallelism": (f"slab{world}" if slab else f"ensemble{world}") if world > 1 else "single-gpu"},
-        "b_alg_bytes_per_step": balg,
-        "b_alg_GBps": balg * value / world / 1e9,  # per GPU
-        "b_alg_frac_of_peak": balg * value / world / 1e9 / HBM_PEAK_GBPS,
+                   "parallelism": parallelism},
+        # bytes the libsw kernels move per step (live modes only, physical
+        # space never in HBM) and the resulting HBM rate per GPU
         "libsw_alg_bytes_per_step": step_alg,
+        "libsw_alg_GBps_per_gpu": step_alg * per_gpu_rate / 1e9,
+        # SURVEY §8(d)'s byte model of a full-array FFT implementation (13
+        # full transforms + 18 state passes per RSW step): bytes libsw does
+        # NOT move; the rate is an equivalence, not a measured bandwidth
+        "reference_byte_model": {"bytes_per_step": balg, "equivalent_GBps_per_gpu": balg * per_gpu_rate / 1e9},
         "roofline": {"bound": "hbm", "kernel": dom["name"], "achieved": achieved, "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                      "alg_bytes_per_launch": dom["alg_bytes"], "avg_us_per_launch": dom["avg_ms"] * 1e3},
         "kernels": [{"name": s["name"], "avg_us": s["avg_ms"] * 1e3, "per_step": s["launches"] / args.profile_steps,
                      "alg_bytes": s["alg_bytes"]} for s in stats],
+        "ensemble": ensemble,
+        "config5": config5,
         "cpu_baseline": cpu,
         # RSWDriver saves a frame every output_freq = floor(output_dt/dt) steps
         # (rsw/RSWDriver.jl:152, output_dt = 0.025/f): 81 steps at 2048²

@@ -14,6 +14,8 @@
  *
  * Conventions
  *  - Plain pointers and sizes only; no exceptions cross the ABI.
+ *  - Host buffers hold fp64 (or, with sw_config.precision = SW_PREC_F32,
+ *    fp32) elements; sizes below are for fp64 and halve for fp32.
  *  - Return codes: 0 = ok, < 0 = error (see SW_E_*); sw_last_error() has text.
  *  - Spectral state layout = Julia column-major (nkr, nl, nfield) of interleaved
  *    complex (re, im) doubles: element (kr, l, f) at ((f*nl + l)*nkr + kr).
@@ -32,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SW_ABI_VERSION 5
+#define SW_ABI_VERSION 6
 
 /* models */
 #define SW_MODEL_RSW 0   /* rsw/RotatingShallowWater.jl: fields (u, v, η), 3×3 L   */
@@ -49,6 +51,15 @@ extern "C" {
 #define SW_STEP_IFMRK4       2 /* Lawson IF-RK4, the build's definition of utils/IFMRK4.jl (A9) */
 #define SW_STEP_ETDRK4       3 /* FF ETDRK4TimeStepper (ThomasYamada.Problem default, :60) */
 #define SW_STEP_FILTERED_RK4 4 /* FF FilteredRK4 (simulation/Parameters.jl:25), RSW/QG2/MLQG */
+
+/* caller-buffer precision (sw_config.precision): the element type of every
+ * host buffer crossing the ABI (state, calcN, history, physical fields).  The
+ * reference's production drivers run T = Float32 (rsw/RSWDriver.jl:164,
+ * swqg/TwoLayerDriver.jl:63): with SW_PREC_F32 their ComplexF32 `prob.sol` and
+ * Float32 `vars` arrays are exchanged as they are; libsw computes in fp64
+ * either way and rounds once on the way out. */
+#define SW_PREC_F64 0    /* ComplexF64 / Float64 buffers (16 / 8 bytes)       */
+#define SW_PREC_F32 1    /* ComplexF32 / Float32 buffers (8 / 4 bytes)        */
 
 /* error codes */
 #define SW_OK            0
@@ -148,6 +159,8 @@ typedef struct sw_config {
    * imposed zonal flows U per layer                                        */
   double  f0, beta;
   double  H[2], b[2], Ulayer[2];
+  /* caller-buffer element type (SW_PREC_*), the reference's `T`            */
+  int32_t precision;
 } sw_config;
 
 typedef struct sw_ctx sw_ctx;
@@ -178,6 +191,20 @@ int sw_set_state(sw_ctx* ctx, const void* sol, size_t bytes);
 /* Array(prob.sol): the (dealiased) state, aliased modes = 0. */
 int sw_get_state(const sw_ctx* ctx, void* sol, size_t bytes);
 
+/* The stepper's memory across steps, for checkpoint/restart with bitwise
+ * continuation (the reference keeps it in the TimeStepper: FF FilteredAB3's
+ * RHS₋₁/RHS₋₂, utils/IFMAB3.jl:15-18 N₋₁/N₋₂, rotated at :165-166).
+ * sw_history_slots: 2 for FilteredAB3 / IFMAB3 (slot 1 = the previous step's
+ * RHS/N, slot 2 = the one before), 0 for the RK4/ETDRK4 steppers (no memory).
+ * Layout as the state.  sw_reset_history: the next three steps start the AB3
+ * steppers with forward Euler, as at clock.step < 3 (a restart from a state
+ * without saved history, which is what the reference's
+ * load_from_snapshot! restart amounts to, rsw/RSWDriver.jl:10-36). */
+int sw_history_slots(const sw_ctx* ctx, int32_t* nslots);
+int sw_get_history(const sw_ctx* ctx, int32_t slot, void* buf, size_t bytes);
+int sw_set_history(sw_ctx* ctx, int32_t slot, const void* buf, size_t bytes);
+int sw_reset_history(sw_ctx* ctx);
+
 int sw_set_clock(sw_ctx* ctx, double t, int64_t step);
 int sw_get_clock(const sw_ctx* ctx, double* t, int64_t* step);
 
@@ -189,7 +216,7 @@ int sw_step(sw_ctx* ctx, int64_t nsteps);
 int sw_calcN(sw_ctx* ctx, const void* sol, void* N, size_t bytes);
 
 /* updatevars! equivalent: one physical field of the current state. */
-int sw_get_physical(sw_ctx* ctx, int32_t field_id, double* out, size_t bytes);
+int sw_get_physical(sw_ctx* ctx, int32_t field_id, void* out, size_t bytes);
 
 /* Scalar diagnostics of the current state (SW_DIAG_*). */
 int sw_diag(sw_ctx* ctx, int32_t diag_id, double* out);
@@ -230,6 +257,12 @@ double sw_step_alg_bytes(const sw_ctx* ctx);
 /* Multi-GPU: write an RCCL unique id (128 bytes); rank 0 calls it and
  * broadcasts the bytes to every rank before sw_create. */
 int sw_comm_unique_id(void* out128);
+
+/* Slab geometry of `slab` for cfg (nx, ny, aliased_fraction, nranks), no GPU
+ * needed: out[0..7] = kc (live kr columns), kcl (columns per
+ * slab), kr0 (first column of the slab), kcn (live columns held), nyl (rows
+ * per slab), y0 (first row), Lr (live l rows), LrP (padded column length). */
+int sw_slab_geometry(const sw_config* cfg, int32_t slab, int32_t out[8]);
 
 #ifdef __cplusplus
 }

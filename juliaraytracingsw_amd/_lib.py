@@ -10,13 +10,14 @@ import os
 
 import numpy as np
 
-SW_ABI_VERSION = 5
+SW_ABI_VERSION = 6
 SW_MODEL_RSW, SW_MODEL_QG2, SW_MODEL_TY, SW_MODEL_MLQG = 0, 1, 2, 3
 SW_STEP_FILTERED_AB3, SW_STEP_IFMAB3, SW_STEP_IFMRK4, SW_STEP_ETDRK4, SW_STEP_FILTERED_RK4 = 0, 1, 2, 3, 4
 SW_OK, SW_E_INVALID, SW_E_NOMEM, SW_E_HIP, SW_E_COMM, SW_E_NAN, SW_E_STATE = 0, -1, -2, -3, -4, -5, -6
 SW_PHYS_U, SW_PHYS_V, SW_PHYS_ETA, SW_PHYS_ZETA, SW_PHYS_Q, SW_PHYS_PSI = 0, 1, 2, 3, 4, 5
 SW_DIAG_NAN, SW_DIAG_KE, SW_DIAG_PE, SW_DIAG_CFL, SW_DIAG_KE2, SW_DIAG_KE1, SW_DIAG_BT = 0, 1, 2, 3, 4, 5, 6
 SW_DIAG_WAVE_KE, SW_DIAG_WAVE_PE, SW_DIAG_GEO_KE, SW_DIAG_GEO_PE = 7, 8, 9, 10
+SW_PREC_F64, SW_PREC_F32 = 0, 1
 
 STEPPERS = {"FilteredAB3": SW_STEP_FILTERED_AB3, "IFMAB3": SW_STEP_IFMAB3, "IFMRK4": SW_STEP_IFMRK4,
             "ETDRK4": SW_STEP_ETDRK4, "FilteredRK4": SW_STEP_FILTERED_RK4}
@@ -27,6 +28,7 @@ EXPORTS = [
     "sw_set_state", "sw_get_state", "sw_set_clock", "sw_get_clock", "sw_step", "sw_calcN",
     "sw_get_physical", "sw_diag", "sw_set_energy_diagnostics", "sw_get_energy_diagnostics",
     "sw_profile_steps", "sw_step_alg_bytes", "sw_comm_unique_id",
+    "sw_history_slots", "sw_get_history", "sw_set_history", "sw_reset_history", "sw_slab_geometry",
 ]
 
 
@@ -58,6 +60,7 @@ class SwConfig(C.Structure):
         ("Ro", C.c_double),
         ("f0", C.c_double), ("beta", C.c_double),
         ("H", C.c_double * 2), ("b", C.c_double * 2), ("Ulayer", C.c_double * 2),
+        ("precision", C.c_int32),
     ]
 
 
@@ -107,6 +110,11 @@ def load(path: str | None = None):
         "sw_profile_steps": (C.c_int, [vp, i64, C.POINTER(SwKernelStat), i32, C.POINTER(i32)]),
         "sw_step_alg_bytes": (dbl, [vp]),
         "sw_comm_unique_id": (C.c_int, [vp]),
+        "sw_history_slots": (C.c_int, [vp, C.POINTER(i32)]),
+        "sw_get_history": (C.c_int, [vp, i32, vp, sz]),
+        "sw_set_history": (C.c_int, [vp, i32, vp, sz]),
+        "sw_reset_history": (C.c_int, [vp]),
+        "sw_slab_geometry": (C.c_int, [C.POINTER(SwConfig), i32, C.POINTER(i32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -121,6 +129,15 @@ def default_config() -> SwConfig:
     cfg = SwConfig()
     lib.sw_config_default(C.byref(cfg))
     return cfg
+
+
+def slab_geometry(cfg: SwConfig, slab: int) -> dict:
+    """sw_slab_geometry: the library's own slab layout (no GPU needed)."""
+    out = (C.c_int32 * 8)()
+    rc = load().sw_slab_geometry(C.byref(cfg), int(slab), out)
+    if rc != SW_OK:
+        raise LibSWError(f"sw_slab_geometry failed (code {rc})", rc)
+    return dict(zip(("kc", "kcl", "kr0", "kcn", "nyl", "y0", "Lr", "LrP"), list(out)))
 
 
 def comm_unique_id() -> bytes:
@@ -148,6 +165,10 @@ class Context:
         nkr, nl, nf = C.c_int32(), C.c_int32(), C.c_int32()
         self._check(self.lib.sw_get_dims(self._h, C.byref(nkr), C.byref(nl), C.byref(nf)), "sw_get_dims")
         self.nkr, self.nl, self.nf = nkr.value, nl.value, nf.value
+        # caller-buffer element types (sw_config.precision, the reference's T)
+        f32 = cfg.precision == SW_PREC_F32
+        self.cdtype = np.dtype(np.complex64 if f32 else np.complex128)
+        self.rdtype = np.dtype(np.float32 if f32 else np.float64)
 
     def _check(self, rc, what):
         if rc != SW_OK:
@@ -164,32 +185,57 @@ class Context:
         except Exception:
             pass
 
-    # -- state: numpy [nf][nl][nkr] complex128 == Julia (nkr, nl, nf) -------
+    # -- state: numpy [nf][nl][nkr] complex == Julia (nkr, nl, nf) ----------
     @property
     def state_shape(self):
         return (self.nf, self.nl, self.nkr)
 
-    def set_state(self, sol):
-        a = np.ascontiguousarray(sol, dtype=np.complex128)
+    def _state_in(self, sol, what):
+        a = np.ascontiguousarray(sol, dtype=self.cdtype)
         if a.shape != self.state_shape:
-            raise ValueError(f"state shape {a.shape} != {self.state_shape}")
+            raise ValueError(f"{what}: shape {a.shape} != {self.state_shape}")
+        return a
+
+    def _state_out(self, out, what):
+        if out is None:
+            return np.empty(self.state_shape, self.cdtype)
+        if out.shape != self.state_shape or out.dtype != self.cdtype or not out.flags.c_contiguous:
+            raise ValueError(f"{what}: out must be C-contiguous {self.cdtype} of the state shape")
+        return out
+
+    def set_state(self, sol):
+        a = self._state_in(sol, "set_state")
         self._check(self.lib.sw_set_state(self._h, a.ctypes.data, a.nbytes), "sw_set_state")
 
     def get_state(self, out=None):
-        """The state as Julia's (nkr, nl, nf) array; ``out`` (C-contiguous
-        complex128 of that shape) is filled in place, as FF's ``prob.sol``."""
-        if out is None:
-            a = np.empty(self.state_shape, np.complex128)
-        else:
-            a = out
-            if a.shape != self.state_shape or a.dtype != np.complex128 or not a.flags.c_contiguous:
-                raise ValueError("get_state: out must be C-contiguous complex128 of the state shape")
+        """The state as Julia's (nkr, nl, nf) array; ``out`` (C-contiguous, of
+        the caller precision and that shape) is filled in place, as FF's
+        ``prob.sol``."""
+        a = self._state_out(out, "get_state")
         self._check(self.lib.sw_get_state(self._h, a.ctypes.data, a.nbytes), "sw_get_state")
         return a
 
+    def history_slots(self):
+        n = C.c_int32()
+        self._check(self.lib.sw_history_slots(self._h, C.byref(n)), "sw_history_slots")
+        return n.value
+
+    def get_history(self, slot, out=None):
+        """RHS/N of ``slot`` (1 or 2) steps ago, state layout (sw_get_history)."""
+        a = self._state_out(out, "get_history")
+        self._check(self.lib.sw_get_history(self._h, int(slot), a.ctypes.data, a.nbytes), "sw_get_history")
+        return a
+
+    def set_history(self, slot, value):
+        a = self._state_in(value, "set_history")
+        self._check(self.lib.sw_set_history(self._h, int(slot), a.ctypes.data, a.nbytes), "sw_set_history")
+
+    def reset_history(self):
+        self._check(self.lib.sw_reset_history(self._h), "sw_reset_history")
+
     def calcN(self, sol):
-        a = np.ascontiguousarray(sol, dtype=np.complex128)
-        out = np.empty(self.state_shape, np.complex128)
+        a = self._state_in(sol, "calcN")
+        out = np.empty(self.state_shape, self.cdtype)
         self._check(self.lib.sw_calcN(self._h, a.ctypes.data, out.ctypes.data, a.nbytes), "sw_calcN")
         return out
 
@@ -205,7 +251,7 @@ class Context:
         self._check(self.lib.sw_step(self._h, int(n)), "sw_step")
 
     def physical(self, field_id, ny, nx):
-        out = np.empty((ny, nx), np.float64)
+        out = np.empty((ny, nx), self.rdtype)
         self._check(self.lib.sw_get_physical(self._h, int(field_id), out.ctypes.data, out.nbytes),
                     "sw_get_physical")
         return out

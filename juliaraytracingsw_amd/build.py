@@ -1,10 +1,17 @@
 """Build libsw.so in-tree with hipcc for gfx950 (no JIT cache, so the .so
-travels to the GPU box with the repository snapshot)."""
+travels to the GPU box with the repository snapshot).
+
+The kernel file is compiled as one translation unit per transform length
+(``-DSW_PART=L``, L = log2 N = 5 … 13) plus the length-independent part
+(``SW_PART=0``: element-wise kernels and the dispatch), in parallel, then
+linked with the host-side API (``sw_api.cpp``)."""
 from __future__ import annotations
 
 import os
 import shutil
 import subprocess
+import tempfile
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
@@ -12,6 +19,7 @@ CSRC = os.path.join(HERE, "csrc")
 SOURCES = ["sw_kernels.hip", "sw_api.cpp"]
 HEADERS = ["sw_fft.hpp", "sw_internal.hpp"]
 OUT = os.path.join(HERE, "libsw.so")
+PARTS = [0, 13, 12, 11, 10, 9, 8, 7, 6, 5]  # longest first (compile time)
 
 
 def hipcc_path():
@@ -29,18 +37,36 @@ def needs_build(out=OUT):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_lib(verbose=False, force=False, out=OUT, extra_flags=()):
-    if not force and not needs_build(out):
-        return out
-    cmd = [hipcc_path(), "-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC", "-shared",
-           "-Wno-unused-result", f"-I{os.path.join(ROOT, 'include')}", "-o", out + ".tmp",
-           *extra_flags, *[os.path.join(CSRC, s) for s in SOURCES],
-           "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
-    if verbose:
-        print(" ".join(cmd))
+def _run(cmd):
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
-        raise RuntimeError(f"hipcc failed ({r.returncode}):\n{r.stderr[-4000:]}")
+        raise RuntimeError(f"hipcc failed ({r.returncode}): {' '.join(cmd)}\n{r.stderr[-4000:]}")
+
+
+def build_lib(verbose=False, force=False, out=OUT, extra_flags=(), jobs=None):
+    if not force and not needs_build(out):
+        return out
+    hipcc = hipcc_path()
+    common = [hipcc, "-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC", "-Wno-unused-result",
+              f"-I{os.path.join(ROOT, 'include')}", *extra_flags]
+    jobs = jobs or min(len(PARTS) + 1, max(1, len(os.sched_getaffinity(0))))
+    with tempfile.TemporaryDirectory(prefix="libsw_build_") as tmp:
+        cmds = []
+        for part in PARTS:
+            cmds.append(common + ["-c", f"-DSW_PART={part}", os.path.join(CSRC, "sw_kernels.hip"),
+                                  "-o", os.path.join(tmp, f"k{part}.o")])
+        cmds.append(common + ["-c", os.path.join(CSRC, "sw_api.cpp"), "-o", os.path.join(tmp, "api.o")])
+        if verbose:
+            for c in cmds:
+                print(" ".join(c))
+        with ThreadPoolExecutor(jobs) as ex:
+            list(ex.map(_run, cmds))
+        objs = [os.path.join(tmp, f"k{p}.o") for p in PARTS] + [os.path.join(tmp, "api.o")]
+        link = [hipcc, "--offload-arch=gfx950", "-fPIC", "-shared", "-o", out + ".tmp", *objs,
+                "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
+        if verbose:
+            print(" ".join(link))
+        _run(link)
     os.replace(out + ".tmp", out)
     return out
 

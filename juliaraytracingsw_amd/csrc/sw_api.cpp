@@ -42,6 +42,7 @@ struct Slab {
   double2* mir = nullptr;                    // calcN inputs, row phase (row in)
   double2* mfr = nullptr;                    // row outputs, row phase
   double2* mfc = nullptr;                    // row outputs, column phase (col_fwd / col_step in)
+  double2* view = nullptr;                   // scratch pointer for collect_full (history slots)
 };
 
 struct sw_ctx {
@@ -68,6 +69,7 @@ struct sw_ctx {
   bool mixed_valid = false;                  // mir == transposed col_inv(sol) (fused pipeline primed)
   bool fuse_all = false;                     // SW_FUSE_ALL=1: fused pass for every pair (experiments)
   double2* stage = nullptr;                  // full (nkr,nl,nf) staging
+  float* stage32 = nullptr;                  // SW_PREC_F32: the caller-precision copy of stage / dflt
   double2* gbuf = nullptr;                   // dist: all-gathered compact slabs
   double* dflt = nullptr;                    // physical staging / reductions
   double* ecols = nullptr;                   // per-column energy sums [global column][SW_NSUM]
@@ -80,8 +82,11 @@ struct sw_ctx {
                                              // process) [rec][kcl][SW_NSUM] column sums
   std::vector<int64_t> diag_steps;
   std::vector<double> diag_t;
+  std::vector<double> esums_host;            // energy sums of the records gathered so far
+  int64_t esums_n = 0;                       // records gathered (sw_get_energy_diagnostics)
   double t = 0.0;
   int64_t step = 0;
+  int64_t euler_until = 0;                   // sw_reset_history: Euler start-up while step < this
   std::string err;
   // profiling
   bool prof = false;
@@ -463,7 +468,7 @@ sw::StepPtrs step_ptrs(const sw_ctx* c, const Slab& s) {
   a.sol = s.sol;
   a.sol_out = (st == SW_STEP_FILTERED_AB3) ? s.sol2 : s.sol;
   a.xs = s.xs;
-  a.euler = c->step < 3 ? 1 : 0;
+  a.euler = (c->step < 3 || c->step < c->euler_until) ? 1 : 0;
   if (st == SW_STEP_IFMRK4 || st == SW_STEP_FILTERED_RK4) {
     a.h0 = s.acc;
   } else if (st == SW_STEP_ETDRK4) {
@@ -603,6 +608,38 @@ size_t full_bytes(const sw_ctx* c) {
   return (size_t)c->nf * g.nkr * g.nl * sizeof(double2);
 }
 
+// caller buffers hold fp64 or (SW_PREC_F32) fp32 elements: the caller's size
+// of a buffer whose fp64 size is f64_bytes
+size_t caller_bytes(const sw_ctx* c, size_t f64_bytes) {
+  return c->cfg.precision == SW_PREC_F32 ? f64_bytes / 2 : f64_bytes;
+}
+
+// host buffer in the caller's precision -> fp64 device array (f64_bytes)
+int upload(sw_ctx* c, const void* host, void* dst, size_t f64_bytes) {
+  if (c->cfg.precision != SW_PREC_F32) {
+    HIPCHK(c, hipMemcpyAsync(dst, host, f64_bytes, hipMemcpyHostToDevice, c->stream));
+    return 0;
+  }
+  const long long n = (long long)(f64_bytes / sizeof(double));
+  HIPCHK(c, hipMemcpyAsync(c->stage32, host, n * sizeof(float), hipMemcpyHostToDevice, c->stream));
+  sw::launch_widen(c->stage32, static_cast<double*>(dst), n, c->stream);
+  HIPCHK(c, hipGetLastError());
+  return 0;
+}
+
+// fp64 device array (f64_bytes) -> host buffer in the caller's precision
+int download(sw_ctx* c, const void* src, void* host, size_t f64_bytes) {
+  if (c->cfg.precision != SW_PREC_F32) {
+    HIPCHK(c, hipMemcpyAsync(host, src, f64_bytes, hipMemcpyDeviceToHost, c->stream));
+    return 0;
+  }
+  const long long n = (long long)(f64_bytes / sizeof(double));
+  sw::launch_narrow(static_cast<const double*>(src), c->stage32, n, c->stream);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(host, c->stage32, n * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+  return 0;
+}
+
 // columns of the full (nkr, nl) array written by slab q's scatter
 void scatter_cols(const Geom& g, int& lo, int& hi) {
   lo = std::min(g.kr0, g.nkr);
@@ -738,6 +775,8 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   if (k.aliased_fraction == 0 && k.model == SW_MODEL_RSW)
     return fail(c, SW_E_INVALID, "RSW needs aliased_fraction > 0 (its calcN uses the dealiased vorticity form)");
   if (k.filter_order < 0) return fail(c, SW_E_INVALID, "filter_order must be >= 0");
+  if (k.precision != SW_PREC_F64 && k.precision != SW_PREC_F32)
+    return fail(c, SW_E_INVALID, "precision must be SW_PREC_F64 or SW_PREC_F32");
   const int P = k.nranks;
   if (!pow2(P) || k.ny / P < 32)
     return fail(c, SW_E_INVALID, "nranks must be a power of two with ny / nranks >= 32");
@@ -854,6 +893,8 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   }
   const Geom& g = c->sl[0].g;
   if ((rc = alloc(c, (void**)&c->stage, full_bytes(c)))) return rc;
+  if (k.precision == SW_PREC_F32)  // >= one physical field in fp32 too
+    if ((rc = alloc(c, (void**)&c->stage32, full_bytes(c) / 2))) return rc;
   if ((rc = alloc(c, (void**)&c->dflt, (size_t)g.nx * g.ny * sizeof(double)))) return rc;
   if ((rc = alloc(c, (void**)&c->flag, 1024 * sizeof(int)))) return rc;
   if ((rc = alloc(c, (void**)&c->ecols, SW_NSUM * (size_t)P * g.kcl * sizeof(double)))) return rc;
@@ -889,7 +930,7 @@ void sw_destroy(sw_ctx* c) {
   if (!c) return;
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (Slab& s : c->sl) free_slab(s);
-  void* ptrs[] = {c->tw_x, c->tw_y, c->stage, c->gbuf, c->dflt, c->flag, c->ecols, c->esum, c->erec};
+  void* ptrs[] = {c->tw_x, c->tw_y, c->stage, c->stage32, c->gbuf, c->dflt, c->flag, c->ecols, c->esum, c->erec};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   if (c->nccl) (void)ncclCommDestroy(c->nccl);
@@ -920,9 +961,9 @@ int sw_get_dims(const sw_ctx* c, int32_t* nkr, int32_t* nl, int32_t* nf) {
 
 int sw_set_state(sw_ctx* c, const void* sol, size_t bytes) {
   if (!ready(c)) return SW_E_STATE;
-  if (!sol || bytes != full_bytes(c)) return fail(c, SW_E_INVALID, "sw_set_state: size mismatch");
+  if (!sol || bytes != caller_bytes(c, full_bytes(c))) return fail(c, SW_E_INVALID, "sw_set_state: size mismatch");
   HIPCHK(c, hipSetDevice(c->cfg.device));
-  HIPCHK(c, hipMemcpyAsync(c->stage, sol, bytes, hipMemcpyHostToDevice, c->stream));
+  if (int rc = upload(c, sol, c->stage, full_bytes(c))) return rc;
   for (Slab& s : c->sl) sw::launch_gather(c->nf, s.g, c->stage, s.sol, c->stream);
   c->mixed_valid = false;
   HIPCHK(c, hipGetLastError());
@@ -933,10 +974,10 @@ int sw_set_state(sw_ctx* c, const void* sol, size_t bytes) {
 int sw_get_state(const sw_ctx* cc, void* sol, size_t bytes) {
   sw_ctx* c = const_cast<sw_ctx*>(cc);
   if (!ready(c)) return SW_E_STATE;
-  if (!sol || bytes != full_bytes(c)) return fail(c, SW_E_INVALID, "sw_get_state: size mismatch");
+  if (!sol || bytes != caller_bytes(c, full_bytes(c))) return fail(c, SW_E_INVALID, "sw_get_state: size mismatch");
   HIPCHK(c, hipSetDevice(c->cfg.device));
   if (int rc = collect_full(c, &Slab::sol)) return rc;
-  HIPCHK(c, hipMemcpyAsync(sol, c->stage, bytes, hipMemcpyDeviceToHost, c->stream));
+  if (int rc = download(c, c->stage, sol, full_bytes(c))) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return SW_OK;
 }
@@ -976,10 +1017,10 @@ int sw_step(sw_ctx* c, int64_t nsteps) {
 
 int sw_calcN(sw_ctx* c, const void* sol, void* N, size_t bytes) {
   if (!ready(c)) return SW_E_STATE;
-  if (!sol || !N || bytes != full_bytes(c)) return fail(c, SW_E_INVALID, "sw_calcN: size mismatch");
+  if (!sol || !N || bytes != caller_bytes(c, full_bytes(c))) return fail(c, SW_E_INVALID, "sw_calcN: size mismatch");
   HIPCHK(c, hipSetDevice(c->cfg.device));
   c->mixed_valid = false;  // mixed arrays are used as scratch
-  HIPCHK(c, hipMemcpyAsync(c->stage, sol, bytes, hipMemcpyHostToDevice, c->stream));
+  if (int rc = upload(c, sol, c->stage, full_bytes(c))) return rc;
   for (Slab& s : c->sl) {
     sw::launch_gather(c->nf, s.g, c->stage, s.xs, c->stream);
     // scratch output: the ring slot that the next step overwrites anyway
@@ -989,7 +1030,7 @@ int sw_calcN(sw_ctx* c, const void* sol, void* N, size_t bytes) {
   }
   if (int rc = calcN(c, &Slab::xs, &Slab::nbuf)) return rc;
   if (int rc = collect_full(c, &Slab::nbuf)) return rc;
-  HIPCHK(c, hipMemcpyAsync(N, c->stage, bytes, hipMemcpyDeviceToHost, c->stream));
+  if (int rc = download(c, c->stage, N, full_bytes(c))) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return SW_OK;
 }
@@ -1015,11 +1056,11 @@ static bool valid_phys_id(const sw_ctx* c, int32_t fid) {
   return fid >= 0 && layer <= 1 && id != SW_PHYS_ETA && id <= 5;
 }
 
-int sw_get_physical(sw_ctx* c, int32_t fid, double* out, size_t bytes) {
+int sw_get_physical(sw_ctx* c, int32_t fid, void* out, size_t bytes) {
   if (!ready(c)) return SW_E_STATE;
   const Geom& g0 = c->sl[0].g;
-  if (!out || bytes != (size_t)g0.nx * g0.ny * sizeof(double))
-    return fail(c, SW_E_INVALID, "sw_get_physical: size mismatch");
+  const size_t pbytes = (size_t)g0.nx * g0.ny * sizeof(double);
+  if (!out || bytes != caller_bytes(c, pbytes)) return fail(c, SW_E_INVALID, "sw_get_physical: size mismatch");
   if (!valid_phys_id(c, fid))
     return fail(c, SW_E_INVALID, c->cfg.model == SW_MODEL_RSW ? "RSW physical ids are 0..3"
                                  : c->cfg.model == SW_MODEL_TY ? "TY physical ids are 0..5, 8, 9"
@@ -1030,7 +1071,7 @@ int sw_get_physical(sw_ctx* c, int32_t fid, double* out, size_t bytes) {
     const size_t rows = (size_t)g0.nyl * g0.nx;
     if (int rc = allgather(c, c->dflt + (size_t)g0.y0 * g0.nx, c->dflt, rows * sizeof(double))) return rc;
   }
-  HIPCHK(c, hipMemcpyAsync(out, c->dflt, bytes, hipMemcpyDeviceToHost, c->stream));
+  if (int rc = download(c, c->dflt, out, pbytes)) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return SW_OK;
 }
@@ -1077,36 +1118,50 @@ static void energies_from_sums(const sw_ctx* c, const double a[SW_NSUM], double&
   }
 }
 
-// `nrec` energy records -> host sums [rec][SW_NSUM].  Single process: dev holds
-// the sums.  One slab per process: dev holds this rank's column sums
-// [rec][kcl][3]; they are gathered and added in global column order, so the
+// Energy records [esums_n, diag_n) -> c->esums_host [rec][SW_NSUM] (each
+// record is gathered once).  Single process: erec holds the sums.  One slab
+// per process (collective): erec holds this rank's column sums
+// [rec][kcl][SW_NSUM]; they are gathered, in chunks that fit the host staging
+// of the host-staged transport, and added in global column order, so the
 // result is bitwise the same for any decomposition.
-static int gather_energy_sums(sw_ctx* c, const double* dev, int64_t nrec, std::vector<double>& out) {
-  out.assign((size_t)nrec * SW_NSUM, 0.0);
-  if (nrec == 0) return 0;
+static int gather_new_energy_sums(sw_ctx* c) {
+  const int64_t n0 = c->esums_n, n1 = c->diag_n;
+  c->esums_host.resize((size_t)n1 * SW_NSUM, 0.0);
+  if (n1 <= n0) return 0;
   if (!c->dist) {
-    HIPCHK(c, hipMemcpyAsync(out.data(), dev, out.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->esums_host.data() + (size_t)n0 * SW_NSUM, c->erec + (size_t)n0 * SW_NSUM,
+                             (size_t)(n1 - n0) * SW_NSUM * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->esums_n = n1;
     return 0;
   }
-  const size_t kcl = c->sl[0].g.kcl, per = (size_t)nrec * kcl * SW_NSUM;
-  std::vector<double> all(per * c->P);
+  const size_t kcl = c->sl[0].g.kcl, rec = kcl * SW_NSUM;  // doubles per record and rank
+  int64_t chunk = n1 - n0;
+  if (c->hostx) chunk = std::max<int64_t>(1, std::min<int64_t>(chunk, c->hbytes / (c->P * rec * sizeof(double))));
+  std::vector<double> all((size_t)chunk * rec * c->P);
   double* tmp = nullptr;
-  HIPCHK(c, hipMalloc((void**)&tmp, per * c->P * sizeof(double)));
-  int rc = allgather(c, dev, tmp, per * sizeof(double));
-  if (!rc && hipMemcpyAsync(all.data(), tmp, all.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream) !=
-                 hipSuccess)
-    rc = fail(c, SW_E_HIP, "energy gather copy failed");
+  HIPCHK(c, hipMalloc((void**)&tmp, all.size() * sizeof(double)));
+  int rc = 0;
+  for (int64_t r0 = n0; r0 < n1 && !rc; r0 += chunk) {
+    const int64_t m = std::min(chunk, n1 - r0);
+    const size_t per = (size_t)m * rec;
+    rc = allgather(c, c->erec + (size_t)r0 * rec, tmp, per * sizeof(double));
+    if (!rc && hipMemcpyAsync(all.data(), tmp, per * c->P * sizeof(double), hipMemcpyDeviceToHost, c->stream) !=
+                   hipSuccess)
+      rc = fail(c, SW_E_HIP, "energy gather copy failed");
+    if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = fail(c, SW_E_HIP, "energy gather sync failed");
+    for (int64_t r = 0; r < m && !rc; ++r)
+      for (int k = 0; k < SW_NSUM; ++k) {
+        double acc = 0.0;
+        for (int q = 0; q < c->P; ++q)
+          for (size_t col = 0; col < kcl; ++col) acc += all[q * per + ((size_t)r * kcl + col) * SW_NSUM + k];
+        c->esums_host[(size_t)(r0 + r) * SW_NSUM + k] = acc;
+      }
+  }
   (void)hipStreamSynchronize(c->stream);
   (void)hipFree(tmp);
   if (rc) return rc;
-  for (int64_t r = 0; r < nrec; ++r)
-    for (int k = 0; k < SW_NSUM; ++k) {
-      double acc = 0.0;
-      for (int q = 0; q < c->P; ++q)
-        for (size_t col = 0; col < kcl; ++col) acc += all[q * per + ((size_t)r * kcl + col) * SW_NSUM + k];
-      out[(size_t)r * SW_NSUM + k] = acc;
-    }
+  c->esums_n = n1;
   return 0;
 }
 
@@ -1199,6 +1254,8 @@ int sw_set_energy_diagnostics(sw_ctx* c, int64_t freq, int64_t capacity) {
   c->diag_n = 0;
   c->diag_steps.clear();
   c->diag_t.clear();
+  c->esums_host.clear();
+  c->esums_n = 0;
   if (c->diag_cap > 0) {
     const size_t per = c->dist ? (size_t)c->sl[0].g.kcl * SW_NSUM : SW_NSUM;
     if (int rc = alloc(c, (void**)&c->erec, (size_t)c->diag_cap * per * sizeof(double))) return rc;
@@ -1216,13 +1273,12 @@ int sw_get_energy_diagnostics(sw_ctx* c, sw_energy_record* out, int64_t max_reco
     return SW_OK;
   }
   const int64_t n = std::min<int64_t>(c->diag_n, max_records);
-  std::vector<double> sums;
-  // one slab per process: every rank gathers every record (collective)
-  if (int rc = gather_energy_sums(c, c->erec, c->dist ? c->diag_n : n, sums)) return rc;
+  // one slab per process: every rank gathers the new records (collective)
+  if (int rc = gather_new_energy_sums(c)) return rc;
   for (int64_t r = 0; r < n; ++r) {
     out[r].step = c->diag_steps[r];
     out[r].t = c->diag_t[r];
-    energies_from_sums(c, &sums[(size_t)SW_NSUM * r], out[r].ke, out[r].ke2, out[r].pe, out[r].wg);
+    energies_from_sums(c, &c->esums_host[(size_t)SW_NSUM * r], out[r].ke, out[r].ke2, out[r].pe, out[r].wg);
   }
   if (n_records) *n_records = n;
   return SW_OK;
@@ -1259,11 +1315,73 @@ int sw_profile_steps(sw_ctx* c, int64_t nsteps, sw_kernel_stat* out, int32_t max
 
 double sw_step_alg_bytes(const sw_ctx* c) {
   if (!ready(c)) return 0.0;
-  const int nstage = c->cfg.stepper == SW_STEP_IFMRK4 ? 4 : 1;
+  const int st = c->cfg.stepper;  // four calcN + update stages per RK4-family step
+  const int nstage = (st == SW_STEP_IFMRK4 || st == SW_STEP_ETDRK4 || st == SW_STEP_FILTERED_RK4) ? 4 : 1;
   if (!use_fused(c))
     return nstage * (kernel_bytes(c, K_COLINV) + kernel_bytes(c, K_ROW) + kernel_bytes(c, K_COLFWD) +
                      kernel_bytes(c, K_UPD));
   return nstage * (kernel_bytes(c, K_ROW) + kernel_bytes(c, K_COLSTEP));  // primed pipeline
+}
+
+// the ring slot holding RHS/N of `slot` steps ago (1 or 2), -1 if none
+static int hist_index(const sw_ctx* c, int32_t slot) {
+  const int st = c->cfg.stepper;
+  if ((st != SW_STEP_FILTERED_AB3 && st != SW_STEP_IFMAB3) || slot < 1 || slot > 2) return -1;
+  return (c->head + 3 - slot) % 3;  // step_ptrs: h1 = hist[(head+2)%3], h2 = hist[(head+1)%3]
+}
+
+int sw_history_slots(const sw_ctx* c, int32_t* nslots) {
+  if (!ready(c) || !nslots) return SW_E_STATE;
+  const int st = c->cfg.stepper;
+  *nslots = (st == SW_STEP_FILTERED_AB3 || st == SW_STEP_IFMAB3) ? 2 : 0;
+  return SW_OK;
+}
+
+int sw_get_history(const sw_ctx* cc, int32_t slot, void* buf, size_t bytes) {
+  sw_ctx* c = const_cast<sw_ctx*>(cc);
+  if (!ready(c)) return SW_E_STATE;
+  const int h = hist_index(c, slot);
+  if (h < 0) return fail(c, SW_E_INVALID, "sw_get_history: no such history slot for this stepper");
+  if (!buf || bytes != caller_bytes(c, full_bytes(c))) return fail(c, SW_E_INVALID, "sw_get_history: size mismatch");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  if (int rc = join_comm(c)) return rc;
+  for (Slab& s : c->sl) s.view = s.hist[h];
+  if (int rc = collect_full(c, &Slab::view)) return rc;
+  if (int rc = download(c, c->stage, buf, full_bytes(c))) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return SW_OK;
+}
+
+int sw_set_history(sw_ctx* c, int32_t slot, const void* buf, size_t bytes) {
+  if (!ready(c)) return SW_E_STATE;
+  const int h = hist_index(c, slot);
+  if (h < 0) return fail(c, SW_E_INVALID, "sw_set_history: no such history slot for this stepper");
+  if (!buf || bytes != caller_bytes(c, full_bytes(c))) return fail(c, SW_E_INVALID, "sw_set_history: size mismatch");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  if (int rc = join_comm(c)) return rc;
+  if (int rc = upload(c, buf, c->stage, full_bytes(c))) return rc;
+  for (Slab& s : c->sl) sw::launch_gather(c->nf, s.g, c->stage, s.hist[h], c->stream);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return SW_OK;
+}
+
+int sw_reset_history(sw_ctx* c) {
+  if (!ready(c)) return SW_E_STATE;
+  c->euler_until = c->step + 3;
+  return SW_OK;
+}
+
+int sw_slab_geometry(const sw_config* cfg, int32_t slab, int32_t out[8]) {
+  if (!cfg || !out || cfg->abi_version != SW_ABI_VERSION) return SW_E_INVALID;
+  const int P = cfg->nranks < 1 ? 1 : cfg->nranks;
+  if (!pow2(P) || !pow2(cfg->nx) || !pow2(cfg->ny) || cfg->nx < 32 || cfg->ny < 32 || cfg->nx > 8192 ||
+      cfg->ny > 8192 || slab < 0 || slab >= P || !(cfg->aliased_fraction >= 0 && cfg->aliased_fraction < 1))
+    return SW_E_INVALID;
+  const Geom g = make_geom(*cfg, P, slab);
+  const int32_t v[8] = {g.kc, g.kcl, g.kr0, g.kcn, g.nyl, g.y0, g.Lr, g.LrP};
+  std::memcpy(out, v, sizeof(v));
+  return SW_OK;
 }
 
 int sw_comm_unique_id(void* out128) {

@@ -1,5 +1,6 @@
 // Shared host/device definitions for libsw (not part of the public ABI).
 #pragma once
+#include <type_traits>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stddef.h>
@@ -409,6 +410,21 @@ enum { ETD_E = 0, ETD_E2, ETD_ZETA, ETD_ALPHA, ETD_BETA, ETD_GAMMA, ETD_N };
 void launch_col_step(int model, int op, const Geom& g, const Phys& p, const StepPtrs& a,
                      const double2* Mf, double2* Minv, const double2* tw_y, hipStream_t s, int f0 = 0,
                      int nfl = -1);
+// the launches of one transform length L = log2 N (sw_kernels.hip; one
+// translation unit per length in the split build, dispatched by log2 N)
+template <int L>
+struct LenOps {
+  static void col_inv(int model, const Geom& g, const Phys& p, const double2* X, double2* M, const double2* tw,
+                      hipStream_t s, int g0, int ng);
+  static void row(int model, const Geom& g, const Phys& p, const double2* Mi, double2* Mo, const double2* tw,
+                  hipStream_t s);
+  static void col_fwd(int model, const Geom& g, const Phys& p, const double2* Mf, double2* N, const double2* X,
+                      const double2* tw, hipStream_t s, int f0, int nfl);
+  static void col_step(int model, int op, const Geom& g, const Phys& p, const StepPtrs& a, const double2* Mf,
+                       double2* Minv, const double2* tw, hipStream_t s, int f0, int nfl);
+  static void col_inv1(const Geom& g, const double2* X, double2* M, const double2* tw, hipStream_t s);
+  static void row_c2r1(const Geom& g, const double2* M, double* out, const double2* tw, hipStream_t s);
+};
 void launch_step_elem(int nf, int op, const Geom& g, const Phys& p, const StepPtrs& a,
                       const double2* N, double2* xs, hipStream_t s);
 void launch_gather(int nf, const Geom& g, const double2* full, double2* compact, hipStream_t s);
@@ -427,6 +443,9 @@ void launch_energy_cols(int model, const Geom& g, const Phys& p, const double2* 
 void launch_energy_final(const double* cols, int ncols, double* out, hipStream_t s);
 // max |f| (sgn = 0) or max f (sgn = 1) as an order-preserving integer key
 void launch_absmax(const double* f, long long n, unsigned long long* out, int sgn, hipStream_t s);
+// fp32 caller buffers (SW_PREC_F32): n reals widened / rounded
+void launch_widen(const float* in, double* out, long long n, hipStream_t s);
+void launch_narrow(const double* in, float* out, long long n, hipStream_t s);
 // ETDRK4 coefficient table of the real diagonal L = -ν K^(2nν) (FF getetdcoeffs)
 void launch_etd_coeffs(const Geom& g, const Phys& p, double* etd, hipStream_t s);
 

@@ -66,7 +66,7 @@ __device__ __forceinline__ double2 zero2() { return make_double2(0.0, 0.0); }
 // grid: (columns, groups); RSW group f reads field f; QG2 group = layer.
 // ===========================================================================
 template <int MODEL, int LOG2N>
-__global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
+static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     k_col_inv(Geom g, Phys p, const double2* __restrict__ X, double2* __restrict__ M,
               const double2* __restrict__ tw, int gbase) {
   using B = Blk<LOG2N>;
@@ -429,7 +429,7 @@ __device__ __forceinline__ void fft_pair(double2 (&w)[2][8], int t, const Twiddl
 }
 
 template <int MODEL, int LOG2N>
-__global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS), (BlkRow<MODEL, LOG2N>::THREADS >= 1024 ? 4 : SW_MINW_ROW))
+static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS), (BlkRow<MODEL, LOG2N>::THREADS >= 1024 ? 4 : SW_MINW_ROW))
     k_row(Geom g, Phys p, const double2* __restrict__ Mi, double2* __restrict__ Mo,
           const double2* __restrict__ tw) {
   using Bk = BlkRow<MODEL, LOG2N>;
@@ -676,7 +676,7 @@ constexpr int model_nf() {
 }
 
 template <int MODEL, int LOG2N>
-__global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
+static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     k_col_fwd(Geom g, Phys p, const double2* __restrict__ Mf, double2* __restrict__ N,
               const double2* __restrict__ X, const double2* __restrict__ tw, int gbase) {
   using B = Blk<LOG2N>;
@@ -1077,7 +1077,7 @@ __device__ __forceinline__ cplx cexp_d(cplx z) {
   const double e = exp(z.re);
   return cplx{e * cos(z.im), e * sin(z.im)};
 }
-__global__ void __launch_bounds__(256) k_etd_coeffs(Geom g, Phys p, double* __restrict__ etd) {
+static __global__ void __launch_bounds__(256) k_etd_coeffs(Geom g, Phys p, double* __restrict__ etd) {
 #pragma clang fp contract(off)
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= g.cfield) return;
@@ -1113,7 +1113,7 @@ __global__ void __launch_bounds__(256) k_etd_coeffs(Geom g, Phys p, double* __re
 // Elementwise (unfused) stepper kernel: N from memory; the stage input x is
 // written to xs (RK4 stages 1-3) for a separate col_inv.
 template <int NF, int OP>
-__global__ void __launch_bounds__(256) k_step_elem(Geom g, Phys p, StepPtrs a, const double2* __restrict__ N,
+static __global__ void __launch_bounds__(256) k_step_elem(Geom g, Phys p, StepPtrs a, const double2* __restrict__ N,
                             double2* __restrict__ xs) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   int kr, j;
@@ -1140,7 +1140,7 @@ __global__ void __launch_bounds__(256) k_step_elem(Geom g, Phys p, StepPtrs a, c
   if (((s) + 1) % SW_SLOT_GROUP == 0) __builtin_amdgcn_sched_barrier(0)
 
 template <int MODEL, int LOG2N, int OP>
-__global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
+static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     k_col_step(Geom g, Phys p, StepPtrs a, const double2* __restrict__ Mf,
                double2* __restrict__ Minv, const double2* __restrict__ tw) {
   using B = Blk<LOG2N>;
@@ -1298,7 +1298,7 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
 // three y-FFTs per block, N never in HBM, old/new state in separate buffers.
 // ===========================================================================
 template <int LOG2N>
-__global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
+static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     k_col_step_fab3_rsw(Geom g, Phys p, StepPtrs a, const double2* __restrict__ Mf,
                         double2* __restrict__ Minv, const double2* __restrict__ tw, int fbase) {
   using B = Blk<LOG2N>;
@@ -1392,7 +1392,7 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
 // state I/O: Julia column-major (nkr, nl, nf) <-> compact live columns
 // ===========================================================================
 // this slab's live columns [kr0, kr0 + kcn) of the full array
-__global__ void k_gather(Geom g, int nf, const double2* __restrict__ full, double2* __restrict__ cmp) {
+static __global__ void k_gather(Geom g, int nf, const double2* __restrict__ full, double2* __restrict__ cmp) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long per = (long long)g.kcn * g.Lr;
   if (i >= per * nf) return;
@@ -1404,7 +1404,7 @@ __global__ void k_gather(Geom g, int nf, const double2* __restrict__ full, doubl
 }
 
 // columns [lo, hi) of the full array from this slab (zero outside live modes)
-__global__ void k_scatter(Geom g, int nf, int lo, int hi, const double2* __restrict__ cmp,
+static __global__ void k_scatter(Geom g, int nf, int lo, int hi, const double2* __restrict__ cmp,
                           double2* __restrict__ full) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const int w = hi - lo;
@@ -1419,7 +1419,7 @@ __global__ void k_scatter(Geom g, int nf, int lo, int hi, const double2* __restr
   full[((long long)f * g.nl + m) * g.nkr + kr] = v;
 }
 
-__global__ void k_nan_check(Geom g, int nf, const double2* __restrict__ cmp, int* flag) {
+static __global__ void k_nan_check(Geom g, int nf, const double2* __restrict__ cmp, int* flag) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   int kr, j;
   int bad = 0;
@@ -1437,7 +1437,7 @@ __global__ void k_nan_check(Geom g, int nf, const double2* __restrict__ cmp, int
 // ===========================================================================
 // field ids: RSW 0 u, 1 v, 2 η, 3 ζ = ik v - il u - f η (rsw/RotatingShallowWater.jl:108)
 //            QG2 layer*8 + {4 q, 5 ψ, 3 ζ = -K² ψ, 0 u = -il ψ, 1 v = ik ψ} (swqg/TwoLayerQG.jl:117-121)
-__global__ void k_make_spec(Geom g, Phys p, int model, int fid, const double2* __restrict__ sol,
+static __global__ void k_make_spec(Geom g, Phys p, int model, int fid, const double2* __restrict__ sol,
                             double2* __restrict__ out) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   int kr, j;
@@ -1486,7 +1486,7 @@ __global__ void k_make_spec(Geom g, Phys p, int model, int fid, const double2* _
 }
 
 template <int LOG2N>
-__global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
+static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     k_col_inv1(Geom g, const double2* __restrict__ X, double2* __restrict__ M,
                const double2* __restrict__ tw) {
   using B = Blk<LOG2N>;
@@ -1516,7 +1516,7 @@ __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
 }
 
 template <int LOG2N>
-__global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
+static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     k_row_c2r1(Geom g, const double2* __restrict__ M, double* __restrict__ out,
                const double2* __restrict__ tw) {
   using B = Blk<LOG2N>;
@@ -1595,7 +1595,7 @@ __device__ __forceinline__ double block_sum(double v, double* sh) {
   return r;
 }
 
-__global__ void __launch_bounds__(256) k_energy_cols(Geom g, Phys p, int model,
+static __global__ void __launch_bounds__(256) k_energy_cols(Geom g, Phys p, int model,
                                                      const double2* __restrict__ sol,
                                                      double* __restrict__ cols) {
   __shared__ double sh[4];
@@ -1648,7 +1648,7 @@ __global__ void __launch_bounds__(256) k_energy_cols(Geom g, Phys p, int model,
   }
 }
 
-__global__ void k_energy_final(const double* __restrict__ cols, int ncols, double* __restrict__ out) {
+static __global__ void k_energy_final(const double* __restrict__ cols, int ncols, double* __restrict__ out) {
   if (threadIdx.x < SW_NSUM) {
     double r = 0.0;
     for (int b = 0; b < ncols; ++b) r += cols[SW_NSUM * b + threadIdx.x];
@@ -1663,7 +1663,7 @@ __device__ __forceinline__ unsigned long long dkey(double d) {
   const unsigned long long b = (unsigned long long)__double_as_longlong(d);
   return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
 }
-__global__ void k_absmax(const double* __restrict__ f, long long n, unsigned long long* out, int sgn) {
+static __global__ void k_absmax(const double* __restrict__ f, long long n, unsigned long long* out, int sgn) {
   double m = sgn ? -INFINITY : 0.0;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
     m = fmax(m, sgn ? f[i] : fabs(f[i]));
@@ -1681,20 +1681,10 @@ __global__ void k_absmax(const double* __restrict__ f, long long n, unsigned lon
 #define SW_LOG2_CASES(X) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13)
 #endif
 
-template <template <int> class F, typename... Args>
-static void dispatch_log2(int log2n, Args&&... args) {
-  switch (log2n) {
-#define SW_CASE(L) \
-  case L:          \
-    F<L>::run(args...); \
-    break;
-    SW_LOG2_CASES(SW_CASE)
-#undef SW_CASE
-    default:
-      break;
-  }
-}
-
+// Split build (juliaraytracingsw_amd/build.py): the length-templated kernels
+// of one transform length per translation unit (-DSW_PART=L, L = 5 … 13), the
+// rest and the dispatch in SW_PART=0; without SW_PART one TU holds all.
+#if !defined(SW_PART) || SW_PART > 0
 template <int L>
 static int col_blocks(const Geom& g) {
   return (g.kcl + Blk<L>::NB - 1) / Blk<L>::NB;
@@ -1709,64 +1699,105 @@ static size_t lds_bytes() {
 }
 
 template <int L>
-struct ColInvL {
-  static void run(int model, const Geom& g, const Phys& p, const double2* X, double2* M,
-                  const double2* tw, hipStream_t s, int g0, int ng) {
-    const dim3 grid(col_blocks<L>(g), ng);
-    if (model == MODEL_RSW)
-      hipLaunchKernelGGL((k_col_inv<MODEL_RSW, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
-    else if (model == MODEL_TY)
-      hipLaunchKernelGGL((k_col_inv<MODEL_TY, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
-    else
-      hipLaunchKernelGGL((k_col_inv<MODEL_QG2, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
-  }
-};
+void LenOps<L>::col_inv(int model, const Geom& g, const Phys& p, const double2* X, double2* M, const double2* tw,
+                        hipStream_t s, int g0, int ng) {
+  const dim3 grid(col_blocks<L>(g), ng);
+  if (model == MODEL_RSW)
+    hipLaunchKernelGGL((k_col_inv<MODEL_RSW, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
+  else if (model == MODEL_TY)
+    hipLaunchKernelGGL((k_col_inv<MODEL_TY, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
+  else
+    hipLaunchKernelGGL((k_col_inv<MODEL_QG2, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
+}
+
 template <int L>
-struct RowL {
-  static void run(int model, const Geom& g, const Phys& p, const double2* Mi, double2* Mo,
-                  const double2* tw, hipStream_t s) {
-    using BR = BlkRow<MODEL_RSW, L>;
-    using BQ = BlkRow<MODEL_QG2, L>;
-    using BT = BlkRow<MODEL_TY, L>;
-    constexpr size_t sh_rsw = row_lds_lines<MODEL_RSW, L>() * FftPlan<L>::LDS * BR::NB * sizeof(double2);
-    constexpr size_t sh_qg2 = FftPlan<L>::LDS * BQ::NB * sizeof(double2);
-    constexpr size_t sh_ty = FftPlan<L>::LDS * BT::NB * sizeof(double2);
-    if (model == MODEL_RSW)
-      hipLaunchKernelGGL((k_row<MODEL_RSW, L>), dim3(g.nyl / BR::NB), dim3(BR::THREADS), sh_rsw, s, g, p, Mi, Mo, tw);
-    else if (model == MODEL_TY)
-      hipLaunchKernelGGL((k_row<MODEL_TY, L>), dim3(g.nyl / BT::NB), dim3(BT::THREADS), sh_ty, s, g, p, Mi, Mo, tw);
-    else
-      hipLaunchKernelGGL((k_row<MODEL_QG2, L>), dim3(g.nyl / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p, Mi, Mo, tw);
-  }
-};
+void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, double2* Mo, const double2* tw,
+                    hipStream_t s) {
+  using BR = BlkRow<MODEL_RSW, L>;
+  using BQ = BlkRow<MODEL_QG2, L>;
+  using BT = BlkRow<MODEL_TY, L>;
+  constexpr size_t sh_rsw = row_lds_lines<MODEL_RSW, L>() * FftPlan<L>::LDS * BR::NB * sizeof(double2);
+  constexpr size_t sh_qg2 = FftPlan<L>::LDS * BQ::NB * sizeof(double2);
+  constexpr size_t sh_ty = FftPlan<L>::LDS * BT::NB * sizeof(double2);
+  if (model == MODEL_RSW)
+    hipLaunchKernelGGL((k_row<MODEL_RSW, L>), dim3(g.nyl / BR::NB), dim3(BR::THREADS), sh_rsw, s, g, p, Mi, Mo, tw);
+  else if (model == MODEL_TY)
+    hipLaunchKernelGGL((k_row<MODEL_TY, L>), dim3(g.nyl / BT::NB), dim3(BT::THREADS), sh_ty, s, g, p, Mi, Mo, tw);
+  else
+    hipLaunchKernelGGL((k_row<MODEL_QG2, L>), dim3(g.nyl / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p, Mi, Mo, tw);
+}
+
 template <int L>
-struct ColFwdL {
-  static void run(int model, const Geom& g, const Phys& p, const double2* Mf, double2* N, const double2* X,
-                  const double2* tw, hipStream_t s, int f0, int nfl) {
-    const dim3 grid(col_blocks<L>(g), nfl);
-    if (model == MODEL_RSW)
-      hipLaunchKernelGGL((k_col_fwd<MODEL_RSW, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, Mf, N, X,
-                         tw, f0);
-    else if (model == MODEL_TY)
-      hipLaunchKernelGGL((k_col_fwd<MODEL_TY, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, Mf, N, X,
-                         tw, f0);
-    else
-      hipLaunchKernelGGL((k_col_fwd<MODEL_QG2, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, Mf, N, X,
-                         tw, f0);
-  }
-};
+void LenOps<L>::col_fwd(int model, const Geom& g, const Phys& p, const double2* Mf, double2* N, const double2* X,
+                        const double2* tw, hipStream_t s, int f0, int nfl) {
+  const dim3 grid(col_blocks<L>(g), nfl);
+  if (model == MODEL_RSW)
+    hipLaunchKernelGGL((k_col_fwd<MODEL_RSW, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, Mf, N, X,
+                       tw, f0);
+  else if (model == MODEL_TY)
+    hipLaunchKernelGGL((k_col_fwd<MODEL_TY, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, Mf, N, X,
+                       tw, f0);
+  else
+    hipLaunchKernelGGL((k_col_fwd<MODEL_QG2, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, Mf, N, X,
+                       tw, f0);
+}
+
 template <int L>
-struct ColInv1L {
-  static void run(const Geom& g, const double2* X, double2* M, const double2* tw, hipStream_t s) {
-    hipLaunchKernelGGL((k_col_inv1<L>), dim3(col_blocks<L>(g)), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, X, M, tw);
-  }
-};
+void LenOps<L>::col_inv1(const Geom& g, const double2* X, double2* M, const double2* tw, hipStream_t s) {
+  hipLaunchKernelGGL((k_col_inv1<L>), dim3(col_blocks<L>(g)), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, X, M, tw);
+}
+
 template <int L>
-struct RowC2r1L {
-  static void run(const Geom& g, const double2* M, double* out, const double2* tw, hipStream_t s) {
-    hipLaunchKernelGGL((k_row_c2r1<L>), dim3(row_blocks<L>(g)), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, M, out, tw);
+void LenOps<L>::row_c2r1(const Geom& g, const double2* M, double* out, const double2* tw, hipStream_t s) {
+  hipLaunchKernelGGL((k_row_c2r1<L>), dim3(row_blocks<L>(g)), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, M, out, tw);
+}
+
+template <int L>
+void LenOps<L>::col_step(int model, int op, const Geom& g, const Phys& p, const StepPtrs& a, const double2* Mf,
+                         double2* Minv, const double2* tw, hipStream_t s, int f0, int nfl) {
+  const dim3 grid(col_blocks<L>(g)), blk(Blk<L>::THREADS);
+  const size_t sh = lds_bytes<L>();
+#define SW_CS(M, O) hipLaunchKernelGGL((k_col_step<M, L, O>), grid, blk, sh, s, g, p, a, Mf, Minv, tw)
+  if (model == MODEL_RSW) {
+    // all three fields: the XCD-interleaved 1-D grid where it applies; a
+    // field range (pipelined slab exchange): one grid row per field
+    const bool all = f0 == 0 && nfl == 3;
+    if (op == OP_FAB3) {
+      if (all && Blk<L>::NB == 1 && g.kcl % 64 == 0)
+        hipLaunchKernelGGL((k_col_step_fab3_rsw<L>), dim3(3 * g.kcl), blk, sh, s, g, p, a, Mf, Minv, tw, -1);
+      else
+        hipLaunchKernelGGL((k_col_step_fab3_rsw<L>), dim3(col_blocks<L>(g), nfl), blk, sh, s, g, p, a, Mf, Minv,
+                           tw, f0);
+    } else if (op == OP_IFMAB3) SW_CS(MODEL_RSW, OP_IFMAB3);
+    else SW_CS(MODEL_RSW, OP_RK4);
+  } else {
+    if (op == OP_FAB3) SW_CS(MODEL_QG2, OP_FAB3);
+    else if (op == OP_IFMAB3) SW_CS(MODEL_QG2, OP_IFMAB3);
+    else SW_CS(MODEL_QG2, OP_RK4);
   }
-};
+#undef SW_CS
+}
+
+#ifdef SW_PART
+template struct LenOps<SW_PART>;
+#endif
+#endif  // length-templated launchers
+
+#if !defined(SW_PART) || SW_PART == 0
+// host-side: dispatch the LOG2N instantiation (N = 32 … 8192)
+template <typename F>
+static void by_len(int log2n, F&& f) {
+  switch (log2n) {
+#define SW_CASE(L)                          \
+  case L:                                   \
+    f(std::integral_constant<int, L>{});    \
+    break;
+    SW_LOG2_CASES(SW_CASE)
+#undef SW_CASE
+    default:
+      break;
+  }
+}
 
 // number of column-pass groups per launch unit: col_inv groups, col_fwd fields
 int col_inv_groups(int model) { return model == MODEL_RSW ? 3 : (model == MODEL_TY ? 5 : 2); }
@@ -1775,52 +1806,24 @@ int col_fields(int model) { return model == MODEL_RSW ? 3 : (model == MODEL_TY ?
 void launch_col_inv(int model, const Geom& g, const Phys& p, const double2* X, double2* Minv,
                     const double2* tw_y, hipStream_t s, int g0, int ng) {
   if (ng < 0) ng = col_inv_groups(model) - g0;
-  dispatch_log2<ColInvL>(g.log2ny, model, g, p, X, Minv, tw_y, s, g0, ng);
+  by_len(g.log2ny, [&](auto L) { LenOps<decltype(L)::value>::col_inv(model, g, p, X, Minv, tw_y, s, g0, ng); });
 }
 void launch_row(int model, const Geom& g, const Phys& p, const double2* Minv, double2* Mfwd,
                 const double2* tw_x, hipStream_t s) {
-  dispatch_log2<RowL>(g.log2nx, model, g, p, Minv, Mfwd, tw_x, s);
+  by_len(g.log2nx, [&](auto L) { LenOps<decltype(L)::value>::row(model, g, p, Minv, Mfwd, tw_x, s); });
 }
 void launch_col_fwd(int model, const Geom& g, const Phys& p, const double2* Mfwd, double2* N,
                     const double2* X, const double2* tw_y, hipStream_t s, int f0, int nfl) {
   if (nfl < 0) nfl = col_fields(model) - f0;
-  dispatch_log2<ColFwdL>(g.log2ny, model, g, p, Mfwd, N, X, tw_y, s, f0, nfl);
+  by_len(g.log2ny, [&](auto L) { LenOps<decltype(L)::value>::col_fwd(model, g, p, Mfwd, N, X, tw_y, s, f0, nfl); });
 }
 
 static inline dim3 mode_grid(const Geom& g) { return dim3((unsigned)((g.cfield + 255) / 256)); }
 
-template <int L>
-struct ColStepL {
-  static void run(int model, int op, const Geom& g, const Phys& p, const StepPtrs& a,
-                  const double2* Mf, double2* Minv, const double2* tw, hipStream_t s, int f0, int nfl) {
-    const dim3 grid(col_blocks<L>(g)), blk(Blk<L>::THREADS);
-    const size_t sh = lds_bytes<L>();
-#define SW_CS(M, O) hipLaunchKernelGGL((k_col_step<M, L, O>), grid, blk, sh, s, g, p, a, Mf, Minv, tw)
-    if (model == MODEL_RSW) {
-      // all three fields: the XCD-interleaved 1-D grid where it applies; a
-      // field range (pipelined slab exchange): one grid row per field
-      const bool all = f0 == 0 && nfl == 3;
-      if (op == OP_FAB3) {
-        if (all && Blk<L>::NB == 1 && g.kcl % 64 == 0)
-          hipLaunchKernelGGL((k_col_step_fab3_rsw<L>), dim3(3 * g.kcl), blk, sh, s, g, p, a, Mf, Minv, tw, -1);
-        else
-          hipLaunchKernelGGL((k_col_step_fab3_rsw<L>), dim3(col_blocks<L>(g), nfl), blk, sh, s, g, p, a, Mf, Minv,
-                             tw, f0);
-      } else if (op == OP_IFMAB3) SW_CS(MODEL_RSW, OP_IFMAB3);
-      else SW_CS(MODEL_RSW, OP_RK4);
-    } else {
-      if (op == OP_FAB3) SW_CS(MODEL_QG2, OP_FAB3);
-      else if (op == OP_IFMAB3) SW_CS(MODEL_QG2, OP_IFMAB3);
-      else SW_CS(MODEL_QG2, OP_RK4);
-    }
-#undef SW_CS
-  }
-};
-
 void launch_col_step(int model, int op, const Geom& g, const Phys& p, const StepPtrs& a,
                      const double2* Mf, double2* Minv, const double2* tw_y, hipStream_t s, int f0, int nfl) {
   if (nfl < 0) nfl = col_fields(model) - f0;
-  dispatch_log2<ColStepL>(g.log2ny, model, op, g, p, a, Mf, Minv, tw_y, s, f0, nfl);
+  by_len(g.log2ny, [&](auto L) { LenOps<decltype(L)::value>::col_step(model, op, g, p, a, Mf, Minv, tw_y, s, f0, nfl); });
 }
 
 void launch_step_elem(int nf, int op, const Geom& g, const Phys& p, const StepPtrs& a,
@@ -1864,11 +1867,11 @@ void launch_make_spec(int model, int fid, const Geom& g, const Phys& p, const do
 }
 
 void launch_col_inv1(const Geom& g, const double2* X, double2* M, const double2* tw_y, hipStream_t s) {
-  dispatch_log2<ColInv1L>(g.log2ny, g, X, M, tw_y, s);
+  by_len(g.log2ny, [&](auto L) { LenOps<decltype(L)::value>::col_inv1(g, X, M, tw_y, s); });
 }
 
 void launch_row_c2r1(const Geom& g, const double2* M, double* out, const double2* tw_x, hipStream_t s) {
-  dispatch_log2<RowC2r1L>(g.log2nx, g, M, out, tw_x, s);
+  by_len(g.log2nx, [&](auto L) { LenOps<decltype(L)::value>::row_c2r1(g, M, out, tw_x, s); });
 }
 
 void launch_energy_cols(int model, const Geom& g, const Phys& p, const double2* sol, double* cols,
@@ -1884,8 +1887,27 @@ void launch_absmax(const double* f, long long n, unsigned long long* out, int sg
   hipLaunchKernelGGL(k_absmax, dim3(1024), dim3(256), 0, s, f, n, out, sgn);
 }
 
+// caller-buffer precision (sw_config.precision = SW_PREC_F32): one rounding
+// on the way out, exact widening on the way in
+static __global__ void k_widen(const float* __restrict__ in, double* __restrict__ out, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    out[i] = (double)in[i];
+}
+static __global__ void k_narrow(const double* __restrict__ in, float* __restrict__ out, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    out[i] = (float)in[i];
+}
+void launch_widen(const float* in, double* out, long long n, hipStream_t s) {
+  hipLaunchKernelGGL(k_widen, dim3(2048), dim3(256), 0, s, in, out, n);
+}
+void launch_narrow(const double* in, float* out, long long n, hipStream_t s) {
+  hipLaunchKernelGGL(k_narrow, dim3(2048), dim3(256), 0, s, in, out, n);
+}
+
 void launch_etd_coeffs(const Geom& g, const Phys& p, double* etd, hipStream_t s) {
   hipLaunchKernelGGL(k_etd_coeffs, mode_grid(g), dim3(256), 0, s, g, p, etd);
 }
+
+#endif  // SW_PART == 0
 
 }  // namespace sw

@@ -222,26 +222,28 @@ def ty_problem(nx=512, seed=5678, device=0, decomposition=None, **over):
     return prob, P
 
 
-def rsw_problem(nx, stepper="FilteredAB3", seed=20261015, device=0, decomposition=None, **over):
-    """RSWDriver.initialize_problem (:134-176) on the GPU in fp64 with the named
-    stepper and the shafer random-phase IC."""
+def rsw_problem(nx, stepper="FilteredAB3", seed=20261015, device=0, decomposition=None, T=np.float64, **over):
+    """RSWDriver.initialize_problem (:134-176) on the GPU (fp64 compute) with the
+    named stepper and the shafer random-phase IC; ``T=np.float32`` gives the
+    driver's Float32 caller arrays (:164)."""
     P = rsw_parameters(nx, **over)
     kw = {"order": P["filter_order"]} if stepper == "FilteredAB3" else {}
     prob = RSW.Problem("gpu", nx=nx, Lx=P["Lx"], dt=P["dt"], f=P["f"], Cg=P["Cg"], nnu=P["nnu"],
                        nu=P["nu"], aliased_fraction=P["aliased_fraction"], stepper=stepper,
-                       use_filter=(P["nutune"] == 0), device=device, decomposition=decomposition, **kw)
+                       use_filter=(P["nutune"] == 0), T=T, device=device, decomposition=decomposition, **kw)
     rng = np.random.default_rng(seed)
     set_shafer_initial_condition(prob, P["Kg"], P["Kw"], P["ag"], P["aw"], P["f"], P["Cg"] ** 2, rng)
     return prob, P
 
 
-def qg2_problem(nx, stepper="IFMAB3", seed=1234, device=0, decomposition=None, **over):
-    """TwoLayerDriver.initialize_problem (:29-68) on the GPU in fp64."""
+def qg2_problem(nx, stepper="IFMAB3", seed=1234, device=0, decomposition=None, T=np.float64, **over):
+    """TwoLayerDriver.initialize_problem (:29-68) on the GPU (fp64 compute;
+    ``T=np.float32`` gives the driver's Float32 caller arrays)."""
     P = qg2_parameters(nx, **over)
     prob = QG2.Problem("gpu", nx=nx, Lx=P["Lx"], dt=P["dt"], f0=P["f"], Cg=P["background_Cg"],
                        U=P["U"], drhorho0=P["drhorho0"], nnu=P["nnu"], nu=P["nu"], mu=P["mu"],
                        aliased_fraction=P["aliased_fraction"], stepper=stepper, use_filter=False,
-                       device=device, decomposition=decomposition)
+                       T=T, device=device, decomposition=decomposition)
     rng = np.random.default_rng(seed)
     set_seed_initial_condition(prob, rng)
     return prob, P

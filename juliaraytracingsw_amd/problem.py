@@ -40,8 +40,11 @@ class Problem:
                  use_filter=False, filter_kw=None, device=0, check_nan=True, T=np.float64,
                  nop_calcN=False, unfused=False, nranks=1, rank=0, local_slabs=1,
                  comm_unique_id=None, exchange=None):
-        if np.dtype(T) != np.float64:
-            raise _lib.LibSWError("this build computes in fp64 (T=Float64) only")
+        # T: the element type of the caller's buffers (prob.sol, vars), as the
+        # reference's Problem(...; T) (rsw/RSWDriver.jl:164 and
+        # swqg/TwoLayerDriver.jl:63 pass Float32); libsw computes in fp64
+        if np.dtype(T) not in (np.dtype(np.float64), np.dtype(np.float32)):
+            raise _lib.LibSWError(f"T must be Float64 or Float32, got {np.dtype(T)}")
         if stepper not in _lib.STEPPERS:
             raise ValueError(f"unknown stepper {stepper!r}; expected one of {list(_lib.STEPPERS)}")
         fk = dict(order=4, innerK=0.65, outerK=1.0, tol=1e-15)
@@ -66,6 +69,7 @@ class Problem:
         cfg.filter_innerK = float(fk["innerK"])
         cfg.filter_outerK = float(fk["outerK"])
         cfg.filter_tol = float(fk["tol"])
+        cfg.precision = _lib.SW_PREC_F32 if np.dtype(T) == np.float32 else _lib.SW_PREC_F64
         cfg.device = int(device)
         cfg.check_nan = 1 if check_nan else 0
         cfg.nop_calcN = 1 if nop_calcN else 0
@@ -87,6 +91,7 @@ class Problem:
         self.grid = TwoDGrid(nx, Lx, ny, Ly, aliased_fraction)
         self.clock = Clock(self.ctx, dt)
         self.params = dict(params)
+        self.T = np.dtype(T).type
         self._efreq = None  # energy-diagnostics frequency recorded on the device
 
     # FF prob.sol (a host copy; assignment uploads and dealiases)

@@ -57,6 +57,12 @@ def host_decomposition(rank: int, world: int, group=None) -> dict:
     return dict(nranks=world, rank=rank, local_slabs=1, exchange=torch_exchange(group))
 
 
+# threads per column-pass block (SW_BLK_THREADS, csrc/sw_internal.hpp); the
+# library reports its own value through sw_slab_geometry (checked by
+# tests/test_abi.py)
+SW_BLK_THREADS = 64
+
+
 def _alias_range(n, af):
     return math.floor((1 - af) / 2 * n) + 1, math.ceil((1 + af) / 2 * n)
 
@@ -69,7 +75,7 @@ def slab_geometry(nx: int, ny: int, aliased_fraction: float, P: int, s: int) -> 
         kcl = (kc + 63) // 64 * 64
     else:
         NT = ny // 8
-        nb = 1 if NT >= 256 else min(256 // NT, 32)
+        nb = 1 if NT >= SW_BLK_THREADS else min(SW_BLK_THREADS // NT, 32)
         gran = max(8, nb)
         kcl = ((kc + P - 1) // P + gran - 1) // gran * gran
     kr0 = s * kcl

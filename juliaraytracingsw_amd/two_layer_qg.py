@@ -14,13 +14,14 @@ from .problem import Diagnostic, Problem as _Problem, increment, stepforward  # 
 
 def Problem(dev="gpu", *, nx=128, ny=None, Lx=2 * np.pi, Ly=None, U=0.5, mu=1e-2, nu=1e-6, nnu=4,
             f0=3.0, Cg=1.0, drhorho0=0.2, stepper="IFMAB3", dt=5e-2, aliased_fraction=1 / 3,
-            T=np.float64, use_filter=False, device=0, check_nan=True, nop_calcN=False, unfused=False,
+            T=np.float32, use_filter=False, device=0, check_nan=True, nop_calcN=False, unfused=False,
             decomposition=None, **stepper_kwargs):
     """``TwoLayerQG.Problem(dev; nx, ny, Lx, Ly, U, μ, ν, nν, f0, Cg, δρρ0, stepper,
     dt, aliased_fraction, T, use_filter, stepper_kwargs...)`` (:55-90).
 
-    Note: the reference defaults to T=Float32; this build computes in fp64
-    (BASELINE parity precision) and rejects other T.
+    ``T`` (default Float32, as the reference's :70) is the element type of
+    the caller-side arrays (``prob.sol``, ``updatevars``); libsw computes in
+    fp64 either way (BASELINE parity precision) and rounds once on output.
     """
     if dev not in ("gpu", "GPU", "GPU()"):
         raise _lib.LibSWError("libsw runs on the GPU only (dev='gpu')")

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--case", default="rsw_fab3")
     ap.add_argument("--n", type=int, default=128)
     ap.add_argument("--steps", type=int, default=6)
+    ap.add_argument("--freq", type=int, default=2)
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     dist.init_process_group("gloo")
@@ -37,8 +38,12 @@ def main():
     prob = sw_cases.libsw_problem(p, decomposition=slab_comm.host_decomposition(rank, world))
     prob.sol = ic
     N = prob.calcN(ic)
-    prob.ctx.set_energy_diagnostics(2, 64)
-    prob.stepforward(a.steps)
+    cap = a.steps // a.freq + 1
+    prob.ctx.set_energy_diagnostics(a.freq, cap)
+    half = a.steps // 2
+    prob.stepforward(half)
+    mid = prob.ctx.energy_diagnostics()  # gathered once; the rest incrementally below
+    prob.stepforward(a.steps - half)
     sol = prob.sol
     phys = M.updatevars(prob)
     ke, pe = np.sum(M.kinetic_energy(prob)), M.potential_energy(prob)
@@ -48,7 +53,7 @@ def main():
         ref = sw_cases.libsw_problem(p)
         ref.sol = ic
         Nr = ref.calcN(ic)
-        ref.ctx.set_energy_diagnostics(2, 64)
+        ref.ctx.set_energy_diagnostics(a.freq, cap)
         ref.stepforward(a.steps)
         pr = M.updatevars(ref)
         res = dict(
@@ -57,7 +62,9 @@ def main():
             physical_equal=bool(all(np.array_equal(phys[k], pr[k]) for k in pr)),
             ke_rel=abs(ke / np.sum(M.kinetic_energy(ref)) - 1),
             pe_rel=abs(pe / M.potential_energy(ref) - 1),
-            records_equal=bool(recs == ref.ctx.energy_diagnostics() and len(recs) == a.steps // 2),
+            records_equal=bool(recs == ref.ctx.energy_diagnostics() and len(recs) == a.steps // a.freq
+                               and mid == recs[:len(mid)] and len(mid) == half // a.freq),
+            n_records=len(recs),
             cfl_equal=bool(cfl == M.cfl(ref)),
             world=world,
         )

@@ -86,3 +86,28 @@ def test_integration_bindings_track_the_header():
     jfields = re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)::", julia)
     assert jfields == hfields
     assert [f[0] for f in _lib.SwConfig._fields_] == hfields
+
+
+@pytest.mark.parametrize("n", [32, 64, 128, 256, 2048, 8192])
+@pytest.mark.parametrize("P", [1, 2, 4, 8])
+def test_slab_geometry_matches_library(lib_path, n, P):
+    """slab_comm.slab_geometry (the host mirror used by the CPU slab
+    rehearsal) = the library's own make_geom (sw_slab_geometry) — ADVICE r01:
+    the mirror once assumed 256-thread column blocks."""
+    from juliaraytracingsw_amd import _lib, slab_comm
+
+    if n // P < 32:
+        pytest.skip("ny / nranks < 32 is rejected")
+    cfg = _lib.default_config()
+    cfg.nx = cfg.ny = n
+    cfg.nranks = P
+    for s in range(P):
+        lib = _lib.slab_geometry(cfg, s)
+        py = slab_comm.slab_geometry(n, n, 1 / 3, P, s)
+        assert {k: lib[k] for k in py} == py, (s, lib, py)
+
+
+def test_precision_field_default(lib_path):
+    from juliaraytracingsw_amd import _lib
+
+    assert _lib.default_config().precision == _lib.SW_PREC_F64

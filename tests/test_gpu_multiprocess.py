@@ -23,12 +23,17 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("case,world", [("rsw_fab3", 2), ("qg2_ifmrk4", 2), ("rsw_ifmab3", 4)])
-def test_one_process_per_slab(case, world, tmp_path):
+@pytest.mark.parametrize("case,world,steps,freq", [("rsw_fab3", 2, 6, 2), ("qg2_ifmrk4", 2, 6, 2),
+                                                   ("rsw_ifmab3", 4, 6, 2),
+                                                   # more records than one host-staged gather holds
+                                                   # before the chunked, incremental gather
+                                                   ("rsw_fab3", 2, 240, 1)])
+def test_one_process_per_slab(case, world, steps, freq, tmp_path):
     out = tmp_path / "res.json"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
-           os.path.join(HERE, "mp_slab_worker.py"), "--case", case, "--out", str(out)]
+           os.path.join(HERE, "mp_slab_worker.py"), "--case", case, "--out", str(out),
+           "--steps", str(steps), "--freq", str(freq)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     res = json.loads(out.read_text())

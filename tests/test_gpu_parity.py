@@ -276,13 +276,13 @@ def _rect_problem(name, nx, ny):
                            stepper=p["stepper"], **fk)
     else:
         prob = QG2.Problem("gpu", nx=nx, ny=ny, dt=dt, nu=1e-30, nnu=4, U=p["U"], mu=p["mu"], f0=p["f0"],
-                           Cg=p["Cg"], drhorho0=p["drhorho0"], stepper=p["stepper"], **fk)
+                           Cg=p["Cg"], drhorho0=p["drhorho0"], stepper=p["stepper"], T=np.float64, **fk)
     prob.sol = pr.sol
     return pr, prob
 
 
 @pytest.mark.parametrize("nx,ny", [(8192, 32), (32, 8192), (4096, 64), (64, 4096)])
-@pytest.mark.parametrize("name", ["rsw_fab3", "qg2_ifmab3", "rsw_ifmrk4"])
+@pytest.mark.parametrize("name", ["rsw_fab3", "qg2_ifmab3", "rsw_ifmrk4", "qg2_ifmrk4"])
 def test_rectangular_long_lines(name, nx, ny):
     """Every transform length up to 8192 (the 4096²/8192² configurations) on
     cheap rectangular grids: x lines of 4096/8192 exercise the row pass, y

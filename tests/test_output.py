@@ -16,6 +16,19 @@ class _Clock:
         self.t, self.step = t, step
 
 
+class _Ctx:
+    """Host stand-in for the libsw context: records sw_reset_history."""
+
+    def __init__(self):
+        self.resets = 0
+
+    def reset_history(self):
+        self.resets += 1
+
+    def history_slots(self):
+        return 2
+
+
 class _Prob:
     """Host stand-in with the Problem attributes output.py reads."""
 
@@ -26,6 +39,7 @@ class _Prob:
         self.model, self.stepper = _lib.SW_MODEL_RSW, "FilteredAB3"
         self.params = {"f": 3.0, "Cg": 1.0}
         self.clock = _Clock()
+        self.ctx = _Ctx()
         self._sol = np.zeros((nf, n, n // 2 + 1), complex)
 
     @property
@@ -58,6 +72,8 @@ def test_output_layout_and_restart(tmp_path):
     q = _Prob(32)
     assert output.restart(q, fn) == 10
     assert np.array_equal(q.sol, states[10]) and q.clock.t == 1.0 and q.clock.step == 10
+    # no history in a snapshot file: the AB3 steppers restart with Euler steps
+    assert q.ctx.resets == 1
 
 
 def test_sequenced_output_rolls_over(tmp_path):
