@@ -3,7 +3,7 @@
 metric) on N MI355X, plus the roofline of the dominant kernel and the CPU
 baseline (the oracle restatement, scipy.fft on the host cores).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode slab|ensemble]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode slab|ensemble] [--grid N]
 
 Defaults: 200 untimed + 2000 timed steps (state resident in HBM).
 
@@ -149,7 +149,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=200)
-    ap.add_argument("--n", type=int, default=2048)
+    # (no option may be a prefix of a torch.distributed.run option: the ranks'
+    # command line passes through its parser)
+    ap.add_argument("--grid", dest="n", type=int, default=2048)
     ap.add_argument("--model", default="rsw", choices=["rsw", "qg2", "ty", "mlqg"])
     ap.add_argument("--stepper", default="FilteredAB3",
                     choices=["FilteredAB3", "IFMAB3", "IFMRK4", "ETDRK4", "FilteredRK4"])

@@ -11,7 +11,7 @@ from juliaraytracingsw_amd import drivers  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--model", default="rsw")
 ap.add_argument("--stepper", default="FilteredAB3")
-ap.add_argument("--n", type=int, default=2048)
+ap.add_argument("--grid", dest="n", type=int, default=2048)
 ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--warmup", type=int, default=5)
 a = ap.parse_args()

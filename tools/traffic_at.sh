@@ -5,11 +5,11 @@
 SO=$1; TAG=$2; M=$3; ST=$4; N=$5; K=$6
 export TMPDIR=/tmp
 O=gpurun_out/tr/$TAG; mkdir -p $O
-P="python tools/prof_step.py --model $M --stepper $ST --n $N --steps $K --warmup 2"
+P="python tools/prof_step.py --model $M --stepper $ST --grid $N --steps $K --warmup 2"
 LIBSW_PATH=$SO timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/f -o run -- $P > $O/f.log 2>&1 || exit 1
 LIBSW_PATH=$SO timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/w -o run -- $P > $O/w.log 2>&1 || exit 2
 python tools/traffic_from_pmc.py $(find $O/f -name '*counter_collection.csv') $(find $O/w -name '*counter_collection.csv') ${M}${N}_$ST $O/t.json > /dev/null || exit 3
-LIBSW_PATH=$SO timeout -k 10 200 python bench.py --no-cpu-baseline --model $M --stepper $ST --n $N --steps $K --warmup 2 --profile-steps 3 > $O/b.json 2> $O/b.err || exit 4
+LIBSW_PATH=$SO timeout -k 10 200 python bench.py --no-cpu-baseline --model $M --stepper $ST --grid $N --steps $K --warmup 2 --profile-steps 3 > $O/b.json 2> $O/b.err || exit 4
 python - $O <<'PY'
 import json, sys
 o = sys.argv[1]
