@@ -43,7 +43,9 @@ def _run(cmd):
         raise RuntimeError(f"hipcc failed ({r.returncode}): {' '.join(cmd)}\n{r.stderr[-4000:]}")
 
 
-def build_lib(verbose=False, force=False, out=OUT, extra_flags=(), jobs=None):
+def build_lib(verbose=False, force=False, out=OUT, extra_flags=(), jobs=None, parts=None):
+    """parts: [L] builds transform length 2^L only (experiments: the dispatch
+    then knows that length alone); default every length."""
     if not force and not needs_build(out):
         return out
     hipcc = hipcc_path()
@@ -52,16 +54,18 @@ def build_lib(verbose=False, force=False, out=OUT, extra_flags=(), jobs=None):
     jobs = jobs or min(len(PARTS) + 1, max(1, len(os.sched_getaffinity(0))))
     with tempfile.TemporaryDirectory(prefix="libsw_build_") as tmp:
         cmds = []
-        for part in PARTS:
-            cmds.append(common + ["-c", f"-DSW_PART={part}", os.path.join(CSRC, "sw_kernels.hip"),
-                                  "-o", os.path.join(tmp, f"k{part}.o")])
+        plist = [0] + [q for q in PARTS if q and (parts is None or q in parts)]
+        only = [f"-DSW_ONLY_LOG2={parts[0]}"] if parts is not None and len(parts) == 1 else []
+        for part in plist:
+            cmds.append(common + only + ["-c", f"-DSW_PART={part}", os.path.join(CSRC, "sw_kernels.hip"),
+                                         "-o", os.path.join(tmp, f"k{part}.o")])
         cmds.append(common + ["-c", os.path.join(CSRC, "sw_api.cpp"), "-o", os.path.join(tmp, "api.o")])
         if verbose:
             for c in cmds:
                 print(" ".join(c))
         with ThreadPoolExecutor(jobs) as ex:
             list(ex.map(_run, cmds))
-        objs = [os.path.join(tmp, f"k{p}.o") for p in PARTS] + [os.path.join(tmp, "api.o")]
+        objs = [os.path.join(tmp, f"k{p}.o") for p in plist] + [os.path.join(tmp, "api.o")]
         link = [hipcc, "--offload-arch=gfx950", "-fPIC", "-shared", "-o", out + ".tmp", *objs,
                 "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
         if verbose:

@@ -921,6 +921,8 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (const char* e = std::getenv("SW_FUSE_ALL")) c->fuse_all = e[0] == '1';
+  // experiments (tools/sweep.sh): SW_CHECK_NAN=0 disables the NaN check of sw_step
+  if (const char* e = std::getenv("SW_CHECK_NAN")) c->cfg.check_nan = e[0] == '1';
   c->stats.resize(K_NKERN);
   for (int i = 0; i < K_NKERN; ++i) c->stats[i].name = kname[i];
   return SW_OK;

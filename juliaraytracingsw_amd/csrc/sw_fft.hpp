@@ -223,7 +223,11 @@ __device__ __forceinline__ void fft_lines(double2 (&v)[C][8], int t, const Twidd
   for (int lNs = S0, ti = (P::REM ? 0 : -1); lNs + 3 <= LOG2N; lNs += 3, ++ti) {
     const int Ns = 1 << lNs;
     const int k = t & (Ns - 1);
+#ifdef SW_EXP_NOTW  // experiment: no twiddle multiplications (wrong results)
+    if (false) {
+#else
     if (lNs > 0) {
+#endif
       const double2 wt = Twiddles<LOG2N>::kPreload ? tw1[ti] : tws.get(ti);
       const double2 w1 = DIR < 0 ? wt : cconj(wt);
       if constexpr (Twiddles<LOG2N>::kPreload) {
@@ -253,6 +257,9 @@ __device__ __forceinline__ void fft_lines(double2 (&v)[C][8], int t, const Twidd
 #pragma unroll
     for (int c = 0; c < C; ++c) dft8<DIR>(v[c]);
     if (lNs + 3 >= LOG2N) break;  // last stage: outputs already at t + r*NT
+#ifdef SW_EXP_NOLDS  // experiment: no LDS exchange in the radix-8 stages (wrong results)
+    continue;
+#endif
     lds_barrier();                // in-place LDS: everyone has loaded this stage's inputs
     const int idxD = ((t >> lNs) << (lNs + 3)) + k;
 #pragma unroll

@@ -216,122 +216,170 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
 // Z[nx-k] = conj(A[k]) + i conj(B[k]); the DC bin keeps real parts only —
 // numpy's c2r rule).
 // ===========================================================================
+// Row-pass addressing (k_row, k_row_c2r1).  Element s of thread t of a row
+// is the x-wavenumber kk_s = t + s·NT for s < 4 and the Hermitian mirror
+// N − t − s·NT for s >= 4 (inverse transforms' inputs), or k = t + s·NT
+// (forward transforms' outputs).  A row's mixed-field offsets are the same
+// for every field, so they are formed once per row: with one slab in closed
+// form (a per-thread term plus a per-s constant, which folds into the scalar
+// base of each load and store), with several slabs from the tile offsets.
+// Dead inputs (kk >= kc) read column 0 of the row (in bounds) and are zeroed;
+// s-slots dead on every thread of the row are skipped (uniform branch).
+#if SW_TILE_I == 2 && SW_LORD_I == 0 && SW_TILE_F == 2 && SW_LORD_F == 1
+#define SW_ROW_CLOSED true
+#else
+#define SW_ROW_CLOSED false
+#endif
 template <int LOG2N>
-__device__ __forceinline__ void load_pair(double2 (&v)[8], int t, const Geom& g,
-                                          const double2* __restrict__ A,
-                                          const double2* __restrict__ B, int y, bool deriv) {
-  SW_OPAQUE_T(t);
-  constexpr int N = 1 << LOG2N, NT = N / 8, half = N / 2;
-  double2 a[8], b[8];
-  int kk[8];
+struct RowIdx {
+  static constexpr int N = 1 << LOG2N, NT = N / 8;
+  // 8192-point lines (128 VGPRs): offsets recomputed per use from 3 terms
+  static constexpr bool kStore = LOG2N < SW_OPAQUE_LOG2;
+  int oi[kStore ? 8 : 1];
+  int ia, ib, row0, f0, t, y;
+  __device__ __forceinline__ static int kk(int t, int s) { return s < 4 ? t + s * NT : N - t - s * NT; }
+  // some thread of the row holds a live inverse input s (uniform)
+  __device__ __forceinline__ static bool inv_any(const Geom& g, int s) {
+    return s < 4 ? s * NT < g.kc : (7 - s) * NT + 1 < g.kc;
+  }
+  // some thread holds a live forward output s, k = t + s NT < kc (uniform)
+  __device__ __forceinline__ static bool fwd_any(const Geom& g, int s) { return s * NT < g.kc; }
+  __device__ __forceinline__ int oinv_calc(const Geom& g, int s) const {
+    const int k = kk(t, s);
+    if (SW_ROW_CLOSED && g.nslab == 1)
+      return k < g.kc ? (s < 4 ? ia + 4 * NT * s : ib + 4 * NT * (8 - s)) : row0;
+    return midx_i(g, k < g.kc ? k : 0, y);
+  }
+  __device__ __forceinline__ void init(const Geom& g, int t_, int y_) {
+    t = t_;
+    y = y_;
+    // one slab: inverse layout 8 (kk >> 1) + (kk & 1) + row term, forward
+    // layout 2 ny (k >> 1) + (k & 1) + row term (mtile_local, A = 2)
+    row0 = (y >> 2) * (g.kcl >> 1) * 8 + (y & 3) * 2;
+    ia = row0 + 8 * (t >> 1) + (t & 1);
+    ib = row0 - 4 * t - 3 * (t & 1);
+    f0 = (y >> 2) * 8 + (y & 3) * 2 + 2 * g.nyl * (t >> 1) + (t & 1);
+    if constexpr (kStore) {
 #pragma unroll
-  for (int s = 0; s < 8; ++s) {  // issue every load first (clamped, unconditional)
-    const int m = t + s * NT;
-    kk[s] = m <= half ? m : N - m;
-    const int o = midx_i(g, kk[s] < g.kc ? kk[s] : 0, y);
-    a[s] = A[o];
-    b[s] = B ? B[o] : zero2();
+      for (int s = 0; s < 8; ++s) oi[s] = oinv_calc(g, s);
+    }
+  }
+  __device__ __forceinline__ int oinv(const Geom& g, int s) const {
+#ifdef SW_EXP_NOHBM  // experiment: every load from one address (L1 hits), no HBM traffic
+    return 0;
+#endif
+    if constexpr (kStore) return oi[s];
+    else return oinv_calc(g, s);
+  }
+  // forward-layout offset of output s (k = t + s NT)
+  __device__ __forceinline__ int ofwd(const Geom& g, int s) const {
+#ifdef SW_EXP_NOHBM
+    return t & 1;
+#endif
+    if (SW_ROW_CLOSED && g.nslab == 1) return f0 + s * NT * g.nyl;
+    return midx(g, t + s * NT, y);
+  }
+};
+
+// a + i b from the x-spectra of a row: z[kk] = a + i b for kk <= N/2,
+// conj(a) + i conj(b) at the mirror (the DC bin keeps real parts only —
+// numpy's c2r rule); dead kk give 0
+__device__ __forceinline__ double2 pair_z(double2 aa, double2 bb, int kk, bool mirror, bool live) {
+  if (kk == 0) {
+    aa.y = 0.0;
+    bb.y = 0.0;
+  }
+  if (mirror) {
+    aa = cconj(aa);
+    bb = cconj(bb);
+  }
+  return live ? make_double2(aa.x - bb.y, aa.y + bb.x) : zero2();
+}
+
+template <int LOG2N>
+__device__ __forceinline__ void load_pair(double2 (&v)[8], const RowIdx<LOG2N>& ri, const Geom& g,
+                                          const double2* __restrict__ A,
+                                          const double2* __restrict__ B, bool deriv) {
+  using R = RowIdx<LOG2N>;
+  double2 a[8], b[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {  // issue every load first
+    a[s] = b[s] = zero2();
+    if (R::inv_any(g, s)) {
+      const int o = ri.oinv(g, s);
+      a[s] = A[o];
+      if (B) b[s] = B[o];
+    }
   }
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
-    const int m = t + s * NT;
+    const int kk = R::kk(ri.t, s);
     double2 aa = a[s], bb = b[s];
     if (deriv) {
-      const double kw = kk[s] * g.mk;
+      const double kw = kk * g.mk;
       aa = cmul_i(aa, kw);
       bb = cmul_i(bb, kw);
     }
-    if (kk[s] == 0) {
-      aa.y = 0.0;
-      bb.y = 0.0;
-    }
-    if (m > half) {
-      aa = cconj(aa);
-      bb = cconj(bb);
-    }
-    const double2 z = make_double2(aa.x - bb.y, aa.y + bb.x);  // a + i b
-    v[s] = kk[s] < g.kc ? z : zero2();
+    v[s] = pair_z(aa, bb, kk, s >= 4 && kk != (R::N >> 1), kk < g.kc);
   }
 }
 
 // load_pair with a per-field x-multiplier m: 0 → 1, 1 → ik, 2 → (ik)² = -k²
 // (B may be null: b = 0)
 template <int LOG2N>
-__device__ __forceinline__ void load_pair_m(double2 (&v)[8], int t, const Geom& g,
+__device__ __forceinline__ void load_pair_m(double2 (&v)[8], const RowIdx<LOG2N>& ri, const Geom& g,
                                             const double2* __restrict__ A, int ma,
-                                            const double2* __restrict__ B, int mb, int y) {
-  SW_OPAQUE_T(t);
-  constexpr int N = 1 << LOG2N, NT = N / 8, half = N / 2;
+                                            const double2* __restrict__ B, int mb) {
+  using R = RowIdx<LOG2N>;
   double2 a[8], b[8];
-  int kk[8];
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
-    const int m = t + s * NT;
-    kk[s] = m <= half ? m : N - m;
-    const int o = midx_i(g, kk[s] < g.kc ? kk[s] : 0, y);
-    a[s] = A[o];
-    b[s] = B ? B[o] : zero2();
+    a[s] = b[s] = zero2();
+    if (R::inv_any(g, s)) {
+      const int o = ri.oinv(g, s);
+      a[s] = A[o];
+      if (B) b[s] = B[o];
+    }
   }
   auto mul = [](double2 x, int mm, double kw) {
     return mm == 0 ? x : (mm == 1 ? cmul_i(x, kw) : cscale(x, -(kw * kw)));
   };
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
-    const int m = t + s * NT;
-    const double kw = kk[s] * g.mk;
-    double2 aa = mul(a[s], ma, kw), bb = mul(b[s], mb, kw);
-    if (kk[s] == 0) {
-      aa.y = 0.0;
-      bb.y = 0.0;
-    }
-    if (m > half) {
-      aa = cconj(aa);
-      bb = cconj(bb);
-    }
-    const double2 z = make_double2(aa.x - bb.y, aa.y + bb.x);  // a + i b
-    v[s] = kk[s] < g.kc ? z : zero2();
+    const int kk = R::kk(ri.t, s);
+    const double kw = kk * g.mk;
+    v[s] = pair_z(mul(a[s], ma, kw), mul(b[s], mb, kw), kk, s >= 4 && kk != (R::N >> 1), kk < g.kc);
   }
 }
 
 // RSW second inverse pair: a = Ĥ, b = ζ̂ = ik V̂ - Uy (x-spectral, per element)
 template <int LOG2N>
-__device__ __forceinline__ void load_eta_zeta(double2 (&v)[8], int t, const Geom& g,
+__device__ __forceinline__ void load_eta_zeta(double2 (&v)[8], const RowIdx<LOG2N>& ri, const Geom& g,
                                               const double2* __restrict__ H,
                                               const double2* __restrict__ V,
-                                              const double2* __restrict__ Uy, int y) {
-  SW_OPAQUE_T(t);
-  constexpr int N = 1 << LOG2N, NT = N / 8, half = N / 2;
+                                              const double2* __restrict__ Uy) {
+  using R = RowIdx<LOG2N>;
   double2 h[8], vv[8], uy[8];
-  int kk[8];
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
-    const int m = t + s * NT;
-    kk[s] = m <= half ? m : N - m;
-    const int o = midx_i(g, kk[s] < g.kc ? kk[s] : 0, y);
-    h[s] = H[o];
-    vv[s] = V[o];
-    uy[s] = Uy[o];
+    h[s] = vv[s] = uy[s] = zero2();
+    if (R::inv_any(g, s)) {
+      const int o = ri.oinv(g, s);
+      h[s] = H[o];
+      vv[s] = V[o];
+      uy[s] = Uy[o];
+    }
   }
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
-    const int m = t + s * NT;
-    double2 aa = h[s], bb = csub(cmul_i(vv[s], kk[s] * g.mk), uy[s]);
-    if (kk[s] == 0) {
-      aa.y = 0.0;
-      bb.y = 0.0;
-    }
-    if (m > half) {
-      aa = cconj(aa);
-      bb = cconj(bb);
-    }
-    const double2 z = make_double2(aa.x - bb.y, aa.y + bb.x);
-    v[s] = kk[s] < g.kc ? z : zero2();
+    const int kk = R::kk(ri.t, s);
+    v[s] = pair_z(h[s], csub(cmul_i(vv[s], kk * g.mk), uy[s]), kk, s >= 4 && kk != (R::N >> 1), kk < g.kc);
   }
 }
 
 // After a forward FFT of z = a + i b (Z[t + s*NT] in v), hand Â[k], B̂[k] for
-// k < kc to emit(k, Â, B̂).  Needs Z[nx-k] from a mirror thread: one LDS
-// round trip.
+// k = t + s NT < kc to emit(k, s, Â, B̂).  Needs Z[nx-k] from a mirror
+// thread: one LDS round trip.
 template <int LOG2N, typename Emit>
 __device__ __forceinline__ void split_pair(const double2 (&v)[8], int t, const Geom& g,
                                            double2* line, Emit emit) {
@@ -344,18 +392,18 @@ __device__ __forceinline__ void split_pair(const double2 (&v)[8], int t, const G
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
     const int k = t + s * NT;
-    if (k < g.kc) {
+    if (RowIdx<LOG2N>::fwd_any(g, s) && k < g.kc) {
       const double2 zk = v[s];
       const double2 zn = line[LP((N - k) & (N - 1))];
       // A = (zk + conj zn) / 2,  B = (zk - conj zn) / (2i)
-      emit(k, make_double2(0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y)),
+      emit(k, s, make_double2(0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y)),
            make_double2(0.5 * (zk.y + zn.y), -0.5 * (zk.x - zn.x)));
     }
   }
 }
 
 // split_pair for C transforms at once (C line buffers `stride` apart, one
-// barrier pair): emit(c, k, Â, B̂).
+// barrier pair): emit(c, k, s, Â, B̂).
 template <int LOG2N, int C, typename Emit>
 __device__ __forceinline__ void split_pairs(const double2 (&v)[C][8], int t, const Geom& g,
                                             double2* line, int stride, Emit emit) {
@@ -370,12 +418,12 @@ __device__ __forceinline__ void split_pairs(const double2 (&v)[C][8], int t, con
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
     const int k = t + s * NT;
-    if (k < g.kc) {
+    if (RowIdx<LOG2N>::fwd_any(g, s) && k < g.kc) {
 #pragma unroll
       for (int c = 0; c < C; ++c) {
         const double2 zk = v[c][s];
         const double2 zn = line[c * stride + LP((N - k) & (N - 1))];
-        emit(c, k, make_double2(0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y)),
+        emit(c, k, s, make_double2(0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y)),
              make_double2(0.5 * (zk.y + zn.y), -0.5 * (zk.x - zn.x)));
       }
     }
@@ -383,11 +431,11 @@ __device__ __forceinline__ void split_pairs(const double2 (&v)[C][8], int t, con
 }
 
 template <int LOG2N>
-__device__ __forceinline__ void store_pair(const double2 (&v)[8], int t, const Geom& g,
+__device__ __forceinline__ void store_pair(const double2 (&v)[8], const RowIdx<LOG2N>& ri, const Geom& g,
                                            double2* line, double2* __restrict__ A,
-                                           double2* __restrict__ B, int y) {
-  split_pair<LOG2N>(v, t, g, line, [&](int k, double2 a, double2 b) {
-    const int o = midx(g, k, y);
+                                           double2* __restrict__ B) {
+  split_pair<LOG2N>(v, ri.t, g, line, [&](int, int s, double2 a, double2 b) {
+    const int o = ri.ofwd(g, s);
     A[o] = a;
     B[o] = b;
   });
@@ -438,6 +486,8 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS), (BlkRo
   const int y = (Bk::NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * Bk::NB + c.ln;
   constexpr int CB = row_lds_lines<MODEL, LOG2N>();
   double2* line = smem + c.ln * CB * FftPlan<LOG2N>::LDS;
+  RowIdx<LOG2N> ri;
+  ri.init(g, c.t, y);
   Twiddles<LOG2N> tws;
   tws.load(c.t, tw);
   const long long MF = g.mfield;
@@ -457,16 +507,16 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS), (BlkRo
     double2 w[2][8];
     // u + i v and η + i ζ, transformed together (fft_lines leaves z[x = t + s*NT])
     if constexpr (CB == 2) {
-      load_pair<LOG2N>(w[0], c.t, g, U, V, y, false);
-      load_eta_zeta<LOG2N>(w[1], c.t, g, H, V, Uy, y);
+      load_pair<LOG2N>(w[0], ri, g, U, V, false);
+      load_eta_zeta<LOG2N>(w[1], ri, g, H, V, Uy);
       fft_pair<LOG2N, +1, CB>(w, c.t, tws, line, LS);
     } else {
       // nx = 8192 (128 VGPRs per thread): one pair at a time, the second
       // pair's loads issued after the first transform; η + iζ (three loads)
       // first, while nothing else is live
-      load_eta_zeta<LOG2N>(w[1], c.t, g, H, V, Uy, y);
+      load_eta_zeta<LOG2N>(w[1], ri, g, H, V, Uy);
       fft_line<LOG2N, +1>(w[1], c.t, tws, line);
-      load_pair<LOG2N>(w[0], c.t, g, U, V, y, false);
+      load_pair<LOG2N>(w[0], ri, g, U, V, false);
       fft_line<LOG2N, +1>(w[0], c.t, tws, line);
     }
     double pc[8];
@@ -478,8 +528,8 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS), (BlkRo
       w[1][s] = make_double2(zeta * u, u * eta);                   // ζu + i uη
     }
     fft_pair<LOG2N, -1, CB>(w, c.t, tws, line, LS);
-    auto emit = [&](int cc, int k, double2 a, double2 b) {
-      const int o = midx(g, k, y);
+    auto emit = [&](int cc, int k, int s, double2 a, double2 b) {
+      const int o = ri.ofwd(g, s);
       if (cc == 0) {
         Mo[o] = cadd(cmul_i(a, -(k * g.mk)), b);
         Mo[MF + o] = a;
@@ -493,7 +543,7 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS), (BlkRo
     } else {
       split_pairs<LOG2N, 1>(reinterpret_cast<const double2(&)[1][8]>(w[0]), c.t, g, line, LS, emit);
       split_pairs<LOG2N, 1>(reinterpret_cast<const double2(&)[1][8]>(w[1]), c.t, g, line, LS,
-                            [&](int, int k, double2 a, double2 b) { emit(1, k, a, b); });
+                            [&](int, int k, int s, double2 a, double2 b) { emit(1, k, s, a, b); });
     }
     // vη (real input: the transform is the spectrum itself)
 #pragma unroll
@@ -503,7 +553,7 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS), (BlkRo
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       const int k = c.t + s * Bk::NT;
-      if (k < g.kc) Mo[4 * MF + midx(g, k, y)] = v[s];
+      if (RowIdx<LOG2N>::fwd_any(g, s) && k < g.kc) Mo[4 * MF + ri.ofwd(g, s)] = v[s];
     }
   } else if constexpr (MODEL == MODEL_TY) {
     // thomasyamada/ThomasYamada.jl:129-262.  Inputs (k_col_inv): 0 ζ, 1 ψ,
@@ -524,14 +574,14 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS), (BlkRo
     const double nRo = -p.Ro;
     double zt[8], ut[8], vt[8], uc[8], vc[8], p6[8], p7[8], p8[8], p9[8], p10[8];
     // ζ + i ut, vt + i uc
-    load_pair_m<LOG2N>(v, c.t, g, F[0], 0, F[2], 0, y);
+    load_pair_m<LOG2N>(v, ri, g, F[0], 0, F[2], 0);
     fft_line<LOG2N, +1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       zt[s] = v[s].x;
       ut[s] = v[s].y;
     }
-    load_pair_m<LOG2N>(v, c.t, g, F[1], 1, F[4], 0, y);
+    load_pair_m<LOG2N>(v, ri, g, F[1], 1, F[4], 0);
     fft_line<LOG2N, +1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
@@ -540,7 +590,7 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS), (BlkRo
       p6[s] = ut[s] * uc[s];
     }
     // vc + i ∂y uc
-    load_pair_m<LOG2N>(v, c.t, g, F[6], 0, F[5], 0, y);
+    load_pair_m<LOG2N>(v, ri, g, F[6], 0, F[5], 0);
     fft_line<LOG2N, +1>(v, c.t, tws, line);
     double2 w[8];
 #pragma unroll
@@ -552,19 +602,19 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS), (BlkRo
       v[s] = make_double2(vt[s] * zt[s], uc[s] * uc[s] - vc[s] * vc[s]);  // p1 + i p4
     }
     fft_line<LOG2N, -1>(w, c.t, tws, line);
-    split_pair<LOG2N>(w, c.t, g, line, [&](int k, double2 a, double2 b) {
+    split_pair<LOG2N>(w, c.t, g, line, [&](int k, int s, double2 a, double2 b) {
       const double kw = k * g.mk;
-      const int o = midx(g, k, y);
+      const int o = ri.ofwd(g, s);
       Mo[o] = cscale(csub(cmul_i(a, kw), cscale(b, kw * kw)), nRo);
       Mo[2 * MF + o] = cscale(b, nRo);
     });
     fft_line<LOG2N, -1>(v, c.t, tws, line);
-    split_pair<LOG2N>(v, c.t, g, line, [&](int k, double2 a, double2 b) {
+    split_pair<LOG2N>(v, c.t, g, line, [&](int k, int s, double2 a, double2 b) {
       const double kw = k * g.mk;
-      Mo[MF + midx(g, k, y)] = cscale(cadd(cmul_i(a, 1.0), cscale(b, kw)), nRo);
+      Mo[MF + ri.ofwd(g, s)] = cscale(cadd(cmul_i(a, 1.0), cscale(b, kw)), nRo);
     });
     // ∂y ut + i ∂x vc
-    load_pair_m<LOG2N>(v, c.t, g, F[3], 0, F[6], 1, y);
+    load_pair_m<LOG2N>(v, ri, g, F[3], 0, F[6], 1);
     fft_line<LOG2N, +1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
@@ -573,11 +623,11 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS), (BlkRo
       v[s] = make_double2(p6[s], p8[s]);
     }
     fft_line<LOG2N, -1>(v, c.t, tws, line);
-    split_pair<LOG2N>(v, c.t, g, line, [&](int k, double2 a, double2 b) {
-      Mo[3 * MF + midx(g, k, y)] = cscale(cadd(cmul_i(a, k * g.mk), b), nRo);
+    split_pair<LOG2N>(v, c.t, g, line, [&](int k, int s, double2 a, double2 b) {
+      Mo[3 * MF + ri.ofwd(g, s)] = cscale(cadd(cmul_i(a, k * g.mk), b), nRo);
     });
     // ∂x vt + i ∂x pc
-    load_pair_m<LOG2N>(v, c.t, g, F[1], 2, F[7], 1, y);
+    load_pair_m<LOG2N>(v, ri, g, F[1], 2, F[7], 1);
     fft_line<LOG2N, +1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
@@ -586,13 +636,13 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS), (BlkRo
       v[s] = make_double2(p7[s], p9[s]);
     }
     fft_line<LOG2N, -1>(v, c.t, tws, line);
-    split_pair<LOG2N>(v, c.t, g, line, [&](int k, double2 a, double2 b) {
-      const int o = midx(g, k, y);
+    split_pair<LOG2N>(v, c.t, g, line, [&](int k, int s, double2 a, double2 b) {
+      const int o = ri.ofwd(g, s);
       Mo[4 * MF + o] = cscale(a, nRo);
       Mo[5 * MF + o] = cscale(b, nRo);
     });
     // ∂y pc
-    load_pair_m<LOG2N>(v, c.t, g, F[8], 0, nullptr, 0, y);
+    load_pair_m<LOG2N>(v, ri, g, F[8], 0, nullptr, 0);
     fft_line<LOG2N, +1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) v[s] = make_double2(p10[s] + vt[s] * v[s].x, 0.0);
@@ -600,31 +650,31 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS), (BlkRo
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       const int k = c.t + s * Bk::NT;
-      if (k < g.kc) Mo[6 * MF + midx(g, k, y)] = cscale(v[s], nRo);
+      if (RowIdx<LOG2N>::fwd_any(g, s) && k < g.kc) Mo[6 * MF + ri.ofwd(g, s)] = cscale(v[s], nRo);
     }
   } else {
     const double2 *Q1 = Mi, *Q2 = Mi + MF, *P1 = Mi + 2 * MF, *P2 = Mi + 3 * MF,
                   *Py1 = Mi + 4 * MF, *Py2 = Mi + 5 * MF;
     double2 q[8];
     // q1 + i q2
-    load_pair<LOG2N>(v, c.t, g, Q1, Q2, y, false);
+    load_pair<LOG2N>(v, ri, g, Q1, Q2, false);
     fft_line<LOG2N, +1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) q[s] = v[s];
     // ψx1 + i ψx2;  ψx q per layer (swqg/TwoLayerQG.jl:169)
-    load_pair<LOG2N>(v, c.t, g, P1, P2, y, true);
+    load_pair<LOG2N>(v, ri, g, P1, P2, true);
     fft_line<LOG2N, +1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) v[s] = make_double2(v[s].x * q[s].x, v[s].y * q[s].y);
     fft_line<LOG2N, -1>(v, c.t, tws, line);
-    store_pair<LOG2N>(v, c.t, g, line, Mo, Mo + MF, y);
+    store_pair<LOG2N>(v, ri, g, line, Mo, Mo + MF);
     // ψy q per layer (:177)
-    load_pair<LOG2N>(v, c.t, g, Py1, Py2, y, false);
+    load_pair<LOG2N>(v, ri, g, Py1, Py2, false);
     fft_line<LOG2N, +1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) v[s] = make_double2(v[s].x * q[s].x, v[s].y * q[s].y);
     fft_line<LOG2N, -1>(v, c.t, tws, line);
-    store_pair<LOG2N>(v, c.t, g, line, Mo + 2 * MF, Mo + 3 * MF, y);
+    store_pair<LOG2N>(v, ri, g, line, Mo + 2 * MF, Mo + 3 * MF);
   }
 }
 
@@ -1528,7 +1578,9 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   Twiddles<LOG2N> tws;
   tws.load(c.t, tw);
   double2 v[8];
-  load_pair<LOG2N>(v, c.t, g, M, nullptr, y, false);
+  RowIdx<LOG2N> ri;
+  ri.init(g, c.t, y);
+  load_pair<LOG2N>(v, ri, g, M, nullptr, false);
   fft_line<LOG2N, +1>(v, c.t, tws, line);
 #pragma unroll
   for (int s = 0; s < 8; ++s) out[(long long)(g.y0 + y) * g.nx + c.t + s * NT] = v[s].x;

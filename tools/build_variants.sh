@@ -1,17 +1,17 @@
 #!/bin/bash
 # Build libsw variants with extra -D flags into sweep_var/<name>.so (perf sweeps).
-# usage: tools/build_variants.sh name1:"-DFOO=1" name2:"-DBAR=2" ...
+# usage: tools/build_variants.sh [--len L] name1:"-DFOO=1" name2:"-DBAR=2" ...
+#   --len L: build transform length 2^L only (fast; benches at that grid only)
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 mkdir -p "$ROOT/sweep_var"
-pids=()
+LEN=None
+if [ "$1" = "--len" ]; then LEN="[$2]"; shift 2; fi
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
-  /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -shared -Wno-unused-result \
-    -I"$ROOT/include" $flags -o "$ROOT/sweep_var/$name.so" \
-    "$ROOT/juliaraytracingsw_amd/csrc/sw_kernels.hip" "$ROOT/juliaraytracingsw_amd/csrc/sw_api.cpp" \
-    -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib &
-  pids+=($!)
+  python3 -c "
+import sys; sys.path.insert(0, '$ROOT')
+from juliaraytracingsw_amd import build
+print(build.build_lib(force=True, out='$ROOT/sweep_var/$name.so', extra_flags='$flags'.split(), parts=$LEN))"
 done
-for p in "${pids[@]}"; do wait $p; done
 ls -la "$ROOT/sweep_var"
