@@ -882,6 +882,32 @@ def rsw_driver_params(nx, Lx=2 * np.pi, aliased_fraction=1 / 3, nnu=4, nutune=20
     return dt, nu
 
 
+def fab3_linear_growth(grid: TwoDGrid, p: RSWParams, dt, order=8):
+    """Largest per-step amplification |z| over the live modes of the linear
+    RSW FilteredAB3 scheme (FF FilteredAB3, SURVEY A7, with the filter applied
+    after the update): sol_{n+1} = filt·(sol_n + dt(23/12 λ sol_n − 16/12 λ
+    sol_{n−1} + 5/12 λ sol_{n−2})) for each eigenvalue λ of the per-mode L
+    (rsw/RotatingShallowWater.jl:242-260): D and D ± iω, D = −ν K^(2nν),
+    ω² = f² + Cg² K².  |z| > 1 means the explicit hyperviscosity outruns the
+    filter and the driver's run blows up (rsw/RSWDriver.jl:213-218)."""
+    K2 = grid.Krsq
+    D = -p.nu * K2 ** p.nnu
+    w = np.sqrt(p.f ** 2 + p.Cg2 * K2)
+    filt = makefilter(grid, order=order)
+    live = grid.live
+    worst = 0.0
+    for lam in (D, D + 1j * w, D - 1j * w):
+        a = dt * lam[live]
+        F = filt[live]
+        co = np.stack([-F * (1 + 23 / 12 * a), F * 16 / 12 * a, -F * 5 / 12 * a], -1)
+        C = np.zeros((a.size, 3, 3), complex)
+        C[:, 0, :] = -co
+        C[:, 1, 0] = 1
+        C[:, 2, 1] = 1
+        worst = max(worst, float(np.abs(np.linalg.eigvals(C)).max()))
+    return worst
+
+
 def qg2_compute_parameters(deformation_radius, intervortex_radius, avg_eddy_velocity, H, f0):
     """swqg/TwoLayerDriver.jl:17-27."""
     c1, c2 = 3.2, 0.36

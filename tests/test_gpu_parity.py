@@ -224,6 +224,66 @@ def test_config1_driver_params_blow_up_like_the_reference():
     prob.close()
 
 
+@pytest.mark.parametrize("n", [512, 1024])
+def test_fab3_driver_params_unstable_grids_report_nan(n):
+    """RSW FilteredAB3 at the RSWDriver parameters is linearly unstable below
+    2048² (tests/test_oracle.py::test_fab3_driver_params_stability_boundary):
+    the run blows up from round-off and libsw reports SW_E_NAN, the driver's
+    throw (rsw/RSWDriver.jl:213-218)."""
+    from juliaraytracingsw_amd import LibSWError, drivers
+
+    prob, _ = drivers.rsw_problem(n, "FilteredAB3")
+    with pytest.raises(LibSWError) as ei:
+        for _ in range(8):
+            prob.stepforward(500)
+    assert ei.value.code == -5
+    prob.close()
+
+
+def test_fab3_driver_params_2048_stays_finite():
+    """The metric configuration is on the stable side of that boundary: 4000
+    steps (0.41 time units) stay finite with the energy bounded."""
+    from juliaraytracingsw_amd import drivers, rotating_shallow_water as RSW
+
+    prob, _ = drivers.rsw_problem(2048, "FilteredAB3")
+    e0 = RSW.energy(prob)
+    prob.stepforward(4000)
+    e1 = RSW.energy(prob)
+    assert np.isfinite(e1) and e1 < 1.1 * e0
+    prob.close()
+
+
+@pytest.mark.parametrize("stepper", ["IFMAB3", "IFMRK4"])
+def test_qg2_energy_records_match_the_undealiased_state_at_driver_params(stepper):
+    """The reference's 2LQG energies read prob.sol after the step
+    (swqg/TwoLayerQG.jl:230-252), aliased modes included.  libsw keeps live
+    modes only; at the TwoLayerDriver set-up (512², q0 =
+    1e-2·randn, swqg/TwoLayerDriver.jl:10-15,29-68) the aliased modes' share
+    of the energy is ~1e-13, so the device-recorded energies match the
+    oracle's UN-dealiased post-step energies to 1e-10 (the strongly nonlinear
+    64² case above shows where that share grows)."""
+    from juliaraytracingsw_amd import two_layer_qg as QG2
+
+    p = sw_cases.case_params(f"qg2_{stepper.lower()}", 512)
+    pr = sw_cases.oracle_problem(p)
+    pr.set_solution(sw_cases.initial_condition(p, pr.grid))
+    prob = sw_cases.libsw_problem(p)
+    prob.sol = pr.sol
+    freq, nsteps = 10, 30
+    KE = QG2.Diagnostic(QG2.kinetic_energy, prob, freq=freq, nsteps=nsteps)
+    PE = QG2.Diagnostic(QG2.potential_energy, prob, freq=freq, nsteps=nsteps)
+    expected = []
+    for s in range(1, nsteps + 1):
+        pr.stepforward(1)
+        if s % freq == 0:
+            expected.append(O.qg2_energies(pr.sol, pr.grid, pr.params))  # full array, not dealiased
+    QG2.stepforward(prob, [KE, PE], nsteps)
+    for i, ((k1, k2), pe) in enumerate(expected, start=1):
+        assert np.allclose(np.atleast_1d(KE.data[i]), (k1, k2), rtol=RTOL, atol=0), (i, KE.data[i], (k1, k2))
+        assert abs(PE.data[i] / pe - 1) < RTOL, (i, PE.data[i], pe)
+    prob.close()
+
+
 def test_invalid_config_fails_loudly():
     from juliaraytracingsw_amd import LibSWError, rotating_shallow_water as RSW
 

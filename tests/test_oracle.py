@@ -362,6 +362,23 @@ def test_config1_fab3_at_driver_nutune_is_unstable():
     assert not np.isfinite(pr.sol).all() or np.abs(pr.sol).max() > 1e6
 
 
+@pytest.mark.parametrize("n,unstable", [(128, True), (512, True), (1024, True), (2048, False)])
+def test_fab3_driver_params_stability_boundary(n, unstable):
+    """RSW FilteredAB3 at the RSWDriver parameters (νtune = 20, cfltune =
+    0.01, filter order 8; rsw/RSWDriver.jl:134-148): the linear scheme's
+    amplification over the live modes.  Below 2048² the explicit
+    hyperviscosity of the corner modes (dt·ν·K⁸ up to ≈ 100 at 512²) outruns
+    the order-8 filter, so BASELINE configs 1 (128²) and 2 (1024²) blow up
+    at the driver's own νtune; from 2048² on the filter wins (|z| = 1 at
+    K = 0)."""
+    dt, nu = O.rsw_driver_params(n)
+    z = O.fab3_linear_growth(O.TwoDGrid(n), O.RSWParams(nu, 4, 3.0, 1.0), dt, order=8)
+    if unstable:
+        assert z > 1.2
+    else:
+        assert z <= 1 + 1e-12
+
+
 # --- golden fixtures -----------------------------------------------------------
 GOLDEN_FILES = sorted(glob.glob(os.path.join(GOLDEN, "*.npz")))
 
