@@ -233,10 +233,12 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
 template <int LOG2N>
 struct RowIdx {
   static constexpr int N = 1 << LOG2N, NT = N / 8;
-  // 8192-point lines (128 VGPRs): offsets recomputed per use from 3 terms
+  // 8192-point lines (128 VGPRs): only t, y are kept; the per-thread terms
+  // are re-derived at each use from an opaque copy of t (SW_OPAQUE_T)
   static constexpr bool kStore = LOG2N < SW_OPAQUE_LOG2;
   int oi[kStore ? 8 : 1];
-  int ia, ib, row0, f0, t, y;
+  int f0s;  // kStore: forward-layout term of k = t
+  int t, y;
   __device__ __forceinline__ static int kk(int t, int s) { return s < 4 ? t + s * NT : N - t - s * NT; }
   // some thread of the row holds a live inverse input s (uniform)
   __device__ __forceinline__ static bool inv_any(const Geom& g, int s) {
@@ -244,24 +246,30 @@ struct RowIdx {
   }
   // some thread holds a live forward output s, k = t + s NT < kc (uniform)
   __device__ __forceinline__ static bool fwd_any(const Geom& g, int s) { return s * NT < g.kc; }
+  // one slab: inverse layout 8 (kk >> 1) + (kk & 1) + row term, forward
+  // layout 2 ny (k >> 1) + (k & 1) + row term (mtile_local, A = 2)
+  __device__ __forceinline__ static int row_inv(const Geom& g, int y) { return (y >> 2) * (g.kcl >> 1) * 8 + (y & 3) * 2; }
+  __device__ __forceinline__ static int fwd0(const Geom& g, int t, int y) {
+    return (y >> 2) * 8 + (y & 3) * 2 + 2 * g.nyl * (t >> 1) + (t & 1);
+  }
   __device__ __forceinline__ int oinv_calc(const Geom& g, int s) const {
-    const int k = kk(t, s);
-    if (SW_ROW_CLOSED && g.nslab == 1)
-      return k < g.kc ? (s < 4 ? ia + 4 * NT * s : ib + 4 * NT * (8 - s)) : row0;
+    int tt = t;
+    SW_OPAQUE_T(tt);
+    const int k = kk(tt, s);
+    if (SW_ROW_CLOSED && g.nslab == 1) {
+      const int r0 = row_inv(g, y);
+      if (k >= g.kc) return r0;
+      return s < 4 ? r0 + 8 * (tt >> 1) + (tt & 1) + 4 * NT * s : r0 - 4 * tt - 3 * (tt & 1) + 4 * NT * (8 - s);
+    }
     return midx_i(g, k < g.kc ? k : 0, y);
   }
   __device__ __forceinline__ void init(const Geom& g, int t_, int y_) {
     t = t_;
     y = y_;
-    // one slab: inverse layout 8 (kk >> 1) + (kk & 1) + row term, forward
-    // layout 2 ny (k >> 1) + (k & 1) + row term (mtile_local, A = 2)
-    row0 = (y >> 2) * (g.kcl >> 1) * 8 + (y & 3) * 2;
-    ia = row0 + 8 * (t >> 1) + (t & 1);
-    ib = row0 - 4 * t - 3 * (t & 1);
-    f0 = (y >> 2) * 8 + (y & 3) * 2 + 2 * g.nyl * (t >> 1) + (t & 1);
     if constexpr (kStore) {
 #pragma unroll
       for (int s = 0; s < 8; ++s) oi[s] = oinv_calc(g, s);
+      f0s = fwd0(g, t, y);
     }
   }
   __device__ __forceinline__ int oinv(const Geom& g, int s) const {
@@ -276,8 +284,10 @@ struct RowIdx {
 #ifdef SW_EXP_NOHBM
     return t & 1;
 #endif
-    if (SW_ROW_CLOSED && g.nslab == 1) return f0 + s * NT * g.nyl;
-    return midx(g, t + s * NT, y);
+    int tt = t;
+    SW_OPAQUE_T(tt);
+    if (SW_ROW_CLOSED && g.nslab == 1) return (kStore ? f0s : fwd0(g, tt, y)) + s * NT * g.nyl;
+    return midx(g, tt + s * NT, y);
   }
 };
 
