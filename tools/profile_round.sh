@@ -10,6 +10,11 @@ mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || exit 1
 echo "bench done"
+# the bench command itself under the kernel tracer: its col_step/row averages
+# must agree with the HIP-event averages bench.py reports (roofline)
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_bench -o run -- python bench.py --no-cpu-baseline > $O/bench_traced.json 2> $O/bench_traced.err || exit 10
+cp $(find $O/trace_bench -name '*kernel_stats.csv') $O/kernel_stats_bench.csv || exit 11
+echo "traced bench done"
 # model grid stepper steps
 CONFIGS="rsw:2048:FilteredAB3:20 rsw:1024:FilteredAB3:20 qg2:2048:IFMAB3:20 rsw:4096:FilteredAB3:10 qg2:8192:IFMRK4:4"
 for c in $CONFIGS; do
