@@ -68,6 +68,7 @@ struct sw_ctx {
   int head = 0;
   bool mixed_valid = false;                  // mir == transposed col_inv(sol) (fused pipeline primed)
   bool fuse_all = false;                     // SW_FUSE_ALL=1: fused pass for every pair (experiments)
+  bool stream_state = false;                 // state/history accesses non-temporal (StepPtrs::stream)
   double2* stage = nullptr;                  // full (nkr,nl,nf) staging
   float* stage32 = nullptr;                  // SW_PREC_F32: the caller-precision copy of stage / dflt
   double2* gbuf = nullptr;                   // dist: all-gathered compact slabs
@@ -248,6 +249,16 @@ double kernel_bytes(const sw_ctx* c, int kid) {
     }
   }
   return b;
+}
+
+bool use_fused(const sw_ctx* c);
+static double step_bytes(const sw_ctx* c) {
+  const int st = c->cfg.stepper;  // four calcN + update stages per RK4-family step
+  const int nstage = (st == SW_STEP_IFMRK4 || st == SW_STEP_ETDRK4 || st == SW_STEP_FILTERED_RK4) ? 4 : 1;
+  if (!use_fused(c))
+    return nstage * (kernel_bytes(c, K_COLINV) + kernel_bytes(c, K_ROW) + kernel_bytes(c, K_COLFWD) +
+                     kernel_bytes(c, K_UPD));
+  return nstage * (kernel_bytes(c, K_ROW) + kernel_bytes(c, K_COLSTEP));  // primed pipeline
 }
 
 struct Timer {
@@ -469,6 +480,7 @@ sw::StepPtrs step_ptrs(const sw_ctx* c, const Slab& s) {
   a.sol_out = (st == SW_STEP_FILTERED_AB3) ? s.sol2 : s.sol;
   a.xs = s.xs;
   a.euler = (c->step < 3 || c->step < c->euler_until) ? 1 : 0;
+  a.stream = c->stream_state ? 1 : 0;
   if (st == SW_STEP_IFMRK4 || st == SW_STEP_FILTERED_RK4) {
     a.h0 = s.acc;
   } else if (st == SW_STEP_ETDRK4) {
@@ -824,6 +836,9 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
     const Geom& g = c->sl[0].g;
     if (g.kc <= 0 || g.Lr <= 0 || g.lc > g.lr2) return fail(c, SW_E_INVALID, "degenerate dealiasing geometry");
   }
+  // device ipow is unrolled over 8 exponent bits (sw_internal.hpp)
+  if (k.nnu < 0 || k.nnu > 255 || k.filter_order < 0 || k.filter_order > 255)
+    return fail(c, SW_E_INVALID, "nnu and filter_order must be in [0, 255]");
 
   Phys& p = c->p;
   p.f = k.f;
@@ -921,6 +936,14 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (const char* e = std::getenv("SW_FUSE_ALL")) c->fuse_all = e[0] == '1';
+  // Cache policy of the stepper state (sw_kernels.hip state_ld): a step
+  // whose traffic on this GPU exceeds the 256 MiB Infinity Cache evicts the
+  // state before the next step reads it, so the state goes non-temporal and
+  // the cache keeps the mixed fields between the passes instead (2048²
+  // FilteredAB3 +7 %); a smaller step keeps the state cached (1024² +9 %
+  // temporal).  SW_STREAM_STATE=0/1 overrides.
+  c->stream_state = step_bytes(c) > 256.0 * 1024 * 1024;
+  if (const char* e = std::getenv("SW_STREAM_STATE")) c->stream_state = e[0] == '1';
   // experiments (tools/sweep.sh): SW_CHECK_NAN=0 disables the NaN check of sw_step
   if (const char* e = std::getenv("SW_CHECK_NAN")) c->cfg.check_nan = e[0] == '1';
   c->stats.resize(K_NKERN);
@@ -1317,12 +1340,7 @@ int sw_profile_steps(sw_ctx* c, int64_t nsteps, sw_kernel_stat* out, int32_t max
 
 double sw_step_alg_bytes(const sw_ctx* c) {
   if (!ready(c)) return 0.0;
-  const int st = c->cfg.stepper;  // four calcN + update stages per RK4-family step
-  const int nstage = (st == SW_STEP_IFMRK4 || st == SW_STEP_ETDRK4 || st == SW_STEP_FILTERED_RK4) ? 4 : 1;
-  if (!use_fused(c))
-    return nstage * (kernel_bytes(c, K_COLINV) + kernel_bytes(c, K_ROW) + kernel_bytes(c, K_COLFWD) +
-                     kernel_bytes(c, K_UPD));
-  return nstage * (kernel_bytes(c, K_ROW) + kernel_bytes(c, K_COLSTEP));  // primed pipeline
+  return step_bytes(c);
 }
 
 // the ring slot holding RHS/N of `slot` steps ago (1 or 2), -1 if none

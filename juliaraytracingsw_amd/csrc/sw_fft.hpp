@@ -122,6 +122,11 @@ struct FftPlan {
 #ifndef SW_TWFLY_LOG2
 #define SW_TWFLY_LOG2 13  // lines of at least 2^this read their stage twiddles per stage
 #endif
+// lines of at least 2^this form the seven powers of a radix-8 stage's
+// twiddle as a chain (two live at a time) instead of all at once
+#ifndef SW_TW_CHAIN_LOG2
+#define SW_TW_CHAIN_LOG2 13
+#endif
 template <int LOG2N>
 struct Twiddles {
   static constexpr bool kPreload = LOG2N < SW_TWFLY_LOG2;
@@ -230,7 +235,7 @@ __device__ __forceinline__ void fft_lines(double2 (&v)[C][8], int t, const Twidd
 #endif
       const double2 wt = Twiddles<LOG2N>::kPreload ? tw1[ti] : tws.get(ti);
       const double2 w1 = DIR < 0 ? wt : cconj(wt);
-      if constexpr (Twiddles<LOG2N>::kPreload) {
+      if constexpr (Twiddles<LOG2N>::kPreload && LOG2N < SW_TW_CHAIN_LOG2) {
         const double2 w2 = cmul(w1, w1), w3 = cmul(w2, w1), w4 = cmul(w2, w2);
         const double2 w5 = cmul(w4, w1), w6 = cmul(w3, w3), w7 = cmul(w4, w3);
 #pragma unroll
@@ -244,7 +249,7 @@ __device__ __forceinline__ void fft_lines(double2 (&v)[C][8], int t, const Twidd
           v[c][7] = cmul(v[c][7], w7);
         }
       } else {
-        // 128-VGPR budget (8192): powers formed as a chain, two live at a time
+        // register budget (8192; SW_TW_CHAIN_LOG2): powers formed as a chain, two live at a time
         double2 wp = w1;
 #pragma unroll
         for (int r = 1; r < 8; ++r) {

@@ -132,13 +132,16 @@ __host__ __device__ inline int midc(const Geom& g, int krl, int y) { return mtil
 __host__ __device__ inline int midc_i(const Geom& g, int krl, int y) { return mtile_c<SW_TILE_I, SW_LORD_I>(g, krl, y); }
 __host__ __device__ inline int midx_i(const Geom& g, int kr, int yl) { return mtile_x<SW_TILE_I, SW_LORD_I>(g, kr, yl); }
 
-// integer power x^n (n >= 0) by repeated squaring
+// integer power x^n (0 <= n < 256, sw_create checks) by repeated squaring:
+// the products of the loop `while (n) { if (n & 1) r *= x; x *= x; n >>= 1; }`
+// in the same order, unrolled over 8 bits with selects, so the update
+// kernels have no control flow here (loads of several modes issue together)
 __host__ __device__ inline double ipow(double x, int n) {
   double r = 1.0;
-  while (n > 0) {
-    if (n & 1) r *= x;
-    x *= x;
-    n >>= 1;
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    r = ((n >> b) & 1) ? r * x : r;
+    x = x * x;
   }
   return r;
 }
@@ -147,10 +150,21 @@ __host__ __device__ inline double ipow(double x, int n) {
 // filt = exp(-decay (K-innerK)^order) for K >= innerK, else 1.
 __host__ __device__ inline double filter_value(const Geom& g, const Phys& p, double k, double l) {
 #pragma clang fp contract(off)
+#ifdef SW_EXP_NOFILT  // experiment: filter evaluation cost (wrong results)
+  return 1.0 + k * l;
+#endif
   const double a = k * g.dx / 3.14159265358979323846, b = l * g.dy / 3.14159265358979323846;
   const double K = sqrt(a * a + b * b);
-  if (K < p.innerK) return 1.0;
-  return exp(-p.decay * ipow(K - p.innerK, p.forder));
+#ifdef SW_FILT_SELECT
+  const double f = exp(-p.decay * ipow(K - p.innerK, p.forder));
+  return K < p.innerK ? 1.0 : f;  // select, no branch
+#else
+  // exp only where the filter acts (a wave whose modes are all inside
+  // innerK skips it: most waves of the low-wavenumber columns)
+  double f = 1.0;
+  if (K >= p.innerK) f = exp(-p.decay * ipow(K - p.innerK, p.forder));
+  return f;
+#endif
 }
 
 struct cplx {
@@ -398,6 +412,7 @@ struct StepPtrs {
   double2* xs;        // IFMRK4 stages 1-3: the stage input written for the next calcN
   int euler;
   int stage;
+  int stream;  // state/history accesses non-temporal (step traffic beyond the Infinity Cache)
   // ETDRK4 (FF ETDRK4TimeStepper): N₁, N₂, the second stage input s₂ and
   // the per-mode coefficient table [E, E2, ζ, α, β, Γ][cfield]
   double2* n1;

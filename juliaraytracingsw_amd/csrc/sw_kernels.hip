@@ -11,6 +11,58 @@
 
 namespace sw {
 
+// Cache policy.  A step streams ≈ 2.5× the 256 MB Infinity Cache (MALL) at
+// 2048²; what is worth keeping there is a mixed field between the kernel
+// that writes it and the next one, which reads it.  Data read or written
+// once per step (the stepper state and history) and mixed fields once read
+// go non-temporal, so they do not evict the mixed fields in flight.
+__device__ __forceinline__ double2 ld_nt(const double2* p) {
+  return make_double2(__builtin_nontemporal_load(&p->x), __builtin_nontemporal_load(&p->y));
+}
+__device__ __forceinline__ void st_nt(double2* p, double2 v) {
+  __builtin_nontemporal_store(v.x, &p->x);
+  __builtin_nontemporal_store(v.y, &p->y);
+}
+// stepper state / history (read and written once per step): non-temporal
+// when NT — the launchers set it (StepPtrs::stream) where a step's traffic
+// exceeds what the Infinity Cache holds (sw_api.cpp); below that the state
+// itself stays cached from one step to the next and temporal wins (1024²
+// FilteredAB3: 19.2k temporal vs 17.6k non-temporal steps/s; 2048²: 5.5k vs
+// 5.9k).  SW_STATE_T forces temporal (experiments).
+template <bool NT>
+__device__ __forceinline__ double2 state_ld(const double2* p) {
+#ifndef SW_STATE_T
+  if constexpr (NT) return ld_nt(p);
+#endif
+  return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void state_st(double2* p, double2 v) {
+#ifndef SW_STATE_T
+  if constexpr (NT) {
+    st_nt(p, v);
+    return;
+  }
+#endif
+  *p = v;
+}
+// mixed-field reads: the row pass's inverse inputs, the column pass's
+// forward inputs (read once; their writer's stores stay temporal)
+__device__ __forceinline__ double2 mix_ld_row(const double2* p) {
+#ifdef SW_MIX_NT_ROW
+  return ld_nt(p);
+#else
+  return *p;
+#endif
+}
+__device__ __forceinline__ double2 mix_ld_col(const double2* p) {
+#ifdef SW_MIX_NT_COL
+  return ld_nt(p);
+#else
+  return *p;
+#endif
+}
+
 // block -> line mapping.  When one line per block and the grid is a multiple
 // of 64, the 8 lines (columns, or rows in the row pass) that share each 128-B
 // chunk of a mixed layout are placed on blocks b, b+8, …, b+56, which the
@@ -273,7 +325,7 @@ struct RowIdx {
     }
   }
   __device__ __forceinline__ int oinv(const Geom& g, int s) const {
-#ifdef SW_EXP_NOHBM  // experiment: every load from one address (L1 hits), no HBM traffic
+#if defined(SW_EXP_NOHBM) || defined(SW_EXP_NOLOAD)  // experiment: every load from one address (L1 hits)
     return 0;
 #endif
     if constexpr (kStore) return oi[s];
@@ -281,7 +333,7 @@ struct RowIdx {
   }
   // forward-layout offset of output s (k = t + s NT)
   __device__ __forceinline__ int ofwd(const Geom& g, int s) const {
-#ifdef SW_EXP_NOHBM
+#if defined(SW_EXP_NOHBM) || defined(SW_EXP_NOSTORE)  // experiment: every store to two addresses
     return t & 1;
 #endif
     int tt = t;
@@ -317,8 +369,8 @@ __device__ __forceinline__ void load_pair(double2 (&v)[8], const RowIdx<LOG2N>& 
     a[s] = b[s] = zero2();
     if (R::inv_any(g, s)) {
       const int o = ri.oinv(g, s);
-      a[s] = A[o];
-      if (B) b[s] = B[o];
+      a[s] = mix_ld_row(A + o);
+      if (B) b[s] = mix_ld_row(B + o);
     }
   }
 #pragma unroll
@@ -347,8 +399,8 @@ __device__ __forceinline__ void load_pair_m(double2 (&v)[8], const RowIdx<LOG2N>
     a[s] = b[s] = zero2();
     if (R::inv_any(g, s)) {
       const int o = ri.oinv(g, s);
-      a[s] = A[o];
-      if (B) b[s] = B[o];
+      a[s] = mix_ld_row(A + o);
+      if (B) b[s] = mix_ld_row(B + o);
     }
   }
   auto mul = [](double2 x, int mm, double kw) {
@@ -375,9 +427,9 @@ __device__ __forceinline__ void load_eta_zeta(double2 (&v)[8], const RowIdx<LOG2
     h[s] = vv[s] = uy[s] = zero2();
     if (R::inv_any(g, s)) {
       const int o = ri.oinv(g, s);
-      h[s] = H[o];
-      vv[s] = V[o];
-      uy[s] = Uy[o];
+      h[s] = mix_ld_row(H + o);
+      vv[s] = mix_ld_row(V + o);
+      uy[s] = mix_ld_row(Uy + o);
     }
   }
 #pragma unroll
@@ -758,7 +810,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   auto load_col = [&](const double2* Mfield) {
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      const double2 t = Mfield[midc(g, krA, c.t + s * NT)];
+      const double2 t = mix_ld_col(Mfield + midc(g, krA, c.t + s * NT));
       v[s] = live ? t : zero2();
     }
   };
@@ -870,6 +922,23 @@ __device__ __forceinline__ void store_vec(double2* __restrict__ X, long long cf,
   for (int f = 0; f < NF; ++f) X[f * cf + i] = make_double2(x[f].re, x[f].im);
 }
 
+// the same for data used once per step (state_ld / state_st policy)
+template <int NF, bool NT>
+__device__ __forceinline__ void load_vec_once(const double2* __restrict__ X, long long cf, long long i,
+                                              cplx x[NF]) {
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    const double2 t = state_ld<NT>(X + f * cf + i);
+    x[f] = cx(t.x, t.y);
+  }
+}
+template <int NF, bool NT>
+__device__ __forceinline__ void store_vec_once(double2* __restrict__ X, long long cf, long long i,
+                                               const cplx x[NF]) {
+#pragma unroll
+  for (int f = 0; f < NF; ++f) state_st<NT>(X + f * cf + i, make_double2(x[f].re, x[f].im));
+}
+
 template <int NF>
 __device__ __forceinline__ void matvec(const cplx M[NF][NF], const cplx x[NF], cplx y[NF]) {
 #pragma clang fp contract(off)
@@ -889,52 +958,62 @@ __device__ __forceinline__ void matvec(const cplx M[NF][NF], const cplx x[NF], c
 //   RHS_F = N_F + (L·sol)_F;  x_F = sol_F + dt·(Euler | AB3);  x_F *= filter.
 // Reads the old state (all fields, for L·sol) from a.sol and writes the new
 // field to a.sol_out (a separate buffer, so fields can be updated one by one).
+// The update proper, on operands already in registers: the old state s (all
+// fields) and field F's RHS₋₁, RHS₋₂ (r1, r2; unused on Euler steps).
+// Returns the new field F (x) and its RHS (history entry).  Branch-free
+// (Euler/AB3 by select), so a kernel can issue several modes' loads at once.
 template <int NF, int F>
-__device__ __forceinline__ cplx op_fab3_field(const Geom& g, const Phys& p, const StepPtrs& a,
-                                              long long i, double k, double l, cplx n) {
+__device__ __forceinline__ void fab3_compute(const Geom& g, const Phys& p, int euler, double k, double l, cplx n,
+                                             const cplx (&s)[NF], double2 r1, double2 r2, cplx& x, cplx& rhs) {
 #pragma clang fp contract(off)
-  const long long cf = g.cfield;
-  cplx L[NF][NF], s[NF];
+  cplx L[NF][NF];
   model_L<NF>(p, k, l, L);
-  load_vec<NF>(a.sol, cf, i, s);
   const double filt = filter_value(g, p, k, l);
   const double dt = p.dt;
   cplx Ls = cx(0.0);
 #pragma unroll
   for (int cc = 0; cc < NF; ++cc) Ls = Ls + L[F][cc] * s[cc];
-  const cplx rhs = cx(n.re + Ls.re, n.im + Ls.im);
-  cplx x;
-  if (a.euler) {
-    x = s[F] + dt * rhs;
-  } else {
-    const double2 r1 = a.h1[F * cf + i], r2 = a.h2[F * cf + i];
-    x = s[F] + dt * cx(23.0 / 12 * rhs.re - 16.0 / 12 * r1.x + 5.0 / 12 * r2.x,
-                       23.0 / 12 * rhs.im - 16.0 / 12 * r1.y + 5.0 / 12 * r2.y);
-  }
-  x = cx(x.re * filt, x.im * filt);
-  a.h0[F * cf + i] = make_double2(rhs.re, rhs.im);
-  a.sol_out[F * cf + i] = make_double2(x.re, x.im);
+  rhs = cx(n.re + Ls.re, n.im + Ls.im);
+  const cplx xe = s[F] + dt * rhs;
+  const cplx xa = s[F] + dt * cx(23.0 / 12 * rhs.re - 16.0 / 12 * r1.x + 5.0 / 12 * r2.x,
+                                 23.0 / 12 * rhs.im - 16.0 / 12 * r1.y + 5.0 / 12 * r2.y);
+  const cplx xx = euler ? xe : xa;
+  x = cx(xx.re * filt, xx.im * filt);
+}
+
+template <int NF, int F, bool NT>
+__device__ __forceinline__ cplx op_fab3_field(const Geom& g, const Phys& p, const StepPtrs& a,
+                                              long long i, double k, double l, cplx n) {
+  const long long cf = g.cfield;
+  cplx s[NF];
+  load_vec_once<NF, NT>(a.sol, cf, i, s);
+  // read even on Euler steps (in bounds); history is used once per step
+  const double2 r1 = state_ld<NT>(a.h1 + F * cf + i), r2 = state_ld<NT>(a.h2 + F * cf + i);
+  cplx x, rhs;
+  fab3_compute<NF, F>(g, p, a.euler, k, l, n, s, r1, r2, x, rhs);
+  state_st<NT>(a.h0 + F * cf + i, make_double2(rhs.re, rhs.im));
+  a.sol_out[F * cf + i] = make_double2(x.re, x.im);  // the next col_inv reads it
   return x;
 }
 
-template <int NF>
+template <int NF, bool NT>
 __device__ __forceinline__ void op_fab3(const Geom& g, const Phys& p, const StepPtrs& a, long long i,
                                         double k, double l, const cplx n[NF], cplx x[NF]) {
-  x[0] = op_fab3_field<NF, 0>(g, p, a, i, k, l, n[0]);
-  x[1] = op_fab3_field<NF, 1>(g, p, a, i, k, l, n[1]);
-  if constexpr (NF == 3) x[2] = op_fab3_field<NF, 2>(g, p, a, i, k, l, n[2]);
+  x[0] = op_fab3_field<NF, 0, NT>(g, p, a, i, k, l, n[0]);
+  x[1] = op_fab3_field<NF, 1, NT>(g, p, a, i, k, l, n[1]);
+  if constexpr (NF == 3) x[2] = op_fab3_field<NF, 2, NT>(g, p, a, i, k, l, n[2]);
 }
 
 // utils/IFMAB3.jl:129-160: Euler for step < 3, else AB3 with E N₋₁, E2 N₋₂;
 // then sol = E·(…); filter.  N becomes history.  E = exp(dt L), E2 =
 // exp(2 dt L) evaluated per mode in closed form (sw_internal.hpp ExpOf).
-template <int NF>
+template <int NF, bool NT>
 __device__ __forceinline__ void op_ifmab3(const Geom& g, const Phys& p, const StepPtrs& a, long long i,
                                           double k, double l, const cplx n[NF], cplx x[NF]) {
 #pragma clang fp contract(off)
   const long long cf = g.cfield;
   cplx s[NF], y[NF];
-  load_vec<NF>(a.sol, cf, i, s);
+  load_vec_once<NF, NT>(a.sol, cf, i, s);
   const double dt = p.dt;
   const auto E = ExpOf<NF>::make(p, k, l, dt);
   if (a.euler) {
@@ -942,8 +1021,8 @@ __device__ __forceinline__ void op_ifmab3(const Geom& g, const Phys& p, const St
     for (int f = 0; f < NF; ++f) y[f] = s[f] + dt * n[f];
   } else {
     cplx r1[NF], r2[NF], e1[NF], e2[NF];
-    load_vec<NF>(a.h1, cf, i, r1);
-    load_vec<NF>(a.h2, cf, i, r2);
+    load_vec_once<NF, NT>(a.h1, cf, i, r1);
+    load_vec_once<NF, NT>(a.h2, cf, i, r2);
     exp_apply(p, E, r1, e1);
     exp_apply(p, exp_double(p, E, dt), r2, e2);
 #pragma unroll
@@ -957,8 +1036,8 @@ __device__ __forceinline__ void op_ifmab3(const Geom& g, const Phys& p, const St
 #pragma unroll
     for (int f = 0; f < NF; ++f) x[f] = cx(x[f].re * filt, x[f].im * filt);
   }
-  store_vec<NF>(a.h0, cf, i, n);
-  store_vec<NF>(a.sol_out, cf, i, x);
+  store_vec_once<NF, NT>(a.h0, cf, i, n);
+  store_vec<NF>(a.sol_out, cf, i, x);  // the next col_inv reads it
 }
 
 // Lawson IF-RK4, one calcN result per stage, H = exp(dt L / 2)
@@ -1119,11 +1198,11 @@ __device__ __forceinline__ void op_frk4(const Geom& g, const Phys& p, const Step
   }
 }
 
-template <int NF, int OP>
+template <int NF, int OP, bool NT = false>
 __device__ __forceinline__ void step_op(const Geom& g, const Phys& p, const StepPtrs& a, long long i,
                                         double k, double l, const cplx n[NF], cplx x[NF]) {
-  if constexpr (OP == OP_FAB3) op_fab3<NF>(g, p, a, i, k, l, n, x);
-  else if constexpr (OP == OP_IFMAB3) op_ifmab3<NF>(g, p, a, i, k, l, n, x);
+  if constexpr (OP == OP_FAB3) op_fab3<NF, NT>(g, p, a, i, k, l, n, x);
+  else if constexpr (OP == OP_IFMAB3) op_ifmab3<NF, NT>(g, p, a, i, k, l, n, x);
   else if constexpr (OP == OP_ETDRK4) op_etdrk4<NF>(g, p, a, i, n, x);
   else if constexpr (OP == OP_FRK4) op_frk4<NF>(g, p, a, i, k, l, n, x);
   else op_rk4<NF>(g, p, a, i, k, l, n, x);
@@ -1172,7 +1251,7 @@ static __global__ void __launch_bounds__(256) k_etd_coeffs(Geom g, Phys p, doubl
 
 // Elementwise (unfused) stepper kernel: N from memory; the stage input x is
 // written to xs (RK4 stages 1-3) for a separate col_inv.
-template <int NF, int OP>
+template <int NF, int OP, bool NT>
 static __global__ void __launch_bounds__(256) k_step_elem(Geom g, Phys p, StepPtrs a, const double2* __restrict__ N,
                             double2* __restrict__ xs) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1180,8 +1259,8 @@ static __global__ void __launch_bounds__(256) k_step_elem(Geom g, Phys p, StepPt
   if (i >= g.cfield || !mode_of(g, i, kr, j)) return;
   const double k = kr * g.mk, l = lwav(g, lrow_of(g, j));
   cplx n[NF], x[NF];
-  load_vec<NF>(N, g.cfield, i, n);
-  step_op<NF, OP>(g, p, a, i, k, l, n, x);
+  load_vec_once<NF, NT>(N, g.cfield, i, n);  // last use of this calcN output
+  step_op<NF, OP, NT>(g, p, a, i, k, l, n, x);
   if (OP == OP_RK4 && a.stage < 4) store_vec<NF>(a.xs, g.cfield, i, x);
 }
 
@@ -1222,7 +1301,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   auto load_col = [&](const double2* Mfield) {
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      const double2 t = Mfield[midc(g, krA, c.t + s * NT)];
+      const double2 t = mix_ld_col(Mfield + midc(g, krA, c.t + s * NT));
       v[s] = live ? t : zero2();
     }
   };
@@ -1255,9 +1334,9 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
         if (live && j >= 0) {
           const long long i = (long long)krl * g.LrP + j;
           const cplx nf = cx(n[s].x, n[s].y);
-          if (f == 0) op_fab3_field<NF, 0>(g, p, a, i, k, lwav(g, m), nf);
-          else if (f == 1) op_fab3_field<NF, 1>(g, p, a, i, k, lwav(g, m), nf);
-          else op_fab3_field<NF, (NF == 3 ? 2 : 1)>(g, p, a, i, k, lwav(g, m), nf);
+          if (f == 0) op_fab3_field<NF, 0, false>(g, p, a, i, k, lwav(g, m), nf);
+          else if (f == 1) op_fab3_field<NF, 1, false>(g, p, a, i, k, lwav(g, m), nf);
+          else op_fab3_field<NF, (NF == 3 ? 2 : 1), false>(g, p, a, i, k, lwav(g, m), nf);
         }
         SW_SLOT_FENCE(s);
       }
@@ -1357,7 +1436,10 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
 //   f=2: N_η = F(Q) - il F((vη)^)     -> η -> H
 // three y-FFTs per block, N never in HBM, old/new state in separate buffers.
 // ===========================================================================
-template <int LOG2N>
+#ifndef SW_CS_GROUP
+#define SW_CS_GROUP 2  // slots per load group of the fused FilteredAB3 update
+#endif
+template <int LOG2N, bool STREAM>
 static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     k_col_step_fab3_rsw(Geom g, Phys p, StepPtrs a, const double2* __restrict__ Mf,
                         double2* __restrict__ Minv, const double2* __restrict__ tw, int fbase) {
@@ -1389,42 +1471,82 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   const long long MF = g.mfield;
   double2 v[8], n[8];
 
-  auto load_col = [&](const double2* Mfield) {
+  auto load_col = [&](double2 (&dst)[8], const double2* Mfield) {
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      const double2 t = Mfield[midc(g, krA, c.t + s * NT)];
-      v[s] = live ? t : zero2();
+#ifdef SW_EXP_CS_NOMIX  // experiment: mixed-field loads from one line (wrong results)
+      const double2 t = Mfield[c.t & 7];
+#else
+      const double2 t = mix_ld_col(Mfield + midc(g, krA, c.t + s * NT));
+#endif
+      dst[s] = live ? t : zero2();
     }
   };
+  const NTerms nt = nterms<MODEL_RSW>(f);
   // ---- N_f (rsw/RotatingShallowWater.jl:174-226; nterms)
-  {
-    const NTerms nt = nterms<MODEL_RSW>(f);
-    load_col(Mf + nt.fa * MF);
+  load_col(v, Mf + nt.fa * MF);
+  fft_line<LOG2N, -1>(v, c.t, tws, line);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) n[s] = apply_mul(v[s], nt.ma, k, lwav(g, c.t + s * NT));
+  if (nt.fb >= 0) {
+    load_col(v, Mf + nt.fb * MF);
     fft_line<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
-    for (int s = 0; s < 8; ++s) n[s] = apply_mul(v[s], nt.ma, k, lwav(g, c.t + s * NT));
-    if (nt.fb >= 0) {
-      load_col(Mf + nt.fb * MF);
-      fft_line<LOG2N, -1>(v, c.t, tws, line);
-#pragma unroll
-      for (int s = 0; s < 8; ++s) n[s] = cadd(n[s], apply_mul(v[s], nt.mb, k, lwav(g, c.t + s * NT)));
-    }
+    for (int s = 0; s < 8; ++s) n[s] = cadd(n[s], apply_mul(v[s], nt.mb, k, lwav(g, c.t + s * NT)));
   }
-  // ---- FilteredAB3 update of field f on the live modes; x = new field f
+  // ---- FilteredAB3 update of field f on the live modes; x = new field f.
+  // Slots in groups of SW_CS_GROUP: all loads of a group are issued before
+  // the first is used (in-bounds clamped addresses, branch-free arithmetic;
+  // dead modes are computed and dropped), one memory round trip per group
+  // instead of two per slot.
   double2 x[8];
+  {
+    const long long cf = g.cfield;
+    // compact fields hold the kcn live columns only: padding lines of a
+    // multi-line block (krl in [kcn, kcl)) read column 0 and store nothing
+    const long long cb = (long long)(live ? krl : 0) * g.LrP;
+    const double2* S = a.sol + cb;
+    const double2* H1 = a.h1 + f * cf + cb;
+    const double2* H2 = a.h2 + f * cf + cb;
+    constexpr int G = SW_CS_GROUP;
 #pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    const int m = c.t + s * NT;
-    const int j = compact_of(g, m);
-    x[s] = zero2();
-    if (live && j >= 0) {
-      const long long i = (long long)krl * g.LrP + j;
-      const cplx nf = cx(n[s].x, n[s].y);
-      cplx r;
-      if (f == 0) r = op_fab3_field<3, 0>(g, p, a, i, k, lwav(g, m), nf);
-      else if (f == 1) r = op_fab3_field<3, 1>(g, p, a, i, k, lwav(g, m), nf);
-      else r = op_fab3_field<3, 2>(g, p, a, i, k, lwav(g, m), nf);
-      x[s] = make_double2(r.re, r.im);
+    for (int s0 = 0; s0 < 8; s0 += G) {
+      cplx st[G][3];
+      double2 r1[G], r2[G];
+#pragma unroll
+      for (int q = 0; q < G; ++q) {
+        const int j = compact_of(g, c.t + (s0 + q) * NT);
+        const int jc = j >= 0 ? j : 0;
+#pragma unroll
+        for (int cc = 0; cc < 3; ++cc) {
+          const double2 t = state_ld<STREAM>(S + cc * cf + jc);
+          st[q][cc] = cx(t.x, t.y);
+        }
+        r1[q] = state_ld<STREAM>(H1 + jc);
+        r2[q] = state_ld<STREAM>(H2 + jc);
+      }
+#pragma unroll
+      for (int q = 0; q < G; ++q) {
+        const int s = s0 + q;
+        const int m = c.t + s * NT;
+        const int j = compact_of(g, m);
+        const double l = lwav(g, m);
+        const cplx nf = cx(n[s].x, n[s].y);
+        cplx r, rhs;
+        if (f == 0) fab3_compute<3, 0>(g, p, a.euler, k, l, nf, st[q], r1[q], r2[q], r, rhs);
+        else if (f == 1) fab3_compute<3, 1>(g, p, a.euler, k, l, nf, st[q], r1[q], r2[q], r, rhs);
+        else fab3_compute<3, 2>(g, p, a.euler, k, l, nf, st[q], r1[q], r2[q], r, rhs);
+#ifdef SW_EXP_CS_NOUPD  // experiment: no stepper update (no state traffic; wrong results)
+        r = nf;
+#endif
+        const bool ok = live && j >= 0;
+        x[s] = ok ? make_double2(r.re, r.im) : zero2();
+        if (ok) {
+          const long long i = cb + j;
+          state_st<STREAM>(a.h0 + f * cf + i, make_double2(rhs.re, rhs.im));
+          state_st<STREAM>(a.sol_out + f * cf + i, make_double2(r.re, r.im));
+        }
+      }
     }
   }
   // ---- inverse transforms of field f for the next calcN (as k_col_inv)
@@ -1781,9 +1903,9 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
   constexpr size_t sh_rsw = row_lds_lines<MODEL_RSW, L>() * FftPlan<L>::LDS * BR::NB * sizeof(double2);
   constexpr size_t sh_qg2 = FftPlan<L>::LDS * BQ::NB * sizeof(double2);
   constexpr size_t sh_ty = FftPlan<L>::LDS * BT::NB * sizeof(double2);
-  if (model == MODEL_RSW)
+  if (model == MODEL_RSW) {
     hipLaunchKernelGGL((k_row<MODEL_RSW, L>), dim3(g.nyl / BR::NB), dim3(BR::THREADS), sh_rsw, s, g, p, Mi, Mo, tw);
-  else if (model == MODEL_TY)
+  } else if (model == MODEL_TY)
     hipLaunchKernelGGL((k_row<MODEL_TY, L>), dim3(g.nyl / BT::NB), dim3(BT::THREADS), sh_ty, s, g, p, Mi, Mo, tw);
   else
     hipLaunchKernelGGL((k_row<MODEL_QG2, L>), dim3(g.nyl / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p, Mi, Mo, tw);
@@ -1825,11 +1947,12 @@ void LenOps<L>::col_step(int model, int op, const Geom& g, const Phys& p, const 
     // field range (pipelined slab exchange): one grid row per field
     const bool all = f0 == 0 && nfl == 3;
     if (op == OP_FAB3) {
-      if (all && Blk<L>::NB == 1 && g.kcl % 64 == 0)
-        hipLaunchKernelGGL((k_col_step_fab3_rsw<L>), dim3(3 * g.kcl), blk, sh, s, g, p, a, Mf, Minv, tw, -1);
+      const bool one = all && Blk<L>::NB == 1 && g.kcl % 64 == 0;
+      const dim3 gr = one ? dim3(3 * g.kcl) : dim3(col_blocks<L>(g), nfl);
+      if (a.stream)
+        hipLaunchKernelGGL((k_col_step_fab3_rsw<L, true>), gr, blk, sh, s, g, p, a, Mf, Minv, tw, one ? -1 : f0);
       else
-        hipLaunchKernelGGL((k_col_step_fab3_rsw<L>), dim3(col_blocks<L>(g), nfl), blk, sh, s, g, p, a, Mf, Minv,
-                           tw, f0);
+        hipLaunchKernelGGL((k_col_step_fab3_rsw<L, false>), gr, blk, sh, s, g, p, a, Mf, Minv, tw, one ? -1 : f0);
     } else if (op == OP_IFMAB3) SW_CS(MODEL_RSW, OP_IFMAB3);
     else SW_CS(MODEL_RSW, OP_RK4);
   } else {
@@ -1890,7 +2013,11 @@ void launch_col_step(int model, int op, const Geom& g, const Phys& p, const Step
 
 void launch_step_elem(int nf, int op, const Geom& g, const Phys& p, const StepPtrs& a,
                       const double2* N, double2* xs, hipStream_t s) {
-#define SW_SE(F, O) hipLaunchKernelGGL((k_step_elem<F, O>), mode_grid(g), dim3(256), 0, s, g, p, a, N, xs)
+#define SW_SE(F, O)                                                                                \
+  do {                                                                                             \
+    if (a.stream) hipLaunchKernelGGL((k_step_elem<F, O, true>), mode_grid(g), dim3(256), 0, s, g, p, a, N, xs); \
+    else hipLaunchKernelGGL((k_step_elem<F, O, false>), mode_grid(g), dim3(256), 0, s, g, p, a, N, xs);       \
+  } while (0)
   if (nf == 4) {
     SW_SE(4, OP_ETDRK4);
   } else if (nf == 3) {
