@@ -1519,7 +1519,12 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
         const int jc = j >= 0 ? j : 0;
 #pragma unroll
         for (int cc = 0; cc < 3; ++cc) {
+#ifdef SW_SOL_NT
           const double2 t = state_ld<STREAM>(S + cc * cf + jc);
+#else
+          // temporal: the three field blocks of a column read it (one L2)
+          const double2 t = S[cc * cf + jc];
+#endif
           st[q][cc] = cx(t.x, t.y);
         }
         r1[q] = state_ld<STREAM>(H1 + jc);
