@@ -53,3 +53,26 @@ def test_qg2_calcN_shell_vanishes():
     got = O.qg2_calcN(sol, g, O.QG2Params(0.01, 0.03, 1e-20, 4, F=18.0))
     ref = np.abs(A.state((A.mul(A.dx(q1, 0), A.dx(q1, 1)),), N)).max()  # an O(1) product's scale
     assert np.abs(got).max() / ref < TOL
+
+
+def test_ty_calcN_quad():
+    """Thomas–Yamada: every term of calcN! (advection of ζ_T, the baroclinic
+    and pressure products, the linear terms) on a four-field few-mode state."""
+    g = O.TwoDGrid(N)
+    flds = A.ty_quad()
+    got = O.ty_calcN(A.state(flds, N), g, O.TYParams(1e-30, 8, 0.7))
+    want = A.state(A.ty_N(*flds, 0.7), N)
+    for f in range(4):
+        assert _rel(got[f], want[f]) < TOL, f
+
+
+def test_mlqg_calcN_pair():
+    """MultiLayerQG (aliased_fraction = 0): advection by U + u, the β/shear
+    background gradient and the bottom drag, unequal layer depths."""
+    g = O.TwoDGrid(N, aliased_fraction=0.0)
+    p = O.MLQGParams(1.0, [0.3, 0.7], [1.0, 0.8], [0.15, -0.05], 0.02, beta=0.4)
+    q1, q2 = A.mlqg_pair()
+    got = O.mlqg_calcN(A.state((q1, q2), N), g, p)
+    want = A.state(A.mlqg_N(q1, q2, p.F1, p.F2, p.U, p.Qy, p.mu), N)
+    for f in range(2):
+        assert _rel(got[f], want[f]) < TOL, f
