@@ -962,17 +962,40 @@ __device__ __forceinline__ void matvec(const cplx M[NF][NF], const cplx x[NF], c
 // fields) and field F's RHS₋₁, RHS₋₂ (r1, r2; unused on Euler steps).
 // Returns the new field F (x) and its RHS (history entry).  Branch-free
 // (Euler/AB3 by select), so a kernel can issue several modes' loads at once.
+// (L·s)_F of the RSW operator (rsw_L) without its zero parts: the same
+// values as the complex matrix-vector product Σ_c L[F][c]·s_c (products by
+// exact zeros and additions of them dropped; at most a zero's sign differs)
+template <int F>
+__device__ __forceinline__ cplx rsw_Ls(const Phys& p, double k, double l, const cplx (&s)[3]) {
+#pragma clang fp contract(off)
+  const double D = -(p.nu * ipow(k * k + l * l, p.nnu));
+  if constexpr (F == 0) {  // [D, f, −i k Cg²]
+    const double c = -k * p.Cg2;
+    return cx((D * s[0].re + p.f * s[1].re) - c * s[2].im, (D * s[0].im + p.f * s[1].im) + c * s[2].re);
+  } else if constexpr (F == 1) {  // [−f, D, −i l Cg²]
+    const double c = -l * p.Cg2, mf = -p.f;
+    return cx((mf * s[0].re + D * s[1].re) - c * s[2].im, (mf * s[0].im + D * s[1].im) + c * s[2].re);
+  } else {  // [−i k, −i l, D]
+    const double mk = -k, ml = -l;
+    return cx((-(mk * s[0].im) - ml * s[1].im) + D * s[2].re, (mk * s[0].re + ml * s[1].re) + D * s[2].im);
+  }
+}
+
 template <int NF, int F>
 __device__ __forceinline__ void fab3_compute(const Geom& g, const Phys& p, int euler, double k, double l, cplx n,
                                              const cplx (&s)[NF], double2 r1, double2 r2, cplx& x, cplx& rhs) {
 #pragma clang fp contract(off)
-  cplx L[NF][NF];
-  model_L<NF>(p, k, l, L);
   const double filt = filter_value(g, p, k, l);
   const double dt = p.dt;
   cplx Ls = cx(0.0);
+  if constexpr (NF == 3) {
+    Ls = rsw_Ls<F>(p, k, l, s);
+  } else {
+    cplx L[NF][NF];
+    model_L<NF>(p, k, l, L);
 #pragma unroll
-  for (int cc = 0; cc < NF; ++cc) Ls = Ls + L[F][cc] * s[cc];
+    for (int cc = 0; cc < NF; ++cc) Ls = Ls + L[F][cc] * s[cc];
+  }
   rhs = cx(n.re + Ls.re, n.im + Ls.im);
   const cplx xe = s[F] + dt * rhs;
   const cplx xa = s[F] + dt * cx(23.0 / 12 * rhs.re - 16.0 / 12 * r1.x + 5.0 / 12 * r2.x,
@@ -1508,14 +1531,27 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     const double2* S = a.sol + cb;
     const double2* H1 = a.h1 + f * cf + cb;
     const double2* H2 = a.h2 + f * cf + cb;
+    // slots in the order 0 1 2 5 6 7 3 4: under the 2/3 rule the slots 3, 4
+    // (m in [3N/8, 5N/8)) are dead on every thread, and a group of them is
+    // skipped (uniform branch)
     constexpr int G = SW_CS_GROUP;
+    constexpr int ord[8] = {0, 1, 2, 5, 6, 7, 3, 4};
+    auto slot_live = [&](int s) { return s * NT < g.lc || (s + 1) * NT > g.lr2; };
 #pragma unroll
     for (int s0 = 0; s0 < 8; s0 += G) {
+      bool any = false;
+#pragma unroll
+      for (int q = 0; q < G; ++q) any = any || slot_live(ord[s0 + q]);
+      if (!any) {
+#pragma unroll
+        for (int q = 0; q < G; ++q) x[ord[s0 + q]] = zero2();
+        continue;
+      }
       cplx st[G][3];
       double2 r1[G], r2[G];
 #pragma unroll
       for (int q = 0; q < G; ++q) {
-        const int j = compact_of(g, c.t + (s0 + q) * NT);
+        const int j = compact_of(g, c.t + ord[s0 + q] * NT);
         const int jc = j >= 0 ? j : 0;
 #pragma unroll
         for (int cc = 0; cc < 3; ++cc) {
@@ -1532,7 +1568,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
       }
 #pragma unroll
       for (int q = 0; q < G; ++q) {
-        const int s = s0 + q;
+        const int s = ord[s0 + q];
         const int m = c.t + s * NT;
         const int j = compact_of(g, m);
         const double l = lwav(g, m);
