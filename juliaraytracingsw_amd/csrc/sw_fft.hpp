@@ -93,7 +93,9 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 #endif
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#ifndef SW_EXP_NOBAR  // experiment: no workgroup barrier (wrong results: the cost of the syncs)
   __builtin_amdgcn_s_barrier();
+#endif
   asm volatile("" ::: "memory");
 #ifdef SW_SCHED_FENCE
   __builtin_amdgcn_sched_barrier(0);
