@@ -235,9 +235,52 @@ def main():
         args.stepper = "FilteredRK4"  # TwoLayerSimulation's stepper
 
     # headline: the configured problem, slab-decomposed over the N GPUs
-    # (or one independent problem per GPU with --mode ensemble)
-    prob, P = make_problem(args.model, args.n, args.stepper, local, decomposition() if slab else None)
-    elapsed = timed(prob, args.warmup, args.steps)
+    # (or one independent problem per GPU with --mode ensemble).  Should the
+    # slab run fail on any rank (the RCCL transport first runs on the
+    # driver's multi-GPU node), every rank falls back to the ensemble
+    # headline, labelled as such, with the error in "slab_error".
+    slab_error = None
+    if slab:
+        # every rank passes each stage's agreement point (an all-reduce of
+        # the failure flag) before the next collective, so a failure on one
+        # rank cannot leave the others waiting in a transpose
+        prob = None
+
+        def stage(fn):
+            nonlocal slab_error
+            if slab_error is None:
+                try:
+                    fn()
+                except Exception as exc:  # noqa: BLE001 - reported in the JSON line
+                    slab_error = f"{type(exc).__name__}: {exc}"
+            return max_over_ranks(1.0 if slab_error else 0.0) == 0
+
+        box = {}
+
+        def create():
+            dec = decomposition()  # collective: the RCCL unique id broadcast
+            # test hook of the fallback path: every rank fails its slab problem,
+            # as an RCCL communicator that cannot be created fails on every rank
+            if os.environ.get("SW_BENCH_FAIL_SLAB") == "1":
+                raise RuntimeError("SW_BENCH_FAIL_SLAB")
+            box["prob"], box["P"] = make_problem(args.model, args.n, args.stepper, local, dec)
+
+        if stage(create) and stage(lambda: box.__setitem__("t", timed(box["prob"], args.warmup, args.steps))):
+            prob, P, elapsed = box["prob"], box["P"], box["t"]
+        else:
+            print(f"[bench] slab headline failed ({slab_error or 'on another rank'}); "
+                  "reporting the ensemble", file=sys.stderr)
+            slab_error = slab_error or "failed on another rank"
+            slab = False
+            parallelism = f"ensemble{world}"
+            if "prob" in box:
+                try:
+                    box["prob"].close()
+                except Exception:  # noqa: BLE001
+                    pass
+    if not slab:
+        prob, P = make_problem(args.model, args.n, args.stepper, local, None)
+        elapsed = timed(prob, args.warmup, args.steps)
 
     # roofline: per-kernel HIP-event durations on libsw's stream
     stats = prob.ctx.profile(args.profile_steps)
@@ -270,7 +313,7 @@ def main():
 
     # extra: BASELINE config 5, TwoLayerQG 8192² IFMRK4 over the N GPUs
     config5 = None
-    if not args.no_config5 and (args.model, args.n, args.stepper) == ("rsw", 2048, "FilteredAB3"):
+    if not args.no_config5 and not slab_error and (args.model, args.n, args.stepper) == ("rsw", 2048, "FilteredAB3"):
         c5, _ = make_problem("qg2", 8192, "IFMRK4", local, decomposition())
         t5 = timed(c5, 3, args.config5_steps)
         s5 = c5.ctx.profile(3)
@@ -351,6 +394,7 @@ def main():
         "kernels": [{"name": s["name"], "avg_us": s["avg_ms"] * 1e3, "per_step": s["launches"] / args.profile_steps,
                      "alg_bytes": s["alg_bytes"]} for s in stats],
         "ensemble": ensemble,
+        "slab_error": slab_error,
         "config5": config5,
         "cpu_baseline": cpu,
         # RSWDriver saves a frame every output_freq = floor(output_dt/dt) steps
