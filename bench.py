@@ -5,7 +5,10 @@ baseline (the oracle restatement, scipy.fft on the host cores).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--mode slab|ensemble] [--grid N]
 
-Defaults: 200 untimed + 2000 timed steps (state resident in HBM).
+Defaults: 200 untimed + 2000 timed steps (state resident in HBM).  When the
+W untimed steps take less than --min-warmup-s (0.1 s) of stepping, more
+untimed steps follow until they have (the GPU's steady state; the count is
+reported as `warmup_extra_steps`); the K timed steps are exactly K.
 
 N > 1: one process per GPU.  Started as `python bench.py --gpus N` (no
 WORLD_SIZE in the environment) the script launches `torch.distributed.run
@@ -27,6 +30,7 @@ Extra keys on the same JSON line (never `value`):
 """
 import argparse
 import json
+import math
 import os
 import socket
 import subprocess
@@ -156,6 +160,8 @@ def main():
     ap.add_argument("--stepper", default="FilteredAB3",
                     choices=["FilteredAB3", "IFMAB3", "IFMRK4", "ETDRK4", "FilteredRK4"])
     ap.add_argument("--profile-steps", type=int, default=50)
+    ap.add_argument("--min-warmup-s", type=float, default=0.1,
+                    help="untimed steps after the W warm-up steps until this much stepping has run (steady state)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-config5", action="store_true")
     ap.add_argument("--config5-steps", type=int, default=20)
@@ -221,8 +227,25 @@ def main():
             return slab_comm.host_decomposition(rank, world)
         return slab_comm.rccl_decomposition(rank, world)
 
-    def timed(prob, warmup, steps):
+    extra_warmup = {}
+
+    def timed(prob, warmup, steps, tag="headline"):
+        # W warm-up steps, then — if they took less than --min-warmup-s of
+        # stepping — more untimed steps until they have: the GPU's clocks and
+        # caches reach their steady state only after tens of ms of load (K =
+        # 20, W = 5: 0.181 ms/step; W = 200: 0.167).  Every rank runs the same
+        # number (the slab transposes are collective); the count is reported.
+        barrier_sync()
+        t0 = time.perf_counter()
         prob.stepforward(warmup)
+        barrier_sync()
+        dt = max_over_ranks(time.perf_counter() - t0)
+        extra = 0
+        if args.min_warmup_s > 0 and dt < args.min_warmup_s:
+            per = dt / warmup if warmup > 0 else 1e-3
+            extra = int(min(100000, math.ceil((args.min_warmup_s - dt) / max(per, 1e-6))))
+            prob.stepforward(extra)
+        extra_warmup[tag] = extra
         barrier_sync()
         t0 = time.perf_counter()
         prob.stepforward(steps)  # sw_step returns when its stream is drained
@@ -304,7 +327,7 @@ def main():
     if slab:
         e, _ = make_problem(args.model, args.n, args.stepper, local, None)
         k = max(1, args.steps // 4)
-        te = timed(e, min(args.warmup, 50), k)
+        te = timed(e, min(args.warmup, 50), k, "ensemble")
         ensemble = {"value": world * k / te, "unit": "timesteps/s", "steps_per_rank": k,
                     "scaling": "weak", "workload": f"{world} independent {args.model.upper()} {args.n}^2 "
                                                   f"{args.stepper} problems, one per GPU"}
@@ -315,7 +338,7 @@ def main():
     config5 = None
     if not args.no_config5 and not slab_error and (args.model, args.n, args.stepper) == ("rsw", 2048, "FilteredAB3"):
         c5, _ = make_problem("qg2", 8192, "IFMRK4", local, decomposition())
-        t5 = timed(c5, 3, args.config5_steps)
+        t5 = timed(c5, 3, args.config5_steps, "config5")
         s5 = c5.ctx.profile(3)
         c5.close()
         del c5
@@ -368,6 +391,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "warmup_extra_steps": extra_warmup.get("headline", 0),
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
         "scaling": "strong" if slab else "weak",
