@@ -25,20 +25,28 @@
 
 namespace sw {
 
-// LDS index of line element i (16-B complex units).  SW_LDS_SWZ = 1: no
+// LDS index of line element i (16-B complex units).  Swizzle: no
 // padding, bits 0-2 XOR bits 3-5 — conflict-free for every access of the
 // transforms (MI355X_MICROARCH.md §LDS: ds_write_b128 serves lanes in groups
 // of 8 over 128 B, ds_read_b128 in groups of 16 over 256 B): the consecutive
 // loads and split stores (aligned 4-blocks stay in place), the radix-4 first
 // stage's stores 4j + r (bank bits = r ^ (j bits 1,2), j bit 0) and the Ns = 4
-// stage's stores 32(t/4) + t%4 + 4r (bank bit 2 = bit 5).  SW_LDS_SWZ = 0: one
+// stage's stores 32(t/4) + t%4 + 4r (bank bit 2 = bit 5).  Padding: one
 // pad element every 8 (LP(i) = i + i/8): conflict-free stores, but 2-way
 // conflicts in the 16-lane read groups (24 % of LDS cycles, round-2 PMC).
-#ifndef SW_LDS_SWZ
-#define SW_LDS_SWZ 1
+// Per transform length: lines of at least 2^SW_LDS_SWZ_LOG2 points swizzle,
+// shorter ones pad (measured: the RSW 2048² row 77.9 → 77.0 µs with the
+// swizzle; the Thomas–Yamada 512² row 26.8 → 27.6 with it: its extra index
+// arithmetic spills there).
+#ifndef SW_LDS_SWZ_LOG2
+#define SW_LDS_SWZ_LOG2 11
 #endif
-__host__ __device__ constexpr int LP(int i) { return SW_LDS_SWZ ? (i ^ ((i >> 3) & 7)) : i + (i >> 3); }
-__host__ __device__ constexpr int lds_line_elems(int N) { return SW_LDS_SWZ ? N : N + N / 8; }
+template <int LOG2N>
+__host__ __device__ constexpr bool lds_swz() { return LOG2N >= SW_LDS_SWZ_LOG2; }
+template <int LOG2N>
+__host__ __device__ constexpr int LP(int i) { return lds_swz<LOG2N>() ? (i ^ ((i >> 3) & 7)) : i + (i >> 3); }
+template <int LOG2N>
+__host__ __device__ constexpr int lds_line_elems() { return lds_swz<LOG2N>() ? (1 << LOG2N) : (1 << LOG2N) + (1 << LOG2N) / 8; }
 
 __device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
@@ -124,7 +132,7 @@ struct FftPlan {
   static constexpr int REM = LOG2N % 3;
   static constexpr int FIRST8 = REM ? REM : 3;               // lNs of the first twiddled stage
   static constexpr int NTW = (LOG2N - FIRST8) / 3;            // twiddled radix-8 stages
-  static constexpr int LDS = lds_line_elems(N);               // complex per line buffer
+  static constexpr int LDS = lds_line_elems<LOG2N>();          // complex per line buffer
 };
 
 // W^(k_i << (LOG2N - lNs_i - 3)) for every twiddled stage i (forward sign).
@@ -173,10 +181,11 @@ __device__ __forceinline__ void load_line(double2 (&v)[8], int t, const double2*
   constexpr int NT = FftPlan<LOG2N>::NT;
   // padding: NT a multiple of 8 (N >= 64) gives LP(t + s*NT) = LP(t) + s*(NT + NT/8);
   // swizzle: NT a multiple of 64 (N >= 512) gives LP(t + s*NT) = LP(t) + s*NT
-  constexpr bool lin = SW_LDS_SWZ ? (NT % 64 == 0) : (NT % 8 == 0);
-  constexpr int step = SW_LDS_SWZ ? NT : NT + NT / 8;
+  constexpr bool swz = lds_swz<LOG2N>();
+  constexpr bool lin = swz ? (NT % 64 == 0) : (NT % 8 == 0);
+  constexpr int step = swz ? NT : NT + NT / 8;
 #pragma unroll
-  for (int s = 0; s < 8; ++s) v[s] = line[lin ? LP(t) + s * step : LP(t + s * NT)];
+  for (int s = 0; s < 8; ++s) v[s] = line[lin ? LP<LOG2N>(t) + s * step : LP<LOG2N>(t + s * NT)];
 }
 
 // C independent transforms of one line each, sharing every barrier (C LDS
@@ -212,7 +221,7 @@ __device__ __forceinline__ void fft_lines(double2 (&v)[C][8], int t, const Twidd
       for (int h = 0; h < 2; ++h) {
         const int j = t + h * NT;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) line[c * stride + LP(4 * j + r)] = v[c][h + 2 * r];
+        for (int r = 0; r < 4; ++r) line[c * stride + LP<LOG2N>(4 * j + r)] = v[c][h + 2 * r];
       }
     lds_barrier();
 #pragma unroll
@@ -228,8 +237,8 @@ __device__ __forceinline__ void fft_lines(double2 (&v)[C][8], int t, const Twidd
 #pragma unroll
       for (int h = 0; h < 4; ++h) {
         const int j = t + h * NT;
-        line[c * stride + LP(2 * j)] = v[c][h];
-        line[c * stride + LP(2 * j + 1)] = v[c][h + 4];
+        line[c * stride + LP<LOG2N>(2 * j)] = v[c][h];
+        line[c * stride + LP<LOG2N>(2 * j + 1)] = v[c][h + 4];
       }
     lds_barrier();
 #pragma unroll
@@ -282,13 +291,13 @@ __device__ __forceinline__ void fft_lines(double2 (&v)[C][8], int t, const Twidd
     const int idxD = ((t >> lNs) << (lNs + 3)) + k;
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-      if (SW_LDS_SWZ ? lNs >= 6 : lNs >= 3) {  // r * Ns moves no bit the index function mixes
-        const int base = LP(idxD);
+      if (lds_swz<LOG2N>() ? lNs >= 6 : lNs >= 3) {  // r * Ns moves no bit the index function mixes
+        const int base = LP<LOG2N>(idxD);
 #pragma unroll
-        for (int r = 0; r < 8; ++r) line[c * stride + base + r * (SW_LDS_SWZ ? Ns : Ns + Ns / 8)] = v[c][r];
+        for (int r = 0; r < 8; ++r) line[c * stride + base + r * (lds_swz<LOG2N>() ? Ns : Ns + Ns / 8)] = v[c][r];
       } else {
 #pragma unroll
-        for (int r = 0; r < 8; ++r) line[c * stride + LP(idxD + r * Ns)] = v[c][r];
+        for (int r = 0; r < 8; ++r) line[c * stride + LP<LOG2N>(idxD + r * Ns)] = v[c][r];
       }
     }
     lds_barrier();

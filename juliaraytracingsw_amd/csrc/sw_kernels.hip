@@ -449,14 +449,14 @@ __device__ __forceinline__ void split_pair(const double2 (&v)[8], int t, const G
   constexpr int N = 1 << LOG2N, NT = N / 8;
   lds_barrier();  // previous LDS readers are done
 #pragma unroll
-  for (int s = 0; s < 8; ++s) line[LP(t + s * NT)] = v[s];
+  for (int s = 0; s < 8; ++s) line[LP<LOG2N>(t + s * NT)] = v[s];
   lds_barrier();
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
     const int k = t + s * NT;
     if (RowIdx<LOG2N>::fwd_any(g, s) && k < g.kc) {
       const double2 zk = v[s];
-      const double2 zn = line[LP((N - k) & (N - 1))];
+      const double2 zn = line[LP<LOG2N>((N - k) & (N - 1))];
       // A = (zk + conj zn) / 2,  B = (zk - conj zn) / (2i)
       emit(k, s, make_double2(0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y)),
            make_double2(0.5 * (zk.y + zn.y), -0.5 * (zk.x - zn.x)));
@@ -475,7 +475,7 @@ __device__ __forceinline__ void split_pairs(const double2 (&v)[C][8], int t, con
 #pragma unroll
   for (int c = 0; c < C; ++c)
 #pragma unroll
-    for (int s = 0; s < 8; ++s) line[c * stride + LP(t + s * NT)] = v[c][s];
+    for (int s = 0; s < 8; ++s) line[c * stride + LP<LOG2N>(t + s * NT)] = v[c][s];
   lds_barrier();
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
@@ -484,7 +484,7 @@ __device__ __forceinline__ void split_pairs(const double2 (&v)[C][8], int t, con
 #pragma unroll
       for (int c = 0; c < C; ++c) {
         const double2 zk = v[c][s];
-        const double2 zn = line[c * stride + LP((N - k) & (N - 1))];
+        const double2 zn = line[c * stride + LP<LOG2N>((N - k) & (N - 1))];
         emit(c, k, s, make_double2(0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y)),
              make_double2(0.5 * (zk.y + zn.y), -0.5 * (zk.x - zn.x)));
       }
