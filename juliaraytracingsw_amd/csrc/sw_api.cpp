@@ -182,6 +182,10 @@ Geom make_geom(const sw_config& k, int P, int s) {
   g.y0 = s * g.nyl;
   g.cfield = (long long)std::max(g.kcn, 1) * g.LrP;
   g.mfield = (long long)g.kcl * g.ny;
+  // inverse mixed-field tiles column-major (sw_internal.hpp mtile_local;
+  // SW_TILE_CM=0 selects row-major)
+  g.tcm = 1;
+  if (const char* e = std::getenv("SW_TILE_CM")) g.tcm = e[0] == '1';
   return g;
 }
 

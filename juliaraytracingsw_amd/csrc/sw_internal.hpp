@@ -52,6 +52,7 @@ struct Geom {
   int y0, nyl, log2nyl;    // first row, local rows
   long long cfield;   // elements per compact field  = max(kcn,1)*LrP
   long long mfield;   // elements per mixed field    = kcl*ny = (P*kcl)*nyl
+  int tcm;            // inverse mixed fields: column-major tiles (mtile_local)
 };
 
 struct Phys {
@@ -105,32 +106,43 @@ __host__ __device__ inline double lwav(const Geom& g, int m) {
 #ifndef SW_LORD_I
 #define SW_LORD_I 0
 #endif
+// Inside a line: cm = 0 row-major (a row's A elements contiguous), cm = 1
+// column-major (a column's B elements contiguous).  The inverse fields are
+// written by the column pass and read by the row pass: column-major, each
+// column block writes one contiguous 64-B half of every line it touches
+// (row-major: four 16-B pieces, every 32-B sector partly written; where the
+// neighbouring column's half arrives after the line left L2 the sectors go
+// out twice).  Measured (MI355X, steps/s): RSW 2048² FilteredAB3 6226 →
+// 6363 (col_step 87.8 → 85.7 µs), 1024² +0.7 %, 4096² +1.2 %, 2LQG 2048²
+// IFMAB3 +1.2 %, 2LQG 8192² IFMRK4 60.5 → 63.0 (col_inv 1117 → 937 µs).
+// Geom::tcm (SW_TILE_CM=0 selects row-major, for comparison); the forward
+// fields, written by the row pass, are row-major.
 template <int A, int ORD>
-__host__ __device__ inline int mtile_local(const Geom& g, int krl, int yl) {
+__host__ __device__ inline int mtile_local(const Geom& g, int krl, int yl, int cm = 0) {
   // (krl, yl) inside one slab-pair block of kcl columns × nyl rows
   constexpr int B = 8 / A;
   const int line = ORD == 0 ? (yl / B) * (g.kcl / A) + krl / A : (krl / A) * (g.nyl / B) + yl / B;
-  return line * 8 + (yl % B) * A + krl % A;
+  return line * 8 + (cm ? (krl % A) * B + yl % B : (yl % B) * A + krl % A);
 }
 template <int A, int ORD>
-__host__ __device__ inline int mtile_c(const Geom& g, int krl, int y) {
-  return (y >> g.log2nyl) * g.nyl * g.kcl + mtile_local<A, ORD>(g, krl, y & (g.nyl - 1));
+__host__ __device__ inline int mtile_c(const Geom& g, int krl, int y, int cm = 0) {
+  return (y >> g.log2nyl) * g.nyl * g.kcl + mtile_local<A, ORD>(g, krl, y & (g.nyl - 1), cm);
 }
 template <int A, int ORD>
-__host__ __device__ inline int mtile_x(const Geom& g, int kr, int yl) {
+__host__ __device__ inline int mtile_x(const Geom& g, int kr, int yl, int cm = 0) {
   int p = 0, krl = kr;
   if (g.nslab > 1) {
     p = kr / g.kcl;
     krl = kr - p * g.kcl;
   }
-  return p * g.nyl * g.kcl + mtile_local<A, ORD>(g, krl, yl);
+  return p * g.nyl * g.kcl + mtile_local<A, ORD>(g, krl, yl, cm);
 }
 // forward fields: row phase / column phase
 __host__ __device__ inline int midx(const Geom& g, int kr, int yl) { return mtile_x<SW_TILE_F, SW_LORD_F>(g, kr, yl); }
 __host__ __device__ inline int midc(const Geom& g, int krl, int y) { return mtile_c<SW_TILE_F, SW_LORD_F>(g, krl, y); }
 // inverse fields: column phase / row phase
-__host__ __device__ inline int midc_i(const Geom& g, int krl, int y) { return mtile_c<SW_TILE_I, SW_LORD_I>(g, krl, y); }
-__host__ __device__ inline int midx_i(const Geom& g, int kr, int yl) { return mtile_x<SW_TILE_I, SW_LORD_I>(g, kr, yl); }
+__host__ __device__ inline int midc_i(const Geom& g, int krl, int y) { return mtile_c<SW_TILE_I, SW_LORD_I>(g, krl, y, g.tcm); }
+__host__ __device__ inline int midx_i(const Geom& g, int kr, int yl) { return mtile_x<SW_TILE_I, SW_LORD_I>(g, kr, yl, g.tcm); }
 
 // integer power x^n (0 <= n < 256, sw_create checks) by repeated squaring:
 // the products of the loop `while (n) { if (n & 1) r *= x; x *= x; n >>= 1; }`

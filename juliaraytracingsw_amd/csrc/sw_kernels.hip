@@ -75,6 +75,28 @@ __device__ __forceinline__ int col_of_block(int b, int nb) {
   return b;
 }
 
+// Column-pass store offset of inverse-field element (krl, y = t + s NT): with
+// one slab in closed form (A = 2, rows' lines contiguous: a per-thread term
+// plus a per-s constant), otherwise midc_i
+template <int NT>
+__device__ __forceinline__ int midc_i_col_base(const Geom& g, int krl, int t) {
+  asm volatile("" : "+v"(t));  // formed at the store, not hoisted over the kernel
+  const int pos = g.tcm ? ((krl & 1) << 2) + (t & 3) : ((t & 3) << 1) + (krl & 1);
+  return ((t >> 2) * (g.kcl >> 1) + (krl >> 1)) * 8 + pos;
+}
+template <int NT, typename F>
+__device__ __forceinline__ void store_col_i(const Geom& g, int krl, int t, F put) {
+  if (SW_TILE_I == 2 && SW_LORD_I == 0 && NT % 4 == 0 && g.nslab == 1) {
+    const int b = midc_i_col_base<NT>(g, krl, t);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) put(s, b + s * (NT >> 2) * (g.kcl >> 1) * 8);
+  } else {
+    asm volatile("" : "+v"(t));
+#pragma unroll
+    for (int s = 0; s < 8; ++s) put(s, midc_i(g, krl, t + s * NT));
+  }
+}
+
 // minimum waves per SIMD requested from the register allocator
 #ifndef SW_MINW_FFT
 #define SW_MINW_FFT 2
@@ -139,8 +161,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   auto store = [&](int o) {  // fft_line leaves Y[t + s*NT] in v[s]
     if (live) {
       double2* Mo = M + (long long)o * g.mfield;
-#pragma unroll
-      for (int s = 0; s < 8; ++s) Mo[midc_i(g, krl, c.t + s * NT)] = v[s];
+      store_col_i<NT>(g, krl, c.t, [&](int s, int o) { Mo[o] = v[s]; });
     }
   };
 
@@ -298,9 +319,12 @@ struct RowIdx {
   }
   // some thread holds a live forward output s, k = t + s NT < kc (uniform)
   __device__ __forceinline__ static bool fwd_any(const Geom& g, int s) { return s * NT < g.kc; }
-  // one slab: inverse layout 8 (kk >> 1) + (kk & 1) + row term, forward
-  // layout 2 ny (k >> 1) + (k & 1) + row term (mtile_local, A = 2)
-  __device__ __forceinline__ static int row_inv(const Geom& g, int y) { return (y >> 2) * (g.kcl >> 1) * 8 + (y & 3) * 2; }
+  // one slab: inverse layout 8 (kk >> 1) + 4 (kk & 1) + row term (column-major
+  // tiles; row-major: (kk & 1) and twice the row term), forward layout
+  // 2 ny (k >> 1) + (k & 1) + row term (mtile_local, A = 2)
+  __device__ __forceinline__ static int row_inv(const Geom& g, int y) {
+    return (y >> 2) * (g.kcl >> 1) * 8 + (y & 3) * (g.tcm ? 1 : 2);
+  }
   __device__ __forceinline__ static int fwd0(const Geom& g, int t, int y) {
     return (y >> 2) * 8 + (y & 3) * 2 + 2 * g.nyl * (t >> 1) + (t & 1);
   }
@@ -311,7 +335,10 @@ struct RowIdx {
     if (SW_ROW_CLOSED && g.nslab == 1) {
       const int r0 = row_inv(g, y);
       if (k >= g.kc) return r0;
-      return s < 4 ? r0 + 8 * (tt >> 1) + (tt & 1) + 4 * NT * s : r0 - 4 * tt - 3 * (tt & 1) + 4 * NT * (8 - s);
+      // mirror kk = (8 - s) NT - tt: 8 (kk >> 1) + KI (kk & 1) = 4 (8 - s) NT - 4 tt + (KI - 4) (tt & 1)
+      const int KI = g.tcm ? 4 : 1;  // offset of an odd kk
+      return s < 4 ? r0 + 8 * (tt >> 1) + KI * (tt & 1) + 4 * NT * s
+                   : r0 - 4 * tt + (KI - 4) * (tt & 1) + 4 * NT * (8 - s);
     }
     return midx_i(g, k < g.kc ? k : 0, y);
   }
@@ -1402,8 +1429,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   auto store = [&](int o) {
     if (live) {
       double2* Mo = Minv + (long long)o * MF;
-#pragma unroll
-      for (int s = 0; s < 8; ++s) Mo[midc_i(g, krl, c.t + s * NT)] = v[s];
+      store_col_i<NT>(g, krl, c.t, [&](int s, int o) { Mo[o] = v[s]; });
     }
   };
   if constexpr (MODEL == MODEL_RSW) {
@@ -1462,8 +1488,14 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
 #ifndef SW_CS_GROUP
 #define SW_CS_GROUP 2  // slots per load group of the fused FilteredAB3 update
 #endif
+// 3 waves/SIMD (<= 168 VGPRs) where 256-thread blocks hold the line: the
+// kernel lands at 160-170 VGPRs and 2 against 3 waves costs ~6 % (87.5 vs 93 µs
+// at 2048²), so the register budget is pinned rather than left to chance
+#ifndef SW_MINW_CS
+#define SW_MINW_CS 2
+#endif
 template <int LOG2N, bool STREAM>
-static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
+static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, (Blk<LOG2N>::THREADS >= 1024 ? 4 : SW_MINW_CS))
     k_col_step_fab3_rsw(Geom g, Phys p, StepPtrs a, const double2* __restrict__ Mf,
                         double2* __restrict__ Minv, const double2* __restrict__ tw, int fbase) {
   using B = Blk<LOG2N>;
@@ -1595,8 +1627,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   auto store = [&](int o) {
     if (live) {
       double2* Mo = Minv + (long long)o * MF;
-#pragma unroll
-      for (int s = 0; s < 8; ++s) Mo[midc_i(g, krl, c.t + s * NT)] = v[s];
+      store_col_i<NT>(g, krl, c.t, [&](int s, int o) { Mo[o] = v[s]; });
     }
   };
 #pragma unroll
@@ -1733,8 +1764,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   }
   fft_line<LOG2N, +1>(v, c.t, tws, line);
   if (live) {
-#pragma unroll
-    for (int s = 0; s < 8; ++s) M[midc_i(g, krl, c.t + s * NT)] = v[s];
+    store_col_i<NT>(g, krl, c.t, [&](int s, int o) { M[o] = v[s]; });
   }
 }
 

@@ -28,48 +28,49 @@ def _exchange(hook, send: np.ndarray, P: int) -> np.ndarray:
 # libsw's tile shapes (sw_internal.hpp): (kr extent A of a 128-B line, line order)
 TILE_F, LORD_F = 2, 1  # forward fields (row outputs)
 TILE_I, LORD_I = 2, 0  # inverse fields (column outputs)
+CM_F, CM_I = 0, 1  # inside a line: row-major (forward), column-major (inverse; Geom::tcm)
 
 
-def _tile_local(krl, yl, A, order, kcl, nyl):
+def _tile_local(krl, yl, A, order, kcl, nyl, cm=0):
     """mtile_local: element offset of (krl, yl) inside one kcl x nyl block."""
     B = 8 // A
     line = (yl // B) * (kcl // A) + krl // A if order == 0 else (krl // A) * (nyl // B) + yl // B
-    return line * 8 + (yl % B) * A + krl % A
+    return line * 8 + ((krl % A) * B + yl % B if cm else (yl % B) * A + krl % A)
 
 
-def _to_col_phase(X, A, order, P, nyl):
+def _to_col_phase(X, A, order, P, nyl, cm=0):
     """[y][krl] (ny x kcl) -> the column-phase buffer (mtile_c), blocks q contiguous."""
     ny, kcl = X.shape
     y, krl = np.meshgrid(np.arange(ny), np.arange(kcl), indexing="ij")
-    off = (y // nyl) * nyl * kcl + _tile_local(krl, y % nyl, A, order, kcl, nyl)
+    off = (y // nyl) * nyl * kcl + _tile_local(krl, y % nyl, A, order, kcl, nyl, cm)
     buf = np.empty(ny * kcl, X.dtype)
     buf[off.ravel()] = X.ravel()
     return buf.reshape(P, nyl * kcl)
 
 
-def _from_row_phase(blocks, A, order, kcl, nyl):
+def _from_row_phase(blocks, A, order, kcl, nyl, cm=0):
     """blocks [p][nyl*kcl] (mtile_x) -> [yl][kr] (nyl x P*kcl)."""
     P = blocks.shape[0]
     yl, kr = np.meshgrid(np.arange(nyl), np.arange(P * kcl), indexing="ij")
-    off = (kr // kcl) * nyl * kcl + _tile_local(kr % kcl, yl, A, order, kcl, nyl)
+    off = (kr // kcl) * nyl * kcl + _tile_local(kr % kcl, yl, A, order, kcl, nyl, cm)
     return blocks.reshape(-1)[off]
 
 
-def _to_row_phase(Y, A, order, kcl, nyl):
+def _to_row_phase(Y, A, order, kcl, nyl, cm=0):
     """[yl][kr] (nyl x P*kcl) -> blocks [q][nyl*kcl] (mtile_x), block q = slab q's columns."""
     P = Y.shape[1] // kcl
     yl, kr = np.meshgrid(np.arange(nyl), np.arange(P * kcl), indexing="ij")
-    off = (kr // kcl) * nyl * kcl + _tile_local(kr % kcl, yl, A, order, kcl, nyl)
+    off = (kr // kcl) * nyl * kcl + _tile_local(kr % kcl, yl, A, order, kcl, nyl, cm)
     buf = np.empty(P * nyl * kcl, Y.dtype)
     buf[off.ravel()] = Y.ravel()
     return buf.reshape(P, nyl * kcl)
 
 
-def _from_col_phase(blocks, A, order, kcl, nyl):
+def _from_col_phase(blocks, A, order, kcl, nyl, cm=0):
     """blocks [q][nyl*kcl] (mtile_c) -> [y][krl] (ny x kcl)."""
     P = blocks.shape[0]
     y, krl = np.meshgrid(np.arange(P * nyl), np.arange(kcl), indexing="ij")
-    off = (y // nyl) * nyl * kcl + _tile_local(krl, y % nyl, A, order, kcl, nyl)
+    off = (y // nyl) * nyl * kcl + _tile_local(krl, y % nyl, A, order, kcl, nyl, cm)
     return blocks.reshape(-1)[off]
 
 
@@ -90,12 +91,12 @@ def slab_calcN_rsw(sol, grid, P, r, hook):
     inv_in = [U, V, H, 1j * l[:, None] * U]
     colph = [np.fft.ifft(X, axis=0) * ny * scale for X in inv_in]  # unnormalised inverse / (nx ny)
     # inverse-direction layout midc_i; staging [q][field][block]
-    send = np.stack([_to_col_phase(c, TILE_I, LORD_I, P, nyl) for c in colph], axis=1)
+    send = np.stack([_to_col_phase(c, TILE_I, LORD_I, P, nyl, CM_I) for c in colph], axis=1)
     recv = _exchange(hook, send, P)  # [p][field][block]
 
     # --- row phase (midx_i) -> [yl][kr]
     def row_field(f):
-        t = _from_row_phase(recv[:, f], TILE_I, LORD_I, kcl, nyl)
+        t = _from_row_phase(recv[:, f], TILE_I, LORD_I, kcl, nyl, CM_I)
         full = np.zeros((nyl, nx // 2 + 1), complex)
         full[:, :kc] = t[:, :kc]
         return full
@@ -118,13 +119,13 @@ def slab_calcN_rsw(sol, grid, P, r, hook):
     for a in outs:
         Y = np.zeros((nyl, P * kcl), complex)
         Y[:, :kc] = a[:, :kc]
-        fwd.append(_to_row_phase(Y, TILE_F, LORD_F, kcl, nyl))  # midx: [q][block]
+        fwd.append(_to_row_phase(Y, TILE_F, LORD_F, kcl, nyl, CM_F))  # midx: [q][block]
     send = np.stack(fwd, axis=1)  # [q][field][block]
     recv = _exchange(hook, send, P)  # [p][field][block]
 
     # --- column phase (midc) -> [y][krl], forward y-FFT, combine
     def col_field(f):
-        return _from_col_phase(recv[:, f], TILE_F, LORD_F, kcl, nyl)
+        return _from_col_phase(recv[:, f], TILE_F, LORD_F, kcl, nyl, CM_F)
 
     FP, FK, FZU, FQ, FVE = (np.fft.fft(col_field(f), axis=0) for f in range(5))
     il = 1j * l[:, None]
