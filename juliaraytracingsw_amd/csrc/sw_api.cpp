@@ -68,6 +68,7 @@ struct sw_ctx {
   int head = 0;
   bool mixed_valid = false;                  // mir == transposed col_inv(sol) (fused pipeline primed)
   bool fuse_all = false;                     // SW_FUSE_ALL=1: fused pass for every pair (experiments)
+  int fwd_step = -1;                         // use_fwd_step: -1 where measured faster, SW_FWD_STEP=0/1 off/on
   bool stream_state = false;                 // state/history accesses non-temporal (StepPtrs::stream)
   double2* stage = nullptr;                  // full (nkr,nl,nf) staging
   float* stage32 = nullptr;                  // SW_PREC_F32: the caller-precision copy of stage / dflt
@@ -214,8 +215,8 @@ double live_field_bytes(const Geom& g) { return 16.0 * g.kcn * g.Lr; }
 double mixed_col_bytes(const Geom& g) { return 16.0 * g.kcn * g.ny; }
 double mixed_row_bytes(const Geom& g) { return 16.0 * g.kc * g.nyl; }
 
-enum KId { K_COLINV = 0, K_ROW, K_COLFWD, K_UPD, K_COLSTEP, K_XCHG, K_NKERN };
-const char* kname[K_NKERN] = {"col_inv", "row", "col_fwd", "update", "col_step", "transpose"};
+enum KId { K_COLINV = 0, K_ROW, K_COLFWD, K_UPD, K_COLSTEP, K_FWDSTEP, K_XCHG, K_NKERN };
+const char* kname[K_NKERN] = {"col_inv", "row", "col_fwd", "update", "col_step", "col_fwd_step", "transpose"};
 
 // state/history bytes of one stepper op per live mode, in live-field units
 // (reads + writes; AB3 steady state; IFMRK4 averaged over its four stages)
@@ -247,6 +248,7 @@ double kernel_bytes(const sw_ctx* c, int kid) {
       case K_COLFWD: b += c->nfwd * Mc + nf * F; break;
       case K_UPD: b += (op_fields(c) + nf) * F; break;  // + N read
       case K_COLSTEP: b += c->nfwd * Mc + op_fields(c) * F + c->ninv * Mc; break;
+      case K_FWDSTEP: b += c->nfwd * Mc + op_fields(c) * F; break;  // N never in HBM
       case K_XCHG:  // bytes leaving this slab in one inverse + one forward transpose
         b += (double)(c->ninv + c->nfwd) * (c->P - 1) * g.kcl * g.nyl * 16.0;
         break;
@@ -256,9 +258,12 @@ double kernel_bytes(const sw_ctx* c, int kid) {
 }
 
 bool use_fused(const sw_ctx* c);
+bool use_fwd_step(const sw_ctx* c);
 static double step_bytes(const sw_ctx* c) {
   const int st = c->cfg.stepper;  // four calcN + update stages per RK4-family step
   const int nstage = (st == SW_STEP_IFMRK4 || st == SW_STEP_ETDRK4 || st == SW_STEP_FILTERED_RK4) ? 4 : 1;
+  if (!use_fused(c) && use_fwd_step(c))
+    return nstage * (kernel_bytes(c, K_COLINV) + kernel_bytes(c, K_ROW) + kernel_bytes(c, K_FWDSTEP));
   if (!use_fused(c))
     return nstage * (kernel_bytes(c, K_COLINV) + kernel_bytes(c, K_ROW) + kernel_bytes(c, K_COLFWD) +
                      kernel_bytes(c, K_UPD));
@@ -419,8 +424,22 @@ int fwd_async(sw_ctx* c) {
   return 0;
 }
 
-// equation.calcN!(N, X, …): col_inv -> transpose -> row -> transpose -> col_fwd
-int calcN(sw_ctx* c, double2* Slab::*X, double2* Slab::*N) {
+sw::StepPtrs step_ptrs(const sw_ctx* c, const Slab& s);
+// the last column pass: col_fwd into N, or (op >= 0) the forward transforms
+// and the stepper update in one kernel (N never in HBM)
+static void last_col_pass(sw_ctx* c, double2* Slab::*X, double2* Slab::*N, int op, int stage, const Slab& s) {
+  if (op < 0) {
+    sw::launch_col_fwd(c->kmodel, s.g, c->p, s.mfc, s.*N, s.*X, c->tw_y, c->stream);
+    return;
+  }
+  sw::StepPtrs a = step_ptrs(c, s);
+  a.stage = stage;
+  sw::launch_col_fwd_step(c->kmodel, op, s.g, c->p, a, s.mfc, c->tw_y, c->stream);
+}
+
+// equation.calcN!(N, X, …): col_inv -> transpose -> row -> transpose -> col_fwd;
+// op >= 0: the stepper update of `op` fused into the col_fwd pass (use_fwd_step)
+int calcN(sw_ctx* c, double2* Slab::*X, double2* Slab::*N, int op = -1, int stage = 0) {
   const int model = c->kmodel;
   if (c->cfg.nop_calcN) {  // NOPcalcN!: N .= 0
     for (Slab& s : c->sl)
@@ -436,6 +455,11 @@ int calcN(sw_ctx* c, double2* Slab::*X, double2* Slab::*N) {
     if (int rc = join_comm(c)) return rc;
     for (Slab& s : c->sl) sw::launch_row(model, s.g, c->p, s.mir, s.mfr, c->tw_x, c->stream);
     if (int rc = fwd_async(c)) return rc;
+    if (op >= 0) {  // every field of a column in one block: all exchanges first
+      for (int f = 0; f < ps.nfc; ++f) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_fwd[f], 0));
+      for (Slab& s : c->sl) last_col_pass(c, X, N, op, stage, s);
+      return 0;
+    }
     for (int f = 0; f < ps.nfc; ++f) {
       HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_fwd[f], 0));
       for (Slab& s : c->sl) sw::launch_col_fwd(model, s.g, c->p, s.mfc, s.*N, s.*X, c->tw_y, c->stream, f, 1);
@@ -453,8 +477,8 @@ int calcN(sw_ctx* c, double2* Slab::*X, double2* Slab::*N) {
   }
   if (int rc = transpose(c, false, c->nfwd)) return rc;
   {
-    Timer tm(c, K_COLFWD);
-    for (Slab& s : c->sl) sw::launch_col_fwd(model, s.g, c->p, s.mfc, s.*N, s.*X, c->tw_y, c->stream);
+    Timer tm(c, op >= 0 ? K_FWDSTEP : K_COLFWD);
+    for (Slab& s : c->sl) last_col_pass(c, X, N, op, stage, s);
   }
   return 0;
 }
@@ -475,6 +499,28 @@ bool use_fused(const sw_ctx* c) {
     return false;
   if (c->fuse_all) return true;
   return c->cfg.model == SW_MODEL_RSW && c->cfg.stepper == SW_STEP_FILTERED_AB3;
+}
+
+// k_col_fwd + k_step_elem as one column pass (k_col_step<…, INV = false>: one
+// block per column, every field's N in registers, the update at each live
+// mode, no N in HBM); the next calcN's col_inv runs separately.  Built for
+// RSW IFMAB3/IFMRK4 and 2LQG FilteredAB3/IFMAB3/IFMRK4 (not MultiLayerQG,
+// whose N adds terms from the calcN input in k_col_fwd), bitwise equal to the
+// two kernels; used where it wins (tools/fwdstep_ab.sh): 2LQG
+// FilteredAB3 on lines up to 2048 points (0 spills; 5409 -> 5601 steps/s at
+// 2048²).  The coupled IF/RK4 updates hold every field's N next to the
+// per-mode exponential and spill (82-180 VGPRs at 2048, 350+ at 8192): 2LQG
+// IFMAB3 2048² 5279 -> 4127, RSW IFMAB3 5358 -> 3916, 2LQG IFMRK4 8192² 62.5
+// -> 44.9.  SW_FWD_STEP=1 forces it on every built pair, =0 off.
+bool use_fwd_step(const sw_ctx* c) {
+  if (c->fwd_step == 0 || c->cfg.unfused || c->cfg.nop_calcN || use_fused(c)) return false;
+  const int m = c->cfg.model, st = c->cfg.stepper;
+  const bool built = (m == SW_MODEL_RSW && (st == SW_STEP_IFMAB3 || st == SW_STEP_IFMRK4)) ||
+                     (m == SW_MODEL_QG2 && (st == SW_STEP_FILTERED_AB3 || st == SW_STEP_IFMAB3 ||
+                                            st == SW_STEP_IFMRK4));
+  if (!built) return false;
+  if (c->fwd_step == 1) return true;
+  return m == SW_MODEL_QG2 && st == SW_STEP_FILTERED_AB3 && c->sl[0].g.log2ny <= 11;
 }
 
 sw::StepPtrs step_ptrs(const sw_ctx* c, const Slab& s) {
@@ -554,6 +600,11 @@ int run_stage(sw_ctx* c, int op, int stage, double2* Slab::*X) {
     // the update then overwrites in place (N -> RHS or N); nbuf aliases it
     if (op != sw::OP_RK4 && op != sw::OP_ETDRK4 && op != sw::OP_FRK4)
       for (Slab& s : c->sl) s.nbuf = s.hist[c->head];
+    if (use_fwd_step(c)) {
+      if (int rc = calcN(c, X, &Slab::nbuf, op, stage)) return rc;
+      c->mixed_valid = false;
+      return 0;
+    }
     if (int rc = calcN(c, X, &Slab::nbuf)) return rc;
     Timer tm(c, K_UPD);
     for (Slab& s : c->sl) {
@@ -940,6 +991,7 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (const char* e = std::getenv("SW_FUSE_ALL")) c->fuse_all = e[0] == '1';
+  if (const char* e = std::getenv("SW_FWD_STEP")) c->fwd_step = e[0] == '1' ? 1 : 0;
   // Cache policy of the stepper state (sw_kernels.hip state_ld): a step
   // whose traffic on this GPU exceeds the 256 MiB Infinity Cache evicts the
   // state before the next step reads it, so the state goes non-temporal and

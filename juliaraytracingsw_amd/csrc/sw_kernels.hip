@@ -1328,7 +1328,10 @@ static __global__ void __launch_bounds__(256) k_step_elem(Geom g, Phys p, StepPt
 #define SW_SLOT_FENCE(s) \
   if (((s) + 1) % SW_SLOT_GROUP == 0) __builtin_amdgcn_sched_barrier(0)
 
-template <int MODEL, int LOG2N, int OP>
+// INV = false: forward + update only (k_col_fwd + k_step_elem in one pass, N
+// never in HBM); the next calcN's k_col_inv runs separately.  STREAM: the
+// state/history cache policy of k_step_elem (StepPtrs::stream).
+template <int MODEL, int LOG2N, int OP, bool INV = true, bool STREAM = false>
 static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     k_col_step(Geom g, Phys p, StepPtrs a, const double2* __restrict__ Mf,
                double2* __restrict__ Minv, const double2* __restrict__ tw) {
@@ -1384,9 +1387,9 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
         if (live && j >= 0) {
           const long long i = (long long)krl * g.LrP + j;
           const cplx nf = cx(n[s].x, n[s].y);
-          if (f == 0) op_fab3_field<NF, 0, false>(g, p, a, i, k, lwav(g, m), nf);
-          else if (f == 1) op_fab3_field<NF, 1, false>(g, p, a, i, k, lwav(g, m), nf);
-          else op_fab3_field<NF, (NF == 3 ? 2 : 1), false>(g, p, a, i, k, lwav(g, m), nf);
+          if (f == 0) op_fab3_field<NF, 0, STREAM>(g, p, a, i, k, lwav(g, m), nf);
+          else if (f == 1) op_fab3_field<NF, 1, STREAM>(g, p, a, i, k, lwav(g, m), nf);
+          else op_fab3_field<NF, (NF == 3 ? 2 : 1), STREAM>(g, p, a, i, k, lwav(g, m), nf);
         }
         SW_SLOT_FENCE(s);
       }
@@ -1407,12 +1410,13 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
 #pragma unroll
         for (int f = 0; f < NF; ++f) n[f] = cx(X[f][s].x, X[f][s].y);
         const long long i = (long long)krl * g.LrP + j;
-        step_op<NF, OP>(g, p, a, i, k, lwav(g, m), n, x);
+        step_op<NF, OP, STREAM>(g, p, a, i, k, lwav(g, m), n, x);
         if (OP == OP_RK4 && a.stage < 4) store_vec<NF>(a.xs, g.cfield, i, x);
       }
       SW_SLOT_FENCE(s);
     }
   }
+  if constexpr (!INV) return;
   const double2* Xs = (OP == OP_RK4 && a.stage < 4) ? a.xs : a.sol_out;
   const double2* Xc = Xs + (long long)(live ? krl : 0) * g.LrP;
   auto load_x = [&](int f, double2 (&x)[8]) {
@@ -2034,6 +2038,27 @@ void LenOps<L>::col_step(int model, int op, const Geom& g, const Phys& p, const 
 #undef SW_CS
 }
 
+template <int L>
+void LenOps<L>::col_fwd_step(int model, int op, const Geom& g, const Phys& p, const StepPtrs& a, const double2* Mf,
+                             const double2* tw, hipStream_t s) {
+  const dim3 grid(col_blocks<L>(g)), blk(Blk<L>::THREADS);
+  const size_t sh = lds_bytes<L>();
+#define SW_FS(M, O)                                                                                         \
+  do {                                                                                                      \
+    if (a.stream) hipLaunchKernelGGL((k_col_step<M, L, O, false, true>), grid, blk, sh, s, g, p, a, Mf, nullptr, tw); \
+    else hipLaunchKernelGGL((k_col_step<M, L, O, false, false>), grid, blk, sh, s, g, p, a, Mf, nullptr, tw);        \
+  } while (0)
+  if (model == MODEL_RSW) {
+    if (op == OP_IFMAB3) SW_FS(MODEL_RSW, OP_IFMAB3);
+    else SW_FS(MODEL_RSW, OP_RK4);
+  } else {
+    if (op == OP_FAB3) SW_FS(MODEL_QG2, OP_FAB3);
+    else if (op == OP_IFMAB3) SW_FS(MODEL_QG2, OP_IFMAB3);
+    else SW_FS(MODEL_QG2, OP_RK4);
+  }
+#undef SW_FS
+}
+
 #ifdef SW_PART
 template struct LenOps<SW_PART>;
 #endif
@@ -2080,6 +2105,11 @@ void launch_col_step(int model, int op, const Geom& g, const Phys& p, const Step
                      const double2* Mf, double2* Minv, const double2* tw_y, hipStream_t s, int f0, int nfl) {
   if (nfl < 0) nfl = col_fields(model) - f0;
   by_len(g.log2ny, [&](auto L) { LenOps<decltype(L)::value>::col_step(model, op, g, p, a, Mf, Minv, tw_y, s, f0, nfl); });
+}
+
+void launch_col_fwd_step(int model, int op, const Geom& g, const Phys& p, const StepPtrs& a,
+                         const double2* Mf, const double2* tw_y, hipStream_t s) {
+  by_len(g.log2ny, [&](auto L) { LenOps<decltype(L)::value>::col_fwd_step(model, op, g, p, a, Mf, tw_y, s); });
 }
 
 void launch_step_elem(int nf, int op, const Geom& g, const Phys& p, const StepPtrs& a,

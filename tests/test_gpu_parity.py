@@ -127,19 +127,25 @@ def test_nop_calcN_linear_exactness():
     prob.close()
 
 
-@pytest.mark.parametrize("fuse_all", [False, True])
+@pytest.mark.parametrize("mode", ["default", "fuse_all", "fwd_step"])
 @pytest.mark.parametrize("name", sw_cases.CASES)
-def test_fused_equals_unfused(name, fuse_all, monkeypatch):
-    """The fused column pass (col_fwd + update + next col_inv in one kernel) and
-    the reference sequence of separate kernels give bitwise-identical states.
-    fuse_all: also force the generic fused kernel on every model/stepper pair."""
-    if fuse_all:
+def test_fused_equals_unfused(name, mode, monkeypatch):
+    """The fused column passes (RSW FilteredAB3: col_fwd + update + next col_inv
+    in one kernel; the coupled-update pairs: col_fwd + update in one kernel)
+    and the reference sequence of separate kernels give bitwise-identical
+    states.  fuse_all: force the generic fully fused kernel on every pair;
+    fwd_step: SW_FWD_STEP=1 (the forward + update kernel on every pair it is
+    built for, not only where it is the default)."""
+    if mode == "fuse_all":
         monkeypatch.setenv("SW_FUSE_ALL", "1")
+    if mode == "fwd_step":
+        monkeypatch.setenv("SW_FWD_STEP", "1")
     p = sw_cases.case_params(name, 128)
     pr = sw_cases.oracle_problem(p)
     pr.set_solution(sw_cases.initial_condition(p, pr.grid))
     a = sw_cases.libsw_problem(p)
     monkeypatch.delenv("SW_FUSE_ALL", raising=False)
+    monkeypatch.delenv("SW_FWD_STEP", raising=False)
     b = sw_cases.libsw_problem(p, unfused=True)
     a.sol = pr.sol
     b.sol = pr.sol

@@ -15,7 +15,11 @@ SHORT = {"k_row": "row", "k_col_step_fab3_rsw": "col_step", "k_col_step": "col_s
 
 
 def short(name):
-    base = name.replace("void ", "").split("(")[0].split("<")[0].replace("sw::", "")
+    full = name.replace("void ", "").split("(")[0].replace("sw::", "")
+    base = full.split("<")[0]
+    targs = [a.strip() for a in full[len(base) + 1:].rstrip(">").split(",")] if "<" in full else []
+    if base == "k_col_step" and len(targs) > 3 and targs[3] == "false":  # k_col_step<M, L, OP, INV = false, …>
+        return "col_fwd_step"
     return SHORT.get(base, base)
 
 
