@@ -259,6 +259,7 @@ double kernel_bytes(const sw_ctx* c, int kid) {
 
 bool use_fused(const sw_ctx* c);
 bool use_fwd_step(const sw_ctx* c);
+bool fwd_step_lds(const sw_ctx* c);
 static double step_bytes(const sw_ctx* c) {
   const int st = c->cfg.stepper;  // four calcN + update stages per RK4-family step
   const int nstage = (st == SW_STEP_IFMRK4 || st == SW_STEP_ETDRK4 || st == SW_STEP_FILTERED_RK4) ? 4 : 1;
@@ -434,7 +435,7 @@ static void last_col_pass(sw_ctx* c, double2* Slab::*X, double2* Slab::*N, int o
   }
   sw::StepPtrs a = step_ptrs(c, s);
   a.stage = stage;
-  sw::launch_col_fwd_step(c->kmodel, op, s.g, c->p, a, s.mfc, c->tw_y, c->stream);
+  sw::launch_col_fwd_step(c->kmodel, op, s.g, c->p, a, s.mfc, c->tw_y, c->stream, fwd_step_lds(c));
 }
 
 // equation.calcN!(N, X, …): col_inv -> transpose -> row -> transpose -> col_fwd;
@@ -520,7 +521,13 @@ bool use_fwd_step(const sw_ctx* c) {
                                             st == SW_STEP_IFMRK4));
   if (!built) return false;
   if (c->fwd_step == 1) return true;
+  if (c->fwd_step == 2) return fwd_step_lds(c);
   return m == SW_MODEL_QG2 && st == SW_STEP_FILTERED_AB3 && c->sl[0].g.log2ny <= 11;
+}
+// the LDS-parked variant (k_col_fwd_step_lds, SW_FWD_STEP=2) where its
+// line buffer and parked N fit one CU's 160 KB
+bool fwd_step_lds(const sw_ctx* c) {
+  return c->fwd_step == 2 && sw::fwd_step_lds_bytes(c->kmodel, c->sl[0].g) <= 160 * 1024;
 }
 
 sw::StepPtrs step_ptrs(const sw_ctx* c, const Slab& s) {
@@ -991,7 +998,7 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (const char* e = std::getenv("SW_FUSE_ALL")) c->fuse_all = e[0] == '1';
-  if (const char* e = std::getenv("SW_FWD_STEP")) c->fwd_step = e[0] == '1' ? 1 : 0;
+  if (const char* e = std::getenv("SW_FWD_STEP")) c->fwd_step = e[0] == '1' ? 1 : (e[0] == '2' ? 2 : 0);
   // Cache policy of the stepper state (sw_kernels.hip state_ld): a step
   // whose traffic on this GPU exceeds the 256 MiB Infinity Cache evicts the
   // state before the next step reads it, so the state goes non-temporal and

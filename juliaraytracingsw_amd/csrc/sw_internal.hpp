@@ -450,14 +450,18 @@ struct LenOps {
   static void col_step(int model, int op, const Geom& g, const Phys& p, const StepPtrs& a, const double2* Mf,
                        double2* Minv, const double2* tw, hipStream_t s, int f0, int nfl);
   static void col_fwd_step(int model, int op, const Geom& g, const Phys& p, const StepPtrs& a, const double2* Mf,
-                           const double2* tw, hipStream_t s);
+                           const double2* tw, hipStream_t s, bool lds);
+  static size_t fwd_step_lds_bytes(int model, const Geom& g);
   static void col_inv1(const Geom& g, const double2* X, double2* M, const double2* tw, hipStream_t s);
   static void row_c2r1(const Geom& g, const double2* M, double* out, const double2* tw, hipStream_t s);
 };
 // k_col_fwd + k_step_elem in one column pass (all fields of a column per
 // block, N in registers): RSW IFMAB3/IFMRK4, 2LQG FilteredAB3/IFMAB3/IFMRK4
+// lds: N parked in LDS, the update loop rolled (k_col_fwd_step_lds), needs
+// fwd_step_lds_bytes(model, g) of LDS per block
 void launch_col_fwd_step(int model, int op, const Geom& g, const Phys& p, const StepPtrs& a,
-                         const double2* Mf, const double2* tw_y, hipStream_t s);
+                         const double2* Mf, const double2* tw_y, hipStream_t s, bool lds = false);
+size_t fwd_step_lds_bytes(int model, const Geom& g);
 void launch_step_elem(int nf, int op, const Geom& g, const Phys& p, const StepPtrs& a,
                       const double2* N, double2* xs, hipStream_t s);
 void launch_gather(int nf, const Geom& g, const double2* full, double2* compact, hipStream_t s);

@@ -1481,6 +1481,79 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
 }
 
 // ===========================================================================
+// col_fwd_step_lds: k_col_fwd + k_step_elem for the coupled updates with each
+// field's N parked in LDS (live rows only, own slots: no barrier) as soon as
+// its forward transforms are done, so that no N array is live in registers
+// beside the per-mode update, which runs as a rolled loop over the slots.
+// Dynamic LDS: NB * (FftPlan::LDS + NF * Lr) double2 (fwd_step_lds_bytes).
+// ===========================================================================
+template <int MODEL, int LOG2N, int OP, bool STREAM>
+static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
+    k_col_fwd_step_lds(Geom g, Phys p, StepPtrs a, const double2* __restrict__ Mf,
+                       const double2* __restrict__ tw) {
+  using B = Blk<LOG2N>;
+  constexpr int NT = B::NT;
+  constexpr int NF = MODEL == MODEL_RSW ? 3 : 2;
+  extern __shared__ double2 smem[];
+  const LineCtx c = line_ctx<LOG2N>();
+  const int krl = (B::NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * B::NB + c.ln;
+  const bool live = krl < g.kcn;
+  if (B::NB == 1 && !live) return;
+  const int krA = krl < g.kcl ? krl : g.kcl - 1;
+  double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
+  double2* park = smem + B::NB * FftPlan<LOG2N>::LDS + (long long)c.ln * NF * g.Lr;
+  Twiddles<LOG2N> tws;
+  tws.load(c.t, tw);
+  const double k = (g.kr0 + krl) * g.mk;
+  const long long MF = g.mfield;
+  double2 v[8], n[8];
+  auto load_col = [&](const double2* Mfield) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const double2 t = mix_ld_col(Mfield + midc(g, krA, c.t + s * NT));
+      v[s] = live ? t : zero2();
+    }
+  };
+  // N_f (nterms), the same arithmetic as k_col_fwd
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    const NTerms nt = nterms<MODEL>(f);
+    load_col(Mf + nt.fa * MF);
+    fft_line<LOG2N, -1>(v, c.t, tws, line);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) n[s] = apply_mul(v[s], nt.ma, k, lwav(g, c.t + s * NT));
+    if (nt.fb >= 0) {
+      load_col(Mf + nt.fb * MF);
+      fft_line<LOG2N, -1>(v, c.t, tws, line);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) n[s] = cadd(n[s], apply_mul(v[s], nt.mb, k, lwav(g, c.t + s * NT)));
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int j = compact_of(g, c.t + s * NT);
+      if (j >= 0) park[f * g.Lr + j] = n[s];
+    }
+  }
+  if (!live) return;
+#pragma unroll 1
+  for (int s = 0; s < 8; ++s) {
+    const int m = c.t + s * NT;
+    const int j = compact_of(g, m);
+    if (j >= 0) {
+      cplx nn[NF], x[NF];
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        const double2 t = park[f * g.Lr + j];
+        nn[f] = cx(t.x, t.y);
+      }
+      const long long i = (long long)krl * g.LrP + j;
+      step_op<NF, OP, STREAM>(g, p, a, i, k, lwav(g, m), nn, x);
+      if (OP == OP_RK4 && a.stage < 4) store_vec<NF>(a.xs, g.cfield, i, x);
+    }
+  }
+}
+
+// ===========================================================================
 // col_step_fab3 (RSW FilteredAB3): one block per (column, field f).  The
 // FilteredAB3 update of field f needs N_f alone (plus the old state for L·sol),
 // and the next calcN's inverse transforms of field f need only the new field f:
@@ -2039,13 +2112,21 @@ void LenOps<L>::col_step(int model, int op, const Geom& g, const Phys& p, const 
 }
 
 template <int L>
+size_t LenOps<L>::fwd_step_lds_bytes(int model, const Geom& g) {
+  return (size_t)Blk<L>::NB * (FftPlan<L>::LDS + (size_t)(model == MODEL_RSW ? 3 : 2) * g.Lr) * sizeof(double2);
+}
+
+template <int L>
 void LenOps<L>::col_fwd_step(int model, int op, const Geom& g, const Phys& p, const StepPtrs& a, const double2* Mf,
-                             const double2* tw, hipStream_t s) {
+                             const double2* tw, hipStream_t s, bool lds) {
   const dim3 grid(col_blocks<L>(g)), blk(Blk<L>::THREADS);
-  const size_t sh = lds_bytes<L>();
+  const size_t sh = lds ? fwd_step_lds_bytes(model, g) : lds_bytes<L>();
 #define SW_FS(M, O)                                                                                         \
   do {                                                                                                      \
-    if (a.stream) hipLaunchKernelGGL((k_col_step<M, L, O, false, true>), grid, blk, sh, s, g, p, a, Mf, nullptr, tw); \
+    if (lds) {                                                                                              \
+      if (a.stream) hipLaunchKernelGGL((k_col_fwd_step_lds<M, L, O, true>), grid, blk, sh, s, g, p, a, Mf, tw); \
+      else hipLaunchKernelGGL((k_col_fwd_step_lds<M, L, O, false>), grid, blk, sh, s, g, p, a, Mf, tw);        \
+    } else if (a.stream) hipLaunchKernelGGL((k_col_step<M, L, O, false, true>), grid, blk, sh, s, g, p, a, Mf, nullptr, tw); \
     else hipLaunchKernelGGL((k_col_step<M, L, O, false, false>), grid, blk, sh, s, g, p, a, Mf, nullptr, tw);        \
   } while (0)
   if (model == MODEL_RSW) {
@@ -2108,8 +2189,13 @@ void launch_col_step(int model, int op, const Geom& g, const Phys& p, const Step
 }
 
 void launch_col_fwd_step(int model, int op, const Geom& g, const Phys& p, const StepPtrs& a,
-                         const double2* Mf, const double2* tw_y, hipStream_t s) {
-  by_len(g.log2ny, [&](auto L) { LenOps<decltype(L)::value>::col_fwd_step(model, op, g, p, a, Mf, tw_y, s); });
+                         const double2* Mf, const double2* tw_y, hipStream_t s, bool lds) {
+  by_len(g.log2ny, [&](auto L) { LenOps<decltype(L)::value>::col_fwd_step(model, op, g, p, a, Mf, tw_y, s, lds); });
+}
+size_t fwd_step_lds_bytes(int model, const Geom& g) {
+  size_t b = 0;
+  by_len(g.log2ny, [&](auto L) { b = LenOps<decltype(L)::value>::fwd_step_lds_bytes(model, g); });
+  return b;
 }
 
 void launch_step_elem(int nf, int op, const Geom& g, const Phys& p, const StepPtrs& a,

@@ -127,7 +127,7 @@ def test_nop_calcN_linear_exactness():
     prob.close()
 
 
-@pytest.mark.parametrize("mode", ["default", "fuse_all", "fwd_step"])
+@pytest.mark.parametrize("mode", ["default", "fuse_all", "fwd_step", "fwd_step_lds"])
 @pytest.mark.parametrize("name", sw_cases.CASES)
 def test_fused_equals_unfused(name, mode, monkeypatch):
     """The fused column passes (RSW FilteredAB3: col_fwd + update + next col_inv
@@ -135,11 +135,14 @@ def test_fused_equals_unfused(name, mode, monkeypatch):
     and the reference sequence of separate kernels give bitwise-identical
     states.  fuse_all: force the generic fully fused kernel on every pair;
     fwd_step: SW_FWD_STEP=1 (the forward + update kernel on every pair it is
-    built for, not only where it is the default)."""
+    built for, not only where it is the default); fwd_step_lds: SW_FWD_STEP=2
+    (its variant with N parked in LDS)."""
     if mode == "fuse_all":
         monkeypatch.setenv("SW_FUSE_ALL", "1")
     if mode == "fwd_step":
         monkeypatch.setenv("SW_FWD_STEP", "1")
+    if mode == "fwd_step_lds":
+        monkeypatch.setenv("SW_FWD_STEP", "2")
     p = sw_cases.case_params(name, 128)
     pr = sw_cases.oracle_problem(p)
     pr.set_solution(sw_cases.initial_condition(p, pr.grid))
