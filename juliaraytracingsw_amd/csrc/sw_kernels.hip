@@ -1487,6 +1487,11 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
 // beside the per-mode update, which runs as a rolled loop over the slots.
 // Dynamic LDS: NB * (FftPlan::LDS + NF * Lr) double2 (fwd_step_lds_bytes).
 // ===========================================================================
+#ifndef SW_FS_UNROLL
+#define SW_FS_UNROLL 1  // slots per update-loop iteration (experiments)
+#endif
+#define SW_PRAGMA_(x) _Pragma(#x)
+#define SW_PRAGMA(x) SW_PRAGMA_(x)
 template <int MODEL, int LOG2N, int OP, bool STREAM>
 static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     k_col_fwd_step_lds(Geom g, Phys p, StepPtrs a, const double2* __restrict__ Mf,
@@ -1535,7 +1540,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     }
   }
   if (!live) return;
-#pragma unroll 1
+  SW_PRAGMA(unroll SW_FS_UNROLL)
   for (int s = 0; s < 8; ++s) {
     const int m = c.t + s * NT;
     const int j = compact_of(g, m);
