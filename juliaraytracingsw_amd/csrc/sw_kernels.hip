@@ -147,8 +147,20 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   constexpr int NT = B::NT;
   extern __shared__ double2 smem[];
   const LineCtx c = line_ctx<LOG2N>();
-  const int krl = (B::NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * B::NB + c.ln;
-  const int grp = gbase + blockIdx.y;
+  int krl, grp;
+  if (MODEL == MODEL_QG2 && gbase < 0) {
+    // both layers, 1-D grid of 2*kcl blocks (NB == 1, kcl a multiple of 64):
+    // the two layer blocks of a column are consecutive on one XCD label
+    // (b % 8), so the second one's reads of q1, q2 (each layer needs both for
+    // ψ) come from that L2 rather than HBM; the 8 columns sharing a 128-B
+    // chunk of the mixed layout stay on one label (speed only)
+    const int b = blockIdx.x, q = b >> 7, r = b & 127, x = r & 7, jj = r >> 3;
+    grp = jj & 1;
+    krl = (q << 6) + (x << 3) + (jj >> 1);
+  } else {
+    krl = (B::NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * B::NB + c.ln;
+    grp = gbase + blockIdx.y;
+  }
   const bool live = krl < g.kcn;
   if (B::NB == 1 && !live) return;  // padding column: nobody reads it
   double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
@@ -2035,6 +2047,14 @@ static size_t lds_bytes() {
   return (size_t)Blk<L>::NB * FftPlan<L>::LDS * sizeof(double2);
 }
 
+// 2LQG col_inv with the two layer blocks of a column paired on one XCD
+// (k_col_inv, gbase < 0), measured (tools/qg_inv_pair_ab.sh): 8192-point
+// columns 949.7 -> 881.3 µs (config 5 61.2 -> 61.9 steps/s); 2048-point
+// columns 47-48 -> 48-50 µs (not used there).  1: on 8192-point lines,
+// 2: every length, 0: never (experiments).
+#ifndef SW_QG_INV_PAIR
+#define SW_QG_INV_PAIR 1
+#endif
 template <int L>
 void LenOps<L>::col_inv(int model, const Geom& g, const Phys& p, const double2* X, double2* M, const double2* tw,
                         hipStream_t s, int g0, int ng) {
@@ -2043,6 +2063,10 @@ void LenOps<L>::col_inv(int model, const Geom& g, const Phys& p, const double2* 
     hipLaunchKernelGGL((k_col_inv<MODEL_RSW, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
   else if (model == MODEL_TY)
     hipLaunchKernelGGL((k_col_inv<MODEL_TY, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
+  else if (g0 == 0 && ng == 2 && Blk<L>::NB == 1 && g.kcl % 64 == 0 &&
+           (SW_QG_INV_PAIR == 2 || (SW_QG_INV_PAIR == 1 && L >= 13)))
+    hipLaunchKernelGGL((k_col_inv<MODEL_QG2, L>), dim3(2 * g.kcl), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X,
+                       M, tw, -1);
   else
     hipLaunchKernelGGL((k_col_inv<MODEL_QG2, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
 }
