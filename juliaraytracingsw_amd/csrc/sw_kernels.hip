@@ -105,6 +105,9 @@ __device__ __forceinline__ void store_col_i(const Geom& g, int krl, int t, F put
 #ifndef SW_MINW_ROW
 #define SW_MINW_ROW 2
 #endif
+#ifndef SW_MINW_ROW_QG  // the 2LQG/MultiLayerQG row
+#define SW_MINW_ROW_QG 2
+#endif
 
 // threads per block: one line of NT = N/8 threads, or several short lines
 // packed into 256 threads
@@ -578,7 +581,9 @@ __device__ __forceinline__ void fft_pair(double2 (&w)[2][8], int t, const Twiddl
 }
 
 template <int MODEL, int LOG2N>
-static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS), (BlkRow<MODEL, LOG2N>::THREADS >= 1024 ? 4 : SW_MINW_ROW))
+static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
+                                         (BlkRow<MODEL, LOG2N>::THREADS >= 1024 ? 4
+                                          : (MODEL == MODEL_QG2 ? SW_MINW_ROW_QG : SW_MINW_ROW)))
     k_row(Geom g, Phys p, const double2* __restrict__ Mi, double2* __restrict__ Mo,
           const double2* __restrict__ tw) {
   using Bk = BlkRow<MODEL, LOG2N>;
