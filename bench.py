@@ -74,11 +74,14 @@ def _cpu_model():
     return None
 
 
-def cpu_baseline(model, stepper, n, grids=(128, 1024, 2048), budget_s=24.0, samples=5):
-    """The oracle (fp64 numpy/scipy restatement of the reference op sequence)
-    on the host cores: at each grid, 3 untimed start-up steps, then the median
-    of `samples` timed samples of k steps, k sized so the whole baseline is
-    about `budget_s` of CPU work (BASELINE.md §3's protocol, bounded)."""
+def cpu_baseline(model, stepper, n, grids=(128, 1024, 2048), samples=5, warm_steps=10, sample_s=1.0,
+                 sample_steps=200):
+    """The oracle — the fp64 numpy/scipy restatement of the reference op
+    sequence, NOT FourierFlows/FFTW (Julia is absent) — on the host cores, by
+    BASELINE.md §3's protocol: at each grid 10 untimed steps (past the AB3
+    Euler start-up), then `samples` timed samples, each of 200 steps or as
+    many as take >= 1 s, whichever comes first; the median.  About 20 s of
+    CPU work in all (the 2048² samples are 3 steps of ≈ 0.45 s)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import statistics
@@ -93,29 +96,30 @@ def cpu_baseline(model, stepper, n, grids=(128, 1024, 2048), budget_s=24.0, samp
     cores = min(affinity, share) if share > 0 else affinity
     O.set_fft_workers(cores)
     grids = sorted(set(grids) | {n})
-    per = budget_s / len(grids)
     by_grid = {}
     for g in grids:
         p = sw_cases.case_params(f"{model}_{SHORT[stepper]}", g)
         pr = sw_cases.oracle_problem(p)
         pr.set_solution(sw_cases.initial_condition(p, pr.grid))
-        t0 = time.perf_counter()
-        pr.stepforward(3)  # the Euler start-up steps (AB3 steppers), untimed; also sizes k
-        k = max(1, int(per / samples / max((time.perf_counter() - t0) / 3, 1e-6)))
-        rates = []
+        pr.stepforward(warm_steps)  # untimed
+        rates, counts = [], []
         for _ in range(samples):
-            t0 = time.perf_counter()
-            pr.stepforward(k)
+            k, t0 = 0, time.perf_counter()
+            while k < sample_steps and time.perf_counter() - t0 < sample_s:
+                pr.stepforward(1)
+                k += 1
             rates.append(k / (time.perf_counter() - t0))
-        by_grid[str(g)] = {"steps_per_s": statistics.median(rates), "steps_per_sample": k,
-                           "samples": samples, "min": min(rates), "max": max(rates)}
+            counts.append(k)
+        by_grid[str(g)] = {"steps_per_s": statistics.median(rates), "steps_per_sample": counts,
+                           "warmup_steps": warm_steps, "samples": samples, "min": min(rates), "max": max(rates)}
     O.set_fft_workers(None)
     return dict(value=by_grid[str(n)]["steps_per_s"], unit="timesteps/s", cores=cores, kind="port",
                 nproc=os.cpu_count(), affinity_cores=affinity, cpu_model=_cpu_model(), by_grid=by_grid,
-                sample=f"{stepper} steps of the {model.upper()} oracle restatement (numpy elementwise + "
-                       f"scipy.fft workers={cores}) at {', '.join(f'{g}²' for g in grids)}: 3 untimed steps, "
-                       f"then the median of {samples} samples of k steps per grid (k in by_grid); value = "
-                       f"the {n}² median")
+                sample=f"{stepper} steps of the {model.upper()} oracle: the repo's fp64 numpy/scipy restatement of "
+                       f"the reference op sequence (numpy elementwise + scipy.fft workers={cores}), not "
+                       f"FourierFlows/FFTW (Julia is not in the image); at {', '.join(f'{g}²' for g in grids)}: "
+                       f"{warm_steps} untimed steps, then the median of {samples} samples of {sample_steps} steps "
+                       f"or >= {sample_s:g} s each (BASELINE.md §3); value = the {n}² median")
 
 
 def _free_port():
@@ -183,7 +187,8 @@ def main():
     if args.dry_run:
         if rank == 0:
             print(json.dumps({"n_gpus": world, "parallelism": parallelism,
-                              "scaling": "strong" if slab else "weak", "rank0_of": world}))
+                              "scaling": ("strong" if slab else "weak") if world > 1 else None,
+                              "rank0_of": world}))
         return
 
     import torch
@@ -394,7 +399,9 @@ def main():
         "warmup_extra_steps": extra_warmup.get("headline", 0),
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "strong" if slab else "weak",
+        # fixed per-GPU work (ensemble) is weak scaling, one problem over N
+        # GPUs strong; a single GPU scales neither way
+        "scaling": ("strong" if slab else "weak") if world > 1 else None,
         "vs_baseline": None,
         "dtype": "f64",
         "data": {"rsw": "synthetic random-phase IC (set_shafer_initial_condition!, seeded)",

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SW_ABI_VERSION 6
+#define SW_ABI_VERSION 7
 
 /* models */
 #define SW_MODEL_RSW 0   /* rsw/RotatingShallowWater.jl: fields (u, v, η), 3×3 L   */
@@ -199,11 +199,27 @@ int sw_get_state(const sw_ctx* ctx, void* sol, size_t bytes);
  * Layout as the state.  sw_reset_history: the next three steps start the AB3
  * steppers with forward Euler, as at clock.step < 3 (a restart from a state
  * without saved history, which is what the reference's
- * load_from_snapshot! restart amounts to, rsw/RSWDriver.jl:10-36). */
+ * load_from_snapshot! restart amounts to, rsw/RSWDriver.jl:10-36); it
+ * counts steps, not the clock (sw_set_clock does not move it).
+ * sw_set_history makes the history valid again and cancels a pending reset. */
 int sw_history_slots(const sw_ctx* ctx, int32_t* nslots);
 int sw_get_history(const sw_ctx* ctx, int32_t slot, void* buf, size_t bytes);
 int sw_set_history(sw_ctx* ctx, int32_t slot, const void* buf, size_t bytes);
 int sw_reset_history(sw_ctx* ctx);
+
+/* Restart blob (ABI 7): the stepper's whole memory in fp64 whatever
+ * sw_config.precision says — libsw keeps state and history in fp64, so a
+ * ComplexF32 copy through sw_get_state / sw_get_history would round them and
+ * the continuation would not be bitwise.  Layout: a 64-byte header (magic
+ * "SWCKPT01", ABI, model, stepper, nx, ny, nf, history slots, pending Euler
+ * start-up steps, t, step), then the state and each history slot as Julia
+ * (nkr, nl, nf) ComplexF64 arrays.  sw_set_checkpoint restores state,
+ * history, clock and start-up count of the same problem (SW_E_INVALID
+ * otherwise); the next sw_step continues bit for bit.  One slab per process:
+ * every rank calls both (collective). */
+int sw_checkpoint_bytes(const sw_ctx* ctx, size_t* bytes);
+int sw_get_checkpoint(const sw_ctx* ctx, void* buf, size_t bytes);
+int sw_set_checkpoint(sw_ctx* ctx, const void* buf, size_t bytes);
 
 int sw_set_clock(sw_ctx* ctx, double t, int64_t step);
 int sw_get_clock(const sw_ctx* ctx, double* t, int64_t* step);

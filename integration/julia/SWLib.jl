@@ -1,150 +1,3 @@
-# Integrating libsw behind the reference's FourierFlows seam
-
-libsw is a C-ABI shared library (`juliaraytracingsw_amd/libsw.so`, header
-`include/sw.h`, ABI 7).  It owns the model state on the GPU and runs whole
-time steps there.  This file is for a maintainer of the reference
-(ndefilippis/JuliaRaytracingSW) who wants the three drivers the north star
-names — `rsw/RSWDriver.jl`, `thomasyamada/TYdriver.jl` and
-`simulation/TwoLayerSimulation.jl` (and `swqg/TwoLayerDriver.jl` alongside) —
-to run their hot loop on an MI355X **without editing them**.
-
-Julia is not installed in this image, so the Julia below
-(`integration/julia/`) is the binding a maintainer adds; it has not been run.
-What is checked here:
-
-* `tests/test_julia_shim.py` (CPU) reads the Julia: the parametric
-  `SWStepper{A} <: AbstractTimeStepper{A}` supertype, the `filter` field, a
-  `Problem` method per driver model, every `ccall` against the `include/sw.h`
-  prototype it binds (name and argument count), `SWConfig` field for field
-  against `struct sw_config`, the run-directory wrappers, and that each
-  SWLib.jl function issues the same C entry points in the same order as its
-  Python twin;
-* `tests/driver_replay.py` is that twin, and `tests/test_gpu_driver_replay.py`
-  (GPU) replays each driver's `start!` statement by statement through it —
-  `RSWDriver` with `T = Float32` and `dev = GPU()`, `TYdriver GPU` start-up
-  and main run, `TwoLayerSimulation` — checked against the CPU oracle, with
-  the C call trace asserted.
-
-FourierFlows (FF) and GeophysicalFlows (GF) are not vendored in the reference
-and their versions are not pinned (SURVEY §8c): the FF/GF names SWLib uses are
-the ones the reference itself calls (`TwoDGrid`, `Problem`, `Clock`,
-`Diagnostic`, `makefilter`, `device_array`, `stepforward!`, `increment!`,
-GF's `MultiLayerQG.Problem` / `set_q!` / `updatevars!` / `energies` /
-`streamfunctionfrompv!`).
-
-## 1. Seams
-
-| Reference seam (file:line) | libsw entry point |
-|---|---|
-| `RotatingShallowWater.Problem(dev; nx, …, stepper, dt, T, …)` (`rsw/RotatingShallowWater.jl:70-99`), `TwoLayerQG.Problem` (`swqg/TwoLayerQG.jl:55-90`), `ThomasYamada.Problem(dev; …, stepper="ETDRK4")` (`thomasyamada/ThomasYamada.jl:55-74`), GF `MultiLayerQG.Problem(2, dev; …, aliased_fraction=0)` (`simulation/TwoLayerSimulation.jl:37-38`); `IFMAB3TimeStepper(equation, dt, dev; …)` (`utils/IFMAB3.jl:68-88`) | `sw_config_default` + `sw_create` |
-| `set_solution!(prob, …)` (`rsw/RotatingShallowWater.jl:309-321`, `swqg/TwoLayerQG.jl:220-228`, `thomasyamada/ThomasYamada.jl:292-317`), GF `set_q!` (`simulation/TwoLayerSimulation.jl:47`); reading `prob.sol` | `sw_set_state`, `sw_get_state` (Julia `(nkr, nl, nf)` `ComplexF64`, or `ComplexF32` with `precision = SW_PREC_F32` for the drivers' `T = Float32`, byte-identical), `sw_set_clock` |
-| `FourierFlows.stepforward!(sol, clock, ts, equation, vars, params, grid)` (`utils/IFMAB3.jl:157`) and `stepforward!(prob, diags, n)` (`rsw/RSWDriver.jl:212`, `swqg/TwoLayerDriver.jl:105`, `thomasyamada/TYdriver.jl:172,217`, `simulation/TwoLayerSimulation.jl:128`) | `sw_step(ctx, n)`; `sw_get_clock` / `sw_set_clock` |
-| `equation.calcN!(N, sol, t, clock, vars, params, grid)` (`rsw/RotatingShallowWater.jl:140`, `swqg/TwoLayerQG.jl:152`, `thomasyamada/ThomasYamada.jl:129`) | `sw_calcN` |
-| `updatevars!(prob)` (`rsw/RotatingShallowWater.jl:101-116`, `swqg/TwoLayerQG.jl:113-129`, `thomasyamada/ThomasYamada.jl:76-101`, GF `MultiLayerQG.updatevars!`), TY `enforce_reality_condition!` (`:103-123`) | `sw_get_physical(ctx, id, out)` |
-| FF `Diagnostic(kinetic_energy / potential_energy / barotropic_energy / wave_geostrophic_energy / energies, prob; freq)` + `increment!` (`rsw/RSWDriver.jl:193-196`, `swqg/TwoLayerDriver.jl:86-89`, `thomasyamada/TYdriver.jl:152-153`, `simulation/TwoLayerSimulation.jl:52`) | `sw_set_energy_diagnostics`, `sw_get_energy_diagnostics` (recorded on the device while stepping) |
-| the driver's NaN test (`rsw/RSWDriver.jl:213-218`, `swqg/TwoLayerDriver.jl:106-111`); `kinetic_energy(prob)` etc. on demand | `sw_step` returns `SW_E_NAN`; `sw_diag(ctx, SW_DIAG_*)` |
-| the TimeStepper's memory (FF FilteredAB3 `RHS₋₁/RHS₋₂`, `utils/IFMAB3.jl:15-18` `N₋₁/N₋₂`) for checkpoint/restart | `sw_checkpoint_bytes` / `sw_get_checkpoint` / `sw_set_checkpoint` (fp64 blob whatever `T`), `sw_history_slots`, `sw_get_history`, `sw_set_history`, `sw_reset_history` |
-| FF `Output` / `saveoutput`, `utils/SequencedOutputs.jl`, `load_from_snapshot!` (`rsw/RSWDriver.jl:10-36`) | unchanged: they read `prob.sol`, which SWLib keeps current on the host |
-
-## 2. Installing it: the reference's own file swap
-
-The reference's sbatch scripts assemble a run directory and swap model files
-by copying (`rsw/mrsw-driver.sbatch` copies `ModifiedShallowWater.jl` over
-`RotatingShallowWater.jl`).  libsw is installed the same way: the model file
-the driver includes becomes a three-line wrapper
-(`integration/julia/<dir>/`) that includes the reference module under
-another name and then `SWLib.attach!`es it.  The drivers and their `*Main.jl`
-launchers are not touched.
-
-```sh
-# rsw/rsw-driver.sbatch (after its cp lines)
-cp RotatingShallowWater.jl $rundir/RotatingShallowWater.ref.jl
-cp $LIBSW/integration/julia/rsw/RotatingShallowWater.jl $LIBSW/integration/julia/SWLib.jl \
-   $LIBSW/juliaraytracingsw_amd/libsw.so $rundir
-# swqg/twolayer-driver.sbatch
-cp TwoLayerQG.jl $rundir/TwoLayerQG.ref.jl
-cp $LIBSW/integration/julia/swqg/TwoLayerQG.jl $LIBSW/integration/julia/SWLib.jl $LIBSW/juliaraytracingsw_amd/libsw.so $rundir
-# thomasyamada/gpu-driver.sbatch (julia TYdriver.jl GPU)
-cp ThomasYamada.jl $rundir/ThomasYamada.ref.jl
-cp $LIBSW/integration/julia/thomasyamada/ThomasYamada.jl $LIBSW/integration/julia/SWLib.jl $LIBSW/juliaraytracingsw_amd/libsw.so $rundir
-# simulation/driver.sbatch
-cp Parameters.jl $rundir/Parameters.ref.jl
-cp $LIBSW/integration/julia/simulation/Parameters.jl $LIBSW/integration/julia/SWLib.jl $LIBSW/juliaraytracingsw_amd/libsw.so $rundir
-```
-
-`LIBSW=<path>` overrides the library location, `LIBSW_DEVICE=<n>` the HIP
-device, `LIBSW_CPU=1` also routes `Problem(CPU())` to libsw (TYdriver's second
-problem, `thomasyamada/TYdriver.jl:181`; without it that one stays the
-reference's FFTW run).
-
-## 3. What happens at each driver line
-
-**The CUDA-only construction path.**  The drivers hard-code `dev = GPU()`
-(`rsw/RSWDriver.jl:135`, `swqg/TwoLayerDriver.jl:30`,
-`simulation/Parameters.jl:28`; `TYdriver.jl:118-121` on `ARGS[1] == "GPU"`).
-In the reference `Problem(GPU())` then runs CUDA code before any stepping:
-`TwoDGrid(GPU())` builds CUFFT plans, `populate_L!` launches `@cuda
-Lop_kernel` (`rsw/RotatingShallowWater.jl:276-289`), `IFMAB3TimeStepper`
-launches `@cuda kernel_exp` (`utils/IFMAB3.jl:44-66`).  `SWLib.attach!` gives
-each model module a `Problem(dev::GPU; kw...)` method — more specific than the
-reference's `Problem(dev::Device = CPU(); …)` — that builds the same
-FourierFlows objects on `CPU()` (host grid with FFTW plans, `Vars`, `Params`,
-`Equation` with the CPU `populate_L!`, `Clock{T}`, `sol`) plus an `SWStepper`
-holding the libsw context, and returns `FourierFlows.Problem(sol, clock,
-equation, grid, vars, params, ts)` as `rsw/RotatingShallowWater.jl:95` does.
-None of the CUDA code runs.  `FourierFlows.device_array(::GPU)` returns `Array`
-(the drivers draw their initial PV with `device_array(dev)(randn(…))`,
-`swqg/TwoLayerDriver.jl:11`, `simulation/TwoLayerSimulation.jl:43`): under
-SWLib, `GPU()` means "state on the libsw device, every array the driver sees
-on the host".
-
-**RSWDriver.start!** (`rsw/RSWDriver.jl:134-226`, `T = Float32`):
-
-| driver line | SWLib | C calls |
-|---|---|---|
-| `:164` `RotatingShallowWater.Problem(dev; …, T=Float32, order, use_filter)` | `rsw_problem` (default stepper `"IFMAB3"`, `:79`) | `sw_config_default`, `sw_create` (`precision = SW_PREC_F32`, `dt = Float32(dt)`) |
-| `:88-131` `set_shafer_initial_condition!` (host FFTW on the host grid) → `:131` `set_solution!` | `load_solution!`, `rsw_updatevars!` | `sw_set_state`, `sw_get_state`, `sw_set_clock`, 4× `sw_get_physical` |
-| `:193-194` `Diagnostic(kinetic_energy, prob; freq)` | host `kinetic_energy(prob)` (the reference's, from `vars.uh`) | — |
-| `:198` `enforce_reality_condition!` | the reference's; its `updatevars!` call dispatches to libsw's | 4× `sw_get_physical` |
-| `:207` CFL from `vars.u`, `vars.v` | host arrays | — |
-| `:212` `stepforward!(prob, diags, output_freq)` | `attach_diagnostics!` (first call), `run_steps!`, `take_records!` | `sw_set_energy_diagnostics`, `sw_step`, `sw_get_state`, `sw_get_energy_diagnostics` ×2 |
-| `:213` `any(isnan.(vars.η))` | after `SW_E_NAN`, `blowup!` sets `vars.η` to NaN: the driver's own throw runs | — |
-| `:219` `updatevars!` | `rsw_updatevars!` | 4× `sw_get_physical` |
-| `:221` `saveoutput` → `Array(prob.sol)` | host `prob.sol` (current after every `stepforward!`) | — |
-
-The clock advances in the Problem's own arithmetic (`clock.t += clock.dt`,
-`utils/IFMAB3.jl:162`; Float32 for this driver); the Diagnostics' `t` entries
-are those host times, their data the device records (fp64 sums of the fp64
-device state).
-
-**TYdriver.start!** (`thomasyamada/TYdriver.jl:111-231`, `julia TYdriver.jl GPU`):
-`Problem(GPU(); …)` → `ty_problem` (`sw_create`, `SW_MODEL_TY`, ETDRK4);
-`set_initial_condition` (host) → `set_solution!` (`sw_set_state`,
-`sw_get_state`, `sw_set_clock`, 7× `sw_get_physical`); the start-up frames:
-`stepforward!(startup_prob, diags, startup_nsubs)` (records every 25 steps:
-`wave_geostrophic_energy`, `barotropic_energy`), `enforce_reality_condition!`
-(4× `sw_get_physical`), `updatevars!` (7×).  `:181` `Problem(CPU(); …)` is the
-reference's FFTW problem, or libsw's with `LIBSW_CPU=1`; `:190` sets
-`prob.clock.t`, and `:191` `set_solution!` pushes it (`sw_set_clock`).
-
-**TwoLayerSimulation.start!** (`simulation/TwoLayerSimulation.jl:13-143`):
-`MultiLayerQG.Problem(2, GPU(); nx, Lx, f₀, H, b, U, μ, β, dt, stepper,
-aliased_fraction=0)` → `mlqg_problem`: GF's own CPU problem supplies grid,
-params, vars, equation and FilteredRK4's `filter`, which the driver reads at
-`:44` (`prob.timestepper.filter`, an `SWStepper` field); `set_q!` (`:47`) →
-host r2c with GF's plan, `sw_set_state` …; `Diagnostic(MultiLayerQG.energies,
-prob; nsteps)` (freq 1) is recorded on the device; frames:
-`stepforward!(prob, diags, nsubs)`, `MultiLayerQG.updatevars!` (8×
-`sw_get_physical`: q, ψ, u, v per layer), `saveoutput` of `vars.ψh` (host).
-
-**Problems libsw does not hold** (a `Problem(CPU())`, any other stepper):
-every method SWLib adds is more specific than the reference's and falls back
-to it with `invoke`; `stepforward!(prob, diags, n)` falls back to FF's loop
-(`stepforward!(prob); increment!(diags)` per step).
-
-## 4. The binding (`integration/julia/SWLib.jl`, verbatim)
-
-```julia
 # SWLib.jl — the FourierFlows-side binding of libsw (include/sw.h, ABI 7).
 #
 # A maintainer's addition to the reference's run directories (INTEGRATION.md
@@ -695,47 +548,3 @@ end
 FourierFlows.device_array(::GPU) = Array
 
 end # module
-```
-
-Errors: every entry point returns `0` or a negative `SW_E_*`; `check` throws
-a Julia `ErrorException` carrying `sw_last_error`, which is how the reference
-surfaces `MethodError` / `DimensionMismatch`; `SW_E_NAN` is turned into the
-drivers' own NaN path (`blowup!`).
-
-## 5. Multi-GPU (slab decomposition)
-
-One Julia process per GPU (e.g. `mpiexecjl -n 8`): rank 0 calls
-`SWLib.comm_unique_id()` (`sw_comm_unique_id`), broadcasts the 128 bytes
-(`MPI.Bcast!`), and every rank calls `SWLib.set_decomposition!(nranks, rank,
-uid)` before the driver builds its problem: `sw_create` then gets
-`nranks = N, rank = r, local_slabs = 1, comm_unique_id = pointer(uid)` and
-`device = r`.  `sw_set_state` takes the full state on every rank (each keeps
-its columns); `sw_get_state`, `sw_get_physical`, `sw_diag` and the energy
-records return full results on every rank, so the driver code is the same
-on each.  Where RCCL is unavailable, `sw_config.exchange` takes a
-`@cfunction` doing `MPI.Alltoall!` on the two host buffers instead.
-
-## 6. Python binding (what the tests and bench use)
-
-`juliaraytracingsw_amd/_lib.py` is the `ctypes` stub (`SwConfig` mirrors
-`sw_config`, `EXPORTS` lists every header symbol and `tests/test_abi.py`
-checks both against the header and the built library).
-`juliaraytracingsw_amd/rotating_shallow_water.py`, `two_layer_qg.py`,
-`thomas_yamada.py`, `multilayer_qg.py` and `drivers.py` mirror the reference's
-module API:
-
-```python
-from juliaraytracingsw_amd import drivers, rotating_shallow_water as RSW
-prob, P = drivers.rsw_problem(2048, "FilteredAB3")   # RSWDriver.initialize_problem
-prob.stepforward(100)                                # stepforward!(prob, diags, 100)
-v = RSW.updatevars(prob)                             # updatevars!(prob): u, v, eta, zeta
-KE = RSW.kinetic_energy(prob)
-```
-
-Multi-GPU from Python (what `bench.py --mode slab` does, one process per GPU):
-
-```python
-from juliaraytracingsw_amd import slab_comm
-dec = slab_comm.rccl_decomposition(rank, world)     # broadcasts the RCCL unique id
-prob, P = drivers.rsw_problem(4096, "FilteredAB3", device=local_rank, decomposition=dec)
-```

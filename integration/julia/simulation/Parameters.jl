@@ -1,0 +1,9 @@
+# Run-directory Parameters.jl of simulation/ under libsw: the reference
+# parameters module (simulation/Parameters.jl, copied as Parameters.ref.jl:
+# device = GPU(), stepper = "FilteredRK4"), then libsw's methods on
+# GeophysicalFlows' MultiLayerQG, the package TwoLayerSimulation.jl loads.
+# Driver.jl and TwoLayerSimulation.jl run unchanged.
+include("Parameters.ref.jl")
+include("SWLib.jl")
+import GeophysicalFlows
+SWLib.attach!(GeophysicalFlows.MultiLayerQG)

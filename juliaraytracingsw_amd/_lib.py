@@ -10,7 +10,7 @@ import os
 
 import numpy as np
 
-SW_ABI_VERSION = 6
+SW_ABI_VERSION = 7
 SW_MODEL_RSW, SW_MODEL_QG2, SW_MODEL_TY, SW_MODEL_MLQG = 0, 1, 2, 3
 SW_STEP_FILTERED_AB3, SW_STEP_IFMAB3, SW_STEP_IFMRK4, SW_STEP_ETDRK4, SW_STEP_FILTERED_RK4 = 0, 1, 2, 3, 4
 SW_OK, SW_E_INVALID, SW_E_NOMEM, SW_E_HIP, SW_E_COMM, SW_E_NAN, SW_E_STATE = 0, -1, -2, -3, -4, -5, -6
@@ -29,6 +29,7 @@ EXPORTS = [
     "sw_get_physical", "sw_diag", "sw_set_energy_diagnostics", "sw_get_energy_diagnostics",
     "sw_profile_steps", "sw_step_alg_bytes", "sw_comm_unique_id",
     "sw_history_slots", "sw_get_history", "sw_set_history", "sw_reset_history", "sw_slab_geometry",
+    "sw_checkpoint_bytes", "sw_get_checkpoint", "sw_set_checkpoint",
 ]
 
 
@@ -115,6 +116,9 @@ def load(path: str | None = None):
         "sw_set_history": (C.c_int, [vp, i32, vp, sz]),
         "sw_reset_history": (C.c_int, [vp]),
         "sw_slab_geometry": (C.c_int, [C.POINTER(SwConfig), i32, C.POINTER(i32)]),
+        "sw_checkpoint_bytes": (C.c_int, [vp, C.POINTER(sz)]),
+        "sw_get_checkpoint": (C.c_int, [vp, vp, sz]),
+        "sw_set_checkpoint": (C.c_int, [vp, vp, sz]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -232,6 +236,20 @@ class Context:
 
     def reset_history(self):
         self._check(self.lib.sw_reset_history(self._h), "sw_reset_history")
+
+    def get_checkpoint(self):
+        """The fp64 restart blob (sw_get_checkpoint) as a uint8 array: state,
+        history, clock, pending Euler start-up steps — exact whatever the
+        caller precision."""
+        n = C.c_size_t()
+        self._check(self.lib.sw_checkpoint_bytes(self._h, C.byref(n)), "sw_checkpoint_bytes")
+        buf = np.empty(n.value, np.uint8)
+        self._check(self.lib.sw_get_checkpoint(self._h, buf.ctypes.data, buf.nbytes), "sw_get_checkpoint")
+        return buf
+
+    def set_checkpoint(self, blob):
+        a = np.ascontiguousarray(blob, dtype=np.uint8)
+        self._check(self.lib.sw_set_checkpoint(self._h, a.ctypes.data, a.nbytes), "sw_set_checkpoint")
 
     def calcN(self, sol):
         a = self._state_in(sol, "calcN")

@@ -88,7 +88,8 @@ struct sw_ctx {
   int64_t esums_n = 0;                       // records gathered (sw_get_energy_diagnostics)
   double t = 0.0;
   int64_t step = 0;
-  int64_t euler_until = 0;                   // sw_reset_history: Euler start-up while step < this
+  int euler_left = 0;                        // sw_reset_history: forward-Euler start-up steps still to run
+                                             // (cleared by sw_set_history; the clock does not move it)
   std::string err;
   // profiling
   bool prof = false;
@@ -536,7 +537,7 @@ sw::StepPtrs step_ptrs(const sw_ctx* c, const Slab& s) {
   a.sol = s.sol;
   a.sol_out = (st == SW_STEP_FILTERED_AB3) ? s.sol2 : s.sol;
   a.xs = s.xs;
-  a.euler = (c->step < 3 || c->step < c->euler_until) ? 1 : 0;
+  a.euler = (c->step < 3 || c->euler_left > 0) ? 1 : 0;
   a.stream = c->stream_state ? 1 : 0;
   if (st == SW_STEP_IFMRK4 || st == SW_STEP_FILTERED_RK4) {
     a.h0 = s.acc;
@@ -665,6 +666,7 @@ int step_once(sw_ctx* c) {
   }
   c->t += c->cfg.dt;
   c->step += 1;
+  if (c->euler_left > 0) c->euler_left -= 1;
   if (rec) {
     if (rsw && st == SW_STEP_FILTERED_AB3) record_energy(c, &Slab::sol2);  // the pre-update buffer
     else if (rsw && (st == SW_STEP_IFMRK4 || st == SW_STEP_FILTERED_RK4))
@@ -844,6 +846,8 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
     return fail(c, SW_E_INVALID, "ETDRK4 (diagonal L) is the Thomas-Yamada stepper and TY steps with ETDRK4 only");
   if (!pow2(k.nx) || !pow2(k.ny) || k.nx < 32 || k.ny < 32 || k.nx > 8192 || k.ny > 8192)
     return fail(c, SW_E_INVALID, "nx, ny must be powers of two in [32, 8192]");
+  if (!sw::length_built(ilog2(k.nx)) || !sw::length_built(ilog2(k.ny)))
+    return fail(c, SW_E_INVALID, "nx or ny: transform length not built into this library (one-length build)");
   if (!(k.aliased_fraction >= 0 && k.aliased_fraction < 1))
     return fail(c, SW_E_INVALID, "aliased_fraction must be in [0,1)");
   if (k.aliased_fraction == 0 && k.model == SW_MODEL_RSW)
@@ -1007,8 +1011,15 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   // temporal).  SW_STREAM_STATE=0/1 overrides.
   c->stream_state = step_bytes(c) > 256.0 * 1024 * 1024;
   if (const char* e = std::getenv("SW_STREAM_STATE")) c->stream_state = e[0] == '1';
-  // experiments (tools/sweep.sh): SW_CHECK_NAN=0 disables the NaN check of sw_step
-  if (const char* e = std::getenv("SW_CHECK_NAN")) c->cfg.check_nan = e[0] == '1';
+  // SW_CHECK_NAN=1 turns the NaN check of sw_step on; only an experiment
+  // build (-DSW_EXPERIMENTS, tools/build_variants.sh) lets =0 turn off a
+  // caller's check_nan = 1
+  if (const char* e = std::getenv("SW_CHECK_NAN")) {
+    if (e[0] == '1') c->cfg.check_nan = 1;
+#ifdef SW_EXPERIMENTS
+    else c->cfg.check_nan = 0;
+#endif
+  }
   c->stats.resize(K_NKERN);
   for (int i = 0; i < K_NKERN; ++i) c->stats[i].name = kname[i];
   return SW_OK;
@@ -1446,12 +1457,99 @@ int sw_set_history(sw_ctx* c, int32_t slot, const void* buf, size_t bytes) {
   for (Slab& s : c->sl) sw::launch_gather(c->nf, s.g, c->stage, s.hist[h], c->stream);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->euler_left = 0;  // the history is valid again: AB3 from the next step (clock.step >= 3)
   return SW_OK;
 }
 
 int sw_reset_history(sw_ctx* c) {
   if (!ready(c)) return SW_E_STATE;
-  c->euler_until = c->step + 3;
+  c->euler_left = 3;
+  return SW_OK;
+}
+
+// --- fp64 restart blob (sw_checkpoint_bytes / sw_get_checkpoint / sw_set_checkpoint)
+namespace {
+struct CkptHeader {
+  char magic[8];                       // "SWCKPT01"
+  int32_t abi, model, stepper, nx, ny, nf, nslots, euler_left;
+  double t;
+  int64_t step;
+  int64_t reserved;
+};
+static_assert(sizeof(CkptHeader) == 64, "checkpoint header is 64 bytes");
+const char kCkptMagic[8] = {'S', 'W', 'C', 'K', 'P', 'T', '0', '1'};
+
+int ckpt_slots(const sw_ctx* c) {
+  const int st = c->cfg.stepper;
+  return (st == SW_STEP_FILTERED_AB3 || st == SW_STEP_IFMAB3) ? 2 : 0;
+}
+size_t ckpt_bytes(const sw_ctx* c) { return sizeof(CkptHeader) + (size_t)(1 + ckpt_slots(c)) * full_bytes(c); }
+}  // namespace
+
+int sw_checkpoint_bytes(const sw_ctx* c, size_t* bytes) {
+  if (!ready(c) || !bytes) return SW_E_STATE;
+  *bytes = ckpt_bytes(c);
+  return SW_OK;
+}
+
+int sw_get_checkpoint(const sw_ctx* cc, void* buf, size_t bytes) {
+  sw_ctx* c = const_cast<sw_ctx*>(cc);
+  if (!ready(c)) return SW_E_STATE;
+  if (!buf || bytes != ckpt_bytes(c)) return fail(c, SW_E_INVALID, "sw_get_checkpoint: size mismatch");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  if (int rc = join_comm(c)) return rc;
+  CkptHeader h{};
+  std::memcpy(h.magic, kCkptMagic, 8);
+  h.abi = SW_ABI_VERSION;
+  h.model = c->cfg.model;
+  h.stepper = c->cfg.stepper;
+  h.nx = c->cfg.nx;
+  h.ny = c->cfg.ny;
+  h.nf = c->nf;
+  h.nslots = ckpt_slots(c);
+  h.euler_left = c->euler_left;
+  h.t = c->t;
+  h.step = c->step;
+  char* out = static_cast<char*>(buf);
+  std::memcpy(out, &h, sizeof(h));
+  const size_t fb = full_bytes(c);
+  for (int k = 0; k <= h.nslots; ++k) {  // fp64 always: no narrowing to the caller precision
+    if (k == 0) {
+      if (int rc = collect_full(c, &Slab::sol)) return rc;
+    } else {
+      const int hi = hist_index(c, k);
+      for (Slab& s : c->sl) s.view = s.hist[hi];
+      if (int rc = collect_full(c, &Slab::view)) return rc;
+    }
+    HIPCHK(c, hipMemcpyAsync(out + sizeof(h) + k * fb, c->stage, fb, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  return SW_OK;
+}
+
+int sw_set_checkpoint(sw_ctx* c, const void* buf, size_t bytes) {
+  if (!ready(c)) return SW_E_STATE;
+  if (!buf || bytes != ckpt_bytes(c)) return fail(c, SW_E_INVALID, "sw_set_checkpoint: size mismatch");
+  CkptHeader h;
+  std::memcpy(&h, buf, sizeof(h));
+  if (std::memcmp(h.magic, kCkptMagic, 8) != 0) return fail(c, SW_E_INVALID, "sw_set_checkpoint: not a libsw checkpoint");
+  if (h.model != c->cfg.model || h.stepper != c->cfg.stepper || h.nx != c->cfg.nx || h.ny != c->cfg.ny ||
+      h.nf != c->nf || h.nslots != ckpt_slots(c) || h.step < 0 || h.euler_left < 0 || h.euler_left > 3)
+    return fail(c, SW_E_INVALID, "sw_set_checkpoint: checkpoint of a different problem or stepper");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  if (int rc = join_comm(c)) return rc;
+  const char* in = static_cast<const char*>(buf);
+  const size_t fb = full_bytes(c);
+  for (int k = 0; k <= h.nslots; ++k) {
+    HIPCHK(c, hipMemcpyAsync(c->stage, in + sizeof(h) + k * fb, fb, hipMemcpyHostToDevice, c->stream));
+    for (Slab& s : c->sl) sw::launch_gather(c->nf, s.g, c->stage, k == 0 ? s.sol : s.hist[hist_index(c, k)], c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // the staging buffer is reused
+  }
+  c->t = h.t;
+  c->step = h.step;
+  c->euler_left = h.euler_left;
+  c->mixed_valid = false;
   return SW_OK;
 }
 

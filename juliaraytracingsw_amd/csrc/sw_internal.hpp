@@ -407,6 +407,9 @@ struct Bufs;  // fwd
 // k_col_inv; col_fwd / col_step: fields); n < 0 = from the first to the last
 int col_inv_groups(int model);
 int col_fields(int model);
+// transform length 2^log2n instantiated in this build (a one-length
+// experiment build, SW_ONLY_LOG2, holds one; sw_create rejects the others)
+bool length_built(int log2n);
 void launch_col_inv(int model, const Geom& g, const Phys& p, const double2* X, double2* Minv,
                     const double2* tw_y, hipStream_t s, int g0 = 0, int ng = -1);
 void launch_row(int model, const Geom& g, const Phys& p, const double2* Minv, double2* Mfwd,

@@ -2195,6 +2195,12 @@ static void by_len(int log2n, F&& f) {
   }
 }
 
+bool length_built(int log2n) {
+  bool ok = false;
+  by_len(log2n, [&](auto) { ok = true; });
+  return ok;
+}
+
 // number of column-pass groups per launch unit: col_inv groups, col_fwd fields
 int col_inv_groups(int model) { return model == MODEL_RSW ? 3 : (model == MODEL_TY ? 5 : 2); }
 int col_fields(int model) { return model == MODEL_RSW ? 3 : (model == MODEL_TY ? 4 : 2); }

@@ -150,9 +150,13 @@ def load_initial_condition_from_file(prob, filename, key):
 
 def checkpoint(prob, filename):
     """Write a restart file: the problem description (``saveproblem``), the
-    state, the clock and the stepper's history (RHS₋₁/RHS₋₂ or N₋₁/N₋₂ of
-    the AB3 steppers, ``sw_get_history``), so that ``restart`` continues
-    bit for bit as if the run had not stopped."""
+    state in the caller's precision (``checkpoint/sol``, for reading), and
+    libsw's fp64 restart blob (``checkpoint/blob``, ``sw_get_checkpoint``):
+    state, stepper history (RHS₋₁/RHS₋₂ or N₋₁/N₋₂ of the AB3 steppers),
+    clock and any pending Euler start-up steps, all in fp64 whatever the
+    problem's ``T`` — so that ``restart`` continues bit for bit as if the run
+    had not stopped (a ``T = Float32`` problem's device state is fp64; a
+    ComplexF32 copy would round it)."""
     out = Output(prob, filename)
     out.saveproblem()
     ctx = prob.ctx
@@ -161,33 +165,25 @@ def checkpoint(prob, filename):
         t, step = ctx.get_clock()
         _put(zf, "checkpoint/t", t)
         _put(zf, "checkpoint/step", step)
-        for k in range(1, ctx.history_slots() + 1):
-            _put(zf, f"checkpoint/history/{k}", ctx.get_history(k))
+        _put(zf, "checkpoint/blob", ctx.get_checkpoint())
     return out
 
 
 def restart(prob, filename, field="sol"):
     """Resume a run on the same grid.
 
-    From a ``checkpoint`` file: state, clock and stepper history, so the
-    continuation equals uninterrupted stepping bitwise.  From an ``Output``
-    file (its last ``snapshots/<field>/<step>``): state and clock (t, step);
-    the history is not in the file, so the AB3 steppers restart with three
-    forward-Euler steps (``sw_reset_history``), as they start at step 0 —
-    which is what the reference's snapshot restart does
-    (``load_from_snapshot!``, rsw/RSWDriver.jl:10-36, clock from zero)."""
+    From a ``checkpoint`` file: the fp64 blob restores state, clock and
+    stepper history, so the continuation equals uninterrupted stepping
+    bitwise (also for ``T = Float32``).  From an ``Output`` file (its last
+    ``snapshots/<field>/<step>``): state and clock (t, step); the history is
+    not in the file, so the AB3 steppers restart with three forward-Euler
+    steps (``sw_reset_history``), as they start at step 0 — which is what the
+    reference's snapshot restart does (``load_from_snapshot!``,
+    rsw/RSWDriver.jl:10-36, clock from zero)."""
     with np.load(filename) as d:
-        if "checkpoint/sol" in d.files:
-            prob.sol = d["checkpoint/sol"]
-            step = int(d["checkpoint/step"])
-            prob.clock.set(float(d["checkpoint/t"]), step)
-            k = 1
-            while f"checkpoint/history/{k}" in d.files:
-                prob.ctx.set_history(k, d[f"checkpoint/history/{k}"])
-                k += 1
-            if k == 1 and prob.ctx.history_slots() > 0:
-                prob.ctx.reset_history()
-            return step
+        if "checkpoint/blob" in d.files:
+            prob.ctx.set_checkpoint(d["checkpoint/blob"])
+            return int(d["checkpoint/step"])
     key = snapshot_keys(filename, field)[-1]
     step = int(key.rsplit("/", 1)[1])
     with np.load(filename) as d:

@@ -47,16 +47,13 @@ def updatevars(prob):
 
 
 def enforce_reality_condition(prob):
-    """``enforce_reality_condition!(prob)`` (:94-117): each field through
-    c2r then r2c.  On a dealiased state that is the projection onto
-    Hermitian-consistent spectra: the kr = 0 column becomes
-    (X(0, l) + conj X(0, -l)) / 2 (numpy's c2r rule); every other
-    live mode is unchanged."""
-    s = prob.sol
-    c0 = s[:, :, 0]
-    mirror = np.conj(np.roll(c0[:, ::-1], 1, axis=1))  # X(0, -l)
-    s[:, :, 0] = 0.5 * (c0 + mirror)
-    prob.sol = s
+    """``enforce_reality_condition!(prob)`` (:103-123): ``dealias!(sol)``, the
+    spectral and physical vars, then ``mul!(sol[:,:,k], grid.rfftplan, …)``
+    for each field.  In Julia ``sol[:,:,k]`` (no ``@views``) is a copy, so
+    those r2c's write into temporaries and the state is left as it is: the
+    function amounts to ``dealias!`` + ``updatevars!`` — which is what this
+    does (the libsw state is dealiased already).  Returns the physical vars."""
+    return updatevars(prob)
 
 
 def baroclinic_energy(prob):

@@ -1,0 +1,515 @@
+"""ctypes twin of integration/julia/SWLib.jl and line-by-line replays of the
+three drivers the north star names, through include/sw.h.
+
+Julia is not installed here, so the Julia shim cannot run.  This module is
+its Python twin: every SWLib.jl function that reaches libsw has a function
+of the same name here (``run_steps!`` -> ``run_steps`` …) issuing the same C
+entry points in the same order (tests/test_julia_shim.py checks that by
+text), plus host stand-ins for the FourierFlows objects the drivers touch
+(Problem, Clock, Diagnostic, vars).  The replays transcribe the drivers'
+``start!`` bodies statement by statement, at test sizes:
+
+* ``rsw_driver_start``   rsw/RSWDriver.jl:134-226 (T = Float32, dev = GPU())
+* ``ty_driver_start``    thomasyamada/TYdriver.jl:111-231 (ARGS = ["GPU"];
+                         the second Problem(CPU()) with LIBSW_CPU=1)
+* ``mlqg_simulation_start`` simulation/TwoLayerSimulation.jl:13-143
+
+Host-side set-up work the Julia drivers do with FFTW on the host grid
+(initial conditions, enforce_reality_condition!'s r2c) is done with numpy
+FFTs on the oracle's grid (test infrastructure).  Every C call is recorded
+in ``Twin.calls``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+import os
+import types
+import weakref
+
+import numpy as np
+
+import sw_oracle as O
+from juliaraytracingsw_amd import _lib
+
+SW_E_NAN = _lib.SW_E_NAN
+STEPPERS = _lib.STEPPERS
+
+
+# --------------------------------------------------------------- FF stand-ins
+class Clock:
+    """FourierFlows Clock{T}: dt, t, step, t advanced in T arithmetic."""
+
+    def __init__(self, T, dt):
+        self.T = T
+        self.dt, self.t, self.step = T(dt), T(0), 0
+
+
+class Equation:
+    def __init__(self, T, dims):
+        self.T, self.dims = np.dtype(np.complex64 if T == np.float32 else np.complex128), dims
+
+
+class Problem:
+    """FourierFlows.Problem(sol, clock, eqn, grid, vars, params, timestepper)."""
+
+    def __init__(self, sol, clock, eqn, grid, vars_, params, ts):
+        self.sol, self.clock, self.eqn, self.grid = sol, clock, eqn, grid
+        self.vars, self.params, self.timestepper = vars_, params, ts
+
+
+class Diagnostic:
+    """FF Diagnostic(calc, prob; freq, nsteps): data[0] = calc(prob) at
+    construction, i = 1 (FF keeps i as the count of entries held)."""
+
+    def __init__(self, calc, prob, *, nsteps, freq=1):
+        n = math.ceil((nsteps + 1) / freq)
+        self.calc, self.prob, self.freq = calc, prob, freq
+        self.value = calc(prob)
+        self.data, self.t, self.steps = [None] * n, np.zeros(n), np.zeros(n, np.int64)
+        self.data[0], self.t[0], self.steps[0] = self.value, float(prob.clock.t), prob.clock.step
+        self.i = 1
+
+
+# ------------------------------------------------------------------- the twin
+class SWStepper:
+    def __init__(self, ctx, filt, model):
+        self.ctx, self.filter, self.model = ctx, filt, model
+        self.freq, self.seen, self.record_t, self.blewup = 0, 0, [], False
+
+
+class Twin:
+    """SWLib.jl, function for function (names without the Julia '!')."""
+
+    def __init__(self):
+        self.lib = _lib.load()
+        self.calls = []
+        self.RECORD = {}
+
+    def c(self, name, *args):
+        self.calls.append(name)
+        return getattr(self.lib, name)(*args)
+
+    def check(self, ts, rc, what):
+        if rc != 0:
+            msg = self.lib.sw_last_error(ts.ctx).decode()
+            raise _lib.LibSWError(f"libsw {what}: {msg} (code {rc})", rc)
+
+    # -- SWLib.config / set_filter! / SWStepper -------------------------------
+    def config(self, model, stepper, *, nx, ny, Lx, Ly, aliased_fraction, dt, T):
+        if stepper not in STEPPERS:
+            raise _lib.LibSWError(f"libsw: stepper {stepper!r} is not built")
+        cfg = _lib.SwConfig()
+        self.c("sw_config_default", C.byref(cfg))
+        cfg.model, cfg.stepper = model, STEPPERS[stepper]
+        cfg.nx, cfg.ny, cfg.Lx, cfg.Ly = nx, ny, Lx, Ly
+        cfg.aliased_fraction, cfg.dt = aliased_fraction, float(T(dt))
+        cfg.precision = _lib.SW_PREC_F32 if T == np.float32 else _lib.SW_PREC_F64
+        cfg.device = int(os.environ.get("LIBSW_DEVICE", "0"))
+        return cfg
+
+    @staticmethod
+    def set_filter(cfg, use_filter, order=4, innerK=0.65, outerK=1.0, tol=1e-15, diagonal=False):
+        cfg.use_filter = 1 if use_filter else 0
+        cfg.filter_order, cfg.filter_innerK, cfg.filter_outerK, cfg.filter_tol = order, innerK, outerK, tol
+        return dict(order=order, innerK=innerK, outerK=outerK, tol=tol)
+
+    def SWStepper(self, cfg, equation, filt):
+        h = C.c_void_p()
+        rc = self.c("sw_create", C.byref(h), C.byref(cfg))
+        if rc != 0:
+            msg = self.lib.sw_last_error(h).decode() if h else "sw_create failed"
+            self.c("sw_destroy", h)
+            raise _lib.LibSWError(f"libsw sw_create: {msg} (code {rc})", rc)
+        ts = SWStepper(h, filt, cfg.model)
+        ts.finalizer = weakref.finalize(ts, lambda: self.c("sw_destroy", h))  # Julia's finalizer
+        return ts
+
+    def destroy(self, prob):
+        """the Julia GC finalising the stepper (``startup_prob = nothing``)"""
+        prob.timestepper.finalizer()
+
+    # -- state traffic ---------------------------------------------------------
+    def upload(self, ts, sol):
+        a = np.ascontiguousarray(sol)
+        self.check(ts, self.c("sw_set_state", ts.ctx, a.ctypes.data, a.nbytes), "sw_set_state")
+
+    def download(self, sol, ts):
+        self.check(ts, self.c("sw_get_state", ts.ctx, sol.ctypes.data, sol.nbytes), "sw_get_state")
+
+    def push_clock(self, ts, clock):
+        self.check(ts, self.c("sw_set_clock", ts.ctx, float(clock.t), int(clock.step)), "sw_set_clock")
+
+    def load_solution(self, prob):
+        ts = prob.timestepper
+        self.upload(ts, prob.sol)
+        self.download(prob.sol, ts)
+        self.push_clock(ts, prob.clock)
+
+    def physical(self, dst, ts, fid):
+        """dst: a host [ny][nx] array (Julia (nx, ny)) or one layer of one"""
+        self.check(ts, self.c("sw_get_physical", ts.ctx, int(fid), dst.ctypes.data, dst.nbytes), "sw_get_physical")
+        return dst
+
+    # -- stepping and records --------------------------------------------------
+    def run_steps(self, sol, clock, ts, n):
+        rc = self.c("sw_step", ts.ctx, int(n))
+        ts.blewup = rc == SW_E_NAN
+        if not ts.blewup:
+            self.check(ts, rc, "sw_step")
+        for _ in range(n):
+            clock.t = clock.T(clock.t + clock.dt)
+            clock.step += 1
+            if ts.freq > 0 and clock.step % ts.freq == 0:
+                ts.record_t.append(float(clock.t))
+        self.download(sol, ts)
+
+    def attach_diagnostics(self, prob, diags):
+        ts = prob.timestepper
+        if not diags:
+            return
+        freq = diags[0].freq
+        if any(d.freq != freq for d in diags):
+            raise _lib.LibSWError("libsw records one diagnostics frequency per problem")
+        if any(d.calc not in self.RECORD for d in diags):
+            raise _lib.LibSWError("libsw records the models' energy diagnostics only")
+        cap = max(len(d.t) for d in diags)
+        self.check(ts, self.c("sw_set_energy_diagnostics", ts.ctx, int(freq), int(cap)), "sw_set_energy_diagnostics")
+        ts.freq, ts.seen = freq, 0
+        ts.record_t.clear()
+
+    def take_records(self, prob, diags):
+        ts = prob.timestepper
+        n = C.c_int64()
+        self.check(ts, self.c("sw_get_energy_diagnostics", ts.ctx, None, 0, C.byref(n)), "sw_get_energy_diagnostics")
+        if n.value <= ts.seen:
+            return
+        recs = (_lib.SwEnergyRecord * n.value)()
+        self.check(ts, self.c("sw_get_energy_diagnostics", ts.ctx, recs, n.value, C.byref(n)),
+                   "sw_get_energy_diagnostics")
+        for k, r in enumerate(recs[ts.seen:n.value]):
+            for d in diags:
+                if d.i >= len(d.t):
+                    continue
+                d.data[d.i] = self.RECORD[d.calc](r, d.value)
+                d.t[d.i] = ts.record_t[ts.seen + k]
+                d.steps[d.i] = r.step
+                d.value = d.data[d.i]
+                d.i += 1
+        ts.seen = n.value
+
+    def stepforward(self, prob, diags, nsteps):
+        """FourierFlows.stepforward!(prob, diags, nsteps) for a libsw problem."""
+        ts = prob.timestepper
+        if ts.freq == 0:
+            self.attach_diagnostics(prob, diags)
+        self.run_steps(prob.sol, prob.clock, ts, nsteps)
+        self.take_records(prob, diags)
+        if ts.blewup:
+            blowup(prob)
+
+
+def blowup(prob):
+    for name in ("η", "q", "u", "v"):
+        if hasattr(prob.vars, name):
+            getattr(prob.vars, name)[...] = np.nan
+
+
+def _host_vars(grid, T, spec, phys, nlayers=None):
+    shape_p = (grid.ny, grid.nx) if nlayers is None else (nlayers, grid.ny, grid.nx)
+    shape_s = (grid.nl, grid.nkr) if nlayers is None else (nlayers, grid.nl, grid.nkr)
+    ct = np.complex64 if T == np.float32 else np.complex128
+    v = types.SimpleNamespace()
+    for n in phys:
+        setattr(v, n, np.zeros(shape_p, T))
+    for n in spec:
+        setattr(v, n, np.zeros(shape_s, ct))
+    return v
+
+
+def _filter(grid, nf, filters, T, **fkw):
+    f = O.makefilter(grid, **fkw) if filters else np.ones((grid.nl, grid.nkr))
+    return np.broadcast_to(f, (nf,) + f.shape).astype(T)
+
+
+# ------------------------------------------------------------------- models
+def rsw_problem(tw, *, nx=128, ny=None, Lx=2 * np.pi, Ly=None, nu=1.0e-16, nnu=4, f=1.0, Cg=1.0,
+                stepper="IFMAB3", dt=5e-2, aliased_fraction=1 / 3, T=np.float64, use_filter=False, **skw):
+    """SWLib.rsw_problem (rsw/RotatingShallowWater.jl:70-99 keywords)."""
+    ny = nx if ny is None else ny
+    Ly = Lx if Ly is None else Ly
+    grid = O.TwoDGrid(nx, Lx, ny=ny, Ly=Ly, aliased_fraction=aliased_fraction)
+    params = types.SimpleNamespace(ν=T(nu), nν=nnu, f=T(f), Cg2=T(Cg ** 2))
+    vars_ = _host_vars(grid, T, ("uh", "vh", "ηh", "ζh"), ("u", "v", "η", "ζ"))
+    eq = Equation(T, (3, grid.nl, grid.nkr))
+    cfg = tw.config(_lib.SW_MODEL_RSW, stepper, nx=nx, ny=ny, Lx=Lx, Ly=Ly, aliased_fraction=aliased_fraction,
+                    dt=dt, T=T)
+    cfg.f, cfg.Cg, cfg.nu, cfg.nnu = float(params.f), Cg, float(params.ν), nnu
+    filters = stepper in ("FilteredAB3", "FilteredRK4") or use_filter
+    fkw = tw.set_filter(cfg, use_filter, **skw)
+    ts = tw.SWStepper(cfg, eq, _filter(grid, 3, filters, T, **fkw))
+    return Problem(np.zeros(eq.dims, eq.T), Clock(T, dt), eq, grid, vars_, params, ts)
+
+
+def ty_problem(tw, *, nx=128, ny=None, Lx=2 * np.pi, Ly=None, nu=3.5e-25, nnu=8, Ro=0.2, stepper="ETDRK4",
+               dt=5e-2, aliased_fraction=1 / 3, T=np.float64):
+    """SWLib.ty_problem (thomasyamada/ThomasYamada.jl:55-74)."""
+    ny = nx if ny is None else ny
+    Ly = Lx if Ly is None else Ly
+    grid = O.TwoDGrid(nx, Lx, ny=ny, Ly=Ly, aliased_fraction=aliased_fraction)
+    params = types.SimpleNamespace(ν=T(nu), nν=nnu, Ro=T(Ro))
+    vars_ = _host_vars(grid, T, ("uch", "vch", "uth", "vth", "ζth", "ψth", "pch", "qch"),
+                       ("uc", "vc", "ut", "vt", "ζt", "ψt", "pc", "qc"))
+    eq = Equation(T, (4, grid.nl, grid.nkr))
+    cfg = tw.config(_lib.SW_MODEL_TY, stepper, nx=nx, ny=ny, Lx=Lx, Ly=Ly, aliased_fraction=aliased_fraction,
+                    dt=dt, T=T)
+    cfg.nu, cfg.nnu, cfg.Ro = float(params.ν), nnu, float(params.Ro)
+    ts = tw.SWStepper(cfg, eq, _filter(grid, 4, False, T))
+    return Problem(np.zeros(eq.dims, eq.T), Clock(T, dt), eq, grid, vars_, params, ts)
+
+
+def mlqg_problem(tw, nlayers, *, nx, Lx, f0, H, b, U, mu, beta, dt, stepper="FilteredRK4", aliased_fraction=1 / 3,
+                 nu=0.0, nnu=1, T=np.float64):
+    """SWLib.mlqg_problem: GF MultiLayerQG.Problem(nlayers, dev; …) keywords
+    (simulation/TwoLayerSimulation.jl:37-38); the host GF problem supplies
+    grid, params and FilteredRK4's filter (FF makefilter defaults)."""
+    assert nlayers == 2
+    grid = O.TwoDGrid(nx, Lx, aliased_fraction=aliased_fraction)
+    params = O.MLQGParams(f0, H, b, U, mu, beta, nu, nnu)
+    vars_ = _host_vars(grid, T, ("qh", "ψh", "uh", "vh"), ("q", "ψ", "u", "v"), nlayers=2)
+    eq = Equation(T, (2, grid.nl, grid.nkr))
+    cfg = tw.config(_lib.SW_MODEL_MLQG, stepper, nx=nx, ny=nx, Lx=Lx, Ly=Lx, aliased_fraction=aliased_fraction,
+                    dt=dt, T=T)
+    cfg.f0, cfg.beta = f0, beta
+    cfg.H[:], cfg.b[:], cfg.Ulayer[:] = [float(x) for x in H], [float(x) for x in b], [float(x) for x in U]
+    cfg.mu, cfg.nu, cfg.nnu = mu, nu, nnu
+    filters = stepper in ("FilteredAB3", "FilteredRK4")
+    tw.set_filter(cfg, filters)
+    ts = tw.SWStepper(cfg, eq, _filter(grid, 2, filters, T))
+    return Problem(np.zeros(eq.dims, eq.T), Clock(T, dt), eq, grid, vars_, params, ts)
+
+
+# -------------------------------------------------- updatevars! on the device
+def rsw_updatevars(tw, prob):
+    v, g, sol, ts = prob.vars, prob.grid, prob.sol, prob.timestepper
+    v.uh[...], v.vh[...], v.ηh[...] = sol[0], sol[1], sol[2]
+    v.ζh[...] = 1j * g.kr[None, :] * v.vh - 1j * g.l[:, None] * v.uh - prob.params.f * v.ηh
+    tw.physical(v.u, ts, 0)
+    tw.physical(v.v, ts, 1)
+    tw.physical(v.η, ts, 2)
+    tw.physical(v.ζ, ts, 3)
+
+
+def ty_updatevars(tw, prob, all_=True):
+    v, g, sol, ts = prob.vars, prob.grid, prob.sol, prob.timestepper
+    v.ζth[...], v.uch[...], v.vch[...], v.pch[...] = sol[0], sol[1], sol[2], sol[3]
+    tw.physical(v.ζt, ts, 3)
+    tw.physical(v.uc, ts, 0)
+    tw.physical(v.vc, ts, 1)
+    tw.physical(v.pc, ts, 2)
+    if not all_:
+        return
+    kr, l = g.kr[None, :], g.l[:, None]
+    v.ψth[...] = -v.ζth * g.invKrsq
+    v.uth[...] = -1j * l * v.ψth
+    v.vth[...] = 1j * kr * v.ψth
+    v.qch[...] = 1j * kr * v.vch - 1j * l * v.uch - v.pch
+    tw.physical(v.ut, ts, 8)
+    tw.physical(v.vt, ts, 9)
+    tw.physical(v.qc, ts, 4)
+
+
+def mlqg_updatevars(tw, prob):
+    v, g, sol, p, ts = prob.vars, prob.grid, prob.sol, prob.params, prob.timestepper
+    v.qh[...] = sol
+    v.ψh[...] = O.mlqg_streamfunction(v.qh.astype(np.complex128), g, p)
+    v.uh[...] = -1j * g.l[:, None] * v.ψh
+    v.vh[...] = 1j * g.kr[None, :] * v.ψh
+    for layer in range(2):
+        for field, fid in ((v.q, 4), (v.ψ, 5), (v.u, 0), (v.v, 1)):
+            tw.physical(field[layer], ts, 8 * layer + fid)
+
+
+# ------------------------------------------------- set_solution! / set_q!
+def rsw_set_solution(tw, prob, u0h, v0h, eta0h):
+    prob.sol[0], prob.sol[1], prob.sol[2] = u0h, v0h, eta0h
+    tw.load_solution(prob)
+    rsw_updatevars(tw, prob)
+
+
+def ty_set_solution(tw, prob, z0h, u0h, v0h, p0h):
+    prob.sol[0], prob.sol[1], prob.sol[2], prob.sol[3] = z0h, u0h, v0h, p0h
+    tw.load_solution(prob)
+    ty_updatevars(tw, prob)
+
+
+def mlqg_set_q(tw, prob, q):
+    prob.vars.qh[...] = np.fft.rfft2(q, axes=(-2, -1))  # GF set_q!: mul!(qh, rfftplan, q)
+    prob.sol[...] = prob.vars.qh
+    tw.load_solution(prob)
+    mlqg_updatevars(tw, prob)
+
+
+# ------------------------------------------------------ the drivers' start!
+def rsw_driver_start(tw, nx=128, nsteps=240, output_freq=20, diags_freq=10, spinup_step=120, seed=20261015,
+                     T=np.float32):
+    """rsw/RSWDriver.jl:134-226 with RSWParameters.jl values, dev = GPU(),
+    T = Float32; nsteps / output_freq / diags_freq at test size."""
+    P = dict(L=2 * np.pi, f=3.0, Cg=1.0, nnu=4, nutune=20.0, cfltune=0.01, filter_order=8, af=1 / 3,
+             Kg=(10, 13), ag=0.2, Kw=(0, 5), aw=0.1)
+    # initialize_problem (:134-176)
+    Lx, dx = P["L"], P["L"] / nx
+    kmax = (nx / 2 - 1) * Lx / (2 * np.pi) * (1 - P["af"])
+    umax = P["ag"] + P["aw"]
+    dt = P["cfltune"] / umax * dx
+    nu = P["nutune"] * dx / (kmax ** (2 * P["nnu"])) / dt
+    use_filter = P["nutune"] == 0
+    prob = rsw_problem(tw, Lx=Lx, nx=nx, dt=dt, f=P["f"], Cg=P["Cg"], T=T, nnu=P["nnu"], nu=nu,
+                       aliased_fraction=P["af"], order=P["filter_order"], use_filter=use_filter)
+    grid, params = prob.grid, prob.params
+    # set_shafer_initial_condition! (:88-132) on the host grid
+    rng = np.random.default_rng(seed)
+    (ugh, vgh, egh), (uwh, vwh, ewh) = O.shafer_ic_parts(grid, P["Kg"], P["Kw"], float(params.f),
+                                                         float(params.Cg2), rng)
+    Umax = np.max(np.sqrt(grid.irfft(ugh) ** 2 + grid.irfft(vgh) ** 2))
+    ugh, vgh, egh = (x * (P["ag"] / Umax) for x in (ugh, vgh, egh))
+    Umax = np.max(np.sqrt(grid.irfft(uwh) ** 2 + grid.irfft(vwh) ** 2))
+    uwh, vwh, ewh = (x * (P["aw"] / Umax) for x in (uwh, vwh, ewh))
+    rsw_set_solution(tw, prob, ugh + uwh, vgh + vwh, egh + ewh)
+    ic = prob.sol.copy()
+    # start! (:184-226)
+    outputs = [("problem",)]
+
+    def kinetic_energy(pr):  # rsw/RotatingShallowWater.jl:323-327 on the host vars
+        v = pr.vars
+        return (O.parsevalsum2(v.uh, grid) + O.parsevalsum2(v.vh, grid)) / (2 * grid.Lx * grid.Ly)
+
+    def potential_energy(pr):  # :329-333
+        return 0.5 * float(params.Cg2) * O.parsevalsum2(pr.vars.ηh, grid) / (grid.Lx * grid.Ly)
+
+    tw.RECORD[kinetic_energy] = lambda r, v: r.ke
+    tw.RECORD[potential_energy] = lambda r, v: r.pe
+    diags = [Diagnostic(kinetic_energy, prob, nsteps=nsteps, freq=diags_freq),
+             Diagnostic(potential_energy, prob, nsteps=nsteps, freq=diags_freq)]
+    # enforce_reality_condition! (:118-133): the reference's method; its
+    # updatevars! is the libsw one, the r2c's are FFTW on the host
+    grid.dealias(prob.sol)
+    rsw_updatevars(tw, prob)
+    prob.vars.uh[...], prob.vars.vh[...], prob.vars.ηh[...] = (grid.rfft(prob.vars.u), grid.rfft(prob.vars.v),
+                                                               grid.rfft(prob.vars.η))
+    outputs.append((prob.clock.step, prob.sol.copy()))
+    cfls = []
+    for step in range(0, round(nsteps / output_freq) + 1):
+        if step % 100 == 0:
+            v = prob.vars
+            cfls.append(float(prob.clock.dt) * max(np.max(np.abs(v.u)) / grid.dx, np.max(np.abs(v.v)) / grid.dy))
+        tw.stepforward(prob, diags, output_freq)
+        if np.any(np.isnan(prob.vars.η)):
+            raise RuntimeError("Solution is NaN")
+        rsw_updatevars(tw, prob)
+        if prob.clock.step >= spinup_step:
+            outputs.append((prob.clock.step, prob.sol.copy()))
+    return prob, diags, outputs, ic, cfls
+
+
+def ty_driver_start(tw, nx=64, startup_dt=3e-2, dt=5e-3, startup_nsteps=200, startup_nsubs=50, nsteps=60,
+                    nsubs=20, seed=5678, libsw_cpu=True):
+    """thomasyamada/TYdriver.jl:111-231 with gpu-setup/Parameters.jl values
+    (Lx = 6π, Ro = 1, ν = 5e-34 (Lx/2π)^16, nν = 8, ETDRK4, annuli k0w = (0, 5/3),
+    k0g = (10/3, 13/3), at = 0, ag = 0.3, aw = 0.1) at test size.  ARGS[1] =
+    "GPU": the start-up problem is libsw's; the second Problem(CPU()) is
+    libsw's with LIBSW_CPU=1 (libsw_cpu), else the reference's CPU path."""
+    P = dict(Lx=6 * np.pi, Ro=1.0, nnu=8, stepper="ETDRK4", k0w=(0.0, 5 / 3), k0g=(10 / 3, 13 / 3),
+             at=0.0, ag=0.3, aw=0.1)
+    nu = 5.0e-34 * (P["Lx"] / (2 * np.pi)) ** 16
+    sp = ty_problem(tw, Lx=P["Lx"], nx=nx, nu=nu, nnu=P["nnu"], Ro=P["Ro"], stepper=P["stepper"], dt=startup_dt)
+    grid = sp.grid
+    ic = O.ty_initial_condition(grid, np.random.default_rng(seed), k0w_range=P["k0w"], k0g_range=P["k0g"],
+                                at=P["at"], ag=P["ag"], aw=P["aw"])
+    ty_set_solution(tw, sp, *ic)
+    ic = sp.sol.copy()
+
+    def wave_geostrophic_energy(pr):
+        return O.ty_energies(pr.sol.copy(), grid)[2]
+
+    def barotropic_energy(pr):
+        return O.ty_energies(pr.sol.copy(), grid)[0]
+
+    tw.RECORD[wave_geostrophic_energy] = lambda r, v: ((r.wg[0], r.wg[1]), (r.wg[2], r.wg[3]))
+    tw.RECORD[barotropic_energy] = lambda r, v: r.ke2
+    diags = [Diagnostic(wave_geostrophic_energy, sp, nsteps=startup_nsteps, freq=25),
+             Diagnostic(barotropic_energy, sp, nsteps=startup_nsteps, freq=25)]
+    outputs = [("startup",)]
+    ty_updatevars(tw, sp)
+    outputs.append((sp.clock.step, sp.sol.copy()))
+    startup_steps = 0
+    for j in range(0, round(startup_nsteps / startup_nsubs) + 1):
+        if j % (4000 / startup_nsubs) == 0:
+            v = sp.vars
+            _ = float(sp.clock.dt) * max(v.uc.max() / grid.dx, v.vc.max() / grid.dy, v.ut.max() / grid.dx,
+                                         v.vt.max() / grid.dy)
+        tw.stepforward(sp, diags, startup_nsubs)
+        startup_steps += startup_nsubs
+        ty_updatevars(tw, sp, all_=False)  # enforce_reality_condition!
+        ty_updatevars(tw, sp)
+    startup_diags = diags
+    outputs.append((sp.clock.step, sp.sol.copy()))
+    if not libsw_cpu:
+        return sp, startup_diags, None, None, outputs, ic, startup_steps
+    prob = ty_problem(tw, Lx=P["Lx"], nx=nx, nu=nu, nnu=P["nnu"], Ro=P["Ro"], stepper=P["stepper"], dt=dt)
+    prob.clock.t = sp.clock.t
+    ty_set_solution(tw, prob, sp.sol[0], sp.sol[1], sp.sol[2], sp.sol[3])
+    tw.destroy(sp)  # startup_prob = nothing
+    diags = [Diagnostic(wave_geostrophic_energy, prob, nsteps=startup_nsteps, freq=25),
+             Diagnostic(barotropic_energy, prob, nsteps=startup_nsteps, freq=25)]
+    ty_updatevars(tw, prob)
+    outputs.append((prob.clock.step, prob.sol.copy()))
+    for j in range(0, round(nsteps / nsubs) + 1):
+        tw.stepforward(prob, diags, nsubs)
+        ty_updatevars(tw, prob, all_=False)
+        ty_updatevars(tw, prob)
+        outputs.append((prob.clock.step, prob.sol.copy()))
+    return prob, startup_diags, diags, None, outputs, ic, startup_steps
+
+
+def mlqg_simulation_start(tw, nx=64, nsteps=100, nsubs=25, seed=1234, amplitude_scale=50.0):
+    """simulation/TwoLayerSimulation.jl:13-143 with simulation/Parameters.jl
+    values (FilteredRK4, f = 1, rd = 1/15, ℓ = 1/2, avg_U = 0.1, H = [½, ½],
+    β = 0, aliased_fraction = 0) at test size; the initial PV amplitude is
+    scaled up (amplitude_scale) so that J(ψ, q) acts within the test's steps."""
+    f0, rd, lv, avg_U, H0 = 1.0, 1 / 15, 1 / 2, 0.1, 1.0
+    c1, c2 = 3.2, 0.36
+    l_star = lv / rd
+    kappa = c2 / math.log(l_star / c1)
+    s = avg_U / l_star
+    mu = 2 * s * kappa / rd
+    b1 = 4 * f0 ** 2 * rd ** 2 / H0 + 1.0
+    Lx = 2 * np.pi
+    dt = 0.02 * (Lx / nx) / avg_U
+    H, b, U = [H0 / 2, H0 / 2], [b1, 1.0], [s, -s]
+    q0_amplitude = 1e-2 * avg_U * amplitude_scale
+    prob = mlqg_problem(tw, 2, nx=nx, Lx=Lx, f0=f0, H=H, b=b, U=U, mu=mu, beta=0.0, dt=dt, stepper="FilteredRK4",
+                        aliased_fraction=0)
+    grid = prob.grid
+    rng = np.random.default_rng(seed)
+    q0 = q0_amplitude * rng.standard_normal((2, grid.ny, grid.nx))
+    q0h = prob.timestepper.filter * np.fft.rfft2(q0, axes=(-2, -1))
+    q0 = np.fft.irfft2(q0h, s=(grid.ny, grid.nx), axes=(-2, -1))
+    mlqg_set_q(tw, prob, q0)
+    ic = prob.sol.copy()
+
+    def energies(pr):
+        KE, PE = O.mlqg_energies(pr.sol.copy(), grid, pr.params)
+        return (tuple(KE), (PE,))
+
+    tw.RECORD[energies] = lambda r, v: ((r.ke, r.ke2), (r.pe,))
+    diags = [Diagnostic(energies, prob, nsteps=nsteps)]
+    outputs = [("problem",)]
+    for j in range(0, round(nsteps / nsubs) + 1):
+        if j % (1000 / nsubs) == 0:
+            v = prob.vars
+            _ = float(prob.clock.dt) * max(v.u.max() / grid.dx, v.v.max() / grid.dy)
+        tw.stepforward(prob, diags, nsubs)
+        mlqg_updatevars(tw, prob)
+        outputs.append((prob.clock.step, prob.vars.ψh.copy()))
+    return prob, diags, outputs, ic

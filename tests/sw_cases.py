@@ -109,5 +109,5 @@ def libsw_problem(p, **kw):
         return RSW.Problem("gpu", nx=p["n"], dt=p["dt"], nu=p["nu"], nnu=p["nnu"], f=p["f"], Cg=p["Cg"],
                            stepper=p["stepper"], **fk, **kw)
     return QG2.Problem("gpu", nx=p["n"], dt=p["dt"], nu=p["nu"], nnu=p["nnu"], U=p["U"], mu=p["mu"],
-                       f0=p["f0"], Cg=p["Cg"], drhorho0=p["drhorho0"], stepper=p["stepper"], T=np.float64,
-                       **fk, **kw)
+                       f0=p["f0"], Cg=p["Cg"], drhorho0=p["drhorho0"], stepper=p["stepper"],
+                       T=kw.pop("T", np.float64), **fk, **kw)

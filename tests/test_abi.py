@@ -78,7 +78,7 @@ def test_integration_bindings_track_the_header():
     abi = int(re.search(r"#define SW_ABI_VERSION (\d+)", hdr).group(1))
     assert _lib.SW_ABI_VERSION == abi
     doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
-    assert int(re.search(r"abi_version::Int32 = (\d+)", doc).group(1)) == abi
+    assert int(re.search(r"const SW_ABI_VERSION = Int32\((\d+)\)", doc).group(1)) == abi
     body = re.search(r"typedef struct sw_config \{(.*?)\} sw_config;", hdr, flags=re.S).group(1)
     body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
     hfields = re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*(?:\[\d+\])?\s*[;,]", body)

@@ -31,3 +31,4 @@ def test_gpus_n_launches_n_ranks_slab(n):
 def test_ensemble_mode_and_single_gpu():
     assert _plan("--gpus", "2", "--mode", "ensemble")["parallelism"] == "ensemble2"
     assert _plan()["parallelism"] == "single-gpu"
+    assert _plan()["scaling"] is None  # one GPU scales neither way

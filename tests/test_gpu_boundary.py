@@ -1,4 +1,4 @@
-"""GPU tests of the ABI-6 boundary additions (include/sw.h):
+"""GPU tests of the ABI-6/7 boundary additions (include/sw.h):
 
 * Float32 caller buffers (``sw_config.precision``): the drivers' ``T=Float32``
   (rsw/RSWDriver.jl:164, swqg/TwoLayerDriver.jl:63) through the exact
@@ -66,22 +66,88 @@ def test_float32_size_checked_by_the_library():
     p32.close()
 
 
+@pytest.mark.parametrize("T", [np.float64, np.float32], ids=["f64", "f32"])
 @pytest.mark.parametrize("name", ["rsw_fab3", "rsw_ifmab3", "qg2_ifmab3", "qg2_ifmrk4", "ty_etdrk4", "mlqg_frk4"])
-def test_checkpoint_restart_bitwise(name, tmp_path):
+def test_checkpoint_restart_bitwise(name, T, tmp_path):
+    """checkpoint + restart continues bitwise, also for T = Float32 caller
+    buffers: the file carries libsw's fp64 blob (state, history, clock), not
+    the fp32-rounded arrays."""
+    if T == np.float32 and name.startswith(("ty", "mlqg")):
+        pytest.skip("T=Float32 is the RSW/2LQG drivers' precision")
     p = sw_cases.case_params(name, 64)
     g = O.TwoDGrid(64, Lx=p.get("Lx", 2 * np.pi), aliased_fraction=p.get("af", 1 / 3))
-    a = sw_cases.libsw_problem(p)
+    a = sw_cases.libsw_problem(p, T=T)
     a.sol = sw_cases.initial_condition(p, g)
     a.stepforward(10)
     fn = str(tmp_path / "ckpt.jld2")
     output.checkpoint(a, fn)
     a.stepforward(7)
-    b = sw_cases.libsw_problem(p)
+    b = sw_cases.libsw_problem(p, T=T)
     assert output.restart(b, fn) == 10
     assert b.ctx.history_slots() == (2 if p["stepper"] in ("FilteredAB3", "IFMAB3") else 0)
     b.stepforward(7)
     assert np.array_equal(a.sol, b.sol)
     assert a.clock.step == b.clock.step == 17 and a.clock.t == b.clock.t
+    with np.load(fn) as d:  # the readable copy is in the caller's precision
+        assert d["checkpoint/sol"].dtype == (np.complex64 if T == np.float32 else np.complex128)
+    a.close()
+    b.close()
+
+
+@pytest.mark.parametrize("name", ["rsw_fab3", "qg2_ifmab3"])
+def test_snapshot_then_checkpoint_restart_one_context(name, tmp_path):
+    """One context restarted from a snapshot (Euler start-up pending) and
+    then from a checkpoint: the checkpoint's stepper memory wins — the run
+    continues with AB3 exactly as the uninterrupted one (the
+    pending Euler steps of the snapshot restart used to survive)."""
+    p = sw_cases.case_params(name, 64)
+    g = O.TwoDGrid(64, aliased_fraction=p.get("af", 1 / 3))
+    a = sw_cases.libsw_problem(p)
+    a.sol = sw_cases.initial_condition(p, g)
+    a.stepforward(50)
+    ck = str(tmp_path / "ckpt.jld2")
+    output.checkpoint(a, ck)
+    a.stepforward(50)
+    sn = str(tmp_path / "snap.jld2")
+    out = output.Output(a, sn)
+    out.saveproblem()
+    out.saveoutput()
+    b = sw_cases.libsw_problem(p)
+    assert output.restart(b, sn) == 100  # 3 Euler steps pending
+    assert output.restart(b, ck) == 50   # ... cancelled by the checkpoint
+    c = sw_cases.libsw_problem(p)
+    assert output.restart(c, ck) == 50
+    b.stepforward(5)
+    c.stepforward(5)
+    assert np.array_equal(b.sol, c.sol)
+    # and the raw history ABI: sw_set_history also cancels a pending reset
+    d = sw_cases.libsw_problem(p)
+    d.sol = c.sol
+    d.clock.set(*c.ctx.get_clock())
+    d.ctx.reset_history()
+    for k in (1, 2):
+        d.ctx.set_history(k, c.ctx.get_history(k))
+    c.stepforward(3)
+    d.stepforward(3)
+    assert np.array_equal(c.sol, d.sol)
+    for q in (a, b, c, d):
+        q.close()
+
+
+def test_checkpoint_rejects_another_problem():
+    pa = sw_cases.case_params("rsw_fab3", 64)
+    pb = sw_cases.case_params("rsw_ifmab3", 64)
+    a, b = sw_cases.libsw_problem(pa), sw_cases.libsw_problem(pb)
+    blob = a.ctx.get_checkpoint()
+    with pytest.raises(_lib.LibSWError):
+        b.ctx.set_checkpoint(blob)
+    with pytest.raises(_lib.LibSWError):
+        a.ctx.set_checkpoint(blob[:-16])
+    bad = blob.copy()
+    bad[0] ^= 1
+    with pytest.raises(_lib.LibSWError):
+        a.ctx.set_checkpoint(bad)
+    a.ctx.set_checkpoint(blob)
     a.close()
     b.close()
 

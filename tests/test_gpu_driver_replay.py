@@ -1,0 +1,179 @@
+"""GPU replays of the three north-star drivers' ``start!`` through the C ABI,
+as the Julia binding (integration/julia/SWLib.jl) issues it — its Python twin
+tests/driver_replay.py — checked against the CPU oracle and by the C call
+trace:
+
+* RSWDriver.start! (rsw/RSWDriver.jl:134-226): dev = GPU(), T = Float32,
+  the default IFMAB3 stepper, KE/PE Diagnostics, frames of output_freq steps;
+* TYdriver.start! (thomasyamada/TYdriver.jl:111-231) with ARGS = ["GPU"]:
+  start-up problem at startup_dt, then the main problem (LIBSW_CPU=1) at dt
+  from the start-up state and clock, wave/geostrophic and barotropic energy
+  Diagnostics every 25 steps;
+* TwoLayerSimulation.start! (simulation/TwoLayerSimulation.jl:13-143):
+  MultiLayerQG FilteredRK4 with aliased_fraction = 0, q̂₀ = filter·rfft(q₀),
+  set_q!, energies every step.
+"""
+import numpy as np
+import pytest
+
+import driver_replay as R
+import sw_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib_loaded(libsw):
+    return libsw
+
+
+def _sub(seq, sub):
+    """index of the first occurrence of the contiguous sub-sequence sub in seq"""
+    for i in range(len(seq) - len(sub) + 1):
+        if seq[i:i + len(sub)] == sub:
+            return i
+    return -1
+
+
+def test_rsw_driver_float32_replay():
+    tw = R.Twin()
+    nsteps, ofreq, dfreq = 240, 20, 10
+    prob, diags, outputs, ic, cfls = R.rsw_driver_start(tw, nx=128, nsteps=nsteps, output_freq=ofreq,
+                                                        diags_freq=dfreq, spinup_step=120)
+    nframes = round(nsteps / ofreq) + 1
+    total = nframes * ofreq
+    # -- the C call sequence of SWLib.jl
+    c = tw.calls
+    assert c[:2] == ["sw_config_default", "sw_create"]
+    i = _sub(c, ["sw_set_state", "sw_get_state", "sw_set_clock"] + ["sw_get_physical"] * 4)
+    assert i >= 0, "set_solution! (load_solution! + updatevars!)"
+    first = _sub(c, ["sw_set_energy_diagnostics", "sw_step", "sw_get_state", "sw_get_energy_diagnostics",
+                     "sw_get_energy_diagnostics"] + ["sw_get_physical"] * 4)
+    assert first > i, "first stepforward!(prob, diags, n) + updatevars!"
+    assert c.count("sw_step") == nframes and c.count("sw_set_energy_diagnostics") == 1
+    assert "sw_calcN" not in c and "sw_diag" not in c  # energies come from the device records
+    # -- Float32 caller buffers (rsw/RSWDriver.jl:164)
+    assert prob.sol.dtype == np.complex64 and prob.vars.u.dtype == np.float32
+    assert all(o[1].dtype == np.complex64 for o in outputs[1:])
+    assert prob.clock.step == total
+    t32 = np.float32(0)
+    for _ in range(total):
+        t32 = np.float32(t32 + prob.clock.dt)
+    assert prob.clock.t == t32 and isinstance(prob.clock.t, np.float32)
+    # -- the oracle: IFMAB3 from the same (Float32) initial state, with the
+    # Problem's Float32 parameters (Params{T}, Clock{T})
+    g = O.TwoDGrid(128)
+    p = O.RSWParams(float(prob.params.ν), 4, float(prob.params.f), 1.0)
+    pr = O.Problem("rsw", "IFMAB3", 128, float(prob.clock.dt), params=p)
+    pr.set_solution(ic.astype(np.complex128))
+    ke, pe = [], []
+    for s in range(total):
+        if (s + 1) % dfreq == 0:  # RSW energies read vars.uh: the input of step s+1's calcN
+            k, e = O.rsw_energies(pr.sol, g, p)
+            ke.append(k)
+            pe.append(e)
+        pr.stepforward(1)
+    # fp32 rounding of the fp64 device state
+    assert O.parity_error(prob.sol.astype(np.complex128), pr.sol, g) < 2e-7
+    n = min(diags[0].i - 1, len(ke))
+    assert n == len(diags[0].t) - 1  # the Diagnostic is full: nsteps / freq records
+    for d, ref in ((diags[0], ke), (diags[1], pe)):
+        got = np.array(d.data[1:1 + n], float)
+        assert np.allclose(got, ref[:n], rtol=1e-9, atol=0), (got[:3], ref[:3])
+        assert list(d.steps[1:1 + n]) == [dfreq * (j + 1) for j in range(n)]
+    # the physical fields the driver reads after each frame (updatevars!)
+    v = O.rsw_updatevars(pr.sol.copy(), g, p)
+    assert np.max(np.abs(prob.vars.η - v["eta"])) < 1e-6 * np.max(np.abs(v["eta"]))
+    assert len(cfls) == 1 and 0 < cfls[0] < 1
+    prob.timestepper.finalizer()
+
+
+def test_ty_driver_replay():
+    tw = R.Twin()
+    sp, sdiags, diags, _, outputs, ic, startup_steps = R.ty_driver_start(
+        tw, nx=64, startup_dt=3e-2, dt=5e-3, startup_nsteps=200, startup_nsubs=50, nsteps=60, nsubs=20)
+    prob = sp  # the main problem
+    c = tw.calls
+    assert c.count("sw_create") == 2
+    assert c.count("sw_destroy") == 1  # startup_prob = nothing
+    # set_solution! of the main problem pushes the start-up clock
+    i = [k for k, x in enumerate(c) if x == "sw_create"][1]
+    assert c[i + 1:i + 4] == ["sw_set_state", "sw_get_state", "sw_set_clock"]
+    main_steps = (round(60 / 20) + 1) * 20
+    assert prob.clock.step == main_steps
+    # -- oracle: start-up at startup_dt, then a fresh problem at dt
+    Lx = 6 * np.pi
+    nu = 5.0e-34 * (Lx / (2 * np.pi)) ** 16
+    tp = O.TYParams(nu, 8, 1.0)
+    a = O.Problem("ty", "ETDRK4", 64, 3e-2, Lx=Lx, params=tp)
+    a.set_solution(ic)
+    rec_s = []
+    for s in range(startup_steps):
+        a.stepforward(1)
+        if (s + 1) % 25 == 0:
+            rec_s.append(O.ty_energies(a.grid.dealias(a.sol.copy()), a.grid))
+    b = O.Problem("ty", "ETDRK4", 64, 5e-3, Lx=Lx, params=tp)
+    b.set_solution(a.sol.copy())
+    rec_m = []
+    for s in range(main_steps):
+        b.stepforward(1)
+        if (s + 1) % 25 == 0:
+            rec_m.append(O.ty_energies(b.grid.dealias(b.sol.copy()), b.grid))
+    assert O.parity_error(prob.sol, b.sol, b.grid) < 1e-10
+    # Diagnostics: wave_geostrophic_energy and barotropic_energy records, on
+    # the dealiased post-step state (the reference's prob.sol also holds the
+    # aliased modes the update has just written: DESIGN §5b)
+    for ds, ref in ((sdiags, rec_s), (diags, rec_m)):
+        wg, bt = ds
+        n = min(wg.i - 1, len(ref))
+        assert n >= 2
+        for j in range(n):
+            bt_ref, _, wg_ref = ref[j]
+            assert np.allclose(np.array(wg.data[1 + j]).ravel(), np.array(wg_ref).ravel(), rtol=1e-9, atol=1e-14)
+            assert np.isclose(bt.data[1 + j], bt_ref, rtol=1e-9, atol=1e-14)
+    # the main problem's clock continues the start-up time (:190)
+    t = 0.0
+    for _ in range(startup_steps):
+        t += 3e-2
+    for _ in range(main_steps):
+        t += 5e-3
+    assert prob.clock.t == pytest.approx(t, rel=1e-14)
+    prob.timestepper.finalizer()
+
+
+def test_two_layer_simulation_replay():
+    tw = R.Twin()
+    nsteps, nsubs = 100, 25
+    prob, diags, outputs, ic = R.mlqg_simulation_start(tw, nx=64, nsteps=nsteps, nsubs=nsubs)
+    total = (round(nsteps / nsubs) + 1) * nsubs
+    c = tw.calls
+    i = _sub(c, ["sw_set_state", "sw_get_state", "sw_set_clock"] + ["sw_get_physical"] * 8)
+    assert i >= 0, "set_q! (load_solution! + MultiLayerQG.updatevars!)"
+    assert c.count("sw_step") == round(nsteps / nsubs) + 1
+    # timestepper.filter is FF's makefilter (the driver multiplies q̂₀ by it, :44)
+    g = prob.grid
+    assert prob.timestepper.filter.shape == (2, g.nl, g.nkr)
+    assert np.array_equal(prob.timestepper.filter[0], O.makefilter(g))
+    # oracle: GF MultiLayerQG restated, FilteredRK4, aliased_fraction = 0
+    pr = O.Problem("mlqg", "FilteredRK4", 64, float(prob.clock.dt), aliased_fraction=0.0, params=prob.params)
+    pr.set_solution(ic)
+    rec = []
+    for _ in range(total):
+        pr.stepforward(1)
+        rec.append(O.mlqg_energies(pr.grid.dealias(pr.sol.copy()), pr.grid, prob.params))
+    assert O.parity_error(prob.sol, pr.sol, pr.grid) < 1e-10
+    E = diags[0]
+    n = E.i - 1
+    assert n == nsteps  # capacity: nsteps + 1 entries, entry 0 at construction
+    for j in range(n):
+        (k1, k2), (pe,) = E.data[1 + j]
+        KE, PE = rec[j]
+        assert np.allclose([k1, k2, pe], [KE[0], KE[1], PE], rtol=1e-9, atol=1e-16)
+    # the nonlinear term acted: energies moved off their initial values
+    assert abs(E.data[n][0][0] - E.data[0][0][0]) > 1e-6 * abs(E.data[0][0][0])
+    # updatevars! after the last frame: ψh on the host, q per layer from the device
+    psih = O.mlqg_streamfunction(pr.sol.copy(), pr.grid, prob.params)
+    assert np.max(np.abs(prob.vars.ψh - psih)) <= 1e-10 * np.max(np.abs(psih))
+    q1 = pr.grid.irfft(pr.sol[0].copy())
+    assert np.max(np.abs(prob.vars.q[0] - q1)) <= 1e-10 * np.max(np.abs(q1))
+    prob.timestepper.finalizer()

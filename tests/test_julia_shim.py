@@ -1,0 +1,212 @@
+"""CPU checks of the Julia drop-in (integration/julia/SWLib.jl).
+
+Julia is not installed here, so the binding is checked by reading it:
+
+* INTEGRATION.md carries SWLib.jl verbatim;
+* ``SWStepper{A} <: AbstractTimeStepper{A}`` — FourierFlows' parametric
+  supertype, as utils/IFMAB3.jl:13 subtypes it — with the ``filter`` field
+  simulation/TwoLayerSimulation.jl:44 reads;
+* a ``Problem(dev::GPU; …)`` method per driver model (RSWDriver.jl,
+  TYdriver.jl, TwoLayerSimulation.jl, TwoLayerDriver.jl) plus the run-directory
+  wrapper that attaches it;
+* every ``ccall`` binds an include/sw.h prototype with the same number of
+  arguments, and ``SWConfig`` is ``struct sw_config`` field for field;
+* each SWLib.jl function that reaches libsw issues the same C entry points,
+  in the same order, as its Python twin in tests/driver_replay.py (which the
+  GPU replay tests run).
+"""
+import inspect
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+JL = os.path.join(ROOT, "integration", "julia")
+SWLIB = os.path.join(JL, "SWLib.jl")
+HEADER = os.path.join(ROOT, "include", "sw.h")
+
+
+def _src():
+    return open(SWLIB).read()
+
+
+def _strip_comments(s):
+    return re.sub(r"#[^\n]*", "", s)
+
+
+def _prototypes():
+    """sw.h: name -> number of parameters of every extern "C" function."""
+    hdr = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    out = {}
+    for ret, name, args in re.findall(r"^\s*(int|void|double|const char\*)\s+(sw_\w+)\(([^)]*)\);", hdr, flags=re.M):
+        a = args.strip()
+        out[name] = 0 if a in ("", "void") else a.count(",") + 1
+    return out
+
+
+def test_integration_md_embeds_the_binding_verbatim():
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    assert "```julia\n" + _src() + "```" in doc
+
+
+def test_stepper_type_is_parametric_with_filter():
+    s = _strip_comments(_src())
+    m = re.search(r"mutable struct SWStepper\{A<:AbstractArray, Tf\} <: AbstractTimeStepper\{A\}(.*?)\nend", s, re.S)
+    assert m, "SWStepper must subtype FourierFlows.AbstractTimeStepper{A} (utils/IFMAB3.jl:13)"
+    assert re.search(r"^\s*filter::Tf", m.group(1), re.M)
+    # the stepper type parameter is the array type of prob.sol
+    assert "A = Array{equation.T, length(equation.dims)}" in s
+
+
+@pytest.mark.parametrize("module,sig,builder", [
+    ("RotatingShallowWater", r"Problem\(dev::FourierFlows\.GPU; kw\.\.\.\) = \$rsw_problem", "rsw_problem"),
+    ("TwoLayerQG", r"Problem\(dev::FourierFlows\.GPU; kw\.\.\.\) = \$qg2_problem", "qg2_problem"),
+    ("ThomasYamada", r"Problem\(dev::FourierFlows\.GPU; kw\.\.\.\) = \$ty_problem", "ty_problem"),
+    ("MultiLayerQG", r"Problem\(nlayers::Int, dev::FourierFlows\.GPU; kw\.\.\.\) = \$mlqg_problem", "mlqg_problem"),
+])
+def test_problem_method_per_driver(module, sig, builder):
+    s = _strip_comments(_src())
+    branch = re.search(rf"name === :{module}\n(.*?)(?:\n    elseif|\n    else)", s, re.S)
+    assert branch, module
+    assert re.search(sig, branch.group(1)), f"{module}: no Problem(GPU) method"
+    # the CPU() method falls back to the reference's own (invoke), unless LIBSW_CPU=1
+    assert "invoke(Problem, Tuple{" in branch.group(1) and "$use_libsw(dev)" in branch.group(1)
+    assert re.search(rf"^function {builder}\(M::Module", s, re.M)
+
+
+@pytest.mark.parametrize("path,module", [
+    ("rsw/RotatingShallowWater.jl", "RotatingShallowWater"),
+    ("swqg/TwoLayerQG.jl", "TwoLayerQG"),
+    ("thomasyamada/ThomasYamada.jl", "ThomasYamada"),
+    ("simulation/Parameters.jl", "GeophysicalFlows.MultiLayerQG"),
+])
+def test_run_directory_wrappers(path, module):
+    s = _strip_comments(open(os.path.join(JL, path)).read())
+    ref = os.path.basename(path).replace(".jl", ".ref.jl")
+    lines = [x.strip() for x in s.splitlines() if x.strip()]
+    assert lines[0] == f'include("{ref}")'
+    assert 'include("SWLib.jl")' in lines
+    assert lines[-1] == f"SWLib.attach!({module})"
+
+
+def test_every_ccall_binds_a_header_prototype():
+    protos = _prototypes()
+    s = _strip_comments(_src())
+    calls = re.findall(r"ccall\(\(:(sw_\w+), libsw\), (\w+(?:\{\w+\})?), \(([^()]*(?:\([^()]*\)[^()]*)*)\)", s)
+    assert len(calls) >= 15
+    seen = set()
+    for name, ret, argtypes in calls:
+        assert name in protos, f"{name} is not declared in include/sw.h"
+        n = len([a for a in argtypes.split(",") if a.strip()])
+        assert n == protos[name], f"{name}: {n} Julia argument types vs {protos[name]} C parameters"
+        seen.add(name)
+    # the entry points the drivers' call sequences need
+    need = {"sw_config_default", "sw_create", "sw_destroy", "sw_last_error", "sw_set_state", "sw_get_state",
+            "sw_set_clock", "sw_step", "sw_get_physical", "sw_set_energy_diagnostics",
+            "sw_get_energy_diagnostics", "sw_comm_unique_id"}
+    assert need <= seen
+
+
+def test_swconfig_is_sw_config_field_for_field():
+    hdr = open(HEADER).read()
+    body = re.search(r"typedef struct sw_config \{(.*?)\} sw_config;", hdr, flags=re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    ctype = {}
+    for decl in body.split(";"):
+        decl = decl.strip()
+        if not decl:
+            continue
+        m = re.match(r"(const void\*|sw_exchange_fn|void\*|int32_t|double)\s+(.*)", decl)
+        assert m, decl
+        for name in m.group(2).split(","):
+            name = name.strip()
+            arr = re.match(r"(\w+)\[(\d+)\]", name)
+            ctype[arr.group(1) if arr else name] = (m.group(1), int(arr.group(2)) if arr else 1)
+    hnames = list(ctype)
+    js = re.search(r"Base\.@kwdef mutable struct SWConfig(.*?)\nend", _src(), flags=re.S).group(1)
+    jfields = re.findall(r"\b([A-Za-z_]\w*)::([\w{},]+)", js)
+    assert [f for f, _ in jfields] == hnames
+    jmap = {"int32_t": "Int32", "double": "Float64", "const void*": "Ptr{Cvoid}", "void*": "Ptr{Cvoid}",
+            "sw_exchange_fn": "Ptr{Cvoid}"}
+    for f, jt in jfields:
+        ct, n = ctype[f]
+        want = jmap[ct] if n == 1 else f"NTuple{{{n},{jmap[ct]}}}"
+        assert jt == want, (f, jt, want)
+
+
+def _julia_functions(src):
+    """name -> body of every top-level `function name(...)` … `end` and
+    one-line `name(...) = …` definition in SWLib.jl."""
+    out = {}
+    lines = _strip_comments(src).splitlines()
+    i = 0
+    while i < len(lines):
+        ln = lines[i]
+        m = re.match(r"^function ([\w!.]+)\(", ln)
+        if m:
+            j = i + 1
+            while not lines[j].startswith("end"):
+                j += 1
+            out.setdefault(m.group(1).split(".")[-1], "\n".join(lines[i:j]))
+            i = j + 1
+            continue
+        m = re.match(r"^([\w!]+)\([^=]*\)(?: where \{[^}]*\})? =", ln)
+        if m:
+            j = i + 1
+            while j < len(lines) and lines[j].startswith(" "):
+                j += 1
+            out.setdefault(m.group(1), "\n".join(lines[i:j]))
+            i = j
+            continue
+        i += 1
+    return out
+
+
+def _c_sequence(text, pattern):
+    return re.findall(pattern, text)
+
+
+@pytest.mark.parametrize("jname,pyname", [
+    ("config", "config"), ("SWStepper", "SWStepper"), ("upload!", "upload"), ("download!", "download"),
+    ("push_clock!", "push_clock"), ("load_solution!", "load_solution"), ("run_steps!", "run_steps"),
+    ("attach_diagnostics!", "attach_diagnostics"), ("take_records!", "take_records"),
+])
+def test_julia_function_matches_its_python_twin(jname, pyname):
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import driver_replay
+
+    jf = _julia_functions(_src())
+    assert jname in jf, f"SWLib.jl has no function {jname}"
+    jseq = _c_sequence(jf[jname], r"ccall\(\(:(sw_\w+)")
+    # helper calls inside the Julia body (upload!/download!/push_clock!/check)
+    body = jf[jname].split("\n", 1)[1] if "\n" in jf[jname] else ""  # without the definition line
+    jhelp = _c_sequence(body, r"\b(upload!|download!|push_clock!|run_steps!|take_records!|attach_diagnostics!)\(")
+    py = inspect.getsource(getattr(driver_replay.Twin, pyname))
+    pseq = _c_sequence(py, r'self\.c\("(sw_\w+)"')
+    phelp = _c_sequence(py, r"self\.(upload|download|push_clock|run_steps|take_records|attach_diagnostics)\(")
+    assert jseq == pseq, (jname, jseq, pseq)
+    assert [h.rstrip("!") for h in jhelp] == phelp, (jname, jhelp, phelp)
+
+
+def test_stepforward_order_matches_twin():
+    """stepforward!(prob, diags, n) of a libsw problem: attach (first call),
+    run the steps, take the records, then the drivers' NaN path."""
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import driver_replay
+
+    s = _strip_comments(_src())
+    body = re.search(r"function FourierFlows\.stepforward!\(prob::FourierFlows\.Problem, diags::(.*?)\nend", s,
+                     re.S).group(1)
+    sw_part = body[body.index("ts = prob.timestepper"):]
+    jorder = re.findall(r"\b(attach_diagnostics!|run_steps!|take_records!|blowup!)\(", sw_part)
+    py = inspect.getsource(driver_replay.Twin.stepforward)
+    porder = re.findall(r"\b(attach_diagnostics|run_steps|take_records|blowup)\(", py)
+    assert [x.rstrip("!") for x in jorder] == porder == ["attach_diagnostics", "run_steps", "take_records",
+                                                          "blowup"]

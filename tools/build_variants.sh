@@ -12,6 +12,6 @@ for spec in "$@"; do
   python3 -c "
 import sys; sys.path.insert(0, '$ROOT')
 from juliaraytracingsw_amd import build
-print(build.build_lib(force=True, out='$ROOT/sweep_var/$name.so', extra_flags='$flags'.split(), parts=$LEN))"
+print(build.build_lib(force=True, out='$ROOT/sweep_var/$name.so', extra_flags=['-DSW_EXPERIMENTS'] + '$flags'.split(), parts=$LEN))"
 done
 ls -la "$ROOT/sweep_var"
