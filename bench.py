@@ -140,11 +140,11 @@ def launch_ranks(n):
     return subprocess.call(cmd, env=env)
 
 
-def make_problem(model, n, stepper, local, dec):
+def make_problem(model, n, stepper, local, dec, over=None):
     from juliaraytracingsw_amd import drivers
 
     if model == "rsw":
-        return drivers.rsw_problem(n, stepper, device=local, decomposition=dec)
+        return drivers.rsw_problem(n, stepper, device=local, decomposition=dec, **(over or {}))
     if model == "ty":
         return drivers.ty_problem(n, device=local, decomposition=dec)
     if model == "mlqg":
@@ -171,6 +171,10 @@ def main():
     ap.add_argument("--config5-steps", type=int, default=20)
     ap.add_argument("--mode", default="slab", choices=["ensemble", "slab"])
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_rsw2048_fab3.json"))
+    ap.add_argument("--nutune", type=float, default=None,
+                    help="RSW: override RSWParameters' νtune (FilteredAB3 below 2048² is linearly unstable at the "
+                         "driver's νtune = 20, DESIGN §4; the kernels' work does not depend on it)")
+    ap.add_argument("--cfltune", type=float, default=None, help="RSW: override RSWParameters' cfltune")
     ap.add_argument("--dry-run", action="store_true",
                     help="print the rank plan (n_gpus, parallelism, scaling) and exit, touching no GPU")
     args = ap.parse_args()
@@ -257,6 +261,7 @@ def main():
         barrier_sync()
         return max_over_ranks(time.perf_counter() - t0)
 
+    over = {k: v for k, v in (("nutune", args.nutune), ("cfltune", args.cfltune)) if v is not None}
     if args.model == "ty":
         args.stepper = "ETDRK4"  # the only Thomas-Yamada stepper
     if args.model == "mlqg":
@@ -291,7 +296,7 @@ def main():
             # as an RCCL communicator that cannot be created fails on every rank
             if os.environ.get("SW_BENCH_FAIL_SLAB") == "1":
                 raise RuntimeError("SW_BENCH_FAIL_SLAB")
-            box["prob"], box["P"] = make_problem(args.model, args.n, args.stepper, local, dec)
+            box["prob"], box["P"] = make_problem(args.model, args.n, args.stepper, local, dec, over)
 
         if stage(create) and stage(lambda: box.__setitem__("t", timed(box["prob"], args.warmup, args.steps))):
             prob, P, elapsed = box["prob"], box["P"], box["t"]
@@ -307,7 +312,7 @@ def main():
                 except Exception:  # noqa: BLE001
                     pass
     if not slab:
-        prob, P = make_problem(args.model, args.n, args.stepper, local, None)
+        prob, P = make_problem(args.model, args.n, args.stepper, local, None, over)
         elapsed = timed(prob, args.warmup, args.steps)
 
     # roofline: per-kernel HIP-event durations on libsw's stream
@@ -408,7 +413,8 @@ def main():
                  "qg2": "synthetic randn PV IC (set_seed_initial_condition!, seeded)",
                  "ty": "synthetic random-phase IC (TYdriver set_initial_condition, seeded)",
                  "mlqg": "synthetic filtered randn PV IC (TwoLayerSimulation, seeded)"}[args.model],
-        "config": {"workload": f"{args.model.upper()} {args.n}^2 {args.stepper} fp64 step, dt={P['dt']:.6g}",
+        "config": {"workload": f"{args.model.upper()} {args.n}^2 {args.stepper} fp64 step, dt={P['dt']:.6g}"
+                               + (f" ({', '.join(f'{k}={v:g}' for k, v in over.items())})" if over else ""),
                    "grid": args.n,
                    "parallelism": parallelism},
         # bytes the libsw kernels move per step (live modes only, physical

@@ -62,7 +62,9 @@ struct sw_ctx {
   hipStream_t comm = nullptr;
   hipEvent_t ev_row = nullptr, ev_join = nullptr;
   hipEvent_t ev_fwd[8] = {}, ev_col[8] = {};
+  hipEvent_t ev_chunk[8] = {};               // row chunk k of the last inverse group has arrived
   bool overlap = false;                      // pipelined exchange (default: RCCL; SW_OVERLAP=0/1)
+  int row_chunks = 1;                        // pipelined: row pass in chunks behind the last inverse transposes
   double2 *tw_x = nullptr, *tw_y = nullptr;
   std::vector<Slab> sl;                      // slabs held by this process
   int head = 0;
@@ -295,19 +297,30 @@ struct Timer {
 // inputs -> row phase; fwd: row outputs -> column phase.  The blocks are
 // contiguous in both layouts, so no pack/unpack kernels exist.  Moves the
 // listed fields on stream `st` (RCCL: one group of sends/receives).
-int transpose_fields(sw_ctx* c, bool inv, const int* fields, int nfl, hipStream_t st) {
+//
+// Rows [r0, r1) of every block (inverse direction, r1 > r0 >= 0: one chunk of
+// the row pass's input): the inverse fields' lines are row-major 2×4 tiles
+// (SW_LORD_I = 0), so rows [r0, r1) (multiples of 4) of a block are the
+// contiguous elements [r0 kcl, r1 kcl) of it in both phases.
+int transpose_fields(sw_ctx* c, bool inv, const int* fields, int nfl, hipStream_t st, int r0 = 0, int r1 = -1) {
   if (c->P == 1 || nfl == 0) return 0;
   const Geom& g0 = c->sl[0].g;
   const size_t blk = (size_t)g0.kcl * g0.nyl;  // elements per (slab pair, field)
   const long long MF = g0.mfield;
+  if (r1 < 0) r1 = g0.nyl;
+  if (r0 != 0 || r1 != g0.nyl) {
+    if (!inv || c->hostx || r0 < 0 || r1 > g0.nyl || r0 % 4 || r1 % 4)
+      return fail(c, SW_E_INVALID, "row-chunked transpose: inverse direction, device transports, rows in 4s");
+  }
+  const size_t off = (size_t)r0 * g0.kcl, cnt = (size_t)(r1 - r0) * g0.kcl;  // within each block
   if (!c->dist) {
     for (int i = 0; i < nfl; ++i) {
       const int o = fields[i];
       for (int p = 0; p < c->P; ++p)
         for (int q = 0; q < c->P; ++q) {
-          const double2* src = (inv ? c->sl[p].mic : c->sl[p].mfr) + o * MF + q * blk;
-          double2* dst = (inv ? c->sl[q].mir : c->sl[q].mfc) + o * MF + p * blk;
-          HIPCHK(c, hipMemcpyAsync(dst, src, blk * sizeof(double2), hipMemcpyDeviceToDevice, st));
+          const double2* src = (inv ? c->sl[p].mic : c->sl[p].mfr) + o * MF + q * blk + off;
+          double2* dst = (inv ? c->sl[q].mir : c->sl[q].mfc) + o * MF + p * blk + off;
+          HIPCHK(c, hipMemcpyAsync(dst, src, cnt * sizeof(double2), hipMemcpyDeviceToDevice, st));
         }
     }
     return 0;
@@ -336,11 +349,11 @@ int transpose_fields(sw_ctx* c, bool inv, const int* fields, int nfl, hipStream_
     double2* dst = (inv ? s.mir : s.mfc) + fields[i] * MF;
     for (int q = 0; q < c->P; ++q) {
       if (q == me) {
-        HIPCHK(c, hipMemcpyAsync(dst + me * blk, src + me * blk, blk * sizeof(double2),
+        HIPCHK(c, hipMemcpyAsync(dst + me * blk + off, src + me * blk + off, cnt * sizeof(double2),
                                  hipMemcpyDeviceToDevice, st));
       } else {
-        NCCLCHK(c, ncclSend(src + q * blk, 2 * blk, ncclDouble, q, c->nccl, st));
-        NCCLCHK(c, ncclRecv(dst + q * blk, 2 * blk, ncclDouble, q, c->nccl, st));
+        NCCLCHK(c, ncclSend(src + q * blk + off, 2 * cnt, ncclDouble, q, c->nccl, st));
+        NCCLCHK(c, ncclRecv(dst + q * blk + off, 2 * cnt, ncclDouble, q, c->nccl, st));
       }
     }
   }
@@ -387,7 +400,10 @@ const PipeSpec& pipe_spec(int model) {
 
 bool pipelined(const sw_ctx* c) { return c->P > 1 && !c->hostx && c->overlap && !c->prof; }
 
-// after the compute stream has launched the producer of inverse group g
+// after the compute stream has launched the producer of inverse group g.
+// The last group goes over in row_chunks chunks of rows, each followed by
+// ev_chunk[k]: the row pass of chunk k starts behind it (rows_pipelined)
+// while the later chunks are in flight.
 int inv_group_async(sw_ctx* c, int g) {
   const PipeSpec& ps = pipe_spec(c->kmodel);
   HIPCHK(c, hipEventRecord(c->ev_col[g], c->stream));
@@ -395,7 +411,13 @@ int inv_group_async(sw_ctx* c, int g) {
   int f[3], n = 0;
   for (int x : ps.inv_out[g])
     if (x >= 0) f[n++] = x;
-  return transpose_fields(c, true, f, n, c->comm);
+  if (g != ps.ninvg - 1 || c->row_chunks <= 1) return transpose_fields(c, true, f, n, c->comm);
+  const int per = c->sl[0].g.nyl / c->row_chunks;
+  for (int k = 0; k < c->row_chunks; ++k) {
+    if (int rc = transpose_fields(c, true, f, n, c->comm, k * per, (k + 1) * per)) return rc;
+    HIPCHK(c, hipEventRecord(c->ev_chunk[k], c->comm));
+  }
+  return 0;
 }
 
 // the compute stream waits for everything queued on the side stream
@@ -405,6 +427,23 @@ int join_comm(sw_ctx* c) {
   HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
   return 0;
 }
+
+// the row pass behind the inverse transposes: all at once after the side
+// stream has drained, or chunk by chunk behind ev_chunk[k]
+int rows_pipelined(sw_ctx* c) {
+  if (c->row_chunks <= 1) {
+    if (int rc = join_comm(c)) return rc;
+    for (Slab& s : c->sl) sw::launch_row(c->kmodel, s.g, c->p, s.mir, s.mfr, c->tw_x, c->stream);
+    return 0;
+  }
+  const int per = c->sl[0].g.nyl / c->row_chunks;
+  for (int k = 0; k < c->row_chunks; ++k) {
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_chunk[k], 0));
+    for (Slab& s : c->sl) sw::launch_row(c->kmodel, s.g, c->p, s.mir, s.mfr, c->tw_x, c->stream, k * per, per);
+  }
+  return 0;
+}
+
 
 // after the compute stream has launched the row pass: forward transposes in
 // column-field order, ev_fwd[f] = inputs of column field f have arrived
@@ -454,8 +493,7 @@ int calcN(sw_ctx* c, double2* Slab::*X, double2* Slab::*N, int op = -1, int stag
       for (Slab& s : c->sl) sw::launch_col_inv(model, s.g, c->p, s.*X, s.mic, c->tw_y, c->stream, g, 1);
       if (int rc = inv_group_async(c, g)) return rc;
     }
-    if (int rc = join_comm(c)) return rc;
-    for (Slab& s : c->sl) sw::launch_row(model, s.g, c->p, s.mir, s.mfr, c->tw_x, c->stream);
+    if (int rc = rows_pipelined(c)) return rc;
     if (int rc = fwd_async(c)) return rc;
     if (op >= 0) {  // every field of a column in one block: all exchanges first
       for (int f = 0; f < ps.nfc; ++f) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_fwd[f], 0));
@@ -565,8 +603,7 @@ int run_stage(sw_ctx* c, int op, int stage, double2* Slab::*X) {
         if (int rc = inv_group_async(c, g)) return rc;
       }
     }
-    if (int rc = join_comm(c)) return rc;
-    for (Slab& s : c->sl) sw::launch_row(model, s.g, c->p, s.mir, s.mfr, c->tw_x, c->stream);
+    if (int rc = rows_pipelined(c)) return rc;
     if (int rc = fwd_async(c)) return rc;
     for (int f = 0; f < ps.nfc; ++f) {  // column field f -> inverse group f
       HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_fwd[f], 0));
@@ -881,6 +918,7 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
     for (int i = 0; i < 8; ++i) {
       HIPCHK(c, hipEventCreateWithFlags(&c->ev_fwd[i], hipEventDisableTiming));
       HIPCHK(c, hipEventCreateWithFlags(&c->ev_col[i], hipEventDisableTiming));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_chunk[i], hipEventDisableTiming));
     }
     // Pipelined by default across GPUs (RCCL over xGMI runs beside the column
     // kernels).  With every slab in this process the "transposes" are copies
@@ -1002,6 +1040,24 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (const char* e = std::getenv("SW_FUSE_ALL")) c->fuse_all = e[0] == '1';
+  // Row-chunked pipeline: with the pipelined exchange, the row
+  // pass runs in chunks of local rows behind the last inverse group's
+  // transposes, in 4 chunks where each per-(peer, field) message of a chunk
+  // stays >= 1 MiB (latency-bound below); SW_ROW_CHUNKS=k forces k (1, 2, 4, 8).
+  // A chunk is a multiple of 64 rows (the row pass's XCD interleave) and of
+  // the row blocks' lines; the inverse tiles must be row-major 2×4.
+  if (P > 1) {
+    const Geom& g = c->sl[0].g;
+    int k = ((size_t)g.kcl * g.nyl * sizeof(double2) / 4 >= ((size_t)1 << 20)) ? 4 : 1;
+    int unit = 64;
+    if (const char* e = std::getenv("SW_ROW_CHUNKS")) {
+      k = std::atoi(e);
+      unit = 1;
+    }
+    unit = std::max(unit, std::max(4, sw::row_lines_per_block(c->kmodel, g.log2nx)));
+    while (k > 1 && (k > 8 || g.nyl % (k * unit) != 0)) k /= 2;
+    c->row_chunks = (SW_TILE_I == 2 && SW_LORD_I == 0 && k > 1) ? k : 1;
+  }
   if (const char* e = std::getenv("SW_FWD_STEP")) c->fwd_step = e[0] == '1' ? 1 : (e[0] == '2' ? 2 : 0);
   // Cache policy of the stepper state (sw_kernels.hip state_ld): a step
   // whose traffic on this GPU exceeds the 256 MiB Infinity Cache evicts the
@@ -1038,6 +1094,7 @@ void sw_destroy(sw_ctx* c) {
   for (int i = 0; i < 8; ++i) {
     if (c->ev_fwd[i]) (void)hipEventDestroy(c->ev_fwd[i]);
     if (c->ev_col[i]) (void)hipEventDestroy(c->ev_col[i]);
+    if (c->ev_chunk[i]) (void)hipEventDestroy(c->ev_chunk[i]);
   }
   if (c->comm) (void)hipStreamDestroy(c->comm);
   if (c->hsend) (void)hipHostFree(c->hsend);

@@ -412,8 +412,11 @@ int col_fields(int model);
 bool length_built(int log2n);
 void launch_col_inv(int model, const Geom& g, const Phys& p, const double2* X, double2* Minv,
                     const double2* tw_y, hipStream_t s, int g0 = 0, int ng = -1);
+// local rows [y0, y0 + nrows) (nrows < 0: to the last); nrows a multiple of
+// row_lines_per_block (and of 4, the mixed tiles' height)
 void launch_row(int model, const Geom& g, const Phys& p, const double2* Minv, double2* Mfwd,
-                const double2* tw_x, hipStream_t s);
+                const double2* tw_x, hipStream_t s, int y0 = 0, int nrows = -1);
+int row_lines_per_block(int model, int log2nx);
 // X: the compact calcN input (TY adds its linear terms from it; unused otherwise)
 void launch_col_fwd(int model, const Geom& g, const Phys& p, const double2* Mfwd, double2* N,
                     const double2* X, const double2* tw_y, hipStream_t s, int f0 = 0, int nfl = -1);
@@ -447,7 +450,7 @@ struct LenOps {
   static void col_inv(int model, const Geom& g, const Phys& p, const double2* X, double2* M, const double2* tw,
                       hipStream_t s, int g0, int ng);
   static void row(int model, const Geom& g, const Phys& p, const double2* Mi, double2* Mo, const double2* tw,
-                  hipStream_t s);
+                  hipStream_t s, int y0, int nrows);
   static void col_fwd(int model, const Geom& g, const Phys& p, const double2* Mf, double2* N, const double2* X,
                       const double2* tw, hipStream_t s, int f0, int nfl);
   static void col_step(int model, int op, const Geom& g, const Phys& p, const StepPtrs& a, const double2* Mf,

@@ -75,6 +75,23 @@ __device__ __forceinline__ int col_of_block(int b, int nb) {
   return b;
 }
 
+// Row pass with two rows per block (RSW, nx = 1024): the four rows that share
+// the 128-B lines of a 2×4 mixed tile span two blocks; dealt in dispatch
+// order they would land on two XCDs, and each XCD's L2 would fetch the lines
+// (round 2 PMC: the 1024² row read 2.1× its bytes).  With the grid a multiple
+// of 16, blocks b and b+8 (one XCD label) take the two row pairs of a tile
+// row group (speed only).  Returns the first row of block b.
+template <int NB>
+__device__ __forceinline__ int row0_of_block(int b, int nb) {
+#ifndef SW_ROW_NOXCD
+  if (NB == 2 && (nb & 15) == 0) {
+    const int q = b >> 4, j = (b >> 3) & 1, x = b & 7;
+    return ((q << 4) + (x << 1) + j) * 2;
+  }
+#endif
+  return b * NB;
+}
+
 // Column-pass store offset of inverse-field element (krl, y = t + s NT): with
 // one slab in closed form (A = 2, rows' lines contiguous: a per-thread term
 // plus a per-s constant), otherwise midc_i
@@ -585,11 +602,14 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
                                          (BlkRow<MODEL, LOG2N>::THREADS >= 1024 ? 4
                                           : (MODEL == MODEL_QG2 ? SW_MINW_ROW_QG : SW_MINW_ROW)))
     k_row(Geom g, Phys p, const double2* __restrict__ Mi, double2* __restrict__ Mo,
-          const double2* __restrict__ tw) {
+          const double2* __restrict__ tw, int yoff) {
   using Bk = BlkRow<MODEL, LOG2N>;
   extern __shared__ double2 smem[];
   const LineCtx c = line_ctx<LOG2N>();
-  const int y = (Bk::NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * Bk::NB + c.ln;
+  // local rows [yoff, yoff + NB gridDim.x): all of them, or one chunk of a
+  // row-chunked launch (the pipelined slab exchange)
+  const int y = yoff + ((Bk::NB == 1) ? col_of_block(blockIdx.x, gridDim.x)
+                                      : row0_of_block<Bk::NB>(blockIdx.x, gridDim.x) + c.ln);
   constexpr int CB = row_lds_lines<MODEL, LOG2N>();
   double2* line = smem + c.ln * CB * FftPlan<LOG2N>::LDS;
   RowIdx<LOG2N> ri;
@@ -2078,7 +2098,8 @@ void LenOps<L>::col_inv(int model, const Geom& g, const Phys& p, const double2* 
 
 template <int L>
 void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, double2* Mo, const double2* tw,
-                    hipStream_t s) {
+                    hipStream_t s, int y0, int nrows) {
+  if (nrows < 0) nrows = g.nyl - y0;
   using BR = BlkRow<MODEL_RSW, L>;
   using BQ = BlkRow<MODEL_QG2, L>;
   using BT = BlkRow<MODEL_TY, L>;
@@ -2086,11 +2107,13 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
   constexpr size_t sh_qg2 = FftPlan<L>::LDS * BQ::NB * sizeof(double2);
   constexpr size_t sh_ty = FftPlan<L>::LDS * BT::NB * sizeof(double2);
   if (model == MODEL_RSW) {
-    hipLaunchKernelGGL((k_row<MODEL_RSW, L>), dim3(g.nyl / BR::NB), dim3(BR::THREADS), sh_rsw, s, g, p, Mi, Mo, tw);
+    hipLaunchKernelGGL((k_row<MODEL_RSW, L>), dim3(nrows / BR::NB), dim3(BR::THREADS), sh_rsw, s, g, p, Mi, Mo, tw,
+                       y0);
   } else if (model == MODEL_TY)
-    hipLaunchKernelGGL((k_row<MODEL_TY, L>), dim3(g.nyl / BT::NB), dim3(BT::THREADS), sh_ty, s, g, p, Mi, Mo, tw);
+    hipLaunchKernelGGL((k_row<MODEL_TY, L>), dim3(nrows / BT::NB), dim3(BT::THREADS), sh_ty, s, g, p, Mi, Mo, tw, y0);
   else
-    hipLaunchKernelGGL((k_row<MODEL_QG2, L>), dim3(g.nyl / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p, Mi, Mo, tw);
+    hipLaunchKernelGGL((k_row<MODEL_QG2, L>), dim3(nrows / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p, Mi, Mo, tw,
+                       y0);
 }
 
 template <int L>
@@ -2211,8 +2234,17 @@ void launch_col_inv(int model, const Geom& g, const Phys& p, const double2* X, d
   by_len(g.log2ny, [&](auto L) { LenOps<decltype(L)::value>::col_inv(model, g, p, X, Minv, tw_y, s, g0, ng); });
 }
 void launch_row(int model, const Geom& g, const Phys& p, const double2* Minv, double2* Mfwd,
-                const double2* tw_x, hipStream_t s) {
-  by_len(g.log2nx, [&](auto L) { LenOps<decltype(L)::value>::row(model, g, p, Minv, Mfwd, tw_x, s); });
+                const double2* tw_x, hipStream_t s, int y0, int nrows) {
+  by_len(g.log2nx, [&](auto L) { LenOps<decltype(L)::value>::row(model, g, p, Minv, Mfwd, tw_x, s, y0, nrows); });
+}
+int row_lines_per_block(int model, int log2nx) {
+  int nb = 1;
+  by_len(log2nx, [&](auto L) {
+    constexpr int l = decltype(L)::value;
+    nb = model == MODEL_RSW ? BlkRow<MODEL_RSW, l>::NB : (model == MODEL_TY ? BlkRow<MODEL_TY, l>::NB
+                                                                            : BlkRow<MODEL_QG2, l>::NB);
+  });
+  return nb;
 }
 void launch_col_fwd(int model, const Geom& g, const Phys& p, const double2* Mfwd, double2* N,
                     const double2* X, const double2* tw_y, hipStream_t s, int f0, int nfl) {

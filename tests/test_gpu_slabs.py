@@ -20,21 +20,26 @@ def _slabbed(p, P, **kw):
     return sw_cases.libsw_problem(p, decomposition=dict(nranks=P, local_slabs=P), **kw)
 
 
-@pytest.mark.parametrize("overlap", [True, False])
+@pytest.mark.parametrize("overlap", [True, False, "chunks"])
 @pytest.mark.parametrize("unfused", [False, True])
 @pytest.mark.parametrize("P", [2, 4])
 @pytest.mark.parametrize("name", sw_cases.ALL_CASES)
 def test_slabs_bitwise(name, P, unfused, overlap, monkeypatch):
     """overlap: the pipelined schedule (column groups launched one by one,
     their transposes on the side stream, events between the streams); else
-    the sequential schedule (SW_OVERLAP=0).  Both bitwise equal P = 1."""
+    the sequential schedule (SW_OVERLAP=0); "chunks": pipelined with the row
+    pass in chunks of rows, each behind its part of the last inverse group's
+    transposes (SW_ROW_CHUNKS).  All bitwise equal P = 1."""
     p = sw_cases.case_params(name, 128)
     pr = sw_cases.oracle_problem(p)
     ic = sw_cases.initial_condition(p, pr.grid)
     a = sw_cases.libsw_problem(p, unfused=unfused)
-    monkeypatch.setenv("SW_OVERLAP", "1" if overlap else "0")
+    monkeypatch.setenv("SW_OVERLAP", "0" if overlap is False else "1")
+    if overlap == "chunks":
+        monkeypatch.setenv("SW_ROW_CHUNKS", "4" if P == 2 else "2")
     b = _slabbed(p, P, unfused=unfused)
     monkeypatch.delenv("SW_OVERLAP", raising=False)
+    monkeypatch.delenv("SW_ROW_CHUNKS", raising=False)
     a.sol = ic
     b.sol = ic
     assert np.array_equal(a.sol, b.sol)
@@ -47,17 +52,21 @@ def test_slabs_bitwise(name, P, unfused, overlap, monkeypatch):
     b.close()
 
 
-@pytest.mark.parametrize("overlap", [True, False])
+@pytest.mark.parametrize("overlap", [True, False, "chunks"])
 @pytest.mark.parametrize("P", [2, 8])
 def test_slabs_bitwise_2048(P, overlap, monkeypatch):
     """The metric configuration (RSW 2048² FilteredAB3) split 2 and 8 ways,
-    pipelined (the RCCL default) and sequential."""
+    pipelined (the RCCL default: at P = 2 its row pass runs in 4 chunks),
+    pipelined in 4 row chunks, and sequential."""
     from juliaraytracingsw_amd import drivers
 
     a, _ = drivers.rsw_problem(2048, "FilteredAB3")
-    monkeypatch.setenv("SW_OVERLAP", "1" if overlap else "0")
+    monkeypatch.setenv("SW_OVERLAP", "0" if overlap is False else "1")
+    if overlap == "chunks":
+        monkeypatch.setenv("SW_ROW_CHUNKS", "4")
     b, _ = drivers.rsw_problem(2048, "FilteredAB3", decomposition=dict(nranks=P, local_slabs=P))
     monkeypatch.delenv("SW_OVERLAP", raising=False)
+    monkeypatch.delenv("SW_ROW_CHUNKS", raising=False)
     a.stepforward(5)
     b.stepforward(5)
     assert np.array_equal(a.sol, b.sol)
