@@ -147,20 +147,24 @@ struct FftPlan {
 #ifndef SW_TW_CHAIN_LOG2
 #define SW_TW_CHAIN_LOG2 13
 #endif
-template <int LOG2N>
+// FLY: read per stage whatever the length (a kernel with little register room)
+template <int LOG2N, bool FLY = (LOG2N >= SW_TWFLY_LOG2)>
 struct Twiddles {
-  static constexpr bool kPreload = LOG2N < SW_TWFLY_LOG2;
+  static constexpr bool kPreload = !FLY;
   double2 w[(kPreload && FftPlan<LOG2N>::NTW > 0) ? FftPlan<LOG2N>::NTW : 1];
   const double2* tab = nullptr;
-  int t0 = 0;
-  __device__ __forceinline__ void load(int t, const double2* __restrict__ tw) {
+  int t0 = 0, sh = 0;
+  // tw: W_L^m of a table of length L = N << tsh (tsh > 0: a longer line's
+  // table, W_N^j = W_L^(j << tsh))
+  __device__ __forceinline__ void load(int t, const double2* __restrict__ tw, int tsh = 0) {
     using P = FftPlan<LOG2N>;
     if constexpr (kPreload) {
 #pragma unroll
-      for (int i = 0; i < P::NTW; ++i) w[i] = tw[index(t, i)];
+      for (int i = 0; i < P::NTW; ++i) w[i] = tw[index(t, i) << tsh];
     } else {
       tab = tw;
       t0 = t;
+      sh = tsh;
     }
   }
   __device__ __forceinline__ static int index(int t, int i) {
@@ -172,7 +176,7 @@ struct Twiddles {
   // W^k of twiddled stage i for this thread
   __device__ __forceinline__ double2 get(int i) const {
     if constexpr (kPreload) return w[i];
-    else return tab[index(t0, i)];
+    else return tab[index(t0, i) << sh];
   }
 };
 
@@ -191,17 +195,19 @@ __device__ __forceinline__ void load_line(double2 (&v)[8], int t, const double2*
 // C independent transforms of one line each, sharing every barrier (C LDS
 // line buffers, `stride` complex apart).  v[c] holds x[t + s*NT] on entry and
 // X[t + s*NT] on exit.  All threads of the block must call this (barriers).
-template <int LOG2N, int DIR, int C>
-__device__ __forceinline__ void fft_lines(double2 (&v)[C][8], int t, const Twiddles<LOG2N>& tws,
+template <int LOG2N, int DIR, int C, bool FLY = (LOG2N >= SW_TWFLY_LOG2)>
+__device__ __forceinline__ void fft_lines(double2 (&v)[C][8], int t, const Twiddles<LOG2N, FLY>& tws,
                                           double2* __restrict__ line, int stride) {
   using P = FftPlan<LOG2N>;
   constexpr int NT = P::NT;
-  SW_OPAQUE_T(t);
+  // opaque t on the long lines and in kernels with little register room (FLY)
+  if constexpr (LOG2N >= SW_OPAQUE_LOG2 || FLY) asm volatile("" : "+v"(t));
   // Opaque copy of the stage twiddles: keeps the compiler from sharing the
   // derived powers w2..w7 across the several transforms of one kernel, which
   // would pin 28 VGPRs per stage for the kernel's whole lifetime.
   double2 tw1[P::NTW > 0 ? P::NTW : 1];
-  if constexpr (Twiddles<LOG2N>::kPreload) {
+  constexpr bool kPre = Twiddles<LOG2N, FLY>::kPreload;
+  if constexpr (kPre) {
 #pragma unroll
     for (int i = 0; i < P::NTW; ++i) {
       tw1[i] = tws.w[i];
@@ -255,9 +261,9 @@ __device__ __forceinline__ void fft_lines(double2 (&v)[C][8], int t, const Twidd
 #else
     if (lNs > 0) {
 #endif
-      const double2 wt = Twiddles<LOG2N>::kPreload ? tw1[ti] : tws.get(ti);
+      const double2 wt = kPre ? tw1[ti] : tws.get(ti);
       const double2 w1 = DIR < 0 ? wt : cconj(wt);
-      if constexpr (Twiddles<LOG2N>::kPreload && LOG2N < SW_TW_CHAIN_LOG2) {
+      if constexpr (kPre && LOG2N < SW_TW_CHAIN_LOG2) {
         const double2 w2 = cmul(w1, w1), w3 = cmul(w2, w1), w4 = cmul(w2, w2);
         const double2 w5 = cmul(w4, w1), w6 = cmul(w3, w3), w7 = cmul(w4, w3);
 #pragma unroll
@@ -308,10 +314,10 @@ __device__ __forceinline__ void fft_lines(double2 (&v)[C][8], int t, const Twidd
 
 // Full transform.  v holds x[t + s*NT] on entry and X[t + s*NT] on exit.
 // All threads of the block must call this (it contains barriers).
-template <int LOG2N, int DIR>
-__device__ __forceinline__ void fft_line(double2 (&v)[8], int t, const Twiddles<LOG2N>& tws,
+template <int LOG2N, int DIR, bool FLY = (LOG2N >= SW_TWFLY_LOG2)>
+__device__ __forceinline__ void fft_line(double2 (&v)[8], int t, const Twiddles<LOG2N, FLY>& tws,
                                          double2* __restrict__ line) {
-  fft_lines<LOG2N, DIR, 1>(reinterpret_cast<double2(&)[1][8]>(v), t, tws, line, 0);
+  fft_lines<LOG2N, DIR, 1, FLY>(reinterpret_cast<double2(&)[1][8]>(v), t, tws, line, 0);
 }
 
 }  // namespace sw

@@ -805,6 +805,149 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
 }
 
 // ===========================================================================
+// 2LQG / MultiLayerQG row with half-length real transforms.  Each real line
+// of N = nx points travels alone as one complex line of M = N/2 points,
+// z[m] = x[2m] + i x[2m+1] (W = exp(-2πi/N), all transforms unnormalised):
+//   c2r: Z[k] = (X[k] + conj X[M-k]) + i conj(W^k) (X[k] - conj X[M-k]),
+//        k < M, then z = IDFT_M(Z)
+//   r2c: Z = DFT_M(z), X[k] = E + W^k O, E = (Z[k] + conj Z[M-k]) / 2,
+//        O = (Z[k] - conj Z[M-k]) / 2i
+// Products of physical fields are products of the re and im parts.  A line
+// buffer holds M points (64 KB at nx = 8192), so two rows, as two blocks of
+// M/8 threads, share a CU where the full-length pair transform of k_row
+// holds one 1024-thread block.  Same outputs as k_row
+// (swqg/TwoLayerQG.jl:157-179): 0,1 ψx q per layer, 2,3 ψy q per layer.
+// Thread t holds k = t + s·M/8; the mirrors M - k are loaded by the thread
+// itself (the same row's lines, cache hits) rather than exchanged in LDS.
+// ===========================================================================
+template <int LOG2N>
+struct RowH {
+  static constexpr int N = 1 << LOG2N, M = N / 2, LM = LOG2N - 1, NTH = M / 8;
+  // inverse-layout offset of wavenumber kk of local row y
+  __device__ __forceinline__ static int inv(const Geom& g, int kk, int y) {
+    if (SW_ROW_CLOSED && g.nslab == 1)
+      return RowIdx<LOG2N>::row_inv(g, y) + 8 * (kk >> 1) + (g.tcm ? 4 : 1) * (kk & 1);
+    return midx_i(g, kk, y);
+  }
+  __device__ __forceinline__ static int fwd(const Geom& g, int k, int y) {
+    if (SW_ROW_CLOSED && g.nslab == 1) return RowIdx<LOG2N>::fwd0(g, k, y);
+    return midx(g, k, y);
+  }
+  // W^(t + s M/8) = W^t · exp(-2πi s/16)
+  __device__ __forceinline__ static double2 wk(double2 wt, int s) {
+    constexpr double c1 = 0.92387953251128675613, s1 = 0.38268343236508977173, h = 0.70710678118654752440;
+    const double cs[8] = {1.0, c1, h, s1, 0.0, -s1, -h, -c1};
+    const double sn[8] = {0.0, s1, h, c1, 1.0, c1, h, s1};
+    if (s == 0) return wt;
+    return cmul(wt, make_double2(cs[s], -sn[s]));
+  }
+};
+
+// c2r input of one real field: v[s] = Z[t + s NTH] (ik-multiplied when deriv).
+// Loads in two batches of four slots (eight loads in flight, 32 VGPRs)
+template <int LOG2N>
+__device__ __forceinline__ void load_real_h(double2 (&v)[8], const Geom& g, int t, int y,
+                                            const double2* __restrict__ A, bool deriv, double2 wt) {
+  using H = RowH<LOG2N>;
+  // offsets and W^k formed per call, not kept across the row's calls
+  asm volatile("" : "+v"(t), "+v"(wt.x), "+v"(wt.y));
+#pragma unroll
+  for (int hb = 0; hb < 2; ++hb) {
+    double2 a[4], b[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int s = 4 * hb + j, k = t + s * H::NTH, km = H::M - k;
+      a[j] = b[j] = zero2();
+      if (s * H::NTH < g.kc) a[j] = mix_ld_row(A + H::inv(g, k < g.kc ? k : 0, y));
+      if (H::M - (s + 1) * H::NTH < g.kc) b[j] = mix_ld_row(A + H::inv(g, km < g.kc ? km : 0, y));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int s = 4 * hb + j, k = t + s * H::NTH, km = H::M - k;
+      double2 x = k < g.kc ? a[j] : zero2(), xm = km < g.kc ? b[j] : zero2();
+      if (k == 0) x.y = 0.0;  // numpy's c2r rule; X[M] is never live
+      if (deriv) {
+        x = cmul_i(x, k * g.mk);
+        xm = cmul_i(xm, km * g.mk);
+      }
+      const double2 S = cadd(x, cconj(xm)), D = csub(x, cconj(xm));
+      const double2 T = cmul(D, cconj(H::wk(wt, s)));
+      v[s] = make_double2(S.x - T.y, S.y + T.x);
+    }
+  }
+}
+
+// r2c output of one real field from v[s] = Z[t + s NTH]: emit(k, s, X[k]) for
+// live k (one LDS round trip for the mirrors Z[M - k])
+template <int LOG2N, typename Emit>
+__device__ __forceinline__ void split_real_h(const double2 (&v)[8], int t, const Geom& g, double2* line,
+                                             double2 wt, Emit emit) {
+  using H = RowH<LOG2N>;
+  asm volatile("" : "+v"(t), "+v"(wt.x), "+v"(wt.y));
+  lds_barrier();  // previous LDS readers are done
+#pragma unroll
+  for (int s = 0; s < 8; ++s) line[LP<H::LM>(t + s * H::NTH)] = v[s];
+  lds_barrier();
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const int k = t + s * H::NTH;
+    if (s * H::NTH < g.kc && k < g.kc) {
+      const double2 zk = v[s];
+      const double2 zn = line[LP<H::LM>((H::M - k) & (H::M - 1))];
+      const double2 E = make_double2(0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y));
+      const double2 O = make_double2(0.5 * (zk.y + zn.y), -0.5 * (zk.x - zn.x));
+      emit(k, s, cadd(E, cmul(H::wk(wt, s), O)));
+    }
+  }
+}
+
+#ifndef SW_MINW_ROW_H
+#define SW_MINW_ROW_H 4
+#endif
+#ifndef SW_ROW_H_FLY
+#define SW_ROW_H_FLY true
+#endif
+template <int LOG2N>
+static __global__ void __launch_bounds__(RowH<LOG2N>::NTH, SW_MINW_ROW_H)
+    k_row_qg_h(Geom g, Phys p, const double2* __restrict__ Mi, double2* __restrict__ Mo,
+               const double2* __restrict__ tw, int yoff) {
+  using H = RowH<LOG2N>;
+  extern __shared__ double2 smem[];
+  const int t = threadIdx.x;
+  const int y = yoff + col_of_block(blockIdx.x, gridDim.x);
+  Twiddles<H::LM, SW_ROW_H_FLY> tws;  // stage twiddles read per stage: register room
+  tws.load(t, tw, 1);                    // W_M^j = W_N^(2j)
+  const double2 wt = tw[t];
+  const long long MF = g.mfield;
+  double2 q[8], v[8];
+#pragma unroll 1
+  for (int l = 0; l < 2; ++l) {
+    load_real_h<LOG2N>(q, g, t, y, Mi + l * MF, false, wt);
+    fft_line<H::LM, +1>(q, t, tws, smem);
+#pragma unroll 1
+    for (int d = 0; d < 2; ++d) {  // ψx q (:169), ψy q (:177)
+      load_real_h<LOG2N>(v, g, t, y, Mi + (d == 0 ? 2 + l : 4 + l) * MF, d == 0, wt);
+      fft_line<H::LM, +1>(v, t, tws, smem);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) v[s] = make_double2(v[s].x * q[s].x, v[s].y * q[s].y);
+      fft_line<H::LM, -1>(v, t, tws, smem);
+      double2* O = Mo + (2 * d + l) * MF;
+      split_real_h<LOG2N>(v, t, g, smem, wt, [&](int k, int, double2 X) { O[H::fwd(g, k, y)] = X; });
+    }
+  }
+}
+
+// lengths whose 2LQG row runs k_row_qg_h (SW_QG_ROW_HALF_MIN: from this
+// log2 nx up; measured in DESIGN.md §3e)
+#ifndef SW_QG_ROW_HALF_MIN
+#define SW_QG_ROW_HALF_MIN 13
+#endif
+template <int LOG2N>
+__host__ __device__ constexpr bool qg_row_half() {
+  return LOG2N >= SW_QG_ROW_HALF_MIN && LOG2N >= 10;
+}
+
+// ===========================================================================
 // col_fwd: forward FFT along y of the row outputs, combine into N (live rows).
 // N_f is the sum of at most two forward y-transforms of row outputs, each
 // with a per-mode multiplier (nterms):
@@ -2111,6 +2254,9 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
                        y0);
   } else if (model == MODEL_TY)
     hipLaunchKernelGGL((k_row<MODEL_TY, L>), dim3(nrows / BT::NB), dim3(BT::THREADS), sh_ty, s, g, p, Mi, Mo, tw, y0);
+  else if constexpr (qg_row_half<L>())
+    hipLaunchKernelGGL((k_row_qg_h<L>), dim3(nrows), dim3(RowH<L>::NTH), FftPlan<L - 1>::LDS * sizeof(double2), s, g,
+                       p, Mi, Mo, tw, y0);
   else
     hipLaunchKernelGGL((k_row<MODEL_QG2, L>), dim3(nrows / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p, Mi, Mo, tw,
                        y0);
@@ -2241,8 +2387,9 @@ int row_lines_per_block(int model, int log2nx) {
   int nb = 1;
   by_len(log2nx, [&](auto L) {
     constexpr int l = decltype(L)::value;
-    nb = model == MODEL_RSW ? BlkRow<MODEL_RSW, l>::NB : (model == MODEL_TY ? BlkRow<MODEL_TY, l>::NB
-                                                                            : BlkRow<MODEL_QG2, l>::NB);
+    nb = model == MODEL_RSW ? BlkRow<MODEL_RSW, l>::NB
+                            : (model == MODEL_TY ? BlkRow<MODEL_TY, l>::NB
+                                                 : (qg_row_half<l>() ? 1 : BlkRow<MODEL_QG2, l>::NB));
   });
   return nb;
 }
