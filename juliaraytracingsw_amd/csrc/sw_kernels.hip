@@ -843,32 +843,64 @@ struct RowH {
   }
 };
 
-// c2r input of one real field: v[s] = Z[t + s NTH] (ik-multiplied when deriv).
-// Loads in two batches of four slots (eight loads in flight, 32 VGPRs)
-template <int LOG2N>
-__device__ __forceinline__ void load_real_h(double2 (&v)[8], const Geom& g, int t, int y,
-                                            const double2* __restrict__ A, bool deriv, double2 wt) {
+// Spectral sources of load_real_h: ld(o) issues the loads of mixed offset o,
+// val(raw, kk) forms the x-spectral value at wavenumber kk.
+struct SrcField {  // A, times ik when deriv
+  const double2* A;
+  bool deriv;
+  using Raw = double2;
+  __device__ __forceinline__ static Raw zero() { return zero2(); }
+  __device__ __forceinline__ Raw ld(int o) const { return mix_ld_row(A + o); }
+  __device__ __forceinline__ double2 val(const Raw& r, int kk, const Geom& g) const {
+    return deriv ? cmul_i(r, kk * g.mk) : r;
+  }
+};
+struct SrcZeta {  // RSW ζ̂ = ik V̂ − Ûy (x-spectral, per element)
+  const double2 *V, *Uy;
+  struct Raw {
+    double2 v, uy;
+  };
+  __device__ __forceinline__ static Raw zero() { return Raw{zero2(), zero2()}; }
+  __device__ __forceinline__ Raw ld(int o) const { return Raw{mix_ld_row(V + o), mix_ld_row(Uy + o)}; }
+  __device__ __forceinline__ double2 val(const Raw& r, int kk, const Geom& g) const {
+    return csub(cmul_i(r.v, kk * g.mk), r.uy);
+  }
+};
+
+// c2r input of one real field: v[s] = Z[t + s NTH].  Loads in two batches of
+// four slots (eight loads per source array in flight)
+template <int LOG2N, typename Src>
+__device__ __forceinline__ void load_real_h(double2 (&v)[8], const Geom& g, int t, int y, const Src& src,
+                                            double2 wt) {
   using H = RowH<LOG2N>;
   // offsets and W^k formed per call, not kept across the row's calls
   asm volatile("" : "+v"(t), "+v"(wt.x), "+v"(wt.y));
 #pragma unroll
   for (int hb = 0; hb < 2; ++hb) {
-    double2 a[4], b[4];
+    typename Src::Raw a[4], b[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int s = 4 * hb + j, k = t + s * H::NTH, km = H::M - k;
-      a[j] = b[j] = zero2();
-      if (s * H::NTH < g.kc) a[j] = mix_ld_row(A + H::inv(g, k < g.kc ? k : 0, y));
-      if (H::M - (s + 1) * H::NTH < g.kc) b[j] = mix_ld_row(A + H::inv(g, km < g.kc ? km : 0, y));
+      a[j] = b[j] = Src::zero();
+      if (s * H::NTH < g.kc) a[j] = src.ld(H::inv(g, k < g.kc ? k : 0, y));
+      if (H::M - (s + 1) * H::NTH < g.kc) b[j] = src.ld(H::inv(g, km < g.kc ? km : 0, y));
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int s = 4 * hb + j, k = t + s * H::NTH, km = H::M - k;
-      double2 x = k < g.kc ? a[j] : zero2(), xm = km < g.kc ? b[j] : zero2();
-      if (k == 0) x.y = 0.0;  // numpy's c2r rule; X[M] is never live
-      if (deriv) {
-        x = cmul_i(x, k * g.mk);
-        xm = cmul_i(xm, km * g.mk);
+      double2 x, xm;
+      if constexpr (std::is_same<Src, SrcField>::value) {  // (the 2LQG row's register budget: this order)
+        x = k < g.kc ? a[j] : zero2();
+        xm = km < g.kc ? b[j] : zero2();
+        if (k == 0) x.y = 0.0;
+        if (src.deriv) {
+          x = cmul_i(x, k * g.mk);
+          xm = cmul_i(xm, km * g.mk);
+        }
+      } else {
+        x = k < g.kc ? src.val(a[j], k, g) : zero2();
+        xm = km < g.kc ? src.val(b[j], km, g) : zero2();
+        if (k == 0) x.y = 0.0;  // numpy's c2r rule; X[M] is never live
       }
       const double2 S = cadd(x, cconj(xm)), D = csub(x, cconj(xm));
       const double2 T = cmul(D, cconj(H::wk(wt, s)));
@@ -922,11 +954,11 @@ static __global__ void __launch_bounds__(RowH<LOG2N>::NTH, SW_MINW_ROW_H)
   double2 q[8], v[8];
 #pragma unroll 1
   for (int l = 0; l < 2; ++l) {
-    load_real_h<LOG2N>(q, g, t, y, Mi + l * MF, false, wt);
+    load_real_h<LOG2N>(q, g, t, y, SrcField{Mi + l * MF, false}, wt);
     fft_line<H::LM, +1>(q, t, tws, smem);
 #pragma unroll 1
     for (int d = 0; d < 2; ++d) {  // ψx q (:169), ψy q (:177)
-      load_real_h<LOG2N>(v, g, t, y, Mi + (d == 0 ? 2 + l : 4 + l) * MF, d == 0, wt);
+      load_real_h<LOG2N>(v, g, t, y, SrcField{Mi + (d == 0 ? 2 + l : 4 + l) * MF, d == 0}, wt);
       fft_line<H::LM, +1>(v, t, tws, smem);
 #pragma unroll
       for (int s = 0; s < 8; ++s) v[s] = make_double2(v[s].x * q[s].x, v[s].y * q[s].y);
@@ -935,6 +967,78 @@ static __global__ void __launch_bounds__(RowH<LOG2N>::NTH, SW_MINW_ROW_H)
       split_real_h<LOG2N>(v, t, g, smem, wt, [&](int k, int, double2 X) { O[H::fwd(g, k, y)] = X; });
     }
   }
+}
+
+// RSW row with half-length real transforms (the vorticity form of k_row,
+// rsw/RotatingShallowWater.jl:140-230): 4 inverse + 5 forward real lines
+// (k_row: 2 + 2 complex pairs and the real vη line as a full complex FFT).
+// Live: u, v, η (then ζ in η's registers), one product line; K̂ is kept in
+// u's registers (dead by then) for P = -ik K̂ + (ζv)^.
+#ifndef SW_MINW_ROW_RSW_H
+#define SW_MINW_ROW_RSW_H 2
+#endif
+template <int LOG2N>
+static __global__ void __launch_bounds__(RowH<LOG2N>::NTH, SW_MINW_ROW_RSW_H)
+    k_row_rsw_h(Geom g, Phys p, const double2* __restrict__ Mi, double2* __restrict__ Mo,
+                const double2* __restrict__ tw, int yoff) {
+  using H = RowH<LOG2N>;
+  extern __shared__ double2 smem[];
+  const int t = threadIdx.x;
+  const int y = yoff + col_of_block(blockIdx.x, gridDim.x);
+  Twiddles<H::LM> tws;
+  tws.load(t, tw, 1);  // W_M^j = W_N^(2j)
+  const double2 wt = tw[t];
+  const long long MF = g.mfield;
+  const double2 *U = Mi, *V = Mi + MF, *Hh = Mi + 2 * MF, *Uy = Mi + 3 * MF;
+  double2 u[8], v[8], e[8], w[8];
+  load_real_h<LOG2N>(u, g, t, y, SrcField{U, false}, wt);
+  fft_line<H::LM, +1>(u, t, tws, smem);
+  load_real_h<LOG2N>(v, g, t, y, SrcField{V, false}, wt);
+  fft_line<H::LM, +1>(v, t, tws, smem);
+  load_real_h<LOG2N>(e, g, t, y, SrcField{Hh, false}, wt);
+  fft_line<H::LM, +1>(e, t, tws, smem);
+  auto prod = [&](const double2 (&a)[8], const double2 (&b)[8]) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) w[s] = make_double2(a[s].x * b[s].x, a[s].y * b[s].y);
+  };
+  // 4: (vη)^
+  prod(v, e);
+  fft_line<H::LM, -1>(w, t, tws, smem);
+  split_real_h<LOG2N>(w, t, g, smem, wt, [&](int k, int, double2 X) { Mo[4 * MF + H::fwd(g, k, y)] = X; });
+  // 3: Q = -ik (uη)^
+  prod(u, e);
+  fft_line<H::LM, -1>(w, t, tws, smem);
+  split_real_h<LOG2N>(w, t, g, smem, wt,
+                      [&](int k, int, double2 X) { Mo[3 * MF + H::fwd(g, k, y)] = cmul_i(X, -(k * g.mk)); });
+  // ζ = vx - uy in η's registers
+  load_real_h<LOG2N>(e, g, t, y, SrcZeta{V, Uy}, wt);
+  fft_line<H::LM, +1>(e, t, tws, smem);
+  // 2: (ζu)^
+  prod(e, u);
+  fft_line<H::LM, -1>(w, t, tws, smem);
+  split_real_h<LOG2N>(w, t, g, smem, wt, [&](int k, int, double2 X) { Mo[2 * MF + H::fwd(g, k, y)] = X; });
+  // 1: K̂, K = (u² + v²)/2; kept in u
+#pragma unroll
+  for (int s = 0; s < 8; ++s)
+    w[s] = make_double2(0.5 * (u[s].x * u[s].x + v[s].x * v[s].x), 0.5 * (u[s].y * u[s].y + v[s].y * v[s].y));
+  fft_line<H::LM, -1>(w, t, tws, smem);
+  split_real_h<LOG2N>(w, t, g, smem, wt, [&](int k, int s, double2 X) {
+    Mo[MF + H::fwd(g, k, y)] = X;
+    u[s] = X;
+  });
+  // 0: P = -ik K̂ + (ζv)^
+  prod(e, v);
+  fft_line<H::LM, -1>(w, t, tws, smem);
+  split_real_h<LOG2N>(w, t, g, smem, wt,
+                      [&](int k, int s, double2 X) { Mo[H::fwd(g, k, y)] = cadd(cmul_i(u[s], -(k * g.mk)), X); });
+}
+
+#ifndef SW_RSW_ROW_HALF_MIN
+#define SW_RSW_ROW_HALF_MIN 12
+#endif
+template <int LOG2N>
+__host__ __device__ constexpr bool rsw_row_half() {
+  return LOG2N >= SW_RSW_ROW_HALF_MIN && LOG2N >= 11;
 }
 
 // lengths whose 2LQG row runs k_row_qg_h (SW_QG_ROW_HALF_MIN: from this
@@ -2250,8 +2354,12 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
   constexpr size_t sh_qg2 = FftPlan<L>::LDS * BQ::NB * sizeof(double2);
   constexpr size_t sh_ty = FftPlan<L>::LDS * BT::NB * sizeof(double2);
   if (model == MODEL_RSW) {
-    hipLaunchKernelGGL((k_row<MODEL_RSW, L>), dim3(nrows / BR::NB), dim3(BR::THREADS), sh_rsw, s, g, p, Mi, Mo, tw,
-                       y0);
+    if constexpr (rsw_row_half<L>())
+      hipLaunchKernelGGL((k_row_rsw_h<L>), dim3(nrows), dim3(RowH<L>::NTH), FftPlan<L - 1>::LDS * sizeof(double2), s,
+                         g, p, Mi, Mo, tw, y0);
+    else
+      hipLaunchKernelGGL((k_row<MODEL_RSW, L>), dim3(nrows / BR::NB), dim3(BR::THREADS), sh_rsw, s, g, p, Mi, Mo,
+                         tw, y0);
   } else if (model == MODEL_TY)
     hipLaunchKernelGGL((k_row<MODEL_TY, L>), dim3(nrows / BT::NB), dim3(BT::THREADS), sh_ty, s, g, p, Mi, Mo, tw, y0);
   else if constexpr (qg_row_half<L>())
@@ -2387,7 +2495,7 @@ int row_lines_per_block(int model, int log2nx) {
   int nb = 1;
   by_len(log2nx, [&](auto L) {
     constexpr int l = decltype(L)::value;
-    nb = model == MODEL_RSW ? BlkRow<MODEL_RSW, l>::NB
+    nb = model == MODEL_RSW ? (rsw_row_half<l>() ? 1 : BlkRow<MODEL_RSW, l>::NB)
                             : (model == MODEL_TY ? BlkRow<MODEL_TY, l>::NB
                                                  : (qg_row_half<l>() ? 1 : BlkRow<MODEL_QG2, l>::NB));
   });
