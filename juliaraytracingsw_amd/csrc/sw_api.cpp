@@ -63,6 +63,7 @@ struct sw_ctx {
   hipEvent_t ev_row = nullptr, ev_join = nullptr;
   hipEvent_t ev_fwd[8] = {}, ev_col[8] = {};
   hipEvent_t ev_chunk[8] = {};               // row chunk k of the last inverse group has arrived
+  hipEvent_t ev_rowc[8] = {};                // row chunk k has been transformed (its forward rows written)
   bool overlap = false;                      // pipelined exchange (default: RCCL; SW_OVERLAP=0/1)
   int row_chunks = 1;                        // pipelined: row pass in chunks behind the last inverse transposes
   double2 *tw_x = nullptr, *tw_y = nullptr;
@@ -190,6 +191,16 @@ Geom make_geom(const sw_config& k, int P, int s) {
   // SW_TILE_CM=0 selects row-major)
   g.tcm = 1;
   if (const char* e = std::getenv("SW_TILE_CM")) g.tcm = e[0] == '1';
+  // forward tiles: lines in column order on one slab (SW_LORD_F; the row
+  // pass's closed-form offsets assume it), in row order on several
+  // (row-chunked forward transposes, §6); SW_FWD_ORD=1 keeps column order
+  int ford = SW_LORD_F;
+  if (P > 1) {
+    ford = 0;
+    if (const char* e = std::getenv("SW_FWD_ORD")) ford = e[0] == '1';
+  }
+  g.fsy = ford ? 1 : g.kcl / 2;
+  g.fsk = ford ? g.nyl / 4 : 1;
   return g;
 }
 
@@ -298,10 +309,11 @@ struct Timer {
 // contiguous in both layouts, so no pack/unpack kernels exist.  Moves the
 // listed fields on stream `st` (RCCL: one group of sends/receives).
 //
-// Rows [r0, r1) of every block (inverse direction, r1 > r0 >= 0: one chunk of
-// the row pass's input): the inverse fields' lines are row-major 2×4 tiles
-// (SW_LORD_I = 0), so rows [r0, r1) (multiples of 4) of a block are the
-// contiguous elements [r0 kcl, r1 kcl) of it in both phases.
+// Rows [r0, r1) of every block (r1 > r0 >= 0: one chunk of the row pass's
+// input, or of its output): the inverse fields' lines are row-major 2×4 tiles
+// (SW_LORD_I = 0) and so are the forward fields' on several slabs (Geom::fsk
+// = 1), so rows [r0, r1) (multiples of 4) of a block are the contiguous
+// elements [r0 kcl, r1 kcl) of it in both phases.
 int transpose_fields(sw_ctx* c, bool inv, const int* fields, int nfl, hipStream_t st, int r0 = 0, int r1 = -1) {
   if (c->P == 1 || nfl == 0) return 0;
   const Geom& g0 = c->sl[0].g;
@@ -309,8 +321,9 @@ int transpose_fields(sw_ctx* c, bool inv, const int* fields, int nfl, hipStream_
   const long long MF = g0.mfield;
   if (r1 < 0) r1 = g0.nyl;
   if (r0 != 0 || r1 != g0.nyl) {
-    if (!inv || c->hostx || r0 < 0 || r1 > g0.nyl || r0 % 4 || r1 % 4)
-      return fail(c, SW_E_INVALID, "row-chunked transpose: inverse direction, device transports, rows in 4s");
+    const bool rows_contig = inv ? (SW_TILE_I == 2 && SW_LORD_I == 0) : (SW_TILE_F == 2 && g0.fsk == 1);
+    if (!rows_contig || c->hostx || r0 < 0 || r1 > g0.nyl || r0 % 4 || r1 % 4)
+      return fail(c, SW_E_INVALID, "row-chunked transpose: row-major tiles, device transports, rows in 4s");
   }
   const size_t off = (size_t)r0 * g0.kcl, cnt = (size_t)(r1 - r0) * g0.kcl;  // within each block
   if (!c->dist) {
@@ -440,6 +453,7 @@ int rows_pipelined(sw_ctx* c) {
   for (int k = 0; k < c->row_chunks; ++k) {
     HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_chunk[k], 0));
     for (Slab& s : c->sl) sw::launch_row(c->kmodel, s.g, c->p, s.mir, s.mfr, c->tw_x, c->stream, k * per, per);
+    HIPCHK(c, hipEventRecord(c->ev_rowc[k], c->stream));
   }
   return 0;
 }
@@ -447,20 +461,35 @@ int rows_pipelined(sw_ctx* c) {
 
 // after the compute stream has launched the row pass: forward transposes in
 // column-field order, ev_fwd[f] = inputs of column field f have arrived
+//
+// With the row pass in chunks (row_chunks > 1, rows_pipelined) the forward
+// transposes follow it chunk by chunk: chunk k of every forward field goes
+// over behind row chunk k (ev_rowc[k]), in column-field order within a chunk,
+// while the row pass transforms chunk k+1; ev_fwd[f] follows the last chunk
+// of column field f's inputs.
 int fwd_async(sw_ctx* c) {
   const PipeSpec& ps = pipe_spec(c->kmodel);
-  HIPCHK(c, hipEventRecord(c->ev_row, c->stream));
-  HIPCHK(c, hipStreamWaitEvent(c->comm, c->ev_row, 0));
-  bool sent[16] = {};
-  for (int fc = 0; fc < ps.nfc; ++fc) {
-    int f[3], n = 0;
-    for (int x : ps.fwd_need[fc])
-      if (x >= 0 && !sent[x]) {
-        f[n++] = x;
-        sent[x] = true;
-      }
-    if (int rc = transpose_fields(c, false, f, n, c->comm)) return rc;
-    HIPCHK(c, hipEventRecord(c->ev_fwd[fc], c->comm));
+  const int K = (c->row_chunks > 1 && SW_TILE_F == 2 && c->sl[0].g.fsk == 1) ? c->row_chunks : 1;
+  if (K <= 1) {
+    HIPCHK(c, hipEventRecord(c->ev_row, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->comm, c->ev_row, 0));
+  }
+  const int per = c->sl[0].g.nyl / K;
+  for (int k = 0; k < K; ++k) {
+    if (K > 1) HIPCHK(c, hipStreamWaitEvent(c->comm, c->ev_rowc[k], 0));
+    bool sent[16] = {};
+    for (int fc = 0; fc < ps.nfc; ++fc) {
+      int f[3], n = 0;
+      for (int x : ps.fwd_need[fc])
+        if (x >= 0 && !sent[x]) {
+          f[n++] = x;
+          sent[x] = true;
+        }
+      const int rc = K > 1 ? transpose_fields(c, false, f, n, c->comm, k * per, (k + 1) * per)
+                           : transpose_fields(c, false, f, n, c->comm);
+      if (rc) return rc;
+      if (k == K - 1) HIPCHK(c, hipEventRecord(c->ev_fwd[fc], c->comm));
+    }
   }
   return 0;
 }
@@ -919,6 +948,7 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
       HIPCHK(c, hipEventCreateWithFlags(&c->ev_fwd[i], hipEventDisableTiming));
       HIPCHK(c, hipEventCreateWithFlags(&c->ev_col[i], hipEventDisableTiming));
       HIPCHK(c, hipEventCreateWithFlags(&c->ev_chunk[i], hipEventDisableTiming));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_rowc[i], hipEventDisableTiming));
     }
     // Pipelined by default across GPUs (RCCL over xGMI runs beside the column
     // kernels).  With every slab in this process the "transposes" are copies
@@ -1045,7 +1075,9 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   // transposes, in 4 chunks where each per-(peer, field) message of a chunk
   // stays >= 1 MiB (latency-bound below); SW_ROW_CHUNKS=k forces k (1, 2, 4, 8).
   // A chunk is a multiple of 64 rows (the row pass's XCD interleave) and of
-  // the row blocks' lines; the inverse tiles must be row-major 2×4.
+  // the row blocks' lines; the inverse tiles must be row-major 2×4.  The
+  // forward transposes follow the row chunks (fwd_async) where the forward
+  // tiles are row-major too (the default on several slabs).
   if (P > 1) {
     const Geom& g = c->sl[0].g;
     int k = ((size_t)g.kcl * g.nyl * sizeof(double2) / 4 >= ((size_t)1 << 20)) ? 4 : 1;
@@ -1095,6 +1127,7 @@ void sw_destroy(sw_ctx* c) {
     if (c->ev_fwd[i]) (void)hipEventDestroy(c->ev_fwd[i]);
     if (c->ev_col[i]) (void)hipEventDestroy(c->ev_col[i]);
     if (c->ev_chunk[i]) (void)hipEventDestroy(c->ev_chunk[i]);
+    if (c->ev_rowc[i]) (void)hipEventDestroy(c->ev_rowc[i]);
   }
   if (c->comm) (void)hipStreamDestroy(c->comm);
   if (c->hsend) (void)hipHostFree(c->hsend);

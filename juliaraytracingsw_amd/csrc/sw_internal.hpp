@@ -53,6 +53,11 @@ struct Geom {
   long long cfield;   // elements per compact field  = max(kcn,1)*LrP
   long long mfield;   // elements per mixed field    = kcl*ny = (P*kcl)*nyl
   int tcm;            // inverse mixed fields: column-major tiles (mtile_local)
+  // forward mixed fields (A = 2, B = 4 tiles): line stride per 4 rows and per
+  // 2 columns — (1, nyl/4): lines in column order (one slab); (kcl/2, 1):
+  // in row order (several slabs: a chunk of rows is contiguous per block, so
+  // the forward transposes can follow the row pass chunk by chunk)
+  int fsy, fsk;
 };
 
 struct Phys {
@@ -137,9 +142,26 @@ __host__ __device__ inline int mtile_x(const Geom& g, int kr, int yl, int cm = 0
   }
   return p * g.nyl * g.kcl + mtile_local<A, ORD>(g, krl, yl, cm);
 }
-// forward fields: row phase / column phase
+// forward fields: row phase / column phase (A = 2: the line order from Geom)
+#if SW_TILE_F == 2
+__host__ __device__ inline int mtile_f_local(const Geom& g, int krl, int yl) {
+  return ((yl >> 2) * g.fsy + (krl >> 1) * g.fsk) * 8 + (yl & 3) * 2 + (krl & 1);
+}
+__host__ __device__ inline int midx(const Geom& g, int kr, int yl) {
+  int p = 0, krl = kr;
+  if (g.nslab > 1) {
+    p = kr / g.kcl;
+    krl = kr - p * g.kcl;
+  }
+  return p * g.nyl * g.kcl + mtile_f_local(g, krl, yl);
+}
+__host__ __device__ inline int midc(const Geom& g, int krl, int y) {
+  return (y >> g.log2nyl) * g.nyl * g.kcl + mtile_f_local(g, krl, y & (g.nyl - 1));
+}
+#else
 __host__ __device__ inline int midx(const Geom& g, int kr, int yl) { return mtile_x<SW_TILE_F, SW_LORD_F>(g, kr, yl); }
 __host__ __device__ inline int midc(const Geom& g, int krl, int y) { return mtile_c<SW_TILE_F, SW_LORD_F>(g, krl, y); }
+#endif
 // inverse fields: column phase / row phase
 __host__ __device__ inline int midc_i(const Geom& g, int krl, int y) { return mtile_c<SW_TILE_I, SW_LORD_I>(g, krl, y, g.tcm); }
 __host__ __device__ inline int midx_i(const Geom& g, int kr, int yl) { return mtile_x<SW_TILE_I, SW_LORD_I>(g, kr, yl, g.tcm); }
