@@ -1,4 +1,4 @@
-# SWLib.jl — the FourierFlows-side binding of libsw (include/sw.h, ABI 7).
+# SWLib.jl — the FourierFlows-side binding of libsw (include/sw.h, ABI 8).
 #
 # A maintainer's addition to the reference's run directories (INTEGRATION.md
 # says how it is installed).  After `SWLib.attach!(Model)` for a model module
@@ -39,7 +39,7 @@ using LinearAlgebra: mul!
 const libsw = get(ENV, "LIBSW", joinpath(@__DIR__, "libsw.so"))
 
 # ---------------------------------------------------------------- include/sw.h
-const SW_ABI_VERSION = Int32(7)
+const SW_ABI_VERSION = Int32(8)
 const SW_MODEL_RSW, SW_MODEL_QG2, SW_MODEL_TY, SW_MODEL_MLQG = Int32(0), Int32(1), Int32(2), Int32(3)
 const STEPPERS = Dict("FilteredAB3" => Int32(0), "IFMAB3" => Int32(1), "IFMRK4" => Int32(2),
                       "ETDRK4" => Int32(3), "FilteredRK4" => Int32(4))
@@ -68,6 +68,7 @@ Base.@kwdef mutable struct SWConfig
     H::NTuple{2,Float64} = (0.5, 0.5); b::NTuple{2,Float64} = (1.0, 0.0)
     Ulayer::NTuple{2,Float64} = (0.0, 0.0)
     precision::Int32 = SW_PREC_F64                      # the reference's T
+    aliased_state::Int32 = 0                            # 1: full-array prob.sol (include/sw.h)
 end
 
 # struct sw_energy_record

@@ -10,7 +10,7 @@ import os
 
 import numpy as np
 
-SW_ABI_VERSION = 7
+SW_ABI_VERSION = 8
 SW_MODEL_RSW, SW_MODEL_QG2, SW_MODEL_TY, SW_MODEL_MLQG = 0, 1, 2, 3
 SW_STEP_FILTERED_AB3, SW_STEP_IFMAB3, SW_STEP_IFMRK4, SW_STEP_ETDRK4, SW_STEP_FILTERED_RK4 = 0, 1, 2, 3, 4
 SW_OK, SW_E_INVALID, SW_E_NOMEM, SW_E_HIP, SW_E_COMM, SW_E_NAN, SW_E_STATE = 0, -1, -2, -3, -4, -5, -6
@@ -62,6 +62,7 @@ class SwConfig(C.Structure):
         ("f0", C.c_double), ("beta", C.c_double),
         ("H", C.c_double * 2), ("b", C.c_double * 2), ("Ulayer", C.c_double * 2),
         ("precision", C.c_int32),
+        ("aliased_state", C.c_int32),
     ]
 
 

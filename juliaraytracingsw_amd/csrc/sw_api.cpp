@@ -43,6 +43,17 @@ struct Slab {
   double2* mfr = nullptr;                    // row outputs, row phase
   double2* mfc = nullptr;                    // row outputs, column phase (col_fwd / col_step in)
   double2* view = nullptr;                   // scratch pointer for collect_full (history slots)
+  // aliased-state tracking (sw_config.aliased_state; one slab, 2LQG): the
+  // modes the 2/3 rule removes, compact in sw_ctx::ga[r] — region 0 the
+  // columns kr >= kc, region 1 the aliased rows of the live columns
+  double2* a_sol[2] = {};                    // post-step state there (the reference's prob.sol)
+  double2* a_zero[2] = {};                   // zeros: the dealiased pre-update state there
+  double2* a_hist[3][2] = {};                // AB3 steppers: N / RHS ring there
+  double2* a_acc[2] = {};                    // IFMRK4: running combination there
+  double2* a_n[2] = {};                      // IFMRK4: calcN output there
+  double2* a_xs[2] = {};                     // stage-input scratch (discarded: calcN dealiases)
+  double2* a_nbuf[2] = {};                   // this calcN's output there (aliases a_hist or a_n)
+  double2* a_mrow = nullptr;                 // row-pass x-spectra kr >= kc of the forward fields
 };
 
 struct sw_ctx {
@@ -93,6 +104,8 @@ struct sw_ctx {
   int64_t step = 0;
   int euler_left = 0;                        // sw_reset_history: forward-Euler start-up steps still to run
                                              // (cleared by sw_set_history; the clock does not move it)
+  bool alias = false;                        // sw_config.aliased_state
+  Geom ga[2]{};                              // its two regions (alias_geom)
   std::string err;
   // profiling
   bool prof = false;
@@ -220,6 +233,31 @@ std::vector<double2> twiddles(int N) {
     tw[m] = make_double2((double)std::cos(a), (double)-std::sin(a));
   }
   return tw;
+}
+
+// The aliased modes FF's dealias! zeroes as two compact regions
+// the mode-wise kernels (k_step_elem, k_energy_cols, k_scatter_modes) walk
+// like the live set: r = 0 the columns kr in [kc, nx/2], every row; r = 1 the
+// live columns, rows l in [lc, lr2) (lrow_of(j) = lc + j).  One slab.
+Geom alias_geom(const Geom& g, int r) {
+  Geom a = g;
+  if (r == 0) {
+    a.kr0 = g.kc;
+    a.kcn = g.nkr - g.kc;
+    a.lc = g.ny;
+    a.lr2 = g.ny;
+    a.Lr = g.ny;
+  } else {
+    a.kr0 = 0;
+    a.kcn = g.kc;
+    a.lc = 0;
+    a.lr2 = g.lc;
+    a.Lr = g.lr2 - g.lc;
+  }
+  a.kcl = a.kcn;
+  a.LrP = (a.Lr + 7) / 8 * 8;
+  a.cfield = (long long)std::max(a.kcn, 1) * a.LrP;
+  return a;
 }
 
 // --- algorithmic bytes per kernel launch ---------------------
@@ -542,13 +580,18 @@ int calcN(sw_ctx* c, double2* Slab::*X, double2* Slab::*N, int op = -1, int stag
   if (int rc = transpose(c, true, c->ninv)) return rc;
   {
     Timer tm(c, K_ROW);
-    for (Slab& s : c->sl) sw::launch_row(model, s.g, c->p, s.mir, s.mfr, c->tw_x, c->stream);
+    for (Slab& s : c->sl)
+      sw::launch_row(model, s.g, c->p, s.mir, s.mfr, c->tw_x, c->stream, 0, -1, c->alias ? s.a_mrow : nullptr);
   }
   if (int rc = transpose(c, false, c->nfwd)) return rc;
   {
     Timer tm(c, op >= 0 ? K_FWDSTEP : K_COLFWD);
     for (Slab& s : c->sl) last_col_pass(c, X, N, op, stage, s);
   }
+  if (c->alias)  // N at the aliased modes (the reference's calcN! writes them: swqg/TwoLayerQG.jl:171,179)
+    for (Slab& s : c->sl)
+      for (int r = 0; r < 2; ++r)
+        sw::launch_col_fwd_alias(s.g, c->ga[r], r, c->p, s.mfc, s.a_mrow, s.a_nbuf[r], c->tw_y, c->stream);
   return 0;
 }
 
@@ -582,7 +625,7 @@ bool use_fused(const sw_ctx* c) {
 // IFMAB3 2048² 5279 -> 4127, RSW IFMAB3 5358 -> 3916, 2LQG IFMRK4 8192² 62.5
 // -> 44.9.  SW_FWD_STEP=1 forces it on every built pair, =0 off.
 bool use_fwd_step(const sw_ctx* c) {
-  if (c->fwd_step == 0 || c->cfg.unfused || c->cfg.nop_calcN || use_fused(c)) return false;
+  if (c->fwd_step == 0 || c->cfg.unfused || c->cfg.nop_calcN || use_fused(c) || c->alias) return false;
   const int m = c->cfg.model, st = c->cfg.stepper;
   const bool built = (m == SW_MODEL_RSW && (st == SW_STEP_IFMAB3 || st == SW_STEP_IFMRK4)) ||
                      (m == SW_MODEL_QG2 && (st == SW_STEP_FILTERED_AB3 || st == SW_STEP_IFMAB3 ||
@@ -596,6 +639,30 @@ bool use_fwd_step(const sw_ctx* c) {
 // line buffer and parked N fit one CU's 160 KB
 bool fwd_step_lds(const sw_ctx* c) {
   return c->fwd_step == 2 && sw::fwd_step_lds_bytes(c->kmodel, c->sl[0].g) <= 160 * 1024;
+}
+
+// aliased-state tracking: this calcN's output at the aliased modes
+void set_alias_nbuf(sw_ctx* c, bool rk4) {
+  if (!c->alias) return;
+  for (Slab& s : c->sl)
+    for (int r = 0; r < 2; ++r) s.a_nbuf[r] = rk4 ? s.a_n[r] : s.a_hist[c->head][r];
+}
+
+sw::StepPtrs alias_step_ptrs(const sw_ctx* c, const Slab& s, int r) {
+  sw::StepPtrs a{};
+  a.sol = s.a_zero[r];
+  a.sol_out = s.a_sol[r];
+  a.xs = s.a_xs[r];
+  a.euler = (c->step < 3 || c->euler_left > 0) ? 1 : 0;
+  a.stream = 0;
+  if (c->cfg.stepper == SW_STEP_IFMRK4) {
+    a.h0 = s.a_acc[r];
+  } else {
+    a.h0 = s.a_hist[c->head][r];
+    a.h1 = s.a_hist[(c->head + 2) % 3][r];
+    a.h2 = s.a_hist[(c->head + 1) % 3][r];
+  }
+  return a;
 }
 
 sw::StepPtrs step_ptrs(const sw_ctx* c, const Slab& s) {
@@ -674,6 +741,7 @@ int run_stage(sw_ctx* c, int op, int stage, double2* Slab::*X) {
     // the update then overwrites in place (N -> RHS or N); nbuf aliases it
     if (op != sw::OP_RK4 && op != sw::OP_ETDRK4 && op != sw::OP_FRK4)
       for (Slab& s : c->sl) s.nbuf = s.hist[c->head];
+    set_alias_nbuf(c, op == sw::OP_RK4);
     if (use_fwd_step(c)) {
       if (int rc = calcN(c, X, &Slab::nbuf, op, stage)) return rc;
       c->mixed_valid = false;
@@ -685,6 +753,14 @@ int run_stage(sw_ctx* c, int op, int stage, double2* Slab::*X) {
       sw::StepPtrs a = step_ptrs(c, s);
       a.stage = stage;
       sw::launch_step_elem(c->nf, op, s.g, c->p, a, s.nbuf, s.xs, c->stream);
+      // the same update at the aliased modes, from the zero (dealiased) state:
+      // the post-step values the reference's update writes there
+      // (utils/IFMAB3.jl:142-160; filter after)
+      for (int r = 0; c->alias && r < 2; ++r) {
+        sw::StepPtrs b = alias_step_ptrs(c, s, r);
+        b.stage = stage;
+        sw::launch_step_elem(c->nf, op, c->ga[r], c->p, b, s.a_nbuf[r], s.a_xs[r], c->stream);
+      }
     }
     c->mixed_valid = false;
   }
@@ -697,6 +773,19 @@ int run_stage(sw_ctx* c, int op, int stage, double2* Slab::*X) {
 // :147-149, 323-333): the pre-update state (FilteredAB3, IFMAB3) or the
 // stage-4 input (IFMRK4).  2LQG's recompute from prob.sol (swqg/TwoLayerQG.jl
 // :230-252), the post-update state.
+// aliased-state tracking: the post-step state's aliased modes add their column
+// sums after the ncols live ones (a full-array parsevalsum, in a fixed order);
+// returns the column count
+int alias_energy_cols(sw_ctx* c, bool post_step_state, int ncols) {
+  if (!c->alias || !post_step_state) return ncols;
+  for (int r = 0; r < 2; ++r) {
+    sw::launch_energy_cols(c->cfg.model, c->ga[r], c->p, c->sl[0].a_sol[r], c->ecols + SW_NSUM * (size_t)ncols,
+                           c->stream);
+    ncols += c->ga[r].kcn;
+  }
+  return ncols;
+}
+
 void record_energy(sw_ctx* c, double2* Slab::*X) {
   if (c->dist) {  // this rank's column sums; added over ranks at retrieval
     const Slab& s = c->sl[0];
@@ -704,7 +793,8 @@ void record_energy(sw_ctx* c, double2* Slab::*X) {
     return;
   }
   for (Slab& s : c->sl) sw::launch_energy_cols(c->cfg.model, s.g, c->p, s.*X, c->ecols + SW_NSUM * s.g.kr0, c->stream);
-  sw::launch_energy_final(c->ecols, c->P * c->sl[0].g.kcl, c->erec + SW_NSUM * c->diag_n, c->stream);
+  const int ncols = alias_energy_cols(c, X == &Slab::sol, c->P * c->sl[0].g.kcl);
+  sw::launch_energy_final(c->ecols, ncols, c->erec + SW_NSUM * c->diag_n, c->stream);
 }
 
 int step_once(sw_ctx* c) {
@@ -858,6 +948,23 @@ void free_slab(Slab& s) {
   if (s.nbuf && s.nbuf != s.hist[0] && s.nbuf != s.hist[1] && s.nbuf != s.hist[2]) (void)hipFree(s.nbuf);
   if (s.mir && s.mir != s.mic) (void)hipFree(s.mir);
   if (s.mfc && s.mfc != s.mfr) (void)hipFree(s.mfc);
+  for (int r = 0; r < 2; ++r) {
+    void* a[] = {s.a_sol[r], s.a_zero[r], s.a_hist[0][r], s.a_hist[1][r], s.a_hist[2][r], s.a_acc[r], s.a_n[r],
+                 s.a_xs[r]};
+    for (void* q : a)
+      if (q) (void)hipFree(q);
+  }
+  if (s.a_mrow) (void)hipFree(s.a_mrow);
+}
+
+// aliased-state tracking: a compact aliased pair <-> c->stage (the full array)
+void alias_scatter(sw_ctx* c, double2* const (&a)[2]) {
+  if (!c->alias) return;
+  for (int r = 0; r < 2; ++r) sw::launch_scatter_modes(c->nf, c->ga[r], a[r], c->stage, c->stream);
+}
+void alias_gather(sw_ctx* c, double2* const (&a)[2]) {
+  if (!c->alias) return;
+  for (int r = 0; r < 2; ++r) sw::launch_gather_modes(c->nf, c->ga[r], c->stage, a[r], c->stream);
 }
 
 }  // namespace
@@ -921,6 +1028,14 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   if (k.filter_order < 0) return fail(c, SW_E_INVALID, "filter_order must be >= 0");
   if (k.precision != SW_PREC_F64 && k.precision != SW_PREC_F32)
     return fail(c, SW_E_INVALID, "precision must be SW_PREC_F64 or SW_PREC_F32");
+  if (k.aliased_state) {
+    if (k.model != SW_MODEL_QG2 ||
+        (k.stepper != SW_STEP_IFMAB3 && k.stepper != SW_STEP_IFMRK4 && k.stepper != SW_STEP_FILTERED_AB3))
+      return fail(c, SW_E_INVALID, "aliased_state: 2LQG with IFMAB3, IFMRK4 or FilteredAB3");
+    if (k.nranks > 1) return fail(c, SW_E_INVALID, "aliased_state: one slab (nranks = 1)");
+    if (!sw::row_alias_built(SW_MODEL_QG2, ilog2(k.nx)))
+      return fail(c, SW_E_INVALID, "aliased_state: nx <= 4096 (the full-length 2LQG row pass)");
+  }
   const int P = k.nranks;
   if (!pow2(P) || k.ny / P < 32)
     return fail(c, SW_E_INVALID, "nranks must be a power of two with ny / nranks >= 32");
@@ -1040,13 +1155,33 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
         if ((rc = alloc(c, (void**)&s.hist[i], c->nf * cb))) return rc;
     }
   }
+  c->alias = k.aliased_state != 0;
+  if (c->alias) {
+    Slab& s = c->sl[0];
+    for (int r = 0; r < 2; ++r) {
+      c->ga[r] = alias_geom(s.g, r);
+      const size_t cb = (size_t)c->nf * c->ga[r].cfield * sizeof(double2);
+      for (double2** q : {&s.a_sol[r], &s.a_zero[r], &s.a_xs[r]})
+        if ((rc = alloc(c, (void**)q, cb))) return rc;
+      if (k.stepper == SW_STEP_IFMRK4) {
+        if ((rc = alloc(c, (void**)&s.a_acc[r], cb))) return rc;
+        if ((rc = alloc(c, (void**)&s.a_n[r], cb))) return rc;
+      } else {
+        for (int i = 0; i < 3; ++i)
+          if ((rc = alloc(c, (void**)&s.a_hist[i][r], cb))) return rc;
+      }
+    }
+    const size_t mrow = (size_t)c->nfwd * (s.g.nkr - s.g.kc) * s.g.ny * sizeof(double2);
+    if ((rc = alloc(c, (void**)&s.a_mrow, mrow))) return rc;
+  }
   const Geom& g = c->sl[0].g;
   if ((rc = alloc(c, (void**)&c->stage, full_bytes(c)))) return rc;
   if (k.precision == SW_PREC_F32)  // >= one physical field in fp32 too
     if ((rc = alloc(c, (void**)&c->stage32, full_bytes(c) / 2))) return rc;
   if ((rc = alloc(c, (void**)&c->dflt, (size_t)g.nx * g.ny * sizeof(double)))) return rc;
   if ((rc = alloc(c, (void**)&c->flag, 1024 * sizeof(int)))) return rc;
-  if ((rc = alloc(c, (void**)&c->ecols, SW_NSUM * (size_t)P * g.kcl * sizeof(double)))) return rc;
+  const size_t ecols = (size_t)P * g.kcl + (c->alias ? (size_t)c->ga[0].kcn + c->ga[1].kcn : 0);
+  if ((rc = alloc(c, (void**)&c->ecols, SW_NSUM * ecols * sizeof(double)))) return rc;
   if ((rc = alloc(c, (void**)&c->esum, (SW_NSUM + 2 * (size_t)P) * sizeof(double)))) return rc;
   if (c->dist) {
     const size_t gb = (size_t)P * c->nf * g.kcl * g.LrP * sizeof(double2);
@@ -1154,6 +1289,7 @@ int sw_set_state(sw_ctx* c, const void* sol, size_t bytes) {
   HIPCHK(c, hipSetDevice(c->cfg.device));
   if (int rc = upload(c, sol, c->stage, full_bytes(c))) return rc;
   for (Slab& s : c->sl) sw::launch_gather(c->nf, s.g, c->stage, s.sol, c->stream);
+  alias_gather(c, c->sl[0].a_sol);  // sol .= q0h keeps them until updatevars!/calcN! dealias
   c->mixed_valid = false;
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1166,6 +1302,7 @@ int sw_get_state(const sw_ctx* cc, void* sol, size_t bytes) {
   if (!sol || bytes != caller_bytes(c, full_bytes(c))) return fail(c, SW_E_INVALID, "sw_get_state: size mismatch");
   HIPCHK(c, hipSetDevice(c->cfg.device));
   if (int rc = collect_full(c, &Slab::sol)) return rc;
+  alias_scatter(c, c->sl[0].a_sol);
   if (int rc = download(c, c->stage, sol, full_bytes(c))) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return SW_OK;
@@ -1217,8 +1354,10 @@ int sw_calcN(sw_ctx* c, const void* sol, void* N, size_t bytes) {
         c->cfg.stepper != SW_STEP_FILTERED_RK4)
       s.nbuf = s.hist[c->head];
   }
+  set_alias_nbuf(c, c->cfg.stepper == SW_STEP_IFMRK4);
   if (int rc = calcN(c, &Slab::xs, &Slab::nbuf)) return rc;
   if (int rc = collect_full(c, &Slab::nbuf)) return rc;
+  alias_scatter(c, c->sl[0].a_nbuf);
   if (int rc = download(c, c->stage, N, full_bytes(c))) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return SW_OK;
@@ -1255,6 +1394,9 @@ int sw_get_physical(sw_ctx* c, int32_t fid, void* out, size_t bytes) {
                                  : c->cfg.model == SW_MODEL_TY ? "TY physical ids are 0..5, 8, 9"
                                                                : "bad QG2 physical id");
   HIPCHK(c, hipSetDevice(c->cfg.device));
+  // updatevars! begins with dealias!(sol, grid) (swqg/TwoLayerQG.jl:115)
+  for (int r = 0; c->alias && r < 2; ++r)
+    HIPCHK(c, hipMemsetAsync(c->sl[0].a_sol[r], 0, (size_t)c->nf * c->ga[r].cfield * sizeof(double2), c->stream));
   if (int rc = physical_to_dflt(c, fid)) return rc;
   if (c->dist) {
     const size_t rows = (size_t)g0.nyl * g0.nx;
@@ -1410,7 +1552,7 @@ int sw_diag(sw_ctx* c, int32_t id, double* out) {
     const Geom& g0 = c->sl[0].g;
     if (int rc = allgather(c, c->ecols + SW_NSUM * g0.kr0, c->ecols, SW_NSUM * (size_t)g0.kcl * sizeof(double))) return rc;
   }
-  sw::launch_energy_final(c->ecols, c->P * c->sl[0].g.kcl, c->esum, c->stream);
+  sw::launch_energy_final(c->ecols, alias_energy_cols(c, true, c->P * c->sl[0].g.kcl), c->esum, c->stream);
   HIPCHK(c, hipGetLastError());
   std::vector<double> sums(SW_NSUM);
   HIPCHK(c, hipMemcpyAsync(sums.data(), c->esum, SW_NSUM * sizeof(double), hipMemcpyDeviceToHost, c->stream));
@@ -1531,6 +1673,7 @@ int sw_get_history(const sw_ctx* cc, int32_t slot, void* buf, size_t bytes) {
   if (int rc = join_comm(c)) return rc;
   for (Slab& s : c->sl) s.view = s.hist[h];
   if (int rc = collect_full(c, &Slab::view)) return rc;
+  alias_scatter(c, c->sl[0].a_hist[h]);
   if (int rc = download(c, c->stage, buf, full_bytes(c))) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return SW_OK;
@@ -1545,6 +1688,7 @@ int sw_set_history(sw_ctx* c, int32_t slot, const void* buf, size_t bytes) {
   if (int rc = join_comm(c)) return rc;
   if (int rc = upload(c, buf, c->stage, full_bytes(c))) return rc;
   for (Slab& s : c->sl) sw::launch_gather(c->nf, s.g, c->stage, s.hist[h], c->stream);
+  alias_gather(c, c->sl[0].a_hist[h]);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->euler_left = 0;  // the history is valid again: AB3 from the next step (clock.step >= 3)
@@ -1606,10 +1750,12 @@ int sw_get_checkpoint(const sw_ctx* cc, void* buf, size_t bytes) {
   for (int k = 0; k <= h.nslots; ++k) {  // fp64 always: no narrowing to the caller precision
     if (k == 0) {
       if (int rc = collect_full(c, &Slab::sol)) return rc;
+      alias_scatter(c, c->sl[0].a_sol);
     } else {
       const int hi = hist_index(c, k);
       for (Slab& s : c->sl) s.view = s.hist[hi];
       if (int rc = collect_full(c, &Slab::view)) return rc;
+      alias_scatter(c, c->sl[0].a_hist[hi]);
     }
     HIPCHK(c, hipMemcpyAsync(out + sizeof(h) + k * fb, c->stage, fb, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1633,6 +1779,7 @@ int sw_set_checkpoint(sw_ctx* c, const void* buf, size_t bytes) {
   for (int k = 0; k <= h.nslots; ++k) {
     HIPCHK(c, hipMemcpyAsync(c->stage, in + sizeof(h) + k * fb, fb, hipMemcpyHostToDevice, c->stream));
     for (Slab& s : c->sl) sw::launch_gather(c->nf, s.g, c->stage, k == 0 ? s.sol : s.hist[hist_index(c, k)], c->stream);
+    alias_gather(c, k == 0 ? c->sl[0].a_sol : c->sl[0].a_hist[hist_index(c, k)]);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipStreamSynchronize(c->stream));  // the staging buffer is reused
   }

@@ -597,12 +597,32 @@ __device__ __forceinline__ void fft_pair(double2 (&w)[2][8], int t, const Twiddl
   }
 }
 
-template <int MODEL, int LOG2N>
+// After split_pair (LDS still holds Z): the aliased x-spectra kc <= k <= nx/2
+// of the pair, A[k] and B[k], into [k - kc][y] of A and B (aliased-state
+// tracking, sw_config.aliased_state)
+template <int LOG2N>
+__device__ __forceinline__ void store_alias_pair(const double2 (&v)[8], int t, const Geom& g, const double2* line,
+                                                 double2* __restrict__ A, double2* __restrict__ B, int y) {
+  constexpr int N = 1 << LOG2N, NT = N / 8;
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const int k = t + s * NT;
+    if (k >= g.kc && k <= N / 2) {
+      const double2 zk = v[s];
+      const double2 zn = line[LP<LOG2N>((N - k) & (N - 1))];
+      const long long o = (long long)(k - g.kc) * g.ny + y;
+      A[o] = make_double2(0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y));
+      B[o] = make_double2(0.5 * (zk.y + zn.y), -0.5 * (zk.x - zn.x));
+    }
+  }
+}
+
+template <int MODEL, int LOG2N, bool ALIAS = false>
 static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
                                          (BlkRow<MODEL, LOG2N>::THREADS >= 1024 ? 4
                                           : (MODEL == MODEL_QG2 ? SW_MINW_ROW_QG : SW_MINW_ROW)))
     k_row(Geom g, Phys p, const double2* __restrict__ Mi, double2* __restrict__ Mo,
-          const double2* __restrict__ tw, int yoff) {
+          const double2* __restrict__ tw, int yoff, double2* __restrict__ Ma) {
   using Bk = BlkRow<MODEL, LOG2N>;
   extern __shared__ double2 smem[];
   const LineCtx c = line_ctx<LOG2N>();
@@ -794,6 +814,8 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
     for (int s = 0; s < 8; ++s) v[s] = make_double2(v[s].x * q[s].x, v[s].y * q[s].y);
     fft_line<LOG2N, -1>(v, c.t, tws, line);
     store_pair<LOG2N>(v, ri, g, line, Mo, Mo + MF);
+    const long long MA = (long long)(g.nkr - g.kc) * g.ny;  // aliased columns × rows per field
+    if constexpr (ALIAS) store_alias_pair<LOG2N>(v, c.t, g, line, Ma, Ma + MA, y);
     // ψy q per layer (:177)
     load_pair<LOG2N>(v, ri, g, Py1, Py2, false);
     fft_line<LOG2N, +1>(v, c.t, tws, line);
@@ -801,6 +823,7 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
     for (int s = 0; s < 8; ++s) v[s] = make_double2(v[s].x * q[s].x, v[s].y * q[s].y);
     fft_line<LOG2N, -1>(v, c.t, tws, line);
     store_pair<LOG2N>(v, ri, g, line, Mo + 2 * MF, Mo + 3 * MF);
+    if constexpr (ALIAS) store_alias_pair<LOG2N>(v, c.t, g, line, Ma + 2 * MA, Ma + 3 * MA, y);
   }
 }
 
@@ -1183,6 +1206,56 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
         }
         Nf[j] = r;
       }
+    }
+  }
+}
+
+// 2LQG N = -il F(A_l) + ik F(B_l) (swqg/TwoLayerQG.jl:171,179) at the aliased
+// modes of region ga (aliased-state tracking, one slab; sw_api.cpp
+// alias_geom): region 0 = the columns kr in [kc, nx/2] (A, B from the row
+// pass's aliased output Ma, [field][kr - kc][y]), region 1 = the rows l in the
+// 2/3-rule band of the live columns (A, B from the forward mixed fields, as
+// k_col_fwd reads them).  The y-transforms and multipliers are k_col_fwd's.
+template <int LOG2N>
+static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
+    k_col_fwd_alias(Geom g, Geom ga, int region, Phys p, const double2* __restrict__ Mf,
+                    const double2* __restrict__ Ma, double2* __restrict__ N, const double2* __restrict__ tw) {
+  using B = Blk<LOG2N>;
+  constexpr int NT = B::NT;
+  extern __shared__ double2 smem[];
+  const LineCtx c = line_ctx<LOG2N>();
+  const int col = blockIdx.x * B::NB + c.ln;  // column of the region
+  const int layer = blockIdx.y;
+  const bool live = col < ga.kcn;
+  const int colA = live ? col : 0;
+  double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
+  Twiddles<LOG2N> tws;
+  tws.load(c.t, tw);
+  const double k = (ga.kr0 + colA) * g.mk;
+  const long long MA = (long long)(g.nkr - g.kc) * g.ny;
+  double2 v[8], acc[8];
+  auto load_col = [&](int f) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int m = c.t + s * NT;
+      const double2 t = region == 0 ? Ma[f * MA + (long long)colA * g.ny + m] : Mf[f * g.mfield + midc(g, colA, m)];
+      v[s] = live ? t : zero2();
+    }
+  };
+  load_col(layer);
+  fft_line<LOG2N, -1>(v, c.t, tws, line);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) acc[s] = apply_mul(v[s], MUL_NIL, k, lwav(g, c.t + s * NT));
+  load_col(2 + layer);
+  fft_line<LOG2N, -1>(v, c.t, tws, line);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) acc[s] = cadd(acc[s], apply_mul(v[s], MUL_PIK, k, lwav(g, c.t + s * NT)));
+  if (live) {
+    double2* Nf = N + (long long)layer * ga.cfield + (long long)col * ga.LrP;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int j = compact_of(ga, c.t + s * NT);
+      if (j >= 0 && j < ga.Lr) Nf[j] = acc[s];
     }
   }
 }
@@ -2039,6 +2112,22 @@ static __global__ void k_scatter(Geom g, int nf, int lo, int hi, const double2* 
   full[((long long)f * g.nl + m) * g.nkr + kr] = v;
 }
 
+// the compact modes of ga only (aliased regions; the other modes untouched)
+static __global__ void k_scatter_modes(Geom ga, int nf, const double2* __restrict__ cmp, double2* __restrict__ full) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  int kr, j;
+  if (i >= ga.cfield || !mode_of(ga, i, kr, j)) return;
+  const int m = lrow_of(ga, j);
+  for (int f = 0; f < nf; ++f) full[((long long)f * ga.nl + m) * ga.nkr + kr] = cmp[f * ga.cfield + i];
+}
+static __global__ void k_gather_modes(Geom ga, int nf, const double2* __restrict__ full, double2* __restrict__ cmp) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  int kr, j;
+  if (i >= ga.cfield || !mode_of(ga, i, kr, j)) return;
+  const int m = lrow_of(ga, j);
+  for (int f = 0; f < nf; ++f) cmp[f * ga.cfield + i] = full[((long long)f * ga.nl + m) * ga.nkr + kr];
+}
+
 static __global__ void k_nan_check(Geom g, int nf, const double2* __restrict__ cmp, int* flag) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   int kr, j;
@@ -2225,7 +2314,7 @@ static __global__ void __launch_bounds__(256) k_energy_cols(Geom g, Phys p, int 
   if (krl < g.kcn) {
     const long long cf = g.cfield;
     const int kr = g.kr0 + krl;
-    const double w = kr == 0 ? 1.0 : 2.0, k = kr * g.mk;
+    const double w = (kr == 0 || 2 * kr == g.nx) ? 1.0 : 2.0, k = kr * g.mk;  // FF parsevalsum
     for (int j = threadIdx.x; j < g.Lr; j += blockDim.x) {
       const long long i = (long long)krl * g.LrP + j;
       if (model == MODEL_RSW) {
@@ -2345,7 +2434,7 @@ void LenOps<L>::col_inv(int model, const Geom& g, const Phys& p, const double2* 
 
 template <int L>
 void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, double2* Mo, const double2* tw,
-                    hipStream_t s, int y0, int nrows) {
+                    hipStream_t s, int y0, int nrows, double2* Ma) {
   if (nrows < 0) nrows = g.nyl - y0;
   using BR = BlkRow<MODEL_RSW, L>;
   using BQ = BlkRow<MODEL_QG2, L>;
@@ -2359,15 +2448,27 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
                          g, p, Mi, Mo, tw, y0);
     else
       hipLaunchKernelGGL((k_row<MODEL_RSW, L>), dim3(nrows / BR::NB), dim3(BR::THREADS), sh_rsw, s, g, p, Mi, Mo,
-                         tw, y0);
+                         tw, y0, nullptr);
   } else if (model == MODEL_TY)
-    hipLaunchKernelGGL((k_row<MODEL_TY, L>), dim3(nrows / BT::NB), dim3(BT::THREADS), sh_ty, s, g, p, Mi, Mo, tw, y0);
+    hipLaunchKernelGGL((k_row<MODEL_TY, L>), dim3(nrows / BT::NB), dim3(BT::THREADS), sh_ty, s, g, p, Mi, Mo, tw, y0,
+                       nullptr);
   else if constexpr (qg_row_half<L>())
     hipLaunchKernelGGL((k_row_qg_h<L>), dim3(nrows), dim3(RowH<L>::NTH), FftPlan<L - 1>::LDS * sizeof(double2), s, g,
-                       p, Mi, Mo, tw, y0);
+                       p, Mi, Mo, tw, y0);  // (no aliased output: row_alias_built)
+  else if (Ma)
+    hipLaunchKernelGGL((k_row<MODEL_QG2, L, true>), dim3(nrows / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p, Mi, Mo,
+                       tw, y0, Ma);
   else
     hipLaunchKernelGGL((k_row<MODEL_QG2, L>), dim3(nrows / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p, Mi, Mo, tw,
-                       y0);
+                       y0, nullptr);
+}
+
+template <int L>
+void LenOps<L>::col_fwd_alias(const Geom& g, const Geom& ga, int region, const Phys& p, const double2* Mf,
+                              const double2* Ma, double2* N, const double2* tw, hipStream_t s) {
+  const dim3 grid((ga.kcn + Blk<L>::NB - 1) / Blk<L>::NB, 2);
+  hipLaunchKernelGGL((k_col_fwd_alias<L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, ga, region, p, Mf, Ma,
+                     N, tw);
 }
 
 template <int L>
@@ -2488,8 +2589,26 @@ void launch_col_inv(int model, const Geom& g, const Phys& p, const double2* X, d
   by_len(g.log2ny, [&](auto L) { LenOps<decltype(L)::value>::col_inv(model, g, p, X, Minv, tw_y, s, g0, ng); });
 }
 void launch_row(int model, const Geom& g, const Phys& p, const double2* Minv, double2* Mfwd,
-                const double2* tw_x, hipStream_t s, int y0, int nrows) {
-  by_len(g.log2nx, [&](auto L) { LenOps<decltype(L)::value>::row(model, g, p, Minv, Mfwd, tw_x, s, y0, nrows); });
+                const double2* tw_x, hipStream_t s, int y0, int nrows, double2* Ma) {
+  by_len(g.log2nx, [&](auto L) { LenOps<decltype(L)::value>::row(model, g, p, Minv, Mfwd, tw_x, s, y0, nrows, Ma); });
+}
+bool row_alias_built(int model, int log2nx) {
+  bool ok = false;
+  by_len(log2nx, [&](auto L) { ok = model == MODEL_QG2 && !qg_row_half<decltype(L)::value>(); });
+  return ok;
+}
+void launch_col_fwd_alias(const Geom& g, const Geom& ga, int region, const Phys& p, const double2* Mfwd,
+                          const double2* Ma, double2* N, const double2* tw_y, hipStream_t s) {
+  if (ga.kcn <= 0) return;
+  by_len(g.log2ny, [&](auto L) { LenOps<decltype(L)::value>::col_fwd_alias(g, ga, region, p, Mfwd, Ma, N, tw_y, s); });
+}
+void launch_scatter_modes(int nf, const Geom& ga, const double2* cmp, double2* full, hipStream_t s) {
+  if (ga.cfield <= 0 || ga.kcn <= 0) return;
+  hipLaunchKernelGGL(k_scatter_modes, dim3((unsigned)((ga.cfield + 255) / 256)), dim3(256), 0, s, ga, nf, cmp, full);
+}
+void launch_gather_modes(int nf, const Geom& ga, const double2* full, double2* cmp, hipStream_t s) {
+  if (ga.cfield <= 0 || ga.kcn <= 0) return;
+  hipLaunchKernelGGL(k_gather_modes, dim3((unsigned)((ga.cfield + 255) / 256)), dim3(256), 0, s, ga, nf, full, cmp);
 }
 int row_lines_per_block(int model, int log2nx) {
   int nb = 1;

@@ -39,7 +39,7 @@ class Problem:
     def __init__(self, model, *, nx, ny, Lx, Ly, dt, aliased_fraction, stepper, params,
                  use_filter=False, filter_kw=None, device=0, check_nan=True, T=np.float64,
                  nop_calcN=False, unfused=False, nranks=1, rank=0, local_slabs=1,
-                 comm_unique_id=None, exchange=None):
+                 comm_unique_id=None, exchange=None, aliased_state=False):
         # T: the element type of the caller's buffers (prob.sol, vars), as the
         # reference's Problem(...; T) (rsw/RSWDriver.jl:164 and
         # swqg/TwoLayerDriver.jl:63 pass Float32); libsw computes in fp64
@@ -74,6 +74,8 @@ class Problem:
         cfg.check_nan = 1 if check_nan else 0
         cfg.nop_calcN = 1 if nop_calcN else 0
         cfg.unfused = 1 if unfused else 0
+        # carry the modes the 2/3 rule removes (2LQG, one slab: include/sw.h)
+        cfg.aliased_state = 1 if aliased_state else 0
         # slab decomposition: nranks slabs; local_slabs == nranks
         # holds them all on this GPU, else this process holds slab `rank` and
         # transposes over RCCL with the broadcast comm_unique_id bytes

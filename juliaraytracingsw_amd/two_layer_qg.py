@@ -15,13 +15,16 @@ from .problem import Diagnostic, Problem as _Problem, increment, stepforward  # 
 def Problem(dev="gpu", *, nx=128, ny=None, Lx=2 * np.pi, Ly=None, U=0.5, mu=1e-2, nu=1e-6, nnu=4,
             f0=3.0, Cg=1.0, drhorho0=0.2, stepper="IFMAB3", dt=5e-2, aliased_fraction=1 / 3,
             T=np.float32, use_filter=False, device=0, check_nan=True, nop_calcN=False, unfused=False,
-            decomposition=None, **stepper_kwargs):
+            decomposition=None, aliased_state=False, **stepper_kwargs):
     """``TwoLayerQG.Problem(dev; nx, ny, Lx, Ly, U, μ, ν, nν, f0, Cg, δρρ0, stepper,
     dt, aliased_fraction, T, use_filter, stepper_kwargs...)`` (:55-90).
 
     ``T`` (default Float32, as the reference's :70) is the element type of
     the caller-side arrays (``prob.sol``, ``updatevars``); libsw computes in
     fp64 either way (BASELINE parity precision) and rounds once on output.
+    ``aliased_state=True`` also carries the modes the 2/3 rule removes, so
+    ``prob.sol``, calcN and the energy diagnostics cover the full array as
+    the reference's do (one slab, nx <= 4096; include/sw.h).
     """
     if dev not in ("gpu", "GPU", "GPU()"):
         raise _lib.LibSWError("libsw runs on the GPU only (dev='gpu')")
@@ -33,7 +36,7 @@ def Problem(dev="gpu", *, nx=128, ny=None, Lx=2 * np.pi, Ly=None, U=0.5, mu=1e-2
                     aliased_fraction=aliased_fraction, stepper=stepper, params=params,
                     use_filter=use_filter, filter_kw=stepper_kwargs, device=device,
                     check_nan=check_nan, T=T, nop_calcN=nop_calcN, unfused=unfused,
-                    **(decomposition or {}))
+                    aliased_state=aliased_state, **(decomposition or {}))
     return prob
 
 

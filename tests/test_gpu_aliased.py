@@ -1,0 +1,190 @@
+"""Aliased-state tracking (sw_config.aliased_state): the
+modes the 2/3 rule removes, carried as the reference carries them.
+
+The reference's 2LQG calcN! dealiases its input in place but returns N on
+every mode (swqg/TwoLayerQG.jl:152-182: rfft of the products, no dealias of
+N), and the IF/AB3 update writes E·dt·(…N…) into prob.sol there
+(utils/IFMAB3.jl:142-160), so between steps prob.sol holds aliased modes,
+which its energies (:230-252) count and the next calcN!/updatevars!
+discards.  With aliased_state = 1 libsw carries them too (one slab, 2LQG,
+nx <= 4096); the oracle keeps the full arrays, so every comparison here is
+over ALL modes of the full (nkr, nl) array, at the strongly nonlinear 64²
+cases of tests/sw_cases.py.
+"""
+import numpy as np
+import pytest
+
+import sw_cases
+import sw_oracle as O
+from juliaraytracingsw_amd import two_layer_qg as QG2
+from juliaraytracingsw_amd._lib import LibSWError
+
+pytestmark = pytest.mark.gpu
+QG_CASES = ["qg2_ifmab3", "qg2_ifmrk4", "qg2_fab3"]
+RTOL = 1e-10
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib_loaded(libsw):
+    return libsw
+
+
+def _setup(name, n=64):
+    p = sw_cases.case_params(name, n)
+    pr = sw_cases.oracle_problem(p)
+    pr.set_solution(sw_cases.initial_condition(p, pr.grid))
+    prob = sw_cases.libsw_problem(p, aliased_state=True)
+    prob.sol = pr.sol
+    return p, pr, prob
+
+
+def _aliased_mask(grid):
+    live = np.zeros((grid.nl, grid.nkr), bool)
+    d = grid.dealias(np.ones((1, grid.nl, grid.nkr), np.complex128))[0]
+    live[d != 0] = True
+    return ~live
+
+
+def _full_err(a, b):
+    return float(np.max(np.abs(a - b)) / np.max(np.abs(b)))
+
+
+@pytest.mark.parametrize("name", QG_CASES)
+def test_full_state_matches_the_reference_array(name):
+    """prob.sol after each of 12 steps equals the oracle's un-dealiased
+    post-step state on every mode, the aliased ones included (nonzero)."""
+    p, pr, prob = _setup(name)
+    mask = _aliased_mask(pr.grid)
+    for s in range(12):
+        pr.stepforward(1)
+        prob.stepforward(1)
+        got = prob.sol
+        assert _full_err(got, pr.sol) < RTOL, (s, _full_err(got, pr.sol))
+    amax = np.max(np.abs(pr.sol[:, mask]))
+    assert amax > 1e-6 * np.max(np.abs(pr.sol))  # the aliased modes are material
+    assert np.max(np.abs(got[:, mask] - pr.sol[:, mask])) <= RTOL * np.max(np.abs(pr.sol))
+    prob.close()
+
+
+@pytest.mark.parametrize("name,n,steps", [("qg2_ifmab3", 512, 6), ("qg2_ifmrk4", 1024, 3)])
+def test_full_state_larger_grids(name, n, steps):
+    """The same on one-line-per-block grids (512², 1024²: the aliased column
+    kernel's other block shape, aliased regions of 86k / 350k modes)."""
+    p, pr, prob = _setup(name, n)
+    pr.stepforward(steps)
+    prob.stepforward(steps)
+    got = prob.sol
+    assert _full_err(got, pr.sol) < RTOL
+    mask = _aliased_mask(pr.grid)
+    assert np.max(np.abs(pr.sol[:, mask])) > 0
+    prob.close()
+
+
+@pytest.mark.parametrize("name", QG_CASES)
+def test_energy_records_of_the_undealiased_state(name):
+    """The device energy records (swqg/TwoLayerDriver.jl:86-89) against the
+    oracle's energies of the UN-dealiased post-step state within 1e-10 — the
+    done-criterion of VERDICT r02 #8 (the default mode is compared with the
+    dealiased state in test_gpu_parity.py)."""
+    p, pr, prob = _setup(name)
+    freq, nsteps = 3, 12
+    KE = QG2.Diagnostic(QG2.kinetic_energy, prob, freq=freq, nsteps=nsteps)
+    PE = QG2.Diagnostic(QG2.potential_energy, prob, freq=freq, nsteps=nsteps)
+    expected, gap = [O.qg2_energies(pr.sol, pr.grid, pr.params)], 0.0
+    for s in range(1, nsteps + 1):
+        pr.stepforward(1)
+        if s % freq == 0:
+            full = O.qg2_energies(pr.sol, pr.grid, pr.params)
+            deal = O.qg2_energies(pr.grid.dealias(pr.sol.copy()), pr.grid, pr.params)
+            gap = max(gap, abs(full[1] / deal[1] - 1), max(abs(a / b - 1) for a, b in zip(full[0], deal[0])))
+            expected.append(full)
+    QG2.stepforward(prob, [KE, PE], nsteps)
+    assert KE.i == len(expected)
+    for i, ((k1, k2), pe) in enumerate(expected):
+        assert np.allclose(np.atleast_1d(KE.data[i]), [k1, k2], rtol=RTOL, atol=0), (i, KE.data[i], (k1, k2))
+        assert abs(PE.data[i] / pe - 1) < RTOL, (i, PE.data[i], pe)
+    print(f"[aliased] {name}: full-array vs dealiased energies differ by up to {gap:.2e} (relative)")
+    # the instantaneous diagnostics read the same full array
+    (k1, k2), pe = O.qg2_energies(pr.sol, pr.grid, pr.params)
+    assert abs(QG2.potential_energy(prob) / pe - 1) < RTOL
+    prob.close()
+
+
+@pytest.mark.parametrize("name", ["qg2_ifmab3", "qg2_ifmrk4"])
+def test_calcN_on_every_mode(name):
+    """sw_calcN returns N on the full array, as the reference's calcN!."""
+    p, pr, prob = _setup(name)
+    pr.stepforward(2)
+    prob.stepforward(2)
+    x = pr.sol.copy()
+    ref = pr.calcN(x.copy(), pr.grid, pr.params)
+    got = prob.calcN(x)
+    mask = _aliased_mask(pr.grid)
+    assert np.max(np.abs(ref[:, mask])) > 1e-3 * np.max(np.abs(ref))
+    assert _full_err(got, ref) < RTOL
+    prob.close()
+
+
+def test_checkpoint_carries_the_aliased_history():
+    """IFMAB3's AB3 combination at the aliased modes needs N of the two
+    previous steps there: a checkpoint/restart continues bitwise on every mode
+    (records included)."""
+    p, pr, prob = _setup("qg2_ifmab3")
+    prob.stepforward(7)
+    blob = prob.ctx.get_checkpoint()
+    prob.stepforward(5)
+    want = prob.sol
+    b = sw_cases.libsw_problem(p, aliased_state=True)
+    b.ctx.set_checkpoint(blob)
+    b.stepforward(5)
+    assert np.array_equal(b.sol, want)
+    assert np.max(np.abs(want[:, _aliased_mask(pr.grid)])) > 0
+    b.close()
+    prob.close()
+
+
+def test_updatevars_dealiases_the_state():
+    """updatevars! begins with dealias!(sol, grid) (swqg/TwoLayerQG.jl:115):
+    after it prob.sol has zeros at the aliased modes, as the reference's."""
+    p, pr, prob = _setup("qg2_ifmab3")
+    prob.stepforward(4)
+    mask = _aliased_mask(pr.grid)
+    assert np.max(np.abs(prob.sol[:, mask])) > 0
+    QG2.updatevars(prob)
+    assert np.max(np.abs(prob.sol[:, mask])) == 0
+    prob.close()
+
+
+def test_default_mode_unchanged():
+    """aliased_state off: live modes only, zeros elsewhere (the round-2
+    behaviour the other parity tests pin)."""
+    p = sw_cases.case_params("qg2_ifmab3", 64)
+    pr = sw_cases.oracle_problem(p)
+    pr.set_solution(sw_cases.initial_condition(p, pr.grid))
+    prob = sw_cases.libsw_problem(p)
+    prob.sol = pr.sol
+    prob.stepforward(5)
+    got = prob.sol
+    assert np.max(np.abs(got[:, _aliased_mask(pr.grid)])) == 0
+    prob.close()
+
+
+@pytest.mark.parametrize("bad", ["rsw", "frk4", "nx8192", "slabs"])
+def test_rejected_where_not_built(bad):
+    """Only where it is built: 2LQG, IFMAB3/IFMRK4/FilteredAB3, one slab, the
+    full-length row pass (nx <= 4096)."""
+    from juliaraytracingsw_amd import _lib
+
+    cfg = _lib.default_config()
+    cfg.model, cfg.stepper, cfg.nx, cfg.ny = _lib.SW_MODEL_QG2, _lib.STEPPERS["IFMAB3"], 64, 64
+    cfg.aliased_state = 1
+    if bad == "rsw":
+        cfg.model = _lib.SW_MODEL_RSW
+    elif bad == "frk4":
+        cfg.stepper = _lib.STEPPERS["FilteredRK4"]
+    elif bad == "nx8192":
+        cfg.nx, cfg.ny = 8192, 32
+    else:
+        cfg.nranks = cfg.local_slabs = 2
+    with pytest.raises(LibSWError, match="aliased_state"):
+        _lib.Context(cfg)

@@ -384,7 +384,9 @@ def test_energy_diagnostics_recorded(name):
     reference's also count the aliased modes the update has just written and
     the next calcN discards (relative 1e-12 (IFMAB3) to 1e-8 (IFMRK4) of the
     energy on this strongly nonlinear 64² case) — compared here against the
-    oracle's dealiased post-step state."""
+    oracle's dealiased post-step state; with sw_config.aliased_state libsw
+    carries those modes too and matches the un-dealiased energies
+    (tests/test_gpu_aliased.py)."""
     from juliaraytracingsw_amd import rotating_shallow_water as RSW, two_layer_qg as QG2
 
     rsw = name.startswith("rsw")
