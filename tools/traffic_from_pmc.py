@@ -10,7 +10,7 @@ import json
 import sys
 from collections import defaultdict
 
-SHORT = {"k_row": "row", "k_col_step_fab3_rsw": "col_step", "k_col_step": "col_step",
+SHORT = {"k_row": "row", "k_row_qg_h": "row", "k_row_rsw_h": "row", "k_col_step_fab3_rsw": "col_step", "k_col_step": "col_step",
          "k_col_inv": "col_inv", "k_col_fwd": "col_fwd", "k_step_elem": "update"}
 
 
