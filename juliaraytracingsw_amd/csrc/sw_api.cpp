@@ -1066,11 +1066,19 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
       HIPCHK(c, hipEventCreateWithFlags(&c->ev_rowc[i], hipEventDisableTiming));
     }
     // Pipelined by default across GPUs (RCCL over xGMI runs beside the column
-    // kernels).  With every slab in this process the "transposes" are copies
-    // through the same HBM the kernels stream, and splitting the column pass
-    // into per-field launches only costs (tools/overlap_check.py, DESIGN.md
-    // §6): sequential by default there.
-    c->overlap = c->dist && !c->hostx;
+    // kernels) where each per-(peer, field) message is >= 1 MiB; below that a
+    // transpose is latency-bound and the per-group schedule's 3 + 3 grouped
+    // send/recv calls per calcN cost more than they overlap, so the
+    // sequential schedule (one group per direction) runs there (e.g. the
+    // 2048² metric problem on 8 GPUs: 360 KB messages).  With every slab in
+    // this process the "transposes" are copies through the same HBM the
+    // kernels stream, and splitting the column pass into per-field launches
+    // only costs (tools/overlap_check.py): sequential there.
+    {
+      const Geom g0 = make_geom(k, P, 0);
+      const size_t msg = (size_t)g0.kcl * g0.nyl * sizeof(double2);
+      c->overlap = c->dist && !c->hostx && msg >= ((size_t)1 << 20);
+    }
     if (const char* e = std::getenv("SW_OVERLAP")) c->overlap = e[0] == '1';
   }
   if (c->dist && !c->hostx) {
