@@ -24,6 +24,8 @@ Extra keys on the same JSON line (never `value`):
   `ensemble` — the ensemble throughput of the same configuration on the N GPUs;
   `config5` — BASELINE config 5 (TwoLayerQG 8192² IFMRK4) decomposed over the
       N GPUs (one GPU at N = 1), steps/s (--no-config5 to skip);
+  `config4` — BASELINE config 4 (RSW 4096² FilteredAB3) decomposed over the N
+      GPUs (one GPU at N = 1), steps/s (--no-config4 to skip);
   `host_boundary` — one state download/upload through the C ABI over PCIe,
       and the rate with the driver's per-frame download;
   `cpu_baseline` — rank 0 at N = 1 only.
@@ -169,6 +171,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-config5", action="store_true")
     ap.add_argument("--config5-steps", type=int, default=20)
+    ap.add_argument("--no-config4", action="store_true")
+    ap.add_argument("--config4-steps", type=int, default=100)
     ap.add_argument("--mode", default="slab", choices=["ensemble", "slab"])
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_rsw2048_fab3.json"))
     ap.add_argument("--nutune", type=float, default=None,
@@ -344,21 +348,29 @@ def main():
         e.close()
         del e
 
-    # extra: BASELINE config 5, TwoLayerQG 8192² IFMRK4 over the N GPUs
-    config5 = None
-    if not args.no_config5 and not slab_error and (args.model, args.n, args.stepper) == ("rsw", 2048, "FilteredAB3"):
-        c5, _ = make_problem("qg2", 8192, "IFMRK4", local, decomposition())
-        t5 = timed(c5, 3, args.config5_steps, "config5")
-        s5 = c5.ctx.profile(3)
-        c5.close()
-        del c5
-        config5 = {"value": args.config5_steps / t5, "unit": "timesteps/s", "n_gpus": world,
-                   "steps": args.config5_steps, "ms_per_step": t5 / args.config5_steps * 1e3,
-                   "scaling": "strong" if world > 1 else None,
-                   "workload": "TwoLayerQG 8192^2 IFMRK4 fp64 (BASELINE config 5), "
-                               + (f"slab{world}" if world > 1 else "single-gpu"),
-                   "kernels": [{"name": s["name"], "avg_us": s["avg_ms"] * 1e3, "per_step": s["launches"] / 3}
-                               for s in s5]}
+    # extras: BASELINE configs 5 (TwoLayerQG 8192² IFMRK4) and 4 (RSW 4096²
+    # FilteredAB3), each one problem slab-decomposed over the N GPUs (one GPU
+    # at N = 1)
+    def extra_config(model, n, stepper, steps, warmup, label):
+        ex, _ = make_problem(model, n, stepper, local, decomposition())
+        te = timed(ex, warmup, steps, label)
+        sx = ex.ctx.profile(3)
+        ex.close()
+        del ex
+        return {"value": steps / te, "unit": "timesteps/s", "n_gpus": world, "steps": steps,
+                "ms_per_step": te / steps * 1e3, "scaling": "strong" if world > 1 else None,
+                "workload": f"{label} fp64, " + (f"slab{world}" if world > 1 else "single-gpu"),
+                "kernels": [{"name": s["name"], "avg_us": s["avg_ms"] * 1e3, "per_step": s["launches"] / 3}
+                            for s in sx]}
+
+    headline_cfg = (args.model, args.n, args.stepper) == ("rsw", 2048, "FilteredAB3")
+    config5 = config4 = None
+    if not args.no_config5 and not slab_error and headline_cfg:
+        config5 = extra_config("qg2", 8192, "IFMRK4", args.config5_steps, 3,
+                               "TwoLayerQG 8192^2 IFMRK4 (BASELINE config 5)")
+    if not args.no_config4 and not slab_error and headline_cfg:
+        config4 = extra_config("rsw", 4096, "FilteredAB3", args.config4_steps, 20,
+                               "RSW 4096^2 FilteredAB3 (BASELINE config 4)")
 
     if rank != 0:
         if dist is not None:
@@ -433,6 +445,7 @@ def main():
         "ensemble": ensemble,
         "slab_error": slab_error,
         "config5": config5,
+        "config4": config4,
         "cpu_baseline": cpu,
         # RSWDriver saves a frame every output_freq = floor(output_dt/dt) steps
         # (rsw/RSWDriver.jl:152, output_dt = 0.025/f): 81 steps at 2048²

@@ -15,7 +15,7 @@ if [ -n "$CHECK" ]; then
   done
 fi
 for r in $(seq $R); do for so in sweep_var/*.so; do n=$(basename $so .so)
-  LIBSW_PATH=$PWD/$so timeout -k 10 180 python bench.py --no-cpu-baseline --no-config5 --steps 2000 --warmup 200 "$@" \
+  LIBSW_PATH=$PWD/$so timeout -k 10 180 python bench.py --no-cpu-baseline --no-config5 --no-config4 --steps 2000 --warmup 200 "$@" \
     > gpurun_out/ab/$n.$r.json 2> gpurun_out/ab/$n.$r.err || { echo "$n failed"; exit 1; }
   echo "r$r $n $(python -c "import json; d=json.load(open('gpurun_out/ab/$n.$r.json')); print(round(d['value'],1), [(k['name'], round(k['avg_us'],1)) for k in d['kernels']])")"
 done; done

@@ -21,7 +21,7 @@ for c in $CONFIGS; do
   tag=${M}${N}_${S}
   X=""; [ -n "$NU" ] && X="--nutune $NU --cfltune $CF"
   timeout -k 10 300 python bench.py --model $M --grid $N --stepper $S --steps $B --warmup 50 --no-cpu-baseline \
-    --no-config5 $X > $O/bench_$tag.json 2> $O/bench_$tag.err || exit 1
+    --no-config5 --no-config4 $X > $O/bench_$tag.json 2> $O/bench_$tag.err || exit 1
   P="python tools/prof_step.py --model $M --grid $N --stepper $S --steps $K $X"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_$tag -o run -- $P > $O/run_$tag.json 2> $O/trace_$tag.err || exit 2
   cp $(find $O/trace_$tag -name '*kernel_stats.csv') $O/kernel_stats_$tag.csv || exit 3

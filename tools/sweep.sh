@@ -11,7 +11,7 @@ for so in sweep_var/*.so; do
     LIBSW_PATH=$PWD/$so timeout -k 10 300 python -m pytest tests/test_gpu_parity.py tests/test_gpu_slabs.py -q -x -k "rsw_fab3" \
       > gpurun_out/sweep/$n.test.log 2>&1 || { echo "$n TESTS FAILED"; tail -5 gpurun_out/sweep/$n.test.log; exit 1; }
   fi
-  SW_CHECK_NAN=${SW_CHECK_NAN:-1} LIBSW_PATH=$PWD/$so timeout -k 10 120 python bench.py --no-cpu-baseline --no-config5 --steps 100 --warmup 10 "$@" \
+  SW_CHECK_NAN=${SW_CHECK_NAN:-1} LIBSW_PATH=$PWD/$so timeout -k 10 120 python bench.py --no-cpu-baseline --no-config5 --no-config4 --steps 100 --warmup 10 "$@" \
     > gpurun_out/sweep/$n.json 2> gpurun_out/sweep/$n.err || { echo "$n failed rc=$?"; exit 1; }
   echo "$n $(python -c "import json,sys; d=json.load(open('gpurun_out/sweep/$n.json')); print(round(d['value'],1), [(k['name'], round(k['avg_us'],1)) for k in d['kernels']])")"
 done
