@@ -185,6 +185,17 @@ def main():
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))
+    # stdout carries exactly one line, the JSON result: everything else a
+    # library prints there (Gloo's connection report, HIP/RCCL notices) goes
+    # to stderr, the result through a duplicate of the original stdout
+    sys.stdout.flush()
+    result_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
+    def emit(obj):
+        result_out.write(json.dumps(obj) + "\n")
+        result_out.flush()
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -194,9 +205,8 @@ def main():
     parallelism = (f"slab{world}" if slab else f"ensemble{world}") if world > 1 else "single-gpu"
     if args.dry_run:
         if rank == 0:
-            print(json.dumps({"n_gpus": world, "parallelism": parallelism,
-                              "scaling": ("strong" if slab else "weak") if world > 1 else None,
-                              "rank0_of": world}))
+            emit({"n_gpus": world, "parallelism": parallelism,
+                  "scaling": ("strong" if slab else "weak") if world > 1 else None, "rank0_of": world})
         return
 
     import torch
@@ -454,7 +464,7 @@ def main():
                           "steps_per_s_with_state_download_every_81_steps":
                               81 / (81 * ms_per_step * 1e-3 + min(tg))},
     }
-    print(json.dumps(out))
+    emit(out)
     if dist is not None:
         dist.destroy_process_group()
 
