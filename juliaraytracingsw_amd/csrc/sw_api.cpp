@@ -443,6 +443,9 @@ const PipeSpec& pipe_spec(int model) {
                                {{0, -1, -1}, {1, 2, -1}, {3, 4, -1}}};
   // QG2: layer l -> Q_l, Ψ_l, Ψy_l; N_l <- ψx q_l, ψy q_l
   static const PipeSpec qg2 = {2, 2, {{0, 2, 4}, {1, 3, 5}}, {{0, 2, -1}, {1, 3, -1}}};
+  // RSW advective form (sw::MODEL_RSWA): U,Uy | V,Vy | H; N_u <- 0, N_v <- 1, N_η <- 2, 3
+  static const PipeSpec rswa = {3, 3, {{0, 3, -1}, {1, 4, -1}, {2, -1, -1}}, {{0, -1, -1}, {1, -1, -1}, {2, 3, -1}}};
+  if (model == sw::MODEL_RSWA) return rswa;
   // TY: k_col_inv groups and k_col_fwd nterms
   static const PipeSpec ty = {5, 4, {{0, 1, -1}, {2, 3, -1}, {4, 5, -1}, {6, -1, -1}, {7, 8, -1}},
                               {{0, 1, 2}, {3, -1, -1}, {4, 5, -1}, {6, -1, -1}}};
@@ -607,10 +610,10 @@ int calcN(sw_ctx* c, double2* Slab::*X, double2* Slab::*N, int op = -1, int stag
 // than the separate kernels.
 bool use_fused(const sw_ctx* c) {
   if (c->cfg.unfused || c->cfg.nop_calcN || c->cfg.model == SW_MODEL_TY || c->cfg.model == SW_MODEL_MLQG ||
-      c->cfg.stepper == SW_STEP_FILTERED_RK4)
+      c->cfg.stepper == SW_STEP_FILTERED_RK4 || c->kmodel == sw::MODEL_RSWA)
     return false;
   if (c->fuse_all) return true;
-  return c->cfg.model == SW_MODEL_RSW && c->cfg.stepper == SW_STEP_FILTERED_AB3;
+  return c->kmodel == SW_MODEL_RSW && c->cfg.stepper == SW_STEP_FILTERED_AB3;
 }
 
 // k_col_fwd + k_step_elem as one column pass (k_col_step<…, INV = false>: one
@@ -627,7 +630,7 @@ bool use_fused(const sw_ctx* c) {
 bool use_fwd_step(const sw_ctx* c) {
   if (c->fwd_step == 0 || c->cfg.unfused || c->cfg.nop_calcN || use_fused(c) || c->alias) return false;
   const int m = c->cfg.model, st = c->cfg.stepper;
-  const bool built = (m == SW_MODEL_RSW && (st == SW_STEP_IFMAB3 || st == SW_STEP_IFMRK4)) ||
+  const bool built = (c->kmodel == SW_MODEL_RSW && (st == SW_STEP_IFMAB3 || st == SW_STEP_IFMRK4)) ||
                      (m == SW_MODEL_QG2 && (st == SW_STEP_FILTERED_AB3 || st == SW_STEP_IFMAB3 ||
                                             st == SW_STEP_IFMRK4));
   if (!built) return false;
@@ -1023,8 +1026,6 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
     return fail(c, SW_E_INVALID, "nx or ny: transform length not built into this library (one-length build)");
   if (!(k.aliased_fraction >= 0 && k.aliased_fraction < 1))
     return fail(c, SW_E_INVALID, "aliased_fraction must be in [0,1)");
-  if (k.aliased_fraction == 0 && k.model == SW_MODEL_RSW)
-    return fail(c, SW_E_INVALID, "RSW needs aliased_fraction > 0 (its calcN uses the dealiased vorticity form)");
   if (k.filter_order < 0) return fail(c, SW_E_INVALID, "filter_order must be >= 0");
   if (k.precision != SW_PREC_F64 && k.precision != SW_PREC_F32)
     return fail(c, SW_E_INVALID, "precision must be SW_PREC_F64 or SW_PREC_F32");
@@ -1124,11 +1125,19 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
 
   c->nf = k.model == SW_MODEL_RSW ? 3 : (k.model == SW_MODEL_TY ? 4 : 2);
   c->kmodel = k.model == SW_MODEL_MLQG ? SW_MODEL_QG2 : k.model;  // MLQG runs the 2LQG kernels
+  // RSW: the vorticity form of the calcN is exact on the live modes of the
+  // 2/3 rule; with aliased_fraction = 0 (no dealiased band) the reference's
+  // advective form runs instead (sw::MODEL_RSWA; SW_RSW_ADV=1 forces it)
+  if (k.model == SW_MODEL_RSW) {
+    bool adv = k.aliased_fraction == 0;
+    if (const char* e = std::getenv("SW_RSW_ADV")) adv = adv || e[0] == '1';
+    if (adv) c->kmodel = sw::MODEL_RSWA;
+  }
   // mixed fields per calcN: RSW U,V,H,Uy in / P,K,ζu,Q,vη out;
   // QG2 Q,Ψ,Ψy per layer in / ψx q, ψy q per layer out; TY ζ,ψ,ût,∂y ut,
   // uc,∂y uc,vc,pc,∂y pc in / 7 combined product spectra out (k_row)
-  c->ninv = k.model == SW_MODEL_RSW ? 4 : (k.model == SW_MODEL_TY ? 9 : 6);
-  c->nfwd = k.model == SW_MODEL_RSW ? 5 : (k.model == SW_MODEL_TY ? 7 : 4);
+  c->ninv = c->kmodel == sw::MODEL_RSWA ? 5 : k.model == SW_MODEL_RSW ? 4 : (k.model == SW_MODEL_TY ? 9 : 6);
+  c->nfwd = c->kmodel == sw::MODEL_RSWA ? 4 : k.model == SW_MODEL_RSW ? 5 : (k.model == SW_MODEL_TY ? 7 : 4);
 
   int rc;
   for (Slab& s : c->sl) {

@@ -26,6 +26,9 @@ namespace sw {
 // MODEL_MLQG (GeophysicalFlows MultiLayerQG, 2 layers) runs the MODEL_QG2
 // kernels; Phys::model selects its streamfunction and linear terms at run time
 enum { MODEL_RSW = 0, MODEL_QG2 = 1, MODEL_TY = 2, MODEL_MLQG = 3 };
+// kernel family only: RSW's calcN in the reference's advective form
+// (aliased_fraction = 0, where the vorticity form of MODEL_RSW is not exact)
+enum { MODEL_RSWA = 4 };
 enum { ST_FAB3 = 0, ST_IFMAB3 = 1, ST_IFMRK4 = 2, ST_ETDRK4 = 3, ST_FRK4 = 4 };
 
 // Grid geometry of one slab in the layouts of DESIGN.md §2 and §6.

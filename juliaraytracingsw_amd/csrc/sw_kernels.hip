@@ -200,7 +200,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   // loads are unconditional from a clamped in-bounds address, then selected:
   // a branch around each load would serialise them (one vmcnt(0) per element)
   const int krc = live ? krl : 0;
-  if constexpr (MODEL == MODEL_RSW) {
+  if constexpr (MODEL == MODEL_RSW || MODEL == MODEL_RSWA) {
     const double2* Xf = X + (long long)grp * g.cfield + (long long)krc * g.LrP;
     double2 x[8];
 #pragma unroll
@@ -213,11 +213,11 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     }
     fft_line<LOG2N, +1>(v, c.t, tws, line);
     store(grp);
-    if (grp == 0) {  // ∂y u: Uy
+    if (grp == 0 || (MODEL == MODEL_RSWA && grp == 1)) {  // ∂y u: Uy (advective form: and ∂y v: Vy)
 #pragma unroll
       for (int s = 0; s < 8; ++s) v[s] = cmul_i(x[s], lwav(g, c.t + s * NT) * scale);
       fft_line<LOG2N, +1>(v, c.t, tws, line);
-      store(3);
+      store(3 + grp);
     }
   } else if constexpr (MODEL == MODEL_TY) {
     // thomasyamada/ThomasYamada.jl:129-262.  Group → (input field, outputs):
@@ -701,6 +701,37 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
       const int k = c.t + s * Bk::NT;
       if (RowIdx<LOG2N>::fwd_any(g, s) && k < g.kc) Mo[4 * MF + ri.ofwd(g, s)] = v[s];
     }
+  } else if constexpr (MODEL == MODEL_RSWA) {
+    // rsw/RotatingShallowWater.jl:140-230 as written (advective form, the
+    // reference's products on every mode; aliased_fraction = 0):
+    //   N_u = -(u ux)^ - (v uy)^,  N_v = -(v vy)^ - (u vx)^,  N_η = -ik (uη)^ - il (vη)^
+    // Inputs (k_col_inv): 0 U, 1 V, 2 H, 3 Uy, 4 Vy.  Outputs (x-spectral):
+    //   0 (u ux + v uy)^, 1 (u vx + v vy)^ -> N_u, N_v = -F_y(…)
+    //   2 Q = -ik (uη)^, 3 (vη)^          -> N_η = F_y(Q) - il F_y((vη)^)
+    const double2 *U = Mi, *V = Mi + MF, *H = Mi + 2 * MF, *Uy = Mi + 3 * MF, *Vy = Mi + 4 * MF;
+    double2 uv[8], pr[8];
+    load_pair<LOG2N>(uv, ri, g, U, V, false);  // u + i v
+    fft_line<LOG2N, +1>(uv, c.t, tws, line);
+    load_pair<LOG2N>(v, ri, g, U, V, true);  // ux + i vx
+    fft_line<LOG2N, +1>(v, c.t, tws, line);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) pr[s] = make_double2(uv[s].x * v[s].x, uv[s].x * v[s].y);
+    load_pair<LOG2N>(v, ri, g, Uy, Vy, false);  // uy + i vy
+    fft_line<LOG2N, +1>(v, c.t, tws, line);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) pr[s] = make_double2(pr[s].x + uv[s].y * v[s].x, pr[s].y + uv[s].y * v[s].y);
+    fft_line<LOG2N, -1>(pr, c.t, tws, line);
+    store_pair<LOG2N>(pr, ri, g, line, Mo, Mo + MF);
+    load_pair<LOG2N>(v, ri, g, H, nullptr, false);  // η
+    fft_line<LOG2N, +1>(v, c.t, tws, line);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) v[s] = make_double2(uv[s].x * v[s].x, uv[s].y * v[s].x);  // uη + i vη
+    fft_line<LOG2N, -1>(v, c.t, tws, line);
+    split_pair<LOG2N>(v, c.t, g, line, [&](int k, int s, double2 a, double2 b) {
+      const int o = ri.ofwd(g, s);
+      Mo[2 * MF + o] = cmul_i(a, -(k * g.mk));
+      Mo[3 * MF + o] = b;
+    });
   } else if constexpr (MODEL == MODEL_TY) {
     // thomasyamada/ThomasYamada.jl:129-262.  Inputs (k_col_inv): 0 ζ, 1 ψ,
     // 2 ût, 3 ∂y ut, 4 uc, 5 ∂y uc, 6 vc, 7 pc, 8 ∂y pc.  Physical fields in
@@ -1095,6 +1126,10 @@ __device__ __forceinline__ NTerms nterms(int f) {
     if (f == 0) return NTerms{0, MUL_ONE, -1, MUL_ONE, -1, MUL_ONE};
     if (f == 1) return NTerms{1, MUL_NIL, 2, MUL_NEG, -1, MUL_ONE};
     return NTerms{3, MUL_ONE, 4, MUL_NIL, -1, MUL_ONE};
+  } else if constexpr (MODEL == MODEL_RSWA) {
+    if (f == 0) return NTerms{0, MUL_NEG, -1, MUL_ONE, -1, MUL_ONE};
+    if (f == 1) return NTerms{1, MUL_NEG, -1, MUL_ONE, -1, MUL_ONE};
+    return NTerms{2, MUL_ONE, 3, MUL_NIL, -1, MUL_ONE};
   } else if constexpr (MODEL == MODEL_TY) {
     if (f == 0) return NTerms{0, MUL_ONE, 1, MUL_L, 2, MUL_L2};
     if (f == 1) return NTerms{3, MUL_ONE, -1, MUL_ONE, -1, MUL_ONE};
@@ -1118,7 +1153,7 @@ __device__ __forceinline__ double2 apply_mul(double2 a, int mul, double k, doubl
 }
 template <int MODEL>
 constexpr int model_nf() {
-  return MODEL == MODEL_RSW ? 3 : (MODEL == MODEL_TY ? 4 : 2);
+  return (MODEL == MODEL_RSW || MODEL == MODEL_RSWA) ? 3 : (MODEL == MODEL_TY ? 4 : 2);
 }
 
 template <int MODEL, int LOG2N>
@@ -2422,6 +2457,8 @@ void LenOps<L>::col_inv(int model, const Geom& g, const Phys& p, const double2* 
   const dim3 grid(col_blocks<L>(g), ng);
   if (model == MODEL_RSW)
     hipLaunchKernelGGL((k_col_inv<MODEL_RSW, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
+  else if (model == MODEL_RSWA)
+    hipLaunchKernelGGL((k_col_inv<MODEL_RSWA, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
   else if (model == MODEL_TY)
     hipLaunchKernelGGL((k_col_inv<MODEL_TY, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
   else if (g0 == 0 && ng == 2 && Blk<L>::NB == 1 && g.kcl % 64 == 0 &&
@@ -2449,9 +2486,14 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
     else
       hipLaunchKernelGGL((k_row<MODEL_RSW, L>), dim3(nrows / BR::NB), dim3(BR::THREADS), sh_rsw, s, g, p, Mi, Mo,
                          tw, y0, nullptr);
-  } else if (model == MODEL_TY)
+  } else if (model == MODEL_TY) {
     hipLaunchKernelGGL((k_row<MODEL_TY, L>), dim3(nrows / BT::NB), dim3(BT::THREADS), sh_ty, s, g, p, Mi, Mo, tw, y0,
                        nullptr);
+  } else if (model == MODEL_RSWA) {
+    using BA = BlkRow<MODEL_RSWA, L>;
+    hipLaunchKernelGGL((k_row<MODEL_RSWA, L>), dim3(nrows / BA::NB), dim3(BA::THREADS),
+                       FftPlan<L>::LDS * BA::NB * sizeof(double2), s, g, p, Mi, Mo, tw, y0, nullptr);
+  }
   else if constexpr (qg_row_half<L>())
     hipLaunchKernelGGL((k_row_qg_h<L>), dim3(nrows), dim3(RowH<L>::NTH), FftPlan<L - 1>::LDS * sizeof(double2), s, g,
                        p, Mi, Mo, tw, y0);  // (no aliased output: row_alias_built)
@@ -2477,6 +2519,9 @@ void LenOps<L>::col_fwd(int model, const Geom& g, const Phys& p, const double2* 
   const dim3 grid(col_blocks<L>(g), nfl);
   if (model == MODEL_RSW)
     hipLaunchKernelGGL((k_col_fwd<MODEL_RSW, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, Mf, N, X,
+                       tw, f0);
+  else if (model == MODEL_RSWA)
+    hipLaunchKernelGGL((k_col_fwd<MODEL_RSWA, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, Mf, N, X,
                        tw, f0);
   else if (model == MODEL_TY)
     hipLaunchKernelGGL((k_col_fwd<MODEL_TY, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, Mf, N, X,
@@ -2580,8 +2625,8 @@ bool length_built(int log2n) {
 }
 
 // number of column-pass groups per launch unit: col_inv groups, col_fwd fields
-int col_inv_groups(int model) { return model == MODEL_RSW ? 3 : (model == MODEL_TY ? 5 : 2); }
-int col_fields(int model) { return model == MODEL_RSW ? 3 : (model == MODEL_TY ? 4 : 2); }
+int col_inv_groups(int model) { return (model == MODEL_RSW || model == MODEL_RSWA) ? 3 : (model == MODEL_TY ? 5 : 2); }
+int col_fields(int model) { return (model == MODEL_RSW || model == MODEL_RSWA) ? 3 : (model == MODEL_TY ? 4 : 2); }
 
 void launch_col_inv(int model, const Geom& g, const Phys& p, const double2* X, double2* Minv,
                     const double2* tw_y, hipStream_t s, int g0, int ng) {
@@ -2614,7 +2659,8 @@ int row_lines_per_block(int model, int log2nx) {
   int nb = 1;
   by_len(log2nx, [&](auto L) {
     constexpr int l = decltype(L)::value;
-    nb = model == MODEL_RSW ? (rsw_row_half<l>() ? 1 : BlkRow<MODEL_RSW, l>::NB)
+    nb = model == MODEL_RSWA ? BlkRow<MODEL_RSWA, l>::NB
+       : model == MODEL_RSW ? (rsw_row_half<l>() ? 1 : BlkRow<MODEL_RSW, l>::NB)
                             : (model == MODEL_TY ? BlkRow<MODEL_TY, l>::NB
                                                  : (qg_row_half<l>() ? 1 : BlkRow<MODEL_QG2, l>::NB));
   });

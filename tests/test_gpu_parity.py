@@ -304,8 +304,6 @@ def test_invalid_config_fails_loudly():
 
     with pytest.raises(LibSWError):
         RSW.Problem("gpu", nx=96)  # not a power of two
-    with pytest.raises(LibSWError):
-        RSW.Problem("gpu", nx=64, aliased_fraction=0.0)
     for bad in (dict(nx=16384), dict(nx=16), dict(nx=64, ny=24), dict(nx=64, aliased_fraction=1.0)):
         with pytest.raises(LibSWError):  # outside [32, 8192], not a power of two, no live modes
             RSW.Problem("gpu", **bad)
