@@ -594,7 +594,8 @@ int calcN(sw_ctx* c, double2* Slab::*X, double2* Slab::*N, int op = -1, int stag
   if (c->alias)  // N at the aliased modes (the reference's calcN! writes them: swqg/TwoLayerQG.jl:171,179)
     for (Slab& s : c->sl)
       for (int r = 0; r < 2; ++r)
-        sw::launch_col_fwd_alias(s.g, c->ga[r], r, c->p, s.mfc, s.a_mrow, s.a_nbuf[r], c->tw_y, c->stream);
+        sw::launch_col_fwd_alias(c->kmodel, s.g, c->ga[r], r, c->p, s.mfc, s.a_mrow, s.a_nbuf[r], c->tw_y,
+                                 c->stream);
   return 0;
 }
 
@@ -780,7 +781,9 @@ int run_stage(sw_ctx* c, int op, int stage, double2* Slab::*X) {
 // sums after the ncols live ones (a full-array parsevalsum, in a fixed order);
 // returns the column count
 int alias_energy_cols(sw_ctx* c, bool post_step_state, int ncols) {
-  if (!c->alias || !post_step_state) return ncols;
+  // 2LQG energies read prob.sol (the post-step state); RSW's read vars.uh,
+  // the dealiased calcN input (rsw/RotatingShallowWater.jl:323-333)
+  if (!c->alias || !post_step_state || c->cfg.model != SW_MODEL_QG2) return ncols;
   for (int r = 0; r < 2; ++r) {
     sw::launch_energy_cols(c->cfg.model, c->ga[r], c->p, c->sl[0].a_sol[r], c->ecols + SW_NSUM * (size_t)ncols,
                            c->stream);
@@ -1030,12 +1033,12 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   if (k.precision != SW_PREC_F64 && k.precision != SW_PREC_F32)
     return fail(c, SW_E_INVALID, "precision must be SW_PREC_F64 or SW_PREC_F32");
   if (k.aliased_state) {
-    if (k.model != SW_MODEL_QG2 ||
+    if ((k.model != SW_MODEL_QG2 && k.model != SW_MODEL_RSW) ||
         (k.stepper != SW_STEP_IFMAB3 && k.stepper != SW_STEP_IFMRK4 && k.stepper != SW_STEP_FILTERED_AB3))
-      return fail(c, SW_E_INVALID, "aliased_state: 2LQG with IFMAB3, IFMRK4 or FilteredAB3");
+      return fail(c, SW_E_INVALID, "aliased_state: RSW or 2LQG with IFMAB3, IFMRK4 or FilteredAB3");
     if (k.nranks > 1) return fail(c, SW_E_INVALID, "aliased_state: one slab (nranks = 1)");
-    if (!sw::row_alias_built(SW_MODEL_QG2, ilog2(k.nx)))
-      return fail(c, SW_E_INVALID, "aliased_state: nx <= 4096 (the full-length 2LQG row pass)");
+    if (!sw::row_alias_built(k.model == SW_MODEL_RSW ? sw::MODEL_RSWA : SW_MODEL_QG2, ilog2(k.nx)))
+      return fail(c, SW_E_INVALID, "aliased_state: 2LQG nx <= 4096 (the full-length 2LQG row pass)");
   }
   const int P = k.nranks;
   if (!pow2(P) || k.ny / P < 32)
@@ -1129,7 +1132,8 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   // 2/3 rule; with aliased_fraction = 0 (no dealiased band) the reference's
   // advective form runs instead (sw::MODEL_RSWA; SW_RSW_ADV=1 forces it)
   if (k.model == SW_MODEL_RSW) {
-    bool adv = k.aliased_fraction == 0;
+    // the aliased modes need the reference's own products (aliased_state)
+    bool adv = k.aliased_fraction == 0 || k.aliased_state;
     if (const char* e = std::getenv("SW_RSW_ADV")) adv = adv || e[0] == '1';
     if (adv) c->kmodel = sw::MODEL_RSWA;
   }

@@ -439,15 +439,17 @@ void launch_col_inv(int model, const Geom& g, const Phys& p, const double2* X, d
                     const double2* tw_y, hipStream_t s, int g0 = 0, int ng = -1);
 // local rows [y0, y0 + nrows) (nrows < 0: to the last); nrows a multiple of
 // row_lines_per_block (and of 4, the mixed tiles' height)
-// Ma (2LQG, one slab, lines up to 4096): also the x-spectra k in [kc, nx/2] of
-// the four forward fields, [field][k - kc][y] (the aliased-state tracking)
+// Ma (2LQG on lines up to 4096, or RSW's advective form; one slab): also the
+// x-spectra k in [kc, nx/2] of the forward fields, [field][k - kc][y] (the
+// aliased-state tracking)
 void launch_row(int model, const Geom& g, const Phys& p, const double2* Minv, double2* Mfwd,
                 const double2* tw_x, hipStream_t s, int y0 = 0, int nrows = -1, double2* Ma = nullptr);
 bool row_alias_built(int model, int log2nx);
-// 2LQG N at the aliased modes of region ga (sw_api.cpp alias_geom): region 0
-// the columns kr >= kc from the row pass's Ma, region 1 the aliased rows of
-// the live columns from the forward mixed fields Mfwd; N compact in ga
-void launch_col_fwd_alias(const Geom& g, const Geom& ga, int region, const Phys& p, const double2* Mfwd,
+// N at the aliased modes of region ga (sw_api.cpp alias_geom; model QG2 or
+// RSWA): region 0 the columns kr >= kc from the row pass's Ma, region 1 the
+// aliased rows of the live columns from the forward mixed fields Mfwd; N
+// compact in ga
+void launch_col_fwd_alias(int model, const Geom& g, const Geom& ga, int region, const Phys& p, const double2* Mfwd,
                           const double2* Ma, double2* N, const double2* tw_y, hipStream_t s);
 // compact modes of ga <-> the full (nkr, nl, nf) array (only those modes)
 void launch_scatter_modes(int nf, const Geom& ga, const double2* compact, double2* full, hipStream_t s);
@@ -487,8 +489,8 @@ struct LenOps {
                       hipStream_t s, int g0, int ng);
   static void row(int model, const Geom& g, const Phys& p, const double2* Mi, double2* Mo, const double2* tw,
                   hipStream_t s, int y0, int nrows, double2* Ma);
-  static void col_fwd_alias(const Geom& g, const Geom& ga, int region, const Phys& p, const double2* Mf,
-                            const double2* Ma, double2* N, const double2* tw, hipStream_t s);
+  static void col_fwd_alias(int model, const Geom& g, const Geom& ga, int region, const Phys& p,
+                            const double2* Mf, const double2* Ma, double2* N, const double2* tw, hipStream_t s);
   static void col_fwd(int model, const Geom& g, const Phys& p, const double2* Mf, double2* N, const double2* X,
                       const double2* tw, hipStream_t s, int f0, int nfl);
   static void col_step(int model, int op, const Geom& g, const Phys& p, const StepPtrs& a, const double2* Mf,

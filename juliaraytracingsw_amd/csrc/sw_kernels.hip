@@ -600,7 +600,7 @@ __device__ __forceinline__ void fft_pair(double2 (&w)[2][8], int t, const Twiddl
 // After split_pair (LDS still holds Z): the aliased x-spectra kc <= k <= nx/2
 // of the pair, A[k] and B[k], into [k - kc][y] of A and B (aliased-state
 // tracking, sw_config.aliased_state)
-template <int LOG2N>
+template <int LOG2N, bool NIK_A = false>
 __device__ __forceinline__ void store_alias_pair(const double2 (&v)[8], int t, const Geom& g, const double2* line,
                                                  double2* __restrict__ A, double2* __restrict__ B, int y) {
   constexpr int N = 1 << LOG2N, NT = N / 8;
@@ -611,7 +611,8 @@ __device__ __forceinline__ void store_alias_pair(const double2 (&v)[8], int t, c
       const double2 zk = v[s];
       const double2 zn = line[LP<LOG2N>((N - k) & (N - 1))];
       const long long o = (long long)(k - g.kc) * g.ny + y;
-      A[o] = make_double2(0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y));
+      const double2 a = make_double2(0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y));
+      A[o] = NIK_A ? cmul_i(a, -(k * g.mk)) : a;  // as the live outputs: Q = -ik (uη)^ (RSW)
       B[o] = make_double2(0.5 * (zk.y + zn.y), -0.5 * (zk.x - zn.x));
     }
   }
@@ -722,6 +723,8 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
     for (int s = 0; s < 8; ++s) pr[s] = make_double2(pr[s].x + uv[s].y * v[s].x, pr[s].y + uv[s].y * v[s].y);
     fft_line<LOG2N, -1>(pr, c.t, tws, line);
     store_pair<LOG2N>(pr, ri, g, line, Mo, Mo + MF);
+    const long long MA = (long long)(g.nkr - g.kc) * g.ny;  // aliased columns × rows per field
+    if constexpr (ALIAS) store_alias_pair<LOG2N>(pr, c.t, g, line, Ma, Ma + MA, y);
     load_pair<LOG2N>(v, ri, g, H, nullptr, false);  // η
     fft_line<LOG2N, +1>(v, c.t, tws, line);
 #pragma unroll
@@ -732,6 +735,7 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
       Mo[2 * MF + o] = cmul_i(a, -(k * g.mk));
       Mo[3 * MF + o] = b;
     });
+    if constexpr (ALIAS) store_alias_pair<LOG2N, true>(v, c.t, g, line, Ma + 2 * MA, Ma + 3 * MA, y);
   } else if constexpr (MODEL == MODEL_TY) {
     // thomasyamada/ThomasYamada.jl:129-262.  Inputs (k_col_inv): 0 ζ, 1 ψ,
     // 2 ût, 3 ∂y ut, 4 uc, 5 ∂y uc, 6 vc, 7 pc, 8 ∂y pc.  Physical fields in
@@ -1245,13 +1249,15 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   }
 }
 
-// 2LQG N = -il F(A_l) + ik F(B_l) (swqg/TwoLayerQG.jl:171,179) at the aliased
-// modes of region ga (aliased-state tracking, one slab; sw_api.cpp
-// alias_geom): region 0 = the columns kr in [kc, nx/2] (A, B from the row
-// pass's aliased output Ma, [field][kr - kc][y]), region 1 = the rows l in the
-// 2/3-rule band of the live columns (A, B from the forward mixed fields, as
-// k_col_fwd reads them).  The y-transforms and multipliers are k_col_fwd's.
-template <int LOG2N>
+// N at the aliased modes of region ga (aliased-state tracking, one slab;
+// sw_api.cpp alias_geom) with k_col_fwd's y-transforms and multipliers
+// (nterms): 2LQG N_l = -il F(A_l) + ik F(B_l) (swqg/TwoLayerQG.jl:171,179),
+// RSW in the advective form (MODEL_RSWA, rsw/RotatingShallowWater.jl:140-230,
+// exact on every mode).  Region 0 = the columns kr in [kc, nx/2] (row outputs
+// from the row pass's aliased output Ma, [field][kr - kc][y]); region 1 = the
+// rows l in the 2/3-rule band of the live columns (the forward mixed fields,
+// as k_col_fwd reads them).  grid: (columns, output fields).
+template <int MODEL, int LOG2N>
 static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     k_col_fwd_alias(Geom g, Geom ga, int region, Phys p, const double2* __restrict__ Mf,
                     const double2* __restrict__ Ma, double2* __restrict__ N, const double2* __restrict__ tw) {
@@ -1260,7 +1266,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   extern __shared__ double2 smem[];
   const LineCtx c = line_ctx<LOG2N>();
   const int col = blockIdx.x * B::NB + c.ln;  // column of the region
-  const int layer = blockIdx.y;
+  const int f = blockIdx.y;                   // output field
   const bool live = col < ga.kcn;
   const int colA = live ? col : 0;
   double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
@@ -1269,24 +1275,27 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   const double k = (ga.kr0 + colA) * g.mk;
   const long long MA = (long long)(g.nkr - g.kc) * g.ny;
   double2 v[8], acc[8];
-  auto load_col = [&](int f) {
+  auto load_col = [&](int fi) {
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       const int m = c.t + s * NT;
-      const double2 t = region == 0 ? Ma[f * MA + (long long)colA * g.ny + m] : Mf[f * g.mfield + midc(g, colA, m)];
+      const double2 t = region == 0 ? Ma[fi * MA + (long long)colA * g.ny + m] : Mf[fi * g.mfield + midc(g, colA, m)];
       v[s] = live ? t : zero2();
     }
   };
-  load_col(layer);
+  const NTerms nt = nterms<MODEL>(f);
+  load_col(nt.fa);
   fft_line<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
-  for (int s = 0; s < 8; ++s) acc[s] = apply_mul(v[s], MUL_NIL, k, lwav(g, c.t + s * NT));
-  load_col(2 + layer);
-  fft_line<LOG2N, -1>(v, c.t, tws, line);
+  for (int s = 0; s < 8; ++s) acc[s] = apply_mul(v[s], nt.ma, k, lwav(g, c.t + s * NT));
+  if (nt.fb >= 0) {
+    load_col(nt.fb);
+    fft_line<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
-  for (int s = 0; s < 8; ++s) acc[s] = cadd(acc[s], apply_mul(v[s], MUL_PIK, k, lwav(g, c.t + s * NT)));
+    for (int s = 0; s < 8; ++s) acc[s] = cadd(acc[s], apply_mul(v[s], nt.mb, k, lwav(g, c.t + s * NT)));
+  }
   if (live) {
-    double2* Nf = N + (long long)layer * ga.cfield + (long long)col * ga.LrP;
+    double2* Nf = N + (long long)f * ga.cfield + (long long)col * ga.LrP;
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       const int j = compact_of(ga, c.t + s * NT);
@@ -2491,8 +2500,12 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
                        nullptr);
   } else if (model == MODEL_RSWA) {
     using BA = BlkRow<MODEL_RSWA, L>;
-    hipLaunchKernelGGL((k_row<MODEL_RSWA, L>), dim3(nrows / BA::NB), dim3(BA::THREADS),
-                       FftPlan<L>::LDS * BA::NB * sizeof(double2), s, g, p, Mi, Mo, tw, y0, nullptr);
+    if (Ma)
+      hipLaunchKernelGGL((k_row<MODEL_RSWA, L, true>), dim3(nrows / BA::NB), dim3(BA::THREADS),
+                         FftPlan<L>::LDS * BA::NB * sizeof(double2), s, g, p, Mi, Mo, tw, y0, Ma);
+    else
+      hipLaunchKernelGGL((k_row<MODEL_RSWA, L>), dim3(nrows / BA::NB), dim3(BA::THREADS),
+                         FftPlan<L>::LDS * BA::NB * sizeof(double2), s, g, p, Mi, Mo, tw, y0, nullptr);
   }
   else if constexpr (qg_row_half<L>())
     hipLaunchKernelGGL((k_row_qg_h<L>), dim3(nrows), dim3(RowH<L>::NTH), FftPlan<L - 1>::LDS * sizeof(double2), s, g,
@@ -2506,11 +2519,15 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
 }
 
 template <int L>
-void LenOps<L>::col_fwd_alias(const Geom& g, const Geom& ga, int region, const Phys& p, const double2* Mf,
-                              const double2* Ma, double2* N, const double2* tw, hipStream_t s) {
-  const dim3 grid((ga.kcn + Blk<L>::NB - 1) / Blk<L>::NB, 2);
-  hipLaunchKernelGGL((k_col_fwd_alias<L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, ga, region, p, Mf, Ma,
-                     N, tw);
+void LenOps<L>::col_fwd_alias(int model, const Geom& g, const Geom& ga, int region, const Phys& p,
+                              const double2* Mf, const double2* Ma, double2* N, const double2* tw, hipStream_t s) {
+  const int nb = (ga.kcn + Blk<L>::NB - 1) / Blk<L>::NB;
+  if (model == MODEL_RSWA)
+    hipLaunchKernelGGL((k_col_fwd_alias<MODEL_RSWA, L>), dim3(nb, 3), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g,
+                       ga, region, p, Mf, Ma, N, tw);
+  else
+    hipLaunchKernelGGL((k_col_fwd_alias<MODEL_QG2, L>), dim3(nb, 2), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g,
+                       ga, region, p, Mf, Ma, N, tw);
 }
 
 template <int L>
@@ -2639,13 +2656,17 @@ void launch_row(int model, const Geom& g, const Phys& p, const double2* Minv, do
 }
 bool row_alias_built(int model, int log2nx) {
   bool ok = false;
-  by_len(log2nx, [&](auto L) { ok = model == MODEL_QG2 && !qg_row_half<decltype(L)::value>(); });
+  by_len(log2nx, [&](auto L) {
+    ok = model == MODEL_RSWA || (model == MODEL_QG2 && !qg_row_half<decltype(L)::value>());
+  });
   return ok;
 }
-void launch_col_fwd_alias(const Geom& g, const Geom& ga, int region, const Phys& p, const double2* Mfwd,
+void launch_col_fwd_alias(int model, const Geom& g, const Geom& ga, int region, const Phys& p, const double2* Mfwd,
                           const double2* Ma, double2* N, const double2* tw_y, hipStream_t s) {
   if (ga.kcn <= 0) return;
-  by_len(g.log2ny, [&](auto L) { LenOps<decltype(L)::value>::col_fwd_alias(g, ga, region, p, Mfwd, Ma, N, tw_y, s); });
+  by_len(g.log2ny, [&](auto L) {
+    LenOps<decltype(L)::value>::col_fwd_alias(model, g, ga, region, p, Mfwd, Ma, N, tw_y, s);
+  });
 }
 void launch_scatter_modes(int nf, const Geom& ga, const double2* cmp, double2* full, hipStream_t s) {
   if (ga.cfield <= 0 || ga.kcn <= 0) return;

@@ -14,7 +14,7 @@ from .problem import Diagnostic, Problem as _Problem, increment, stepforward  # 
 def Problem(dev="gpu", *, nx=128, ny=None, Lx=2 * np.pi, Ly=None, nu=1.0e-16, nnu=4, f=1.0, Cg=1.0,
             stepper="IFMAB3", dt=5e-2, aliased_fraction=1 / 3, T=np.float64, use_filter=False,
             device=0, check_nan=True, nop_calcN=False, unfused=False,
-            decomposition=None, **stepper_kwargs):
+            decomposition=None, aliased_state=False, **stepper_kwargs):
     """``RotatingShallowWater.Problem(dev; nx, ny, Lx, Ly, ν, nν, f, Cg, stepper,
     dt, aliased_fraction, T, use_filter, stepper_kwargs...)`` (:70-99).
 
@@ -31,7 +31,7 @@ def Problem(dev="gpu", *, nx=128, ny=None, Lx=2 * np.pi, Ly=None, nu=1.0e-16, nn
                     aliased_fraction=aliased_fraction, stepper=stepper, params=params,
                     use_filter=use_filter, filter_kw=stepper_kwargs, device=device,
                     check_nan=check_nan, T=T, nop_calcN=nop_calcN, unfused=unfused,
-                    **(decomposition or {}))
+                    **(decomposition or {}), aliased_state=aliased_state)
     prob.params["Cg2"] = float(Cg) ** 2
     return prob
 

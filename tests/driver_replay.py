@@ -106,7 +106,7 @@ class Twin:
         cfg.aliased_fraction, cfg.dt = aliased_fraction, float(T(dt))
         cfg.precision = _lib.SW_PREC_F32 if T == np.float32 else _lib.SW_PREC_F64
         cfg.device = int(os.environ.get("LIBSW_DEVICE", "0"))
-        if model == _lib.SW_MODEL_QG2:
+        if model in (_lib.SW_MODEL_RSW, _lib.SW_MODEL_QG2):
             cfg.aliased_state = 1 if os.environ.get("LIBSW_ALIASED_STATE", "0") == "1" else 0
         return cfg
 
