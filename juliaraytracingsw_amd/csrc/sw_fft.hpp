@@ -110,15 +110,19 @@ __device__ __forceinline__ void lds_barrier() {
 #endif
 }
 
-// Opaque thread index on lines of at least 2^SW_OPAQUE_LOG2 points (1024
-// threads, 128 VGPRs): the addresses a helper derives from t (LDS offsets of
+// Opaque thread index on lines of at least 2^SW_OPAQUE_LOG2 points (512 or
+// 1024 threads, 128 VGPRs): the addresses a helper derives from t (LDS offsets of
 // every FFT stage, mirror indices, tile offsets) are recomputed per call (a
 // few integer ops) instead of being shared across the kernel's many calls and
 // spilled for its whole life.  8192²: RSW row 2892 → 2278 µs (spills 67 →
 // 23), 2LQG row 2308 → 2158 µs (20 → 0); shorter lines measured neutral to
-// slower (TY 512² col_inv +23 %), so they keep the shared addresses.
+// slower (TY 512² col_inv +23 %), so they keep the shared addresses.  Round 3:
+// 4096-point lines too, with the per-stage twiddles below and 4 waves per
+// SIMD for their 512-thread blocks (two blocks per CU instead of one): RSW
+// 4096² col_step 405 -> 382 µs, 2LQG 4096² row 533 -> 440, col_fwd 140 -> 126
+// (tools/ab_lean.sh).
 #ifndef SW_OPAQUE_LOG2
-#define SW_OPAQUE_LOG2 13
+#define SW_OPAQUE_LOG2 12
 #endif
 #define SW_OPAQUE_T(t)                                                  \
   do {                                                                  \
@@ -137,15 +141,17 @@ struct FftPlan {
 
 // W^(k_i << (LOG2N - lNs_i - 3)) for every twiddled stage i (forward sign).
 // Lines of 8192 points run 1024 threads per block, which caps a thread at
-// 128 VGPRs: there the stage twiddles are read from the (L1-resident) table
-// at each stage instead of being held in registers for the whole kernel.
+// 128 VGPRs, and 4096-point lines 512 threads at 4 waves per SIMD (two
+// blocks per CU), the same cap: there the stage twiddles are read from the
+// (L1-resident) table at each stage instead of being held in registers for
+// the whole kernel.
 #ifndef SW_TWFLY_LOG2
-#define SW_TWFLY_LOG2 13  // lines of at least 2^this read their stage twiddles per stage
+#define SW_TWFLY_LOG2 12  // lines of at least 2^this read their stage twiddles per stage
 #endif
 // lines of at least 2^this form the seven powers of a radix-8 stage's
 // twiddle as a chain (two live at a time) instead of all at once
 #ifndef SW_TW_CHAIN_LOG2
-#define SW_TW_CHAIN_LOG2 13
+#define SW_TW_CHAIN_LOG2 12
 #endif
 // FLY: read per stage whatever the length (a kernel with little register room)
 template <int LOG2N, bool FLY = (LOG2N >= SW_TWFLY_LOG2)>

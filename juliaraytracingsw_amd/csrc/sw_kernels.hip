@@ -119,6 +119,10 @@ __device__ __forceinline__ void store_col_i(const Geom& g, int krl, int t, F put
 #define SW_MINW_FFT 2
 #endif
 #define SW_MINW(L) (Blk<L>::THREADS >= 1024 ? 4 : SW_MINW_FFT)
+// the column passes of the RSW/2LQG families: blocks of 512 threads (4096-
+// point lines) at 4 waves per SIMD too (128 VGPRs: two blocks per CU; round 3,
+// sw_fft.hpp SW_OPAQUE_LOG2); Thomas-Yamada's hold more per line and keep 2
+#define SW_MINW_M(M, L) (Blk<L>::THREADS >= (M == MODEL_TY ? 1024 : 512) ? 4 : SW_MINW_FFT)
 #ifndef SW_MINW_ROW
 #define SW_MINW_ROW 2
 #endif
@@ -160,7 +164,7 @@ __device__ __forceinline__ double2 zero2() { return make_double2(0.0, 0.0); }
 // grid: (columns, groups); RSW group f reads field f; QG2 group = layer.
 // ===========================================================================
 template <int MODEL, int LOG2N>
-static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
+static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, LOG2N))
     k_col_inv(Geom g, Phys p, const double2* __restrict__ X, double2* __restrict__ M,
               const double2* __restrict__ tw, int gbase) {
   using B = Blk<LOG2N>;
@@ -1100,9 +1104,9 @@ __host__ __device__ constexpr bool rsw_row_half() {
 }
 
 // lengths whose 2LQG row runs k_row_qg_h (SW_QG_ROW_HALF_MIN: from this
-// log2 nx up; measured in DESIGN.md §3e)
+// log2 nx up; measured in DESIGN.md §3e: 8192 -12 %, 4096 -3 %, 2048 neutral)
 #ifndef SW_QG_ROW_HALF_MIN
-#define SW_QG_ROW_HALF_MIN 13
+#define SW_QG_ROW_HALF_MIN 12
 #endif
 template <int LOG2N>
 __host__ __device__ constexpr bool qg_row_half() {
@@ -1161,7 +1165,7 @@ constexpr int model_nf() {
 }
 
 template <int MODEL, int LOG2N>
-static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
+static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, LOG2N))
     k_col_fwd(Geom g, Phys p, const double2* __restrict__ Mf, double2* __restrict__ N,
               const double2* __restrict__ X, const double2* __restrict__ tw, int gbase) {
   using B = Blk<LOG2N>;
@@ -1258,7 +1262,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
 // rows l in the 2/3-rule band of the live columns (the forward mixed fields,
 // as k_col_fwd reads them).  grid: (columns, output fields).
 template <int MODEL, int LOG2N>
-static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
+static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, LOG2N))
     k_col_fwd_alias(Geom g, Geom ga, int region, Phys p, const double2* __restrict__ Mf,
                     const double2* __restrict__ Ma, double2* __restrict__ N, const double2* __restrict__ tw) {
   using B = Blk<LOG2N>;
@@ -1978,7 +1982,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
 #define SW_MINW_CS 2
 #endif
 template <int LOG2N, bool STREAM>
-static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, (Blk<LOG2N>::THREADS >= 1024 ? 4 : SW_MINW_CS))
+static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, (Blk<LOG2N>::THREADS >= 512 ? 4 : SW_MINW_CS))
     k_col_step_fab3_rsw(Geom g, Phys p, StepPtrs a, const double2* __restrict__ Mf,
                         double2* __restrict__ Minv, const double2* __restrict__ tw, int fbase) {
   using B = Blk<LOG2N>;
@@ -2507,15 +2511,17 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
       hipLaunchKernelGGL((k_row<MODEL_RSWA, L>), dim3(nrows / BA::NB), dim3(BA::THREADS),
                          FftPlan<L>::LDS * BA::NB * sizeof(double2), s, g, p, Mi, Mo, tw, y0, nullptr);
   }
-  else if constexpr (qg_row_half<L>())
+  else if (Ma) {  // aliased-state tracking: the full-length row (row_alias_built: lines up to 4096)
+    if constexpr (L <= 12)
+      hipLaunchKernelGGL((k_row<MODEL_QG2, L, true>), dim3(nrows / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p, Mi,
+                         Mo, tw, y0, Ma);
+  } else if constexpr (qg_row_half<L>()) {
     hipLaunchKernelGGL((k_row_qg_h<L>), dim3(nrows), dim3(RowH<L>::NTH), FftPlan<L - 1>::LDS * sizeof(double2), s, g,
-                       p, Mi, Mo, tw, y0);  // (no aliased output: row_alias_built)
-  else if (Ma)
-    hipLaunchKernelGGL((k_row<MODEL_QG2, L, true>), dim3(nrows / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p, Mi, Mo,
-                       tw, y0, Ma);
-  else
+                       p, Mi, Mo, tw, y0);
+  } else {
     hipLaunchKernelGGL((k_row<MODEL_QG2, L>), dim3(nrows / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p, Mi, Mo, tw,
                        y0, nullptr);
+  }
 }
 
 template <int L>
@@ -2657,7 +2663,7 @@ void launch_row(int model, const Geom& g, const Phys& p, const double2* Minv, do
 bool row_alias_built(int model, int log2nx) {
   bool ok = false;
   by_len(log2nx, [&](auto L) {
-    ok = model == MODEL_RSWA || (model == MODEL_QG2 && !qg_row_half<decltype(L)::value>());
+    ok = model == MODEL_RSWA || (model == MODEL_QG2 && decltype(L)::value <= 12);
   });
   return ok;
 }
