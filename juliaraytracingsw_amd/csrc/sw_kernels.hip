@@ -339,12 +339,13 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
 #else
 #define SW_ROW_CLOSED false
 #endif
-template <int LOG2N>
+// LEAN: the row kernel runs at 128 VGPRs (row_fly): per-use offsets
+template <int LOG2N, bool LEAN = false>
 struct RowIdx {
   static constexpr int N = 1 << LOG2N, NT = N / 8;
   // 8192-point lines (128 VGPRs): only t, y are kept; the per-thread terms
   // are re-derived at each use from an opaque copy of t (SW_OPAQUE_T)
-  static constexpr bool kStore = LOG2N < SW_OPAQUE_LOG2;
+  static constexpr bool kStore = LOG2N < SW_OPAQUE_LOG2 && !LEAN;
   int oi[kStore ? 8 : 1];
   int f0s;  // kStore: forward-layout term of k = t
   int t, y;
@@ -366,7 +367,7 @@ struct RowIdx {
   }
   __device__ __forceinline__ int oinv_calc(const Geom& g, int s) const {
     int tt = t;
-    SW_OPAQUE_T(tt);
+    if constexpr (LOG2N >= SW_OPAQUE_LOG2 || LEAN) asm volatile("" : "+v"(tt));
     const int k = kk(tt, s);
     if (SW_ROW_CLOSED && g.nslab == 1) {
       const int r0 = row_inv(g, y);
@@ -400,7 +401,7 @@ struct RowIdx {
     return t & 1;
 #endif
     int tt = t;
-    SW_OPAQUE_T(tt);
+    if constexpr (LOG2N >= SW_OPAQUE_LOG2 || LEAN) asm volatile("" : "+v"(tt));
     if (SW_ROW_CLOSED && g.nslab == 1) return (kStore ? f0s : fwd0(g, tt, y)) + s * NT * g.nyl;
     return midx(g, tt + s * NT, y);
   }
@@ -421,11 +422,11 @@ __device__ __forceinline__ double2 pair_z(double2 aa, double2 bb, int kk, bool m
   return live ? make_double2(aa.x - bb.y, aa.y + bb.x) : zero2();
 }
 
-template <int LOG2N>
-__device__ __forceinline__ void load_pair(double2 (&v)[8], const RowIdx<LOG2N>& ri, const Geom& g,
+template <int LOG2N, bool LEAN = false>
+__device__ __forceinline__ void load_pair(double2 (&v)[8], const RowIdx<LOG2N, LEAN>& ri, const Geom& g,
                                           const double2* __restrict__ A,
                                           const double2* __restrict__ B, bool deriv) {
-  using R = RowIdx<LOG2N>;
+  using R = RowIdx<LOG2N, LEAN>;
   double2 a[8], b[8];
 #pragma unroll
   for (int s = 0; s < 8; ++s) {  // issue every load first
@@ -451,11 +452,11 @@ __device__ __forceinline__ void load_pair(double2 (&v)[8], const RowIdx<LOG2N>& 
 
 // load_pair with a per-field x-multiplier m: 0 → 1, 1 → ik, 2 → (ik)² = -k²
 // (B may be null: b = 0)
-template <int LOG2N>
-__device__ __forceinline__ void load_pair_m(double2 (&v)[8], const RowIdx<LOG2N>& ri, const Geom& g,
+template <int LOG2N, bool LEAN = false>
+__device__ __forceinline__ void load_pair_m(double2 (&v)[8], const RowIdx<LOG2N, LEAN>& ri, const Geom& g,
                                             const double2* __restrict__ A, int ma,
                                             const double2* __restrict__ B, int mb) {
-  using R = RowIdx<LOG2N>;
+  using R = RowIdx<LOG2N, LEAN>;
   double2 a[8], b[8];
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
@@ -478,12 +479,12 @@ __device__ __forceinline__ void load_pair_m(double2 (&v)[8], const RowIdx<LOG2N>
 }
 
 // RSW second inverse pair: a = Ĥ, b = ζ̂ = ik V̂ - Uy (x-spectral, per element)
-template <int LOG2N>
-__device__ __forceinline__ void load_eta_zeta(double2 (&v)[8], const RowIdx<LOG2N>& ri, const Geom& g,
+template <int LOG2N, bool LEAN = false>
+__device__ __forceinline__ void load_eta_zeta(double2 (&v)[8], const RowIdx<LOG2N, LEAN>& ri, const Geom& g,
                                               const double2* __restrict__ H,
                                               const double2* __restrict__ V,
                                               const double2* __restrict__ Uy) {
-  using R = RowIdx<LOG2N>;
+  using R = RowIdx<LOG2N, LEAN>;
   double2 h[8], vv[8], uy[8];
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
@@ -505,10 +506,10 @@ __device__ __forceinline__ void load_eta_zeta(double2 (&v)[8], const RowIdx<LOG2
 // After a forward FFT of z = a + i b (Z[t + s*NT] in v), hand Â[k], B̂[k] for
 // k = t + s NT < kc to emit(k, s, Â, B̂).  Needs Z[nx-k] from a mirror
 // thread: one LDS round trip.
-template <int LOG2N, typename Emit>
+template <int LOG2N, bool LEAN = false, typename Emit>
 __device__ __forceinline__ void split_pair(const double2 (&v)[8], int t, const Geom& g,
                                            double2* line, Emit emit) {
-  SW_OPAQUE_T(t);
+  if constexpr (LOG2N >= SW_OPAQUE_LOG2 || LEAN) asm volatile("" : "+v"(t));
   constexpr int N = 1 << LOG2N, NT = N / 8;
   lds_barrier();  // previous LDS readers are done
 #pragma unroll
@@ -555,11 +556,11 @@ __device__ __forceinline__ void split_pairs(const double2 (&v)[C][8], int t, con
   }
 }
 
-template <int LOG2N>
-__device__ __forceinline__ void store_pair(const double2 (&v)[8], const RowIdx<LOG2N>& ri, const Geom& g,
+template <int LOG2N, bool LEAN = false>
+__device__ __forceinline__ void store_pair(const double2 (&v)[8], const RowIdx<LOG2N, LEAN>& ri, const Geom& g,
                                            double2* line, double2* __restrict__ A,
                                            double2* __restrict__ B) {
-  split_pair<LOG2N>(v, ri.t, g, line, [&](int, int s, double2 a, double2 b) {
+  split_pair<LOG2N, LEAN>(v, ri.t, g, line, [&](int, int s, double2 a, double2 b) {
     const int o = ri.ofwd(g, s);
     A[o] = a;
     B[o] = b;
@@ -622,10 +623,23 @@ __device__ __forceinline__ void store_alias_pair(const double2 (&v)[8], int t, c
   }
 }
 
+// The 2LQG row from 2048-point lines (SW_QG_ROW_FLY_MIN): stage twiddles read
+// per stage and the thread index opaque per transform (Twiddles<…, FLY>), 116
+// VGPRs, 4 waves per SIMD — 2048²: 85 -> 76 µs, config 3 +2-3 %
+// (tools/ab_lean11.sh); the same measures slow the RSW kernels there (row
+// 77 -> 82, col_step 85 -> 92 µs), which keep theirs.
+#ifndef SW_QG_ROW_FLY_MIN
+#define SW_QG_ROW_FLY_MIN 11
+#endif
+template <int MODEL, int LOG2N>
+__host__ __device__ constexpr bool row_fly() {
+  return LOG2N >= SW_TWFLY_LOG2 || (MODEL == MODEL_QG2 && LOG2N >= SW_QG_ROW_FLY_MIN);
+}
 template <int MODEL, int LOG2N, bool ALIAS = false>
 static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
                                          (BlkRow<MODEL, LOG2N>::THREADS >= 1024 ? 4
-                                          : (MODEL == MODEL_QG2 ? SW_MINW_ROW_QG : SW_MINW_ROW)))
+                                          : (MODEL == MODEL_QG2 ? (row_fly<MODEL, LOG2N>() ? 4 : SW_MINW_ROW_QG)
+                                                                : SW_MINW_ROW)))
     k_row(Geom g, Phys p, const double2* __restrict__ Mi, double2* __restrict__ Mo,
           const double2* __restrict__ tw, int yoff, double2* __restrict__ Ma) {
   using Bk = BlkRow<MODEL, LOG2N>;
@@ -637,9 +651,9 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
                                       : row0_of_block<Bk::NB>(blockIdx.x, gridDim.x) + c.ln);
   constexpr int CB = row_lds_lines<MODEL, LOG2N>();
   double2* line = smem + c.ln * CB * FftPlan<LOG2N>::LDS;
-  RowIdx<LOG2N> ri;
+  RowIdx<LOG2N, row_fly<MODEL, LOG2N>()> ri;
   ri.init(g, c.t, y);
-  Twiddles<LOG2N> tws;
+  Twiddles<LOG2N, row_fly<MODEL, LOG2N>()> tws;
   tws.load(c.t, tw);
   const long long MF = g.mfield;
   double2 v[8];
