@@ -186,26 +186,48 @@ struct Twiddles {
   }
 };
 
-template <int LOG2N>
+// LDS index with the layout chosen explicitly (SWZ: the swizzle; else the
+// padding).  Wave-local transforms (WL below) always swizzle: their regions
+// tile a longer line buffer without padding.
+template <bool SWZ>
+__host__ __device__ constexpr int LPs(int i) { return SWZ ? (i ^ ((i >> 3) & 7)) : i + (i >> 3); }
+
+template <int LOG2N, bool SWZ = lds_swz<LOG2N>()>
 __device__ __forceinline__ void load_line(double2 (&v)[8], int t, const double2* __restrict__ line) {
   constexpr int NT = FftPlan<LOG2N>::NT;
   // padding: NT a multiple of 8 (N >= 64) gives LP(t + s*NT) = LP(t) + s*(NT + NT/8);
   // swizzle: NT a multiple of 64 (N >= 512) gives LP(t + s*NT) = LP(t) + s*NT
-  constexpr bool swz = lds_swz<LOG2N>();
-  constexpr bool lin = swz ? (NT % 64 == 0) : (NT % 8 == 0);
-  constexpr int step = swz ? NT : NT + NT / 8;
+  constexpr bool lin = SWZ ? (NT % 64 == 0) : (NT % 8 == 0);
+  constexpr int step = SWZ ? NT : NT + NT / 8;
 #pragma unroll
-  for (int s = 0; s < 8; ++s) v[s] = line[lin ? LP<LOG2N>(t) + s * step : LP<LOG2N>(t + s * NT)];
+  for (int s = 0; s < 8; ++s) v[s] = line[lin ? LPs<SWZ>(t) + s * step : LPs<SWZ>(t + s * NT)];
+}
+
+// LDS ordering inside one wave (wave-local transforms): a wave's LDS
+// instructions execute in order, so its own exchange needs no workgroup
+// barrier; the wait keeps the compiler and the counters honest.
+__device__ __forceinline__ void wave_lds_fence() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+template <bool WL>
+__device__ __forceinline__ void stage_sync() {
+  if constexpr (WL) wave_lds_fence();
+  else lds_barrier();
 }
 
 // C independent transforms of one line each, sharing every barrier (C LDS
 // line buffers, `stride` complex apart).  v[c] holds x[t + s*NT] on entry and
 // X[t + s*NT] on exit.  All threads of the block must call this (barriers).
-template <int LOG2N, int DIR, int C, bool FLY = (LOG2N >= SW_TWFLY_LOG2)>
+// WL: wave-local — the line's NT threads are one wave (NT = 64, N = 512) and
+// `line` is that wave's own region: exchanges are ordered by wave_lds_fence,
+// not by workgroup barriers, and the layout is the swizzle.
+template <int LOG2N, int DIR, int C, bool FLY = (LOG2N >= SW_TWFLY_LOG2), bool WL = false>
 __device__ __forceinline__ void fft_lines(double2 (&v)[C][8], int t, const Twiddles<LOG2N, FLY>& tws,
                                           double2* __restrict__ line, int stride) {
   using P = FftPlan<LOG2N>;
   constexpr int NT = P::NT;
+  constexpr bool SWZ = WL || lds_swz<LOG2N>();
+  static_assert(!WL || NT == 64, "a wave-local transform is one wave's line");
   // opaque t on the long lines and in kernels with little register room (FLY)
   if constexpr (LOG2N >= SW_OPAQUE_LOG2 || FLY) asm volatile("" : "+v"(t));
   // Opaque copy of the stage twiddles: keeps the compiler from sharing the
@@ -226,35 +248,35 @@ __device__ __forceinline__ void fft_lines(double2 (&v)[C][8], int t, const Twidd
       dft4<DIR>(v[c][0], v[c][2], v[c][4], v[c][6]);
       dft4<DIR>(v[c][1], v[c][3], v[c][5], v[c][7]);
     }
-    lds_barrier();
+    stage_sync<WL>();
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int j = t + h * NT;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) line[c * stride + LP<LOG2N>(4 * j + r)] = v[c][h + 2 * r];
+        for (int r = 0; r < 4; ++r) line[c * stride + LPs<SWZ>(4 * j + r)] = v[c][h + 2 * r];
       }
-    lds_barrier();
+    stage_sync<WL>();
 #pragma unroll
-    for (int c = 0; c < C; ++c) load_line<LOG2N>(v[c], t, line + c * stride);
+    for (int c = 0; c < C; ++c) load_line<LOG2N, SWZ>(v[c], t, line + c * stride);
   } else if constexpr (P::REM == 1) {  // radix-2, Ns = 1: butterflies j = t + h*NT, h < 4
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
       for (int h = 0; h < 4; ++h) dft2<DIR>(v[c][h], v[c][h + 4]);
-    lds_barrier();
+    stage_sync<WL>();
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
       for (int h = 0; h < 4; ++h) {
         const int j = t + h * NT;
-        line[c * stride + LP<LOG2N>(2 * j)] = v[c][h];
-        line[c * stride + LP<LOG2N>(2 * j + 1)] = v[c][h + 4];
+        line[c * stride + LPs<SWZ>(2 * j)] = v[c][h];
+        line[c * stride + LPs<SWZ>(2 * j + 1)] = v[c][h + 4];
       }
-    lds_barrier();
+    stage_sync<WL>();
 #pragma unroll
-    for (int c = 0; c < C; ++c) load_line<LOG2N>(v[c], t, line + c * stride);
+    for (int c = 0; c < C; ++c) load_line<LOG2N, SWZ>(v[c], t, line + c * stride);
   }
   // radix-8 stages
   constexpr int S0 = P::REM ? P::REM : 0;
@@ -299,22 +321,22 @@ __device__ __forceinline__ void fft_lines(double2 (&v)[C][8], int t, const Twidd
 #ifdef SW_EXP_NOLDS  // experiment: no LDS exchange in the radix-8 stages (wrong results)
     continue;
 #endif
-    lds_barrier();                // in-place LDS: everyone has loaded this stage's inputs
+    stage_sync<WL>();                // in-place LDS: everyone has loaded this stage's inputs
     const int idxD = ((t >> lNs) << (lNs + 3)) + k;
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-      if (lds_swz<LOG2N>() ? lNs >= 6 : lNs >= 3) {  // r * Ns moves no bit the index function mixes
-        const int base = LP<LOG2N>(idxD);
+      if (SWZ ? lNs >= 6 : lNs >= 3) {  // r * Ns moves no bit the index function mixes
+        const int base = LPs<SWZ>(idxD);
 #pragma unroll
-        for (int r = 0; r < 8; ++r) line[c * stride + base + r * (lds_swz<LOG2N>() ? Ns : Ns + Ns / 8)] = v[c][r];
+        for (int r = 0; r < 8; ++r) line[c * stride + base + r * (SWZ ? Ns : Ns + Ns / 8)] = v[c][r];
       } else {
 #pragma unroll
-        for (int r = 0; r < 8; ++r) line[c * stride + LP<LOG2N>(idxD + r * Ns)] = v[c][r];
+        for (int r = 0; r < 8; ++r) line[c * stride + LPs<SWZ>(idxD + r * Ns)] = v[c][r];
       }
     }
-    lds_barrier();
+    stage_sync<WL>();
 #pragma unroll
-    for (int c = 0; c < C; ++c) load_line<LOG2N>(v[c], t, line + c * stride);
+    for (int c = 0; c < C; ++c) load_line<LOG2N, SWZ>(v[c], t, line + c * stride);
   }
 }
 
@@ -324,6 +346,109 @@ template <int LOG2N, int DIR, bool FLY = (LOG2N >= SW_TWFLY_LOG2)>
 __device__ __forceinline__ void fft_line(double2 (&v)[8], int t, const Twiddles<LOG2N, FLY>& tws,
                                          double2* __restrict__ line) {
   fft_lines<LOG2N, DIR, 1, FLY>(reinterpret_cast<double2(&)[1][8]>(v), t, tws, line, 0);
+}
+
+// ---------------------------------------------------------------------------
+// 2048-point transforms over the four waves of a 256-thread line, decimated
+// by 4 across the waves (N = 4 Q, Q = 512 = one wave × 8 points): one
+// workgroup-wide LDS exchange per transform, the other two exchanges inside
+// each wave (wave_lds_fence, no s_barrier) in that wave's region R_w = line +
+// w Q of the line buffer.  With W = exp(DIR 2πi/N):
+//   DIF (fft4w_dif, natural in → decimated out):
+//     X[4m + c] = Σ_n W_Q^(nm) · W^(nc) Σ_q x[n + Qq] W_4^(qc)
+//     the radix-4 over q and the twiddle W^(nc) in the registers of thread
+//     t (n = t, t + 256), y_c[n] to R_c, then wave c runs the Q-point
+//     transform: on exit lane j of wave c holds X[4(j + 64 r) + c] in v[r].
+//   DIT (fft4w_dit, that decimated order in → natural out):
+//     X[k + Qp] = Σ_c W_4^(cp) · W^(ck) Y_c[k],  Y_c = DFT_Q(x[4m + c])
+//     wave c's Q-point transform, Y_c to R_c, then thread t reads Y_c[t],
+//     Y_c[t + 256] of every c: on exit v[s] = X[t + 256 s].
+// Physical-space work between the two (pointwise products) is order-blind.
+// wt = W_N^t with the forward sign (the length-N table), tq the Q-point
+// stage twiddles of lane t & 63 (Twiddles<9>::load(t & 63, tw, 2)).
+// Callers keep the workgroup-wide rule of fft_lines: no thread may still be
+// reading the line buffer (other than its own wave's region) on entry.
+// ---------------------------------------------------------------------------
+template <int DIR, int K>
+__device__ __forceinline__ double2 w8_mul(double2 a) {  // a · W_8^K, W_8 = exp(DIR 2πi/8)
+  const double c = 0.70710678118654752440084436210485;
+  if constexpr (K == 0) return a;
+  else if constexpr (K == 1) return make_double2(c * (a.x - DIR * a.y), c * (a.y + DIR * a.x));
+  else if constexpr (K == 2) return (DIR < 0) ? make_double2(a.y, -a.x) : make_double2(-a.y, a.x);
+  else return make_double2(c * (-a.x - DIR * a.y), c * (-a.y + DIR * a.x));
+}
+
+template <int DIR, int C>
+__device__ __forceinline__ void fft4w_dif(double2 (&v)[C][8], int t, double2 wt, const Twiddles<9>& tq,
+                                          double2* __restrict__ line, int stride) {
+  constexpr int Q = 512;
+  const double2 w1 = DIR < 0 ? wt : cconj(wt);
+  const double2 w2 = cmul(w1, w1), w3 = cmul(w2, w1);
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    dft4<DIR>(v[c][0], v[c][2], v[c][4], v[c][6]);  // n = t
+    dft4<DIR>(v[c][1], v[c][3], v[c][5], v[c][7]);  // n = t + 256
+    v[c][2] = cmul(v[c][2], w1);
+    v[c][4] = cmul(v[c][4], w2);
+    v[c][6] = cmul(v[c][6], w3);
+    v[c][3] = w8_mul<DIR, 1>(cmul(v[c][3], w1));
+    v[c][5] = w8_mul<DIR, 2>(cmul(v[c][5], w2));
+    v[c][7] = w8_mul<DIR, 3>(cmul(v[c][7], w3));
+  }
+  const int b = LPs<true>(t);
+#pragma unroll
+  for (int c = 0; c < C; ++c)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      line[c * stride + q * Q + b] = v[c][2 * q];
+      line[c * stride + q * Q + b + 256] = v[c][2 * q + 1];
+    }
+  lds_barrier();
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6), j = t & 63;
+  double2* reg = line + w * Q;
+#pragma unroll
+  for (int c = 0; c < C; ++c) load_line<9, true>(v[c], j, reg + c * stride);
+  fft_lines<9, DIR, C, false, true>(v, j, tq, reg, stride);
+}
+
+template <int DIR, int C>
+__device__ __forceinline__ void fft4w_dit(double2 (&v)[C][8], int t, double2 wt, const Twiddles<9>& tq,
+                                          double2* __restrict__ line, int stride) {
+  constexpr int Q = 512;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6), j = t & 63;
+  double2* reg = line + w * Q;
+  fft_lines<9, DIR, C, false, true>(v, j, tq, reg, stride);  // Y_w[j + 64 r] in v[r]
+  const int bj = LPs<true>(j);
+#pragma unroll
+  for (int c = 0; c < C; ++c)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) reg[c * stride + bj + 64 * r] = v[c][r];
+  lds_barrier();
+  const double2 w1 = DIR < 0 ? wt : cconj(wt);
+  const double2 w2 = cmul(w1, w1), w3 = cmul(w2, w1);
+  const int b = LPs<true>(t);
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    double2 a[4], e[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      a[q] = line[c * stride + q * Q + b];
+      e[q] = line[c * stride + q * Q + b + 256];
+    }
+    a[1] = cmul(a[1], w1);
+    a[2] = cmul(a[2], w2);
+    a[3] = cmul(a[3], w3);
+    e[1] = w8_mul<DIR, 1>(cmul(e[1], w1));
+    e[2] = w8_mul<DIR, 2>(cmul(e[2], w2));
+    e[3] = w8_mul<DIR, 3>(cmul(e[3], w3));
+    dft4<DIR>(a[0], a[1], a[2], a[3]);
+    dft4<DIR>(e[0], e[1], e[2], e[3]);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      v[c][2 * p] = a[p];
+      v[c][2 * p + 1] = e[p];
+    }
+  }
 }
 
 }  // namespace sw

@@ -631,6 +631,16 @@ __device__ __forceinline__ void store_alias_pair(const double2 (&v)[8], int t, c
 #ifndef SW_QG_ROW_FLY_MIN
 #define SW_QG_ROW_FLY_MIN 11
 #endif
+// RSW rows of 2048 points run the 4-wave decimated transforms (one
+// workgroup barrier pair per transform instead of three; SW_ROW4W=0: the
+// Stockham fft_lines)
+#ifndef SW_ROW4W
+#define SW_ROW4W 1
+#endif
+template <int LOG2N>
+__host__ __device__ constexpr bool row4w() {
+  return SW_ROW4W && LOG2N == 11;
+}
 template <int MODEL, int LOG2N>
 __host__ __device__ constexpr bool row_fly() {
   return LOG2N >= SW_TWFLY_LOG2 || (MODEL == MODEL_QG2 && LOG2N >= SW_QG_ROW_FLY_MIN);
@@ -670,8 +680,20 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
     const double2 *U = Mi, *V = Mi + MF, *H = Mi + 2 * MF, *Uy = Mi + 3 * MF;
     constexpr int LS = FftPlan<LOG2N>::LDS;  // two line buffers per row
     double2 w[2][8];
+    // 2048-point rows: the 4-wave decimated transforms (sw_fft.hpp fft4w_*)
+    constexpr bool W4 = row4w<LOG2N>() && CB == 2 && Bk::NB == 1;
+    Twiddles<9> tq;
+    double2 wt4 = zero2();
+    if constexpr (W4) {
+      tq.load(c.t & 63, tw, 2);
+      wt4 = tw[c.t];
+    }
     // u + i v and η + i ζ, transformed together (fft_lines leaves z[x = t + s*NT])
-    if constexpr (CB == 2) {
+    if constexpr (W4) {
+      load_pair<LOG2N>(w[0], ri, g, U, V, false);
+      load_eta_zeta<LOG2N>(w[1], ri, g, H, V, Uy);
+      fft4w_dif<+1, 2>(w, c.t, wt4, tq, line, LS);
+    } else if constexpr (CB == 2) {
       load_pair<LOG2N>(w[0], ri, g, U, V, false);
       load_eta_zeta<LOG2N>(w[1], ri, g, H, V, Uy);
       fft_pair<LOG2N, +1, CB>(w, c.t, tws, line, LS);
@@ -692,7 +714,8 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
       w[0][s] = make_double2(0.5 * (u * u + vv * vv), zeta * vv);  // K + i ζv
       w[1][s] = make_double2(zeta * u, u * eta);                   // ζu + i uη
     }
-    fft_pair<LOG2N, -1, CB>(w, c.t, tws, line, LS);
+    if constexpr (W4) fft4w_dit<-1, 2>(w, c.t, wt4, tq, line, LS);
+    else fft_pair<LOG2N, -1, CB>(w, c.t, tws, line, LS);
     auto emit = [&](int cc, int k, int s, double2 a, double2 b) {
       const int o = ri.ofwd(g, s);
       if (cc == 0) {
@@ -714,7 +737,8 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
 #pragma unroll
     for (int s = 0; s < 8; ++s) v[s] = make_double2(pc[s], 0.0);
     lds_barrier();  // split_pairs' mirror reads are done
-    fft_line<LOG2N, -1>(v, c.t, tws, line);
+    if constexpr (W4) fft4w_dit<-1, 1>(reinterpret_cast<double2(&)[1][8]>(v), c.t, wt4, tq, line, LS);
+    else fft_line<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       const int k = c.t + s * Bk::NT;
