@@ -349,106 +349,133 @@ __device__ __forceinline__ void fft_line(double2 (&v)[8], int t, const Twiddles<
 }
 
 // ---------------------------------------------------------------------------
-// 2048-point transforms over the four waves of a 256-thread line, decimated
-// by 4 across the waves (N = 4 Q, Q = 512 = one wave × 8 points): one
-// workgroup-wide LDS exchange per transform, the other two exchanges inside
-// each wave (wave_lds_fence, no s_barrier) in that wave's region R_w = line +
-// w Q of the line buffer.  With W = exp(DIR 2πi/N):
-//   DIF (fft4w_dif, natural in → decimated out):
-//     X[4m + c] = Σ_n W_Q^(nm) · W^(nc) Σ_q x[n + Qq] W_4^(qc)
-//     the radix-4 over q and the twiddle W^(nc) in the registers of thread
-//     t (n = t, t + 256), y_c[n] to R_c, then wave c runs the Q-point
-//     transform: on exit lane j of wave c holds X[4(j + 64 r) + c] in v[r].
-//   DIT (fft4w_dit, that decimated order in → natural out):
-//     X[k + Qp] = Σ_c W_4^(cp) · W^(ck) Y_c[k],  Y_c = DFT_Q(x[4m + c])
-//     wave c's Q-point transform, Y_c to R_c, then thread t reads Y_c[t],
-//     Y_c[t + 256] of every c: on exit v[s] = X[t + 256 s].
-// Physical-space work between the two (pointwise products) is order-blind.
-// wt = W_N^t with the forward sign (the length-N table), tq the Q-point
-// stage twiddles of lane t & 63 (Twiddles<9>::load(t & 63, tw, 2)).
-// Callers keep the workgroup-wide rule of fft_lines: no thread may still be
-// reading the line buffer (other than its own wave's region) on entry.
+// Transforms of N = 512·W points over the W waves (NT = 64 W threads) of a
+// line, decimated by W across the waves (Q = 512 = one wave × 8 points): one
+// workgroup-wide LDS exchange per transform, the other two inside each wave
+// (wave_lds_fence, no s_barrier) in that wave's region R_w = line + w Q of
+// the line buffer.  W = 2, 4, 8: 1024-, 2048-, 4096-point lines.  With
+// ω = exp(DIR 2πi/N), thread t holding x[t + NT s]:
+//   DIF (fftw_dif, natural in → decimated out):
+//     X[W m + c] = Σ_n ω_Q^(nm) · ω^(nc) Σ_q x[n + Qq] ω_W^(qc)
+//     the radix-W over q and the twiddle ω^(nc) in the registers of thread
+//     t (n = t + NT h, h < 8/W: x[n + Qq] is v[h + (8/W) q]), y_c[n] to R_c,
+//     then wave c runs the Q-point transform: on exit lane j of wave c
+//     holds X[W (j + 64 r) + c] in v[r].
+//   DIT (fftw_dit, that decimated order in → natural out):
+//     X[k + Qp] = Σ_c ω_W^(cp) · ω^(ck) Y_c[k],  Y_c = DFT_Q(x[W m + c])
+//     wave c's Q-point transform, Y_c to R_c, then thread t reads Y_c[t +
+//     NT h] of every c: on exit v[s] = X[t + NT s].
+// ω^(ck) for k = t + NT h is ω^(ct) ω_8^(hc).  Physical-space work between
+// the two (pointwise products) is order-blind.  tab: the forward-sign table
+// of length N << TSH (ω^t = conj^… of tab[t << TSH], read per call); tq: the
+// Q-point stage twiddles of lane t & 63 (Twiddles<9, FLY>::load(t & 63, tab,
+// log2(N / 512) + TSH)).  PRE: a
+// workgroup barrier before the DIF's exchange writes (some thread may still
+// be reading the line buffer) or before the DIT's first writes, which go to
+// the wave's own region (needed when another wave may still read it).
 // ---------------------------------------------------------------------------
-template <int DIR, int K>
-__device__ __forceinline__ double2 w8_mul(double2 a) {  // a · W_8^K, W_8 = exp(DIR 2πi/8)
+// a · ω_8^k, ω_8 = exp(DIR 2πi/8), k in 0..3 (a constant once the callers'
+// loops are unrolled)
+template <int DIR>
+__device__ __forceinline__ double2 w8_mul(double2 a, int k) {
   const double c = 0.70710678118654752440084436210485;
-  if constexpr (K == 0) return a;
-  else if constexpr (K == 1) return make_double2(c * (a.x - DIR * a.y), c * (a.y + DIR * a.x));
-  else if constexpr (K == 2) return (DIR < 0) ? make_double2(a.y, -a.x) : make_double2(-a.y, a.x);
-  else return make_double2(c * (-a.x - DIR * a.y), c * (-a.y + DIR * a.x));
+  if (k == 0) return a;
+  if (k == 1) return make_double2(c * (a.x - DIR * a.y), c * (a.y + DIR * a.x));
+  if (k == 2) return (DIR < 0) ? make_double2(a.y, -a.x) : make_double2(-a.y, a.x);
+  return make_double2(c * (-a.x - DIR * a.y), c * (-a.y + DIR * a.x));
 }
 
-template <int DIR, int C>
-__device__ __forceinline__ void fft4w_dif(double2 (&v)[C][8], int t, double2 wt, const Twiddles<9>& tq,
-                                          double2* __restrict__ line, int stride) {
-  constexpr int Q = 512;
-  const double2 w1 = DIR < 0 ? wt : cconj(wt);
-  const double2 w2 = cmul(w1, w1), w3 = cmul(w2, w1);
-#pragma unroll
-  for (int c = 0; c < C; ++c) {
-    dft4<DIR>(v[c][0], v[c][2], v[c][4], v[c][6]);  // n = t
-    dft4<DIR>(v[c][1], v[c][3], v[c][5], v[c][7]);  // n = t + 256
-    v[c][2] = cmul(v[c][2], w1);
-    v[c][4] = cmul(v[c][4], w2);
-    v[c][6] = cmul(v[c][6], w3);
-    v[c][3] = w8_mul<DIR, 1>(cmul(v[c][3], w1));
-    v[c][5] = w8_mul<DIR, 2>(cmul(v[c][5], w2));
-    v[c][7] = w8_mul<DIR, 3>(cmul(v[c][7], w3));
+// in-place DFT-W (natural order) of a[0..W)
+template <int W, int DIR>
+__device__ __forceinline__ void dft_w(double2 (&a)[W]) {
+  if constexpr (W == 2) dft2<DIR>(a[0], a[1]);
+  else if constexpr (W == 4) dft4<DIR>(a[0], a[1], a[2], a[3]);
+  else dft8<DIR>(a);
+}
+
+// pw[c] = ω^(c t), c < W (pw[0] unused)
+template <int W, int DIR>
+__device__ __forceinline__ void tw_powers(double2 wt, double2 (&pw)[W]) {
+  pw[0] = make_double2(1.0, 0.0);
+  if constexpr (W > 1) pw[1] = DIR < 0 ? wt : cconj(wt);
+  if constexpr (W > 2) {
+    pw[2] = cmul(pw[1], pw[1]);
+    pw[3] = cmul(pw[2], pw[1]);
   }
+  if constexpr (W > 4) {
+    pw[4] = cmul(pw[2], pw[2]);
+    pw[5] = cmul(pw[4], pw[1]);
+    pw[6] = cmul(pw[3], pw[3]);
+    pw[7] = cmul(pw[4], pw[3]);
+  }
+}
+
+template <int W, int DIR, int C, bool PRE = true, bool FLY = false, int TSH = 0>
+__device__ __forceinline__ void fftw_dif(double2 (&v)[C][8], int t, const double2* __restrict__ tab,
+                                         const Twiddles<9, FLY>& tq, double2* __restrict__ line, int stride) {
+  constexpr int Q = 512, NT = 64 * W, HN = 8 / W;
+  static_assert(W == 2 || W == 4 || W == 8, "1024-, 2048- or 4096-point lines");
+  double2 pw[W];
+  tw_powers<W, DIR>(tab[t << TSH], pw);
+#pragma unroll
+  for (int c = 0; c < C; ++c)
+#pragma unroll
+    for (int h = 0; h < HN; ++h) {
+      double2 a[W];
+#pragma unroll
+      for (int q = 0; q < W; ++q) a[q] = v[c][h + HN * q];
+      dft_w<W, DIR>(a);
+      v[c][h] = a[0];
+#pragma unroll
+      for (int q = 1; q < W; ++q) v[c][h + HN * q] = w8_mul<DIR>(cmul(a[q], pw[q]), h * q);
+    }
+  if constexpr (PRE) lds_barrier();
   const int b = LPs<true>(t);
 #pragma unroll
   for (int c = 0; c < C; ++c)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      line[c * stride + q * Q + b] = v[c][2 * q];
-      line[c * stride + q * Q + b + 256] = v[c][2 * q + 1];
-    }
+    for (int q = 0; q < W; ++q)
+#pragma unroll
+      for (int h = 0; h < HN; ++h) line[c * stride + q * Q + b + NT * h] = v[c][h + HN * q];
   lds_barrier();
   const int w = __builtin_amdgcn_readfirstlane(t >> 6), j = t & 63;
   double2* reg = line + w * Q;
 #pragma unroll
   for (int c = 0; c < C; ++c) load_line<9, true>(v[c], j, reg + c * stride);
-  fft_lines<9, DIR, C, false, true>(v, j, tq, reg, stride);
+  fft_lines<9, DIR, C, FLY, true>(v, j, tq, reg, stride);
 }
 
-template <int DIR, int C>
-__device__ __forceinline__ void fft4w_dit(double2 (&v)[C][8], int t, double2 wt, const Twiddles<9>& tq,
-                                          double2* __restrict__ line, int stride) {
-  constexpr int Q = 512;
+template <int W, int DIR, int C, bool FLY = false, int TSH = 0, bool PRE = false>
+__device__ __forceinline__ void fftw_dit(double2 (&v)[C][8], int t, const double2* __restrict__ tab,
+                                         const Twiddles<9, FLY>& tq, double2* __restrict__ line, int stride) {
+  constexpr int Q = 512, NT = 64 * W, HN = 8 / W;
+  static_assert(W == 2 || W == 4 || W == 8, "1024-, 2048- or 4096-point lines");
+  if constexpr (PRE) lds_barrier();
   const int w = __builtin_amdgcn_readfirstlane(t >> 6), j = t & 63;
   double2* reg = line + w * Q;
-  fft_lines<9, DIR, C, false, true>(v, j, tq, reg, stride);  // Y_w[j + 64 r] in v[r]
+  fft_lines<9, DIR, C, FLY, true>(v, j, tq, reg, stride);  // Y_w[j + 64 r] in v[r]
   const int bj = LPs<true>(j);
 #pragma unroll
   for (int c = 0; c < C; ++c)
 #pragma unroll
     for (int r = 0; r < 8; ++r) reg[c * stride + bj + 64 * r] = v[c][r];
   lds_barrier();
-  const double2 w1 = DIR < 0 ? wt : cconj(wt);
-  const double2 w2 = cmul(w1, w1), w3 = cmul(w2, w1);
+  double2 pw[W];
+  tw_powers<W, DIR>(tab[t << TSH], pw);
   const int b = LPs<true>(t);
 #pragma unroll
-  for (int c = 0; c < C; ++c) {
-    double2 a[4], e[4];
+  for (int c = 0; c < C; ++c)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      a[q] = line[c * stride + q * Q + b];
-      e[q] = line[c * stride + q * Q + b + 256];
-    }
-    a[1] = cmul(a[1], w1);
-    a[2] = cmul(a[2], w2);
-    a[3] = cmul(a[3], w3);
-    e[1] = w8_mul<DIR, 1>(cmul(e[1], w1));
-    e[2] = w8_mul<DIR, 2>(cmul(e[2], w2));
-    e[3] = w8_mul<DIR, 3>(cmul(e[3], w3));
-    dft4<DIR>(a[0], a[1], a[2], a[3]);
-    dft4<DIR>(e[0], e[1], e[2], e[3]);
+    for (int h = 0; h < HN; ++h) {
+      double2 a[W];
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      v[c][2 * p] = a[p];
-      v[c][2 * p + 1] = e[p];
+      for (int q = 0; q < W; ++q) a[q] = line[c * stride + q * Q + b + NT * h];
+#pragma unroll
+      for (int q = 1; q < W; ++q) a[q] = w8_mul<DIR>(cmul(a[q], pw[q]), h * q);
+      dft_w<W, DIR>(a);
+#pragma unroll
+      for (int p = 0; p < W; ++p) v[c][h + HN * p] = a[p];
     }
-  }
 }
 
 }  // namespace sw

@@ -631,15 +631,27 @@ __device__ __forceinline__ void store_alias_pair(const double2 (&v)[8], int t, c
 #ifndef SW_QG_ROW_FLY_MIN
 #define SW_QG_ROW_FLY_MIN 11
 #endif
-// RSW rows of 2048 points run the 4-wave decimated transforms (one
-// workgroup barrier pair per transform instead of three; SW_ROW4W=0: the
-// Stockham fft_lines)
+// Row transforms of 1024-4096 points (the full-length RSW/2LQG rows, the
+// half-length rows' M = nx/2 lines) run decimated across the line's W waves
+// (sw_fft.hpp fftw_*: one workgroup exchange per transform instead of three;
+// SW_ROW4W=0: the Stockham fft_lines).  Returns W, or 0.
 #ifndef SW_ROW4W
 #define SW_ROW4W 1
 #endif
 template <int LOG2N>
-__host__ __device__ constexpr bool row4w() {
-  return SW_ROW4W && LOG2N == 11;
+__host__ __device__ constexpr int roww() {
+  return (SW_ROW4W && LOG2N >= 10 && LOG2N <= 12) ? (1 << (LOG2N - 9)) : 0;
+}
+// the half-length rows' M-point lines (k_row_qg_h, k_row_rsw_h): measured
+// neutral at 4096² (M = 2048, W = 4: RSW row 407 vs 409 µs) and slower at
+// 8192² (M = 4096, W = 8: 2LQG row 1876 vs 1819 µs, 4 spills at 128 VGPRs),
+// so off by default (SW_ROWH_W=1: on)
+#ifndef SW_ROWH_W
+#define SW_ROWH_W 0
+#endif
+template <int LM>
+__host__ __device__ constexpr int roww_h() {
+  return SW_ROWH_W ? roww<LM>() : 0;
 }
 template <int MODEL, int LOG2N>
 __host__ __device__ constexpr bool row_fly() {
@@ -680,19 +692,15 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
     const double2 *U = Mi, *V = Mi + MF, *H = Mi + 2 * MF, *Uy = Mi + 3 * MF;
     constexpr int LS = FftPlan<LOG2N>::LDS;  // two line buffers per row
     double2 w[2][8];
-    // 2048-point rows: the 4-wave decimated transforms (sw_fft.hpp fft4w_*)
-    constexpr bool W4 = row4w<LOG2N>() && CB == 2 && Bk::NB == 1;
+    // the decimated transforms (roww): physical x in the DIF's order
+    constexpr int W = CB == 2 ? roww<LOG2N>() : 0;
     Twiddles<9> tq;
-    double2 wt4 = zero2();
-    if constexpr (W4) {
-      tq.load(c.t & 63, tw, 2);
-      wt4 = tw[c.t];
-    }
+    if constexpr (W > 0) tq.load(c.t & 63, tw, LOG2N - 9);
     // u + i v and η + i ζ, transformed together (fft_lines leaves z[x = t + s*NT])
-    if constexpr (W4) {
+    if constexpr (W > 0) {
       load_pair<LOG2N>(w[0], ri, g, U, V, false);
       load_eta_zeta<LOG2N>(w[1], ri, g, H, V, Uy);
-      fft4w_dif<+1, 2>(w, c.t, wt4, tq, line, LS);
+      fftw_dif<W, +1, 2, false>(w, c.t, tw, tq, line, LS);
     } else if constexpr (CB == 2) {
       load_pair<LOG2N>(w[0], ri, g, U, V, false);
       load_eta_zeta<LOG2N>(w[1], ri, g, H, V, Uy);
@@ -714,7 +722,7 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
       w[0][s] = make_double2(0.5 * (u * u + vv * vv), zeta * vv);  // K + i ζv
       w[1][s] = make_double2(zeta * u, u * eta);                   // ζu + i uη
     }
-    if constexpr (W4) fft4w_dit<-1, 2>(w, c.t, wt4, tq, line, LS);
+    if constexpr (W > 0) fftw_dit<W, -1, 2>(w, c.t, tw, tq, line, LS);
     else fft_pair<LOG2N, -1, CB>(w, c.t, tws, line, LS);
     auto emit = [&](int cc, int k, int s, double2 a, double2 b) {
       const int o = ri.ofwd(g, s);
@@ -737,7 +745,7 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
 #pragma unroll
     for (int s = 0; s < 8; ++s) v[s] = make_double2(pc[s], 0.0);
     lds_barrier();  // split_pairs' mirror reads are done
-    if constexpr (W4) fft4w_dit<-1, 1>(reinterpret_cast<double2(&)[1][8]>(v), c.t, wt4, tq, line, LS);
+    if constexpr (W > 0) fftw_dit<W, -1, 1>(reinterpret_cast<double2(&)[1][8]>(v), c.t, tw, tq, line, LS);
     else fft_line<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
@@ -878,27 +886,41 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
   } else {
     const double2 *Q1 = Mi, *Q2 = Mi + MF, *P1 = Mi + 2 * MF, *P2 = Mi + 3 * MF,
                   *Py1 = Mi + 4 * MF, *Py2 = Mi + 5 * MF;
+    // the decimated transforms (roww): physical x in the DIF's order
+    constexpr int W = roww<LOG2N>();
+    constexpr bool FL = row_fly<MODEL, LOG2N>();
+    Twiddles<9, FL> tq;
+    if constexpr (W > 0) tq.load(c.t & 63, tw, LOG2N - 9);
+    using V1 = double2(&)[1][8];
+    auto inv = [&](double2(&x)[8]) {
+      if constexpr (W > 0) fftw_dif<W, +1, 1, true, FL>(reinterpret_cast<V1>(x), c.t, tw, tq, line, 0);
+      else fft_line<LOG2N, +1>(x, c.t, tws, line);
+    };
+    auto fwd = [&](double2(&x)[8]) {
+      if constexpr (W > 0) fftw_dit<W, -1, 1, FL>(reinterpret_cast<V1>(x), c.t, tw, tq, line, 0);
+      else fft_line<LOG2N, -1>(x, c.t, tws, line);
+    };
     double2 q[8];
     // q1 + i q2
     load_pair<LOG2N>(v, ri, g, Q1, Q2, false);
-    fft_line<LOG2N, +1>(v, c.t, tws, line);
+    inv(v);
 #pragma unroll
     for (int s = 0; s < 8; ++s) q[s] = v[s];
     // ψx1 + i ψx2;  ψx q per layer (swqg/TwoLayerQG.jl:169)
     load_pair<LOG2N>(v, ri, g, P1, P2, true);
-    fft_line<LOG2N, +1>(v, c.t, tws, line);
+    inv(v);
 #pragma unroll
     for (int s = 0; s < 8; ++s) v[s] = make_double2(v[s].x * q[s].x, v[s].y * q[s].y);
-    fft_line<LOG2N, -1>(v, c.t, tws, line);
+    fwd(v);
     store_pair<LOG2N>(v, ri, g, line, Mo, Mo + MF);
     const long long MA = (long long)(g.nkr - g.kc) * g.ny;  // aliased columns × rows per field
     if constexpr (ALIAS) store_alias_pair<LOG2N>(v, c.t, g, line, Ma, Ma + MA, y);
     // ψy q per layer (:177)
     load_pair<LOG2N>(v, ri, g, Py1, Py2, false);
-    fft_line<LOG2N, +1>(v, c.t, tws, line);
+    inv(v);
 #pragma unroll
     for (int s = 0; s < 8; ++s) v[s] = make_double2(v[s].x * q[s].x, v[s].y * q[s].y);
-    fft_line<LOG2N, -1>(v, c.t, tws, line);
+    fwd(v);
     store_pair<LOG2N>(v, ri, g, line, Mo + 2 * MF, Mo + 3 * MF);
     if constexpr (ALIAS) store_alias_pair<LOG2N>(v, c.t, g, line, Ma + 2 * MA, Ma + 3 * MA, y);
   }
@@ -1051,18 +1073,31 @@ static __global__ void __launch_bounds__(RowH<LOG2N>::NTH, SW_MINW_ROW_H)
   tws.load(t, tw, 1);                    // W_M^j = W_N^(2j)
   const double2 wt = tw[t];
   const long long MF = g.mfield;
+  // the decimated transforms (roww) of the M-point lines
+  constexpr int W = roww_h<H::LM>();
+  Twiddles<9, SW_ROW_H_FLY> tq;
+  if constexpr (W > 0) tq.load(t & 63, tw, H::LM - 9 + 1);
+  using V1 = double2(&)[1][8];
+  auto inv = [&](double2(&x)[8]) {
+    if constexpr (W > 0) fftw_dif<W, +1, 1, true, SW_ROW_H_FLY, 1>(reinterpret_cast<V1>(x), t, tw, tq, smem, 0);
+    else fft_line<H::LM, +1>(x, t, tws, smem);
+  };
+  auto fwd = [&](double2(&x)[8]) {
+    if constexpr (W > 0) fftw_dit<W, -1, 1, SW_ROW_H_FLY, 1>(reinterpret_cast<V1>(x), t, tw, tq, smem, 0);
+    else fft_line<H::LM, -1>(x, t, tws, smem);
+  };
   double2 q[8], v[8];
 #pragma unroll 1
   for (int l = 0; l < 2; ++l) {
     load_real_h<LOG2N>(q, g, t, y, SrcField{Mi + l * MF, false}, wt);
-    fft_line<H::LM, +1>(q, t, tws, smem);
+    inv(q);
 #pragma unroll 1
     for (int d = 0; d < 2; ++d) {  // ψx q (:169), ψy q (:177)
       load_real_h<LOG2N>(v, g, t, y, SrcField{Mi + (d == 0 ? 2 + l : 4 + l) * MF, d == 0}, wt);
-      fft_line<H::LM, +1>(v, t, tws, smem);
+      inv(v);
 #pragma unroll
       for (int s = 0; s < 8; ++s) v[s] = make_double2(v[s].x * q[s].x, v[s].y * q[s].y);
-      fft_line<H::LM, -1>(v, t, tws, smem);
+      fwd(v);
       double2* O = Mo + (2 * d + l) * MF;
       split_real_h<LOG2N>(v, t, g, smem, wt, [&](int k, int, double2 X) { O[H::fwd(g, k, y)] = X; });
     }
@@ -1088,47 +1123,63 @@ static __global__ void __launch_bounds__(RowH<LOG2N>::NTH, SW_MINW_ROW_RSW_H)
   Twiddles<H::LM> tws;
   tws.load(t, tw, 1);  // W_M^j = W_N^(2j)
   const double2 wt = tw[t];
+  // the decimated transforms (roww) of the M-point lines; PRE: a barrier
+  // first (the previous split's mirror reads span every wave's region)
+  constexpr int W = roww_h<H::LM>();
+  Twiddles<9> tq;
+  if constexpr (W > 0) tq.load(t & 63, tw, H::LM - 9 + 1);
+  using V1 = double2(&)[1][8];
+  auto inv = [&](double2(&x)[8]) {
+    if constexpr (W > 0) fftw_dif<W, +1, 1, true, false, 1>(reinterpret_cast<V1>(x), t, tw, tq, smem, 0);
+    else fft_line<H::LM, +1>(x, t, tws, smem);
+  };
+  auto fwd = [&](double2(&x)[8], auto pre) {
+    if constexpr (W > 0) fftw_dit<W, -1, 1, false, 1, decltype(pre)::value>(reinterpret_cast<V1>(x), t, tw, tq, smem, 0);
+    else fft_line<H::LM, -1>(x, t, tws, smem);
+  };
+  using Pre = std::true_type;
+  using NoPre = std::false_type;
   const long long MF = g.mfield;
   const double2 *U = Mi, *V = Mi + MF, *Hh = Mi + 2 * MF, *Uy = Mi + 3 * MF;
   double2 u[8], v[8], e[8], w[8];
   load_real_h<LOG2N>(u, g, t, y, SrcField{U, false}, wt);
-  fft_line<H::LM, +1>(u, t, tws, smem);
+  inv(u);
   load_real_h<LOG2N>(v, g, t, y, SrcField{V, false}, wt);
-  fft_line<H::LM, +1>(v, t, tws, smem);
+  inv(v);
   load_real_h<LOG2N>(e, g, t, y, SrcField{Hh, false}, wt);
-  fft_line<H::LM, +1>(e, t, tws, smem);
+  inv(e);
   auto prod = [&](const double2 (&a)[8], const double2 (&b)[8]) {
 #pragma unroll
     for (int s = 0; s < 8; ++s) w[s] = make_double2(a[s].x * b[s].x, a[s].y * b[s].y);
   };
   // 4: (vη)^
   prod(v, e);
-  fft_line<H::LM, -1>(w, t, tws, smem);
+  fwd(w, NoPre{});
   split_real_h<LOG2N>(w, t, g, smem, wt, [&](int k, int, double2 X) { Mo[4 * MF + H::fwd(g, k, y)] = X; });
   // 3: Q = -ik (uη)^
   prod(u, e);
-  fft_line<H::LM, -1>(w, t, tws, smem);
+  fwd(w, Pre{});
   split_real_h<LOG2N>(w, t, g, smem, wt,
                       [&](int k, int, double2 X) { Mo[3 * MF + H::fwd(g, k, y)] = cmul_i(X, -(k * g.mk)); });
   // ζ = vx - uy in η's registers
   load_real_h<LOG2N>(e, g, t, y, SrcZeta{V, Uy}, wt);
-  fft_line<H::LM, +1>(e, t, tws, smem);
+  inv(e);
   // 2: (ζu)^
   prod(e, u);
-  fft_line<H::LM, -1>(w, t, tws, smem);
+  fwd(w, NoPre{});
   split_real_h<LOG2N>(w, t, g, smem, wt, [&](int k, int, double2 X) { Mo[2 * MF + H::fwd(g, k, y)] = X; });
   // 1: K̂, K = (u² + v²)/2; kept in u
 #pragma unroll
   for (int s = 0; s < 8; ++s)
     w[s] = make_double2(0.5 * (u[s].x * u[s].x + v[s].x * v[s].x), 0.5 * (u[s].y * u[s].y + v[s].y * v[s].y));
-  fft_line<H::LM, -1>(w, t, tws, smem);
+  fwd(w, Pre{});
   split_real_h<LOG2N>(w, t, g, smem, wt, [&](int k, int s, double2 X) {
     Mo[MF + H::fwd(g, k, y)] = X;
     u[s] = X;
   });
   // 0: P = -ik K̂ + (ζv)^
   prod(e, v);
-  fft_line<H::LM, -1>(w, t, tws, smem);
+  fwd(w, Pre{});
   split_real_h<LOG2N>(w, t, g, smem, wt,
                       [&](int k, int s, double2 X) { Mo[H::fwd(g, k, y)] = cadd(cmul_i(u[s], -(k * g.mk)), X); });
 }
