@@ -207,6 +207,8 @@ __device__ __forceinline__ void load_line(double2 (&v)[8], int t, const double2*
 // instructions execute in order, so its own exchange needs no workgroup
 // barrier; the wait keeps the compiler and the counters honest.
 __device__ __forceinline__ void wave_lds_fence() {
+  // (without the wait, in-order LDS alone would order it: measured slower,
+  // row 75.6 vs 74.9 µs)
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 template <bool WL>

@@ -503,6 +503,33 @@ __device__ __forceinline__ void load_eta_zeta(double2 (&v)[8], const RowIdx<LOG2
   }
 }
 
+// RSW inverse pairs u + i v and η + i ζ from one read of U, V, H, Uy
+template <int LOG2N, bool LEAN = false>
+__device__ __forceinline__ void load_uv_eta_zeta(double2 (&w)[2][8], const RowIdx<LOG2N, LEAN>& ri, const Geom& g,
+                                                 const double2* __restrict__ U, const double2* __restrict__ V,
+                                                 const double2* __restrict__ H, const double2* __restrict__ Uy) {
+  using R = RowIdx<LOG2N, LEAN>;
+  double2 u[8], vv[8], h[8], uy[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    u[s] = vv[s] = h[s] = uy[s] = zero2();
+    if (R::inv_any(g, s)) {
+      const int o = ri.oinv(g, s);
+      u[s] = mix_ld_row(U + o);
+      vv[s] = mix_ld_row(V + o);
+      h[s] = mix_ld_row(H + o);
+      uy[s] = mix_ld_row(Uy + o);
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const int kk = R::kk(ri.t, s);
+    const bool mir = s >= 4 && kk != (R::N >> 1), live = kk < g.kc;
+    w[0][s] = pair_z(u[s], vv[s], kk, mir, live);
+    w[1][s] = pair_z(h[s], csub(cmul_i(vv[s], kk * g.mk), uy[s]), kk, mir, live);
+  }
+}
+
 // After a forward FFT of z = a + i b (Z[t + s*NT] in v), hand Â[k], B̂[k] for
 // k = t + s NT < kc to emit(k, s, Â, B̂).  Needs Z[nx-k] from a mirror
 // thread: one LDS round trip.
@@ -698,8 +725,7 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
     if constexpr (W > 0) tq.load(c.t & 63, tw, LOG2N - 9);
     // u + i v and η + i ζ, transformed together (fft_lines leaves z[x = t + s*NT])
     if constexpr (W > 0) {
-      load_pair<LOG2N>(w[0], ri, g, U, V, false);
-      load_eta_zeta<LOG2N>(w[1], ri, g, H, V, Uy);
+      load_uv_eta_zeta<LOG2N>(w, ri, g, U, V, H, Uy);  // V read once (row 74.9 -> 73.5 µs)
       fftw_dif<W, +1, 2, false>(w, c.t, tw, tq, line, LS);
     } else if constexpr (CB == 2) {
       load_pair<LOG2N>(w[0], ri, g, U, V, false);
