@@ -480,4 +480,60 @@ __device__ __forceinline__ void fftw_dit(double2 (&v)[C][8], int t, const double
     }
 }
 
+// fftw_dit (DIR = -1) of z = a + i b, two real signals in the DIF's order,
+// with the pair split of the natural-order spectrum (split_pairs) folded
+// into the exchange: each wave's sub-spectrum Y_w is split into the two real
+// signals' sub-spectra before the radix-W combination,
+//   A_w[k] = (Y_w[k] + conj Y_w[Q - k]) / 2,  B_w[k] = (Y_w[k] - conj Y_w[Q - k]) / 2i
+//   Â[k + Qp] = Σ_w ω_W^(wp) ω^(wk) A_w[k]   (likewise B̂)
+// (conj Z[N - K] is the same combination of conj Y_w[Q - k]), so the split
+// costs reads of the mirrored sub-spectra instead of a second exchange.
+// emit(c, K, s, Â[K], B̂[K]) for the live K = t + NT s < kc.  v is left
+// undefined.  Entry rule as fftw_dit; the line buffer is read on exit.
+template <int W, int C, bool FLY = false, int TSH = 0, bool PRE = false, typename Emit>
+__device__ __forceinline__ void fftw_dit_split(double2 (&v)[C][8], int t, int kc, const double2* __restrict__ tab,
+                                               const Twiddles<9, FLY>& tq, double2* __restrict__ line, int stride,
+                                               Emit emit) {
+  constexpr int Q = 512, NT = 64 * W, HN = 8 / W, DIR = -1;
+  static_assert(W == 2 || W == 4 || W == 8, "1024-, 2048- or 4096-point lines");
+  if constexpr (PRE) lds_barrier();
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6), j = t & 63;
+  double2* reg = line + w * Q;
+  fft_lines<9, DIR, C, FLY, true>(v, j, tq, reg, stride);  // Y_w[j + 64 r] in v[r]
+  const int bj = LPs<true>(j);
+#pragma unroll
+  for (int c = 0; c < C; ++c)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) reg[c * stride + bj + 64 * r] = v[c][r];
+  lds_barrier();
+  double2 pw[W];
+  tw_powers<W, DIR>(tab[t << TSH], pw);
+#pragma unroll
+  for (int h = 0; h < HN; ++h) {
+    if (NT * h >= kc) continue;  // no live output K = t + NT h + Q p (uniform)
+    const int k = t + NT * h, km = (Q - k) & (Q - 1);
+    const int bk = LPs<true>(k), bm = LPs<true>(km);
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      double2 A[W], B[W];
+#pragma unroll
+      for (int q = 0; q < W; ++q) {
+        const double2 y = line[c * stride + q * Q + bk], ym = line[c * stride + q * Q + bm];
+        A[q] = make_double2(0.5 * (y.x + ym.x), 0.5 * (y.y - ym.y));
+        B[q] = make_double2(0.5 * (y.y + ym.y), -0.5 * (y.x - ym.x));
+      }
+#pragma unroll
+      for (int q = 1; q < W; ++q) {
+        A[q] = w8_mul<DIR>(cmul(A[q], pw[q]), h * q);
+        B[q] = w8_mul<DIR>(cmul(B[q], pw[q]), h * q);
+      }
+      dft_w<W, DIR>(A);
+      dft_w<W, DIR>(B);
+#pragma unroll
+      for (int p = 0; p < W; ++p)
+        if (k + Q * p < kc) emit(c, k + Q * p, h + HN * p, A[p], B[p]);
+    }
+  }
+}
+
 }  // namespace sw

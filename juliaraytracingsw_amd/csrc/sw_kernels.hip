@@ -676,6 +676,13 @@ __host__ __device__ constexpr int roww() {
 #ifndef SW_ROWH_W
 #define SW_ROWH_W 0
 #endif
+// the rows' pair splits folded into the decimated forward transforms
+// (sw_fft.hpp fftw_dit_split): bitwise-tested (GPU parity at 2048) but
+// measured slower — RSW row 73.7 -> 74.7, 2LQG row 74.3 -> 76.7 µs (the
+// radix-W combination done twice costs more VALU than the second exchange)
+#ifndef SW_SPLIT_FOLD
+#define SW_SPLIT_FOLD 0
+#endif
 template <int LM>
 __host__ __device__ constexpr int roww_h() {
   return SW_ROWH_W ? roww<LM>() : 0;
@@ -748,8 +755,10 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
       w[0][s] = make_double2(0.5 * (u * u + vv * vv), zeta * vv);  // K + i ζv
       w[1][s] = make_double2(zeta * u, u * eta);                   // ζu + i uη
     }
-    if constexpr (W > 0) fftw_dit<W, -1, 2>(w, c.t, tw, tq, line, LS);
-    else fft_pair<LOG2N, -1, CB>(w, c.t, tws, line, LS);
+    if constexpr (W == 0 || !SW_SPLIT_FOLD) {
+      if constexpr (W > 0) fftw_dit<W, -1, 2>(w, c.t, tw, tq, line, LS);
+      else fft_pair<LOG2N, -1, CB>(w, c.t, tws, line, LS);
+    }
     auto emit = [&](int cc, int k, int s, double2 a, double2 b) {
       const int o = ri.ofwd(g, s);
       if (cc == 0) {
@@ -760,7 +769,9 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
         Mo[3 * MF + o] = cmul_i(b, -(k * g.mk));
       }
     };
-    if constexpr (CB == 2) {
+    if constexpr (W > 0 && SW_SPLIT_FOLD) {
+      fftw_dit_split<W, 2>(w, c.t, g.kc, tw, tq, line, LS, emit);
+    } else if constexpr (CB == 2) {
       split_pairs<LOG2N, 2>(w, c.t, g, line, LS, emit);
     } else {
       split_pairs<LOG2N, 1>(reinterpret_cast<const double2(&)[1][8]>(w[0]), c.t, g, line, LS, emit);
@@ -932,13 +943,26 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
     inv(v);
 #pragma unroll
     for (int s = 0; s < 8; ++s) q[s] = v[s];
+    // fwd + store_pair (the split folded into the transform where it can be)
+    auto fwd_store = [&](double2* A, double2* B) {
+      if constexpr (W > 0 && SW_SPLIT_FOLD && !ALIAS) {
+        fftw_dit_split<W, 1, FL>(reinterpret_cast<V1>(v), c.t, g.kc, tw, tq, line, 0,
+                                 [&](int, int, int s, double2 a, double2 b) {
+                                   const int o = ri.ofwd(g, s);
+                                   A[o] = a;
+                                   B[o] = b;
+                                 });
+      } else {
+        fwd(v);
+        store_pair<LOG2N>(v, ri, g, line, A, B);
+      }
+    };
     // ψx1 + i ψx2;  ψx q per layer (swqg/TwoLayerQG.jl:169)
     load_pair<LOG2N>(v, ri, g, P1, P2, true);
     inv(v);
 #pragma unroll
     for (int s = 0; s < 8; ++s) v[s] = make_double2(v[s].x * q[s].x, v[s].y * q[s].y);
-    fwd(v);
-    store_pair<LOG2N>(v, ri, g, line, Mo, Mo + MF);
+    fwd_store(Mo, Mo + MF);
     const long long MA = (long long)(g.nkr - g.kc) * g.ny;  // aliased columns × rows per field
     if constexpr (ALIAS) store_alias_pair<LOG2N>(v, c.t, g, line, Ma, Ma + MA, y);
     // ψy q per layer (:177)
@@ -946,8 +970,7 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
     inv(v);
 #pragma unroll
     for (int s = 0; s < 8; ++s) v[s] = make_double2(v[s].x * q[s].x, v[s].y * q[s].y);
-    fwd(v);
-    store_pair<LOG2N>(v, ri, g, line, Mo + 2 * MF, Mo + 3 * MF);
+    fwd_store(Mo + 2 * MF, Mo + 3 * MF);
     if constexpr (ALIAS) store_alias_pair<LOG2N>(v, c.t, g, line, Ma + 2 * MA, Ma + 3 * MA, y);
   }
 }
