@@ -368,10 +368,11 @@ __device__ __forceinline__ void fft_line(double2 (&v)[8], int t, const Twiddles<
 //     wave c's Q-point transform, Y_c to R_c, then thread t reads Y_c[t +
 //     NT h] of every c: on exit v[s] = X[t + NT s].
 // ω^(ck) for k = t + NT h is ω^(ct) ω_8^(hc).  Physical-space work between
-// the two (pointwise products) is order-blind.  tab: the forward-sign table
-// of length N << TSH (ω^t = conj^… of tab[t << TSH], read per call); tq: the
-// Q-point stage twiddles of lane t & 63 (Twiddles<9, FLY>::load(t & 63, tab,
-// log2(N / 512) + TSH)).  PRE: a
+// the two (pointwise products) is order-blind.  wt = W_N^t with the forward
+// sign, read once per kernel (a read here would put a memory wait, which
+// also drains the stores in flight, in every transform); tq: the Q-point
+// stage twiddles of lane t & 63 (Twiddles<9, FLY>::load(t & 63, tab,
+// log2(N_tab / 512)) for a forward-sign table of length N_tab).  PRE: a
 // workgroup barrier before the DIF's exchange writes (some thread may still
 // be reading the line buffer) or before the DIT's first writes, which go to
 // the wave's own region (needed when another wave may still read it).
@@ -412,13 +413,13 @@ __device__ __forceinline__ void tw_powers(double2 wt, double2 (&pw)[W]) {
   }
 }
 
-template <int W, int DIR, int C, bool PRE = true, bool FLY = false, int TSH = 0>
-__device__ __forceinline__ void fftw_dif(double2 (&v)[C][8], int t, const double2* __restrict__ tab,
+template <int W, int DIR, int C, bool PRE = true, bool FLY = false>
+__device__ __forceinline__ void fftw_dif(double2 (&v)[C][8], int t, double2 wt,
                                          const Twiddles<9, FLY>& tq, double2* __restrict__ line, int stride) {
   constexpr int Q = 512, NT = 64 * W, HN = 8 / W;
   static_assert(W == 2 || W == 4 || W == 8, "1024-, 2048- or 4096-point lines");
   double2 pw[W];
-  tw_powers<W, DIR>(tab[t << TSH], pw);
+  tw_powers<W, DIR>(wt, pw);
 #pragma unroll
   for (int c = 0; c < C; ++c)
 #pragma unroll
@@ -447,8 +448,8 @@ __device__ __forceinline__ void fftw_dif(double2 (&v)[C][8], int t, const double
   fft_lines<9, DIR, C, FLY, true>(v, j, tq, reg, stride);
 }
 
-template <int W, int DIR, int C, bool FLY = false, int TSH = 0, bool PRE = false>
-__device__ __forceinline__ void fftw_dit(double2 (&v)[C][8], int t, const double2* __restrict__ tab,
+template <int W, int DIR, int C, bool FLY = false, bool PRE = false>
+__device__ __forceinline__ void fftw_dit(double2 (&v)[C][8], int t, double2 wt,
                                          const Twiddles<9, FLY>& tq, double2* __restrict__ line, int stride) {
   constexpr int Q = 512, NT = 64 * W, HN = 8 / W;
   static_assert(W == 2 || W == 4 || W == 8, "1024-, 2048- or 4096-point lines");
@@ -463,7 +464,7 @@ __device__ __forceinline__ void fftw_dit(double2 (&v)[C][8], int t, const double
     for (int r = 0; r < 8; ++r) reg[c * stride + bj + 64 * r] = v[c][r];
   lds_barrier();
   double2 pw[W];
-  tw_powers<W, DIR>(tab[t << TSH], pw);
+  tw_powers<W, DIR>(wt, pw);
   const int b = LPs<true>(t);
 #pragma unroll
   for (int c = 0; c < C; ++c)
@@ -490,8 +491,8 @@ __device__ __forceinline__ void fftw_dit(double2 (&v)[C][8], int t, const double
 // costs reads of the mirrored sub-spectra instead of a second exchange.
 // emit(c, K, s, Â[K], B̂[K]) for the live K = t + NT s < kc.  v is left
 // undefined.  Entry rule as fftw_dit; the line buffer is read on exit.
-template <int W, int C, bool FLY = false, int TSH = 0, bool PRE = false, typename Emit>
-__device__ __forceinline__ void fftw_dit_split(double2 (&v)[C][8], int t, int kc, const double2* __restrict__ tab,
+template <int W, int C, bool FLY = false, bool PRE = false, typename Emit>
+__device__ __forceinline__ void fftw_dit_split(double2 (&v)[C][8], int t, int kc, double2 wt,
                                                const Twiddles<9, FLY>& tq, double2* __restrict__ line, int stride,
                                                Emit emit) {
   constexpr int Q = 512, NT = 64 * W, HN = 8 / W, DIR = -1;
@@ -507,7 +508,7 @@ __device__ __forceinline__ void fftw_dit_split(double2 (&v)[C][8], int t, int kc
     for (int r = 0; r < 8; ++r) reg[c * stride + bj + 64 * r] = v[c][r];
   lds_barrier();
   double2 pw[W];
-  tw_powers<W, DIR>(tab[t << TSH], pw);
+  tw_powers<W, DIR>(wt, pw);
 #pragma unroll
   for (int h = 0; h < HN; ++h) {
     if (NT * h >= kc) continue;  // no live output K = t + NT h + Q p (uniform)

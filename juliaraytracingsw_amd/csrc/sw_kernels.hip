@@ -729,11 +729,15 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
     // the decimated transforms (roww): physical x in the DIF's order
     constexpr int W = CB == 2 ? roww<LOG2N>() : 0;
     Twiddles<9> tq;
-    if constexpr (W > 0) tq.load(c.t & 63, tw, LOG2N - 9);
+    double2 wt = zero2();
+    if constexpr (W > 0) {
+      tq.load(c.t & 63, tw, LOG2N - 9);
+      wt = tw[c.t];
+    }
     // u + i v and η + i ζ, transformed together (fft_lines leaves z[x = t + s*NT])
     if constexpr (W > 0) {
       load_uv_eta_zeta<LOG2N>(w, ri, g, U, V, H, Uy);  // V read once (row 74.9 -> 73.5 µs)
-      fftw_dif<W, +1, 2, false>(w, c.t, tw, tq, line, LS);
+      fftw_dif<W, +1, 2, false>(w, c.t, wt, tq, line, LS);
     } else if constexpr (CB == 2) {
       load_pair<LOG2N>(w[0], ri, g, U, V, false);
       load_eta_zeta<LOG2N>(w[1], ri, g, H, V, Uy);
@@ -756,7 +760,7 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
       w[1][s] = make_double2(zeta * u, u * eta);                   // ζu + i uη
     }
     if constexpr (W == 0 || !SW_SPLIT_FOLD) {
-      if constexpr (W > 0) fftw_dit<W, -1, 2>(w, c.t, tw, tq, line, LS);
+      if constexpr (W > 0) fftw_dit<W, -1, 2>(w, c.t, wt, tq, line, LS);
       else fft_pair<LOG2N, -1, CB>(w, c.t, tws, line, LS);
     }
     auto emit = [&](int cc, int k, int s, double2 a, double2 b) {
@@ -770,7 +774,7 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
       }
     };
     if constexpr (W > 0 && SW_SPLIT_FOLD) {
-      fftw_dit_split<W, 2>(w, c.t, g.kc, tw, tq, line, LS, emit);
+      fftw_dit_split<W, 2>(w, c.t, g.kc, wt, tq, line, LS, emit);
     } else if constexpr (CB == 2) {
       split_pairs<LOG2N, 2>(w, c.t, g, line, LS, emit);
     } else {
@@ -782,7 +786,7 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
 #pragma unroll
     for (int s = 0; s < 8; ++s) v[s] = make_double2(pc[s], 0.0);
     lds_barrier();  // split_pairs' mirror reads are done
-    if constexpr (W > 0) fftw_dit<W, -1, 1>(reinterpret_cast<double2(&)[1][8]>(v), c.t, tw, tq, line, LS);
+    if constexpr (W > 0) fftw_dit<W, -1, 1>(reinterpret_cast<double2(&)[1][8]>(v), c.t, wt, tq, line, LS);
     else fft_line<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
@@ -925,16 +929,25 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
                   *Py1 = Mi + 4 * MF, *Py2 = Mi + 5 * MF;
     // the decimated transforms (roww): physical x in the DIF's order
     constexpr int W = roww<LOG2N>();
+    // the lean row (row_fly) reads the wave-local stage twiddles per stage
+    // and W_N^t at each transform: held in registers they spill (8-33 VGPRs
+    // at 128); a 64-entry LDS table of the stage twiddles spilled 26 and read
+    // 88-91 against 74.5-75 µs (round 3, interleaved A/B)
     constexpr bool FL = row_fly<MODEL, LOG2N>();
     Twiddles<9, FL> tq;
-    if constexpr (W > 0) tq.load(c.t & 63, tw, LOG2N - 9);
+    double2 wt = zero2();
+    if constexpr (W > 0) {
+      tq.load(c.t & 63, tw, LOG2N - 9);
+      if constexpr (!FL) wt = tw[c.t];
+    }
+    auto wnt = [&]() { return FL ? tw[c.t] : wt; };
     using V1 = double2(&)[1][8];
     auto inv = [&](double2(&x)[8]) {
-      if constexpr (W > 0) fftw_dif<W, +1, 1, true, FL>(reinterpret_cast<V1>(x), c.t, tw, tq, line, 0);
+      if constexpr (W > 0) fftw_dif<W, +1, 1, true, FL>(reinterpret_cast<V1>(x), c.t, wnt(), tq, line, 0);
       else fft_line<LOG2N, +1>(x, c.t, tws, line);
     };
     auto fwd = [&](double2(&x)[8]) {
-      if constexpr (W > 0) fftw_dit<W, -1, 1, FL>(reinterpret_cast<V1>(x), c.t, tw, tq, line, 0);
+      if constexpr (W > 0) fftw_dit<W, -1, 1, FL>(reinterpret_cast<V1>(x), c.t, wnt(), tq, line, 0);
       else fft_line<LOG2N, -1>(x, c.t, tws, line);
     };
     double2 q[8];
@@ -946,7 +959,7 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
     // fwd + store_pair (the split folded into the transform where it can be)
     auto fwd_store = [&](double2* A, double2* B) {
       if constexpr (W > 0 && SW_SPLIT_FOLD && !ALIAS) {
-        fftw_dit_split<W, 1, FL>(reinterpret_cast<V1>(v), c.t, g.kc, tw, tq, line, 0,
+        fftw_dit_split<W, 1, FL>(reinterpret_cast<V1>(v), c.t, g.kc, wnt(), tq, line, 0,
                                  [&](int, int, int s, double2 a, double2 b) {
                                    const int o = ri.ofwd(g, s);
                                    A[o] = a;
@@ -1125,14 +1138,18 @@ static __global__ void __launch_bounds__(RowH<LOG2N>::NTH, SW_MINW_ROW_H)
   // the decimated transforms (roww) of the M-point lines
   constexpr int W = roww_h<H::LM>();
   Twiddles<9, SW_ROW_H_FLY> tq;
-  if constexpr (W > 0) tq.load(t & 63, tw, H::LM - 9 + 1);
+  double2 wm = zero2();
+  if constexpr (W > 0) {
+    tq.load(t & 63, tw, H::LM - 9 + 1);
+    wm = tw[2 * t];  // W_M^t
+  }
   using V1 = double2(&)[1][8];
   auto inv = [&](double2(&x)[8]) {
-    if constexpr (W > 0) fftw_dif<W, +1, 1, true, SW_ROW_H_FLY, 1>(reinterpret_cast<V1>(x), t, tw, tq, smem, 0);
+    if constexpr (W > 0) fftw_dif<W, +1, 1, true, SW_ROW_H_FLY>(reinterpret_cast<V1>(x), t, wm, tq, smem, 0);
     else fft_line<H::LM, +1>(x, t, tws, smem);
   };
   auto fwd = [&](double2(&x)[8]) {
-    if constexpr (W > 0) fftw_dit<W, -1, 1, SW_ROW_H_FLY, 1>(reinterpret_cast<V1>(x), t, tw, tq, smem, 0);
+    if constexpr (W > 0) fftw_dit<W, -1, 1, SW_ROW_H_FLY>(reinterpret_cast<V1>(x), t, wm, tq, smem, 0);
     else fft_line<H::LM, -1>(x, t, tws, smem);
   };
   double2 q[8], v[8];
@@ -1176,14 +1193,18 @@ static __global__ void __launch_bounds__(RowH<LOG2N>::NTH, SW_MINW_ROW_RSW_H)
   // first (the previous split's mirror reads span every wave's region)
   constexpr int W = roww_h<H::LM>();
   Twiddles<9> tq;
-  if constexpr (W > 0) tq.load(t & 63, tw, H::LM - 9 + 1);
+  double2 wm = zero2();
+  if constexpr (W > 0) {
+    tq.load(t & 63, tw, H::LM - 9 + 1);
+    wm = tw[2 * t];  // W_M^t
+  }
   using V1 = double2(&)[1][8];
   auto inv = [&](double2(&x)[8]) {
-    if constexpr (W > 0) fftw_dif<W, +1, 1, true, false, 1>(reinterpret_cast<V1>(x), t, tw, tq, smem, 0);
+    if constexpr (W > 0) fftw_dif<W, +1, 1, true, false>(reinterpret_cast<V1>(x), t, wm, tq, smem, 0);
     else fft_line<H::LM, +1>(x, t, tws, smem);
   };
   auto fwd = [&](double2(&x)[8], auto pre) {
-    if constexpr (W > 0) fftw_dit<W, -1, 1, false, 1, decltype(pre)::value>(reinterpret_cast<V1>(x), t, tw, tq, smem, 0);
+    if constexpr (W > 0) fftw_dit<W, -1, 1, false, decltype(pre)::value>(reinterpret_cast<V1>(x), t, wm, tq, smem, 0);
     else fft_line<H::LM, -1>(x, t, tws, smem);
   };
   using Pre = std::true_type;
