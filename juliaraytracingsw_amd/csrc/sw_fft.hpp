@@ -150,6 +150,9 @@ struct FftPlan {
 #endif
 // lines of at least 2^this form the seven powers of a radix-8 stage's
 // twiddle as a chain (two live at a time) instead of all at once
+#ifndef SW_TW_AHEAD
+#define SW_TW_AHEAD 0
+#endif
 #ifndef SW_TW_CHAIN_LOG2
 #define SW_TW_CHAIN_LOG2 12
 #endif
@@ -244,6 +247,13 @@ __device__ __forceinline__ void fft_lines(double2 (&v)[C][8], int t, const Twidd
       asm volatile("" : "+v"(tw1[i].x), "+v"(tw1[i].y));
     }
   }
+  // read per stage (FLY): SW_TW_AHEAD=1 issues each stage's table read one
+  // stage ahead (the first at entry), so a transform exposes one memory wait
+  // instead of one per stage.  Measured neutral (round 3, config 5: col_fwd
+  // 550 -> 537, row 1822 -> 1813, col_inv 876 -> 895 µs; config 4 ±0.3 %):
+  // the other waves of the CU cover those waits, so off
+  double2 twn = make_double2(1.0, 0.0);
+  if constexpr (!kPre && P::NTW > 0 && SW_TW_AHEAD) twn = tws.get(0);
   if constexpr (P::REM == 2) {  // radix-4, Ns = 1: butterflies j = t, t + NT
 #pragma unroll
     for (int c = 0; c < C; ++c) {
@@ -291,7 +301,15 @@ __device__ __forceinline__ void fft_lines(double2 (&v)[C][8], int t, const Twidd
 #else
     if (lNs > 0) {
 #endif
-      const double2 wt = kPre ? tw1[ti] : tws.get(ti);
+      double2 wt;
+      if constexpr (kPre) {
+        wt = tw1[ti];
+      } else if constexpr (SW_TW_AHEAD) {
+        wt = twn;
+        if (ti + 1 < P::NTW) twn = tws.get(ti + 1);
+      } else {
+        wt = tws.get(ti);
+      }
       const double2 w1 = DIR < 0 ? wt : cconj(wt);
       if constexpr (kPre && LOG2N < SW_TW_CHAIN_LOG2) {
         const double2 w2 = cmul(w1, w1), w3 = cmul(w2, w1), w4 = cmul(w2, w2);
