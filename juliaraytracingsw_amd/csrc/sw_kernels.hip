@@ -658,10 +658,10 @@ __device__ __forceinline__ void store_alias_pair(const double2 (&v)[8], int t, c
 #ifndef SW_QG_ROW_FLY_MIN
 #define SW_QG_ROW_FLY_MIN 11
 #endif
-// Row transforms of 1024-4096 points (the full-length RSW/2LQG rows, the
-// half-length rows' M = nx/2 lines) run decimated across the line's W waves
-// (sw_fft.hpp fftw_*: one workgroup exchange per transform instead of three;
-// SW_ROW4W=0: the Stockham fft_lines).  Returns W, or 0.
+// Row transforms of 1024-4096 points (the full-length RSW/2LQG rows; the
+// half-length rows' M = nx/2 lines with SW_ROWH_W) run decimated across the
+// line's W waves (sw_fft.hpp fftw_*: one workgroup exchange per transform
+// instead of three; SW_ROW4W=0: the Stockham fft_lines).  Returns W, or 0.
 #ifndef SW_ROW4W
 #define SW_ROW4W 1
 #endif
