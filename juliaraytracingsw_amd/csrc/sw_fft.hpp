@@ -226,7 +226,10 @@ __device__ __forceinline__ void stage_sync() {
 // WL: wave-local — the line's NT threads are one wave (NT = 64, N = 512) and
 // `line` is that wave's own region: exchanges are ordered by wave_lds_fence,
 // not by workgroup barriers, and the layout is the swizzle.
-template <int LOG2N, int DIR, int C, bool FLY = (LOG2N >= SW_TWFLY_LOG2), bool WL = false>
+// SHARE: no opaque copy of the stage twiddles — the compiler may keep their
+// powers for every transform of the kernel (registers for VALU; for kernels
+// whose occupancy is set by LDS, not registers)
+template <int LOG2N, int DIR, int C, bool FLY = (LOG2N >= SW_TWFLY_LOG2), bool WL = false, bool SHARE = false>
 __device__ __forceinline__ void fft_lines(double2 (&v)[C][8], int t, const Twiddles<LOG2N, FLY>& tws,
                                           double2* __restrict__ line, int stride) {
   using P = FftPlan<LOG2N>;
@@ -244,7 +247,7 @@ __device__ __forceinline__ void fft_lines(double2 (&v)[C][8], int t, const Twidd
 #pragma unroll
     for (int i = 0; i < P::NTW; ++i) {
       tw1[i] = tws.w[i];
-      asm volatile("" : "+v"(tw1[i].x), "+v"(tw1[i].y));
+      if constexpr (!SHARE) asm volatile("" : "+v"(tw1[i].x), "+v"(tw1[i].y));
     }
   }
   // read per stage (FLY): SW_TW_AHEAD=1 issues each stage's table read one
@@ -431,7 +434,7 @@ __device__ __forceinline__ void tw_powers(double2 wt, double2 (&pw)[W]) {
   }
 }
 
-template <int W, int DIR, int C, bool PRE = true, bool FLY = false>
+template <int W, int DIR, int C, bool PRE = true, bool FLY = false, bool SHARE = false>
 __device__ __forceinline__ void fftw_dif(double2 (&v)[C][8], int t, double2 wt,
                                          const Twiddles<9, FLY>& tq, double2* __restrict__ line, int stride) {
   constexpr int Q = 512, NT = 64 * W, HN = 8 / W;
@@ -463,10 +466,10 @@ __device__ __forceinline__ void fftw_dif(double2 (&v)[C][8], int t, double2 wt,
   double2* reg = line + w * Q;
 #pragma unroll
   for (int c = 0; c < C; ++c) load_line<9, true>(v[c], j, reg + c * stride);
-  fft_lines<9, DIR, C, FLY, true>(v, j, tq, reg, stride);
+  fft_lines<9, DIR, C, FLY, true, SHARE>(v, j, tq, reg, stride);
 }
 
-template <int W, int DIR, int C, bool FLY = false, bool PRE = false>
+template <int W, int DIR, int C, bool FLY = false, bool PRE = false, bool SHARE = false>
 __device__ __forceinline__ void fftw_dit(double2 (&v)[C][8], int t, double2 wt,
                                          const Twiddles<9, FLY>& tq, double2* __restrict__ line, int stride) {
   constexpr int Q = 512, NT = 64 * W, HN = 8 / W;
@@ -474,7 +477,7 @@ __device__ __forceinline__ void fftw_dit(double2 (&v)[C][8], int t, double2 wt,
   if constexpr (PRE) lds_barrier();
   const int w = __builtin_amdgcn_readfirstlane(t >> 6), j = t & 63;
   double2* reg = line + w * Q;
-  fft_lines<9, DIR, C, FLY, true>(v, j, tq, reg, stride);  // Y_w[j + 64 r] in v[r]
+  fft_lines<9, DIR, C, FLY, true, SHARE>(v, j, tq, reg, stride);  // Y_w[j + 64 r] in v[r]
   const int bj = LPs<true>(j);
 #pragma unroll
   for (int c = 0; c < C; ++c)

@@ -683,6 +683,13 @@ __host__ __device__ constexpr int roww() {
 #ifndef SW_SPLIT_FOLD
 #define SW_SPLIT_FOLD 0
 #endif
+// the RSW row (two blocks per CU, set by its LDS) keeping the wave-local
+// stage twiddle powers for all its transforms (fft_lines SHARE: 218 VGPRs,
+// 3 % fewer fp64 instructions): measured neutral (71.4-73.3 vs 71.0-71.5
+// µs), off
+#ifndef SW_ROW_TW_SHARE
+#define SW_ROW_TW_SHARE 0
+#endif
 template <int LM>
 __host__ __device__ constexpr int roww_h() {
   return SW_ROWH_W ? roww<LM>() : 0;
@@ -737,7 +744,7 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
     // u + i v and η + i ζ, transformed together (fft_lines leaves z[x = t + s*NT])
     if constexpr (W > 0) {
       load_uv_eta_zeta<LOG2N>(w, ri, g, U, V, H, Uy);  // V read once (row 74.9 -> 73.5 µs)
-      fftw_dif<W, +1, 2, false>(w, c.t, wt, tq, line, LS);
+      fftw_dif<W, +1, 2, false, false, SW_ROW_TW_SHARE>(w, c.t, wt, tq, line, LS);
     } else if constexpr (CB == 2) {
       load_pair<LOG2N>(w[0], ri, g, U, V, false);
       load_eta_zeta<LOG2N>(w[1], ri, g, H, V, Uy);
@@ -760,7 +767,7 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
       w[1][s] = make_double2(zeta * u, u * eta);                   // ζu + i uη
     }
     if constexpr (W == 0 || !SW_SPLIT_FOLD) {
-      if constexpr (W > 0) fftw_dit<W, -1, 2>(w, c.t, wt, tq, line, LS);
+      if constexpr (W > 0) fftw_dit<W, -1, 2, false, false, SW_ROW_TW_SHARE>(w, c.t, wt, tq, line, LS);
       else fft_pair<LOG2N, -1, CB>(w, c.t, tws, line, LS);
     }
     auto emit = [&](int cc, int k, int s, double2 a, double2 b) {
@@ -786,7 +793,8 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
 #pragma unroll
     for (int s = 0; s < 8; ++s) v[s] = make_double2(pc[s], 0.0);
     lds_barrier();  // split_pairs' mirror reads are done
-    if constexpr (W > 0) fftw_dit<W, -1, 1>(reinterpret_cast<double2(&)[1][8]>(v), c.t, wt, tq, line, LS);
+    if constexpr (W > 0)
+      fftw_dit<W, -1, 1, false, false, SW_ROW_TW_SHARE>(reinterpret_cast<double2(&)[1][8]>(v), c.t, wt, tq, line, LS);
     else fft_line<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
