@@ -669,10 +669,12 @@ template <int LOG2N>
 __host__ __device__ constexpr int roww() {
   return (SW_ROW4W && LOG2N >= 10 && LOG2N <= 12) ? (1 << (LOG2N - 9)) : 0;
 }
-// the half-length rows' M-point lines (k_row_qg_h, k_row_rsw_h): measured
-// neutral at 4096² (M = 2048, W = 4: RSW row 407 vs 409 µs) and slower at
-// 8192² (M = 4096, W = 8: 2LQG row 1876 vs 1819 µs, 4 spills at 128 VGPRs),
-// so off by default (SW_ROWH_W=1: on)
+// the half-length rows' M-point lines: the RSW row (k_row_rsw_h, 2 waves
+// per SIMD) at 4096² (M = 2048, W = 4: row 401-407 -> 398 µs, config 4 one
+// GPU 1274 -> 1286 steps/s); the 2LQG row (k_row_qg_h, 128 VGPRs) spills
+// with them (4096²: row 426 -> 525 µs; 8192², W = 8: 1823 -> 3150 µs, 54
+// spills) and keeps Stockham, as does the RSW row at 8192² (unmeasured).
+// SW_ROWH_W=1: every half row.
 #ifndef SW_ROWH_W
 #define SW_ROWH_W 0
 #endif
@@ -690,9 +692,9 @@ __host__ __device__ constexpr int roww() {
 #ifndef SW_ROW_TW_SHARE
 #define SW_ROW_TW_SHARE 0
 #endif
-template <int LM>
+template <int LM, bool RSW = false>
 __host__ __device__ constexpr int roww_h() {
-  return SW_ROWH_W ? roww<LM>() : 0;
+  return (SW_ROWH_W || (RSW && LM == 11)) ? roww<LM>() : 0;
 }
 template <int MODEL, int LOG2N>
 __host__ __device__ constexpr bool row_fly() {
@@ -1199,7 +1201,7 @@ static __global__ void __launch_bounds__(RowH<LOG2N>::NTH, SW_MINW_ROW_RSW_H)
   const double2 wt = tw[t];
   // the decimated transforms (roww) of the M-point lines; PRE: a barrier
   // first (the previous split's mirror reads span every wave's region)
-  constexpr int W = roww_h<H::LM>();
+  constexpr int W = roww_h<H::LM, true>();
   Twiddles<9> tq;
   double2 wm = zero2();
   if constexpr (W > 0) {
