@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SW_ABI_VERSION 8
+#define SW_ABI_VERSION 9
 
 /* models */
 #define SW_MODEL_RSW 0   /* rsw/RotatingShallowWater.jl: fields (u, v, η), 3×3 L   */
@@ -273,6 +273,42 @@ int sw_set_energy_diagnostics(sw_ctx* ctx, int64_t freq, int64_t capacity);
  * One slab per process: every rank must call it (it gathers the slabs). */
 int sw_get_energy_diagnostics(sw_ctx* ctx, sw_energy_record* out, int64_t max_records,
                               int64_t* n_records);
+
+/* ABI 9.  stepforward!(prob, nsteps) (nsteps >= 1) whose last step also
+ * yields, in *rec, the energies FF's Diagnostic functions read right after
+ * it (kinetic_energy(prob), potential_energy(prob) …: the record semantics
+ * above, independent of sw_set_energy_diagnostics).  For a caller that defers
+ * FF's per-step stepforward!(sol, clock, ts, …) calls (utils/IFMAB3.jl:157)
+ * and runs them when FF's increment! (after every step of FF's
+ * stepforward!(prob, diags, n)) asks for an energy: integration/julia/SWLib.jl.
+ * SW_E_NAN as sw_step (rec is filled first).  One slab per process: every
+ * rank calls it (collective). */
+int sw_step_record(sw_ctx* ctx, int64_t nsteps, sw_energy_record* rec);
+
+/* ABI 9.  The slab exchange of a decomposed problem explained (DESIGN.md §6;
+ * the reference has no multi-GPU path: north-star scope): nsteps steps of the
+ * production schedule (the state advances), each timed with events on the
+ * compute stream.  One slab per process: every rank calls it (collective). */
+#define SW_XPORT_NONE  0   /* one slab                                            */
+#define SW_XPORT_RCCL  1   /* one slab per process, RCCL grouped send/recv         */
+#define SW_XPORT_HOST  2   /* one slab per process, the caller's exchange hook     */
+#define SW_XPORT_LOCAL 3   /* every slab in this process (device copies)           */
+typedef struct sw_comm_stats {
+  int32_t nranks;          /* P, slabs of the decomposition                        */
+  int32_t transport;       /* SW_XPORT_*                                           */
+  int32_t rccl_ranks;      /* ncclCommCount of libsw's communicator (0: no RCCL)   */
+  int32_t pipelined;       /* 1: transposes on the side stream per field group
+                              (event-ordered); 0: sequential on the compute stream */
+  int32_t row_chunks;      /* pipelined: the row pass in this many chunks behind
+                              the last inverse group's transposes                  */
+  int32_t reserved;
+  double  step_us;         /* compute-stream time per step                         */
+  double  exposed_us;      /* per step: compute-stream time spent waiting for the
+                              transposes (sequential: the transposes themselves)   */
+  double  bytes_sent;      /* per step: bytes this slab's transposes send to the
+                              other slabs                                          */
+} sw_comm_stats;
+int sw_comm_profile(sw_ctx* ctx, int64_t nsteps, sw_comm_stats* out);
 
 /* Per-kernel HIP-event timing of `nsteps` steps (the state advances).
  * Fills up to max_stats entries; *n_stats receives the count. */

@@ -1,4 +1,4 @@
-# SWLib.jl — the FourierFlows-side binding of libsw (include/sw.h, ABI 8).
+# SWLib.jl — the FourierFlows-side binding of libsw (include/sw.h, ABI 9).
 #
 # A maintainer's addition to the reference's run directories (INTEGRATION.md
 # says how it is installed).  After `SWLib.attach!(Model)` for a model module
@@ -16,14 +16,21 @@
 #     GPU() device means "state on the libsw device, every array the driver
 #     sees on the host".  `Problem(CPU())` stays the reference's own FFTW path
 #     unless LIBSW_CPU=1.
-#   * `stepforward!(prob, diags, n)` (rsw/RSWDriver.jl:212,
+#   * FourierFlows' own `stepforward!(prob, diags, n)` (rsw/RSWDriver.jl:212,
 #     swqg/TwoLayerDriver.jl:105, TYdriver.jl:172,217,
-#     TwoLayerSimulation.jl:128) runs the n steps on the device, fills the
-#     energy Diagnostics from records the device kept while stepping, and
-#     leaves prob.sol current (one device->host copy per call).
+#     TwoLayerSimulation.jl:128) runs unchanged: its per-step seam
+#     `stepforward!(sol, clock, ts::SWStepper, …)` (the method
+#     utils/IFMAB3.jl:157 defines for its own stepper) only counts the step;
+#     the counted steps run on the device in one `sw_step` when the host next
+#     needs the state — an energy Diagnostic's value at FF's `increment!`
+#     (`sw_step_record`), `updatevars!`, `set_solution!` — and prob.sol is
+#     downloaded only there, never per step.
 #   * `set_solution!` / `set_q!`, `updatevars!`, `enforce_reality_condition!`
-#     of a libsw problem go through the C ABI; for any other problem the
-#     reference's own method runs (`invoke`).
+#     and the energy functions the Diagnostics call, of a libsw problem, go
+#     through the C ABI; for any other problem the reference's own method runs
+#     (`invoke`).  SWLib defines no FourierFlows method whose arguments are
+#     all FourierFlows' (or Base's) types: the only FF function it extends is
+#     the per-step seam, on `ts::SWStepper`.
 #
 # FourierFlows / GeophysicalFlows are not vendored in the reference (SURVEY
 # §8c); the FF/GF names used here are the ones the reference itself calls.
@@ -39,11 +46,13 @@ using LinearAlgebra: mul!
 const libsw = get(ENV, "LIBSW", joinpath(@__DIR__, "libsw.so"))
 
 # ---------------------------------------------------------------- include/sw.h
-const SW_ABI_VERSION = Int32(8)
+const SW_ABI_VERSION = Int32(9)
 const SW_MODEL_RSW, SW_MODEL_QG2, SW_MODEL_TY, SW_MODEL_MLQG = Int32(0), Int32(1), Int32(2), Int32(3)
 const STEPPERS = Dict("FilteredAB3" => Int32(0), "IFMAB3" => Int32(1), "IFMRK4" => Int32(2),
                       "ETDRK4" => Int32(3), "FilteredRK4" => Int32(4))
 const SW_E_NAN = Cint(-5)
+const SW_DIAG_KE, SW_DIAG_PE, SW_DIAG_KE2, SW_DIAG_KE1, SW_DIAG_BT = Int32(1), Int32(2), Int32(4), Int32(5), Int32(6)
+const SW_DIAG_WAVE_KE = Int32(7)   # .. SW_DIAG_GEO_PE = 10
 const SW_PREC_F64, SW_PREC_F32 = Int32(0), Int32(1)
 # sw_get_physical ids: RSW u v η ζ; 2LQG/MLQG layer*8 + (u 0, v 1, ζ 3, q 4, ψ 5);
 # TY u_c 0, v_c 1, p_c 2, ζ_T 3, q_c 4, ψ_T 5, u_T 8, v_T 9
@@ -85,10 +94,11 @@ mutable struct SWStepper{A<:AbstractArray, Tf} <: AbstractTimeStepper{A}
     filter::Tf             # FF makefilter(equation; kw...) or ones: drivers read it
                            # (simulation/TwoLayerSimulation.jl:44)
     model::Int32
-    freq::Int              # energy Diagnostic frequency recorded on the device (0: none)
-    seen::Int              # device records already handed to the Diagnostics
-    record_t::Vector{Float64}   # clock.t (the Problem's T arithmetic) at each record step
-    blewup::Bool           # the last sw_step returned SW_E_NAN
+    pending::Int           # steps FF's loop has taken that the device has not run yet
+    synced::Bool           # prob.sol (host) holds the device state
+    rec::SWEnergyRecord    # energies after the last device step (or of the set state)
+    rec_step::Int          # clock.step of `rec` (-1: none)
+    blewup::Bool           # the last device step returned SW_E_NAN
     uid::Vector{UInt8}     # keeps the RCCL unique id alive with the context
 end
 
@@ -154,7 +164,8 @@ function SWStepper(cfg::SWConfig, equation, filter)
         error("libsw sw_create: ", msg, " (code ", rc, ")")
     end
     A = Array{equation.T, length(equation.dims)}
-    ts = SWStepper{A, typeof(filter)}(h[], filter, cfg.model, 0, 0, Float64[], false, uid)
+    rec0 = SWEnergyRecord(0, 0.0, 0.0, 0.0, 0.0, (0.0, 0.0, 0.0, 0.0))
+    ts = SWStepper{A, typeof(filter)}(h[], filter, cfg.model, 0, true, rec0, -1, false, uid)
     finalizer(t -> ccall((:sw_destroy, libsw), Cvoid, (Ptr{Cvoid},), t.ctx), ts)
     return ts
 end
@@ -182,9 +193,11 @@ push_clock!(ts::SWStepper, clock) =
 # the clock pushed (TYdriver.jl:190 sets prob.clock.t before set_solution!)
 function load_solution!(prob)
     ts = prob.timestepper
+    ts.pending = 0                 # steps counted before a new state are void
     upload!(ts, prob.sol)
     download!(prob.sol, ts)
     push_clock!(ts, prob.clock)
+    ts.synced, ts.rec_step, ts.blewup = true, -1, false
     return nothing
 end
 
@@ -204,106 +217,88 @@ physical!(dst::Array{T,3}, ts::SWStepper, id::Integer, layer::Integer) where {T}
     end
 
 # ------------------------------------------------------- stepping and records
-# FF's per-step seam (utils/IFMAB3.jl:157 is the method this one replaces):
-# one step on the device, prob.sol current afterwards (FF's own per-step loop)
+# FF's per-step seam (the method utils/IFMAB3.jl:157 defines for its own
+# stepper; FF's stepforward!(prob) and stepforward!(prob, diags, n) loops call
+# it once per step).  Here it only counts the step and advances the clock in
+# the Problem's own arithmetic (clock.t += clock.dt, utils/IFMAB3.jl:162-163):
+# no C call, no host copy.  The counted steps run when the host next needs
+# the device state (sync!, device_energy).
 function FourierFlows.stepforward!(sol, clock, ts::SWStepper, equation, vars, params, grid)
-    run_steps!(sol, clock, ts, 1)
-    ts.blewup && error("Solution is NaN")
+    ts.pending += 1
+    ts.synced = false
+    clock.t += clock.dt
+    clock.step += 1
     return nothing
 end
 
-function run_steps!(sol, clock, ts::SWStepper, n::Int)
+# run the counted steps on the device (one sw_step)
+function flush!(prob)
+    ts = prob.timestepper
+    ts.pending > 0 || return nothing
+    n, ts.pending = ts.pending, 0
     rc = ccall((:sw_step, libsw), Cint, (Ptr{Cvoid}, Int64), ts.ctx, n)
     ts.blewup = rc == SW_E_NAN
     ts.blewup || check(ts, rc, "sw_step")
-    # the clock in the Problem's own arithmetic (clock.t += clock.dt per step,
-    # utils/IFMAB3.jl:162-163), remembering t at every recorded step
-    for _ in 1:n
-        clock.t += clock.dt
-        clock.step += 1
-        ts.freq > 0 && clock.step % ts.freq == 0 && push!(ts.record_t, clock.t)
-    end
-    download!(sol, ts)        # device -> host, dealiased (NaN included after a blow-up)
-    return nothing
-end
-
-# FF Diagnostic(kinetic_energy / …, prob; freq, nsteps) (rsw/RSWDriver.jl:193-196,
-# swqg/TwoLayerDriver.jl:86-89, TYdriver.jl:152-153,194-195,
-# TwoLayerSimulation.jl:52) -> energies recorded on the device while
-# stepping (sw_set_energy_diagnostics): no host round trip per diagnostic
-const RECORD = IdDict{Any,Function}()     # Diagnostic calc -> record -> value
-
-function attach_diagnostics!(prob, diags)
-    ts = prob.timestepper
-    isempty(diags) && return nothing
-    freq = first(diags).freq
-    all(d -> d.freq == freq, diags) || error("libsw records one diagnostics frequency per problem")
-    all(d -> haskey(RECORD, d.calc), diags) || error("libsw records the models' energy diagnostics only")
-    cap = maximum(length(d.t) for d in diags)
-    check(ts, ccall((:sw_set_energy_diagnostics, libsw), Cint, (Ptr{Cvoid}, Int64, Int64), ts.ctx, freq, cap),
-          "sw_set_energy_diagnostics")
-    ts.freq, ts.seen = freq, 0
-    empty!(ts.record_t)
-    return nothing
-end
-
-# FF increment!(diag) for every record the device kept since the last call
-function take_records!(prob, diags)
-    ts = prob.timestepper
-    n = Ref{Int64}(0)
-    check(ts, ccall((:sw_get_energy_diagnostics, libsw), Cint, (Ptr{Cvoid}, Ptr{SWEnergyRecord}, Int64, Ref{Int64}),
-                    ts.ctx, C_NULL, 0, n), "sw_get_energy_diagnostics")
-    n[] > ts.seen || return nothing
-    recs = Vector{SWEnergyRecord}(undef, n[])
-    check(ts, ccall((:sw_get_energy_diagnostics, libsw), Cint, (Ptr{Cvoid}, Ptr{SWEnergyRecord}, Int64, Ref{Int64}),
-                    ts.ctx, recs, n[], n), "sw_get_energy_diagnostics")
-    for (k, r) in enumerate(recs[ts.seen+1:n[]]), d in diags
-        d.i < length(d.t) || continue
-        d.i += 1
-        d.data[d.i] = RECORD[d.calc](r, d.value)
-        d.t[d.i] = ts.record_t[ts.seen + k]
-        d.steps[d.i] = r.step
-        d.value = d.data[d.i]
-    end
-    ts.seen = n[]
-    return nothing
-end
-
-# FF's stepforward!(prob, diags, nsteps) and stepforward!(prob, nsteps): a
-# libsw problem steps n times on the device; any other problem runs FF's
-# loop (stepforward!(prob); increment!(diags) per step, restated)
-function FourierFlows.stepforward!(prob::FourierFlows.Problem, diags::AbstractVector{<:AbstractDiagnostic},
-                                   nsteps::Int)
-    if !is_sw(prob)
-        for _ in 1:nsteps
-            FourierFlows.stepforward!(prob)
-            FourierFlows.increment!(diags)
-        end
-        return nothing
-    end
-    ts = prob.timestepper
-    ts.freq == 0 && attach_diagnostics!(prob, diags)
-    run_steps!(prob.sol, prob.clock, ts, nsteps)
-    take_records!(prob, diags)
     ts.blewup && blowup!(prob)
     return nothing
 end
-function FourierFlows.stepforward!(prob::FourierFlows.Problem, nsteps::Int)
-    if !is_sw(prob)
-        for _ in 1:nsteps
-            FourierFlows.stepforward!(prob)
-        end
-        return nothing
-    end
-    run_steps!(prob.sol, prob.clock, prob.timestepper, nsteps)
-    prob.timestepper.blewup && blowup!(prob)
+
+# prob.sol current on the host (device -> host, dealiased; NaN after a blow-up)
+function sync!(prob)
+    ts = prob.timestepper
+    flush!(prob)
+    ts.synced || download!(prob.sol, ts)
+    ts.synced = true
     return nothing
 end
+
+# The value FF's increment! stores for an energy Diagnostic (after every step
+# of stepforward!(prob, diags, n), at clock.step % freq == 0): the counted
+# steps run with the energies of the last one recorded on the device
+# (sw_step_record: RSW's vars.uh/vh/ηh = the last calcN's input, 2LQG's
+# prob.sol, …); several Diagnostics at one step share that record.  With no
+# step since the state was set (Diagnostic's own first call), sw_diag of the
+# state itself.
+function device_energy(prob, pick)
+    ts = prob.timestepper
+    if ts.pending > 0
+        n, ts.pending = ts.pending, 0
+        r = Ref{SWEnergyRecord}()
+        rc = ccall((:sw_step_record, libsw), Cint, (Ptr{Cvoid}, Int64, Ref{SWEnergyRecord}), ts.ctx, n, r)
+        ts.blewup = rc == SW_E_NAN
+        ts.blewup || check(ts, rc, "sw_step_record")
+        ts.rec, ts.rec_step = r[], prob.clock.step
+        ts.blewup && blowup!(prob)
+    elseif ts.rec_step != prob.clock.step
+        ts.rec, ts.rec_step = diag_record(ts, prob.clock), prob.clock.step
+    end
+    return as_T(real(eltype(prob.sol)), pick(ts.rec))
+end
+as_T(T, x::Real) = T(x)
+as_T(T, x::Tuple) = map(y -> as_T(T, y), x)
+as_T(T, x::AbstractVector) = T.(x)
+
+function diag_record(ts, clock)
+    d(id) = (x = Ref{Float64}(0.0);
+             check(ts, ccall((:sw_diag, libsw), Cint, (Ptr{Cvoid}, Int32, Ref{Float64}), ts.ctx, id, x), "sw_diag");
+             x[])
+    ts.model == SW_MODEL_TY &&
+        return SWEnergyRecord(clock.step, clock.t, d(SW_DIAG_KE), d(SW_DIAG_BT), d(SW_DIAG_PE),
+                              ntuple(i -> d(SW_DIAG_WAVE_KE + Int32(i - 1)), 4))
+    return SWEnergyRecord(clock.step, clock.t, d(SW_DIAG_KE1), d(SW_DIAG_KE2), d(SW_DIAG_PE), (0.0, 0.0, 0.0, 0.0))
+end
+
+# FF Diagnostic calc -> the record entry it returns (rsw/RSWDriver.jl:193-196,
+# swqg/TwoLayerDriver.jl:86-89, TYdriver.jl:152-153,194-195,
+# TwoLayerSimulation.jl:52)
+const RECORD = IdDict{Any,Function}()
 
 # After SW_E_NAN the drivers' own test finds the NaN and throws "Solution is
 # NaN" (rsw/RSWDriver.jl:213-218 tests vars.η, swqg/TwoLayerDriver.jl:106-111
 # vars.q: in the reference calcN! leaves them NaN); prob.sol holds the
-# non-finite state.
+# non-finite state.  (The device runs the counted steps at the next energy
+# Diagnostic step or updatevars!, so a blow-up shows at the first of those
+# after it.)
 function blowup!(prob)
     for name in (:η, :q, :u, :v)
         hasproperty(prob.vars, name) && fill!(getproperty(prob.vars, name), NaN)
@@ -402,6 +397,8 @@ end
 # current) host sol, the four physical fields by libsw's c2r
 function rsw_updatevars!(prob)
     vars, grid, sol, ts = prob.vars, prob.grid, prob.sol, prob.timestepper
+    sync!(prob)
+    FourierFlows.dealias!(sol, grid)   # :104 (the device's copy is dealiased by sw_get_physical)
     @. vars.uh = @view sol[:, :, 1]
     @. vars.vh = @view sol[:, :, 2]
     @. vars.ηh = @view sol[:, :, 3]
@@ -414,6 +411,8 @@ end
 # swqg/TwoLayerQG.jl:113-129
 function qg2_updatevars!(M, prob)
     vars, grid, sol, params, ts = prob.vars, prob.grid, prob.sol, prob.params, prob.timestepper
+    sync!(prob)
+    FourierFlows.dealias!(sol, grid)   # :115 (the device's copy is dealiased by sw_get_physical)
     @. vars.qh = sol
     M.streamfunctionfrompv!(vars.ψh, vars.qh, grid, params)
     @. vars.ζh = -grid.Krsq * vars.ψh
@@ -430,6 +429,7 @@ end
 # :103-123 (all = false: its mul! into the copies sol[:,:,k] leave sol as it is)
 function ty_updatevars!(prob; all=true)
     vars, grid, sol, ts = prob.vars, prob.grid, prob.sol, prob.timestepper
+    sync!(prob)
     @. vars.ζth = sol[:, :, 1]; @. vars.uch = sol[:, :, 2]
     @. vars.vch = sol[:, :, 3]; @. vars.pch = sol[:, :, 4]
     physical!(vars.ζt, ts, 3); physical!(vars.uc, ts, 0); physical!(vars.vc, ts, 1); physical!(vars.pc, ts, 2)
@@ -446,6 +446,7 @@ end
 # then q, ψ, u, v per layer
 function mlqg_updatevars!(M, prob)
     vars, grid, sol, params, ts = prob.vars, prob.grid, prob.sol, prob.params, prob.timestepper
+    sync!(prob)
     @. vars.qh = sol
     M.streamfunctionfrompv!(vars.ψh, vars.qh, params, grid)
     @. vars.uh = -im * grid.l * vars.ψh
@@ -457,8 +458,18 @@ function mlqg_updatevars!(M, prob)
 end
 
 # ------------------------------------------------------------------ attach!
-shape_like(v::Tuple, xs...) = v isa Tuple{<:AbstractVector,<:AbstractVector} ?
-    (collect(xs[1]), collect(xs[2])) : (Tuple(xs[1]), Tuple(xs[2]))
+# The model's energy functions FF's Diagnostics call (kinetic_energy(prob) …,
+# rsw/RotatingShallowWater.jl:326,332, swqg/TwoLayerQG.jl:242,252,
+# thomasyamada/ThomasYamada.jl:340-354, GF MultiLayerQG.energies): for a libsw
+# problem the device's value (device_energy), else the reference's (invoke).
+function energy_methods!(M::Module, picks::Pair{Symbol,<:Function}...)
+    for (name, pick) in picks
+        RECORD[getfield(M, name)] = pick
+        @eval M $name(prob::FourierFlows.Problem) =
+            $is_sw(prob) ? $device_energy(prob, $pick) : invoke($name, Tuple{Any}, prob)
+    end
+    return nothing
+end
 
 use_libsw(::CPU) = get(ENV, "LIBSW_CPU", "0") == "1"
 
@@ -486,8 +497,7 @@ function attach!(M::Module)
             updatevars!(prob::FourierFlows.Problem) =
                 $is_sw(prob) ? $rsw_updatevars!(prob) : invoke(updatevars!, Tuple{Any}, prob)
         end
-        RECORD[M.kinetic_energy] = (r, v) -> r.ke
-        RECORD[M.potential_energy] = (r, v) -> r.pe
+        energy_methods!(M, :kinetic_energy => r -> r.ke, :potential_energy => r -> r.pe)
     elseif name === :TwoLayerQG
         @eval M begin
             Problem(dev::FourierFlows.GPU; kw...) = $qg2_problem($M; kw...)
@@ -502,8 +512,7 @@ function attach!(M::Module)
             updatevars!(prob::FourierFlows.Problem) =
                 $is_sw(prob) ? $qg2_updatevars!($M, prob) : invoke(updatevars!, Tuple{Any}, prob)
         end
-        RECORD[M.kinetic_energy] = (r, v) -> (r.ke, r.ke2)
-        RECORD[M.potential_energy] = (r, v) -> r.pe
+        energy_methods!(M, :kinetic_energy => r -> (r.ke, r.ke2), :potential_energy => r -> r.pe)
     elseif name === :ThomasYamada
         @eval M begin
             Problem(dev::FourierFlows.GPU; kw...) = $ty_problem($M; kw...)
@@ -522,9 +531,8 @@ function attach!(M::Module)
                 $is_sw(prob) ? $ty_updatevars!(prob; all=false) :
                                invoke(enforce_reality_condition!, Tuple{Any}, prob)
         end
-        RECORD[M.barotropic_energy] = (r, v) -> r.ke2
-        RECORD[M.baroclinic_energy] = (r, v) -> (r.ke, r.pe)
-        RECORD[M.wave_geostrophic_energy] = (r, v) -> ((r.wg[1], r.wg[2]), (r.wg[3], r.wg[4]))
+        energy_methods!(M, :barotropic_energy => r -> r.ke2, :baroclinic_energy => r -> (r.ke, r.pe),
+                        :wave_geostrophic_energy => r -> ((r.wg[1], r.wg[2]), (r.wg[3], r.wg[4])))
     elseif name === :MultiLayerQG
         @eval M begin
             Problem(nlayers::Int, dev::FourierFlows.GPU; kw...) = $mlqg_problem($M, nlayers; kw...)
@@ -541,7 +549,8 @@ function attach!(M::Module)
             updatevars!(prob::FourierFlows.Problem) =
                 $is_sw(prob) ? $mlqg_updatevars!($M, prob) : invoke(updatevars!, Tuple{Any}, prob)
         end
-        RECORD[M.energies] = (r, v) -> shape_like(v, (r.ke, r.ke2), (r.pe,))
+        # GF's energies(prob): per-layer KE vector, PE vector (nlayers - 1)
+        energy_methods!(M, :energies => r -> ([r.ke, r.ke2], [r.pe]))
     else
         error("SWLib.attach!: no libsw model for module $name")
     end
@@ -550,7 +559,12 @@ end
 
 # TwoLayerSimulation.jl:43 and TwoLayerDriver.jl:11 draw their initial PV as
 # device_array(dev)(randn(...)) with dev = GPU(): under SWLib the driver's
-# arrays live on the host
-FourierFlows.device_array(::GPU) = Array
+# arrays live on the host.  This is SWLib's own function, not a method of
+# FourierFlows.device_array: the run-directory wrappers of those two drivers
+# (integration/julia/swqg/TwoLayerQG.jl, simulation/Parameters.jl) bind it as
+# Main.device_array before the driver's `using FourierFlows` /
+# `using GeophysicalFlows`, so only those run directories see it.
+device_array(::GPU) = Array
+device_array(dev) = FourierFlows.device_array(dev)
 
 end # module

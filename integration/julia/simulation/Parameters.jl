@@ -7,3 +7,6 @@ include("Parameters.ref.jl")
 include("SWLib.jl")
 import GeophysicalFlows
 SWLib.attach!(GeophysicalFlows.MultiLayerQG)
+# The driver's device_array(GPU()) (simulation/TwoLayerSimulation.jl:43) ->
+# host Array (SWLib.device_array; bound before its `using GeophysicalFlows`)
+const device_array = SWLib.device_array

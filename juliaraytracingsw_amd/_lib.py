@@ -10,7 +10,7 @@ import os
 
 import numpy as np
 
-SW_ABI_VERSION = 8
+SW_ABI_VERSION = 9
 SW_MODEL_RSW, SW_MODEL_QG2, SW_MODEL_TY, SW_MODEL_MLQG = 0, 1, 2, 3
 SW_STEP_FILTERED_AB3, SW_STEP_IFMAB3, SW_STEP_IFMRK4, SW_STEP_ETDRK4, SW_STEP_FILTERED_RK4 = 0, 1, 2, 3, 4
 SW_OK, SW_E_INVALID, SW_E_NOMEM, SW_E_HIP, SW_E_COMM, SW_E_NAN, SW_E_STATE = 0, -1, -2, -3, -4, -5, -6
@@ -29,7 +29,8 @@ EXPORTS = [
     "sw_get_physical", "sw_diag", "sw_set_energy_diagnostics", "sw_get_energy_diagnostics",
     "sw_profile_steps", "sw_step_alg_bytes", "sw_comm_unique_id",
     "sw_history_slots", "sw_get_history", "sw_set_history", "sw_reset_history", "sw_slab_geometry",
-    "sw_checkpoint_bytes", "sw_get_checkpoint", "sw_set_checkpoint",
+    "sw_checkpoint_bytes", "sw_get_checkpoint", "sw_set_checkpoint", "sw_step_record",
+    "sw_comm_profile",
 ]
 
 
@@ -69,6 +70,15 @@ class SwConfig(C.Structure):
 class SwEnergyRecord(C.Structure):
     _fields_ = [("step", C.c_int64), ("t", C.c_double), ("ke", C.c_double), ("ke2", C.c_double),
                 ("pe", C.c_double), ("wg", C.c_double * 4)]
+
+
+class SwCommStats(C.Structure):
+    _fields_ = [("nranks", C.c_int32), ("transport", C.c_int32), ("rccl_ranks", C.c_int32),
+                ("pipelined", C.c_int32), ("row_chunks", C.c_int32), ("reserved", C.c_int32),
+                ("step_us", C.c_double), ("exposed_us", C.c_double), ("bytes_sent", C.c_double)]
+
+
+XPORT_NAMES = {0: "none", 1: "rccl", 2: "host-staged", 3: "in-process"}
 
 
 class SwKernelStat(C.Structure):
@@ -120,6 +130,8 @@ def load(path: str | None = None):
         "sw_checkpoint_bytes": (C.c_int, [vp, C.POINTER(sz)]),
         "sw_get_checkpoint": (C.c_int, [vp, vp, sz]),
         "sw_set_checkpoint": (C.c_int, [vp, vp, sz]),
+        "sw_step_record": (C.c_int, [vp, i64, C.POINTER(SwEnergyRecord)]),
+        "sw_comm_profile": (C.c_int, [vp, i64, C.POINTER(SwCommStats)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -295,6 +307,30 @@ class Context:
         self._check(self.lib.sw_get_energy_diagnostics(self._h, buf, min(cap, n.value), C.byref(n)),
                     "sw_get_energy_diagnostics")
         return [(buf[i].step, buf[i].t, buf[i].ke, buf[i].ke2, buf[i].pe, tuple(buf[i].wg)) for i in range(n.value)]
+
+    def step_record(self, n=1):
+        """sw_step_record: n steps, the energies FF's Diagnostic functions read
+        after the last one -> (step, t, ke, ke2, pe, wg).  SW_E_NAN raises
+        LibSWError with ``.record`` set."""
+        r = SwEnergyRecord()
+        rc = self.lib.sw_step_record(self._h, int(n), C.byref(r))
+        rec = (r.step, r.t, r.ke, r.ke2, r.pe, tuple(r.wg))
+        if rc != SW_OK:
+            e = LibSWError(f"sw_step_record: {self.lib.sw_last_error(self._h).decode()} (code {rc})", rc)
+            e.record = rec
+            raise e
+        return rec
+
+    def comm_profile(self, nsteps):
+        """sw_comm_profile: nsteps steps of the production schedule (the state
+        advances; collective on one slab per process) -> the exchange's
+        transport, schedule and per-step exposed transpose time of this rank."""
+        st = SwCommStats()
+        self._check(self.lib.sw_comm_profile(self._h, int(nsteps), C.byref(st)), "sw_comm_profile")
+        return dict(nranks=st.nranks, transport=XPORT_NAMES.get(st.transport, str(st.transport)),
+                    rccl_ranks=st.rccl_ranks, schedule="pipelined" if st.pipelined else "sequential",
+                    row_chunks=st.row_chunks, step_us=st.step_us, exposed_transpose_us=st.exposed_us,
+                    sent_bytes_per_step=st.bytes_sent)
 
     def profile(self, nsteps):
         st = (SwKernelStat * 16)()

@@ -100,6 +100,17 @@ struct sw_ctx {
   std::vector<double> diag_t;
   std::vector<double> esums_host;            // energy sums of the records gathered so far
   int64_t esums_n = 0;                       // records gathered (sw_get_energy_diagnostics)
+  // sw_step_record: the last step of the call records into erec1 ([SW_NSUM]
+  // sums, or this rank's [kcl][SW_NSUM] column sums)
+  bool force_rec = false;
+  double* erec1 = nullptr;
+  // sw_comm_profile: event pairs on the compute stream around every wait for
+  // the side stream's transposes (pipelined) or around each transpose run on
+  // it (sequential), and the bytes a slab sends to the other slabs
+  bool time_waits = false;
+  std::vector<hipEvent_t> wev;
+  int nwait = 0;
+  double xbytes = 0.0;
   double t = 0.0;
   int64_t step = 0;
   int euler_left = 0;                        // sw_reset_history: forward-Euler start-up steps still to run
@@ -341,6 +352,20 @@ struct Timer {
   }
 };
 
+// the compute stream waits for an event of the side stream (sw_comm_profile:
+// timed — the span between the two events is comm time the compute stream
+// could not hide)
+int wait_comm(sw_ctx* c, hipEvent_t ev) {
+  const bool tm = c->time_waits && c->nwait + 2 <= (int)c->wev.size();
+  if (tm) HIPCHK(c, hipEventRecord(c->wev[c->nwait], c->stream));
+  HIPCHK(c, hipStreamWaitEvent(c->stream, ev, 0));
+  if (tm) {
+    HIPCHK(c, hipEventRecord(c->wev[c->nwait + 1], c->stream));
+    c->nwait += 2;
+  }
+  return 0;
+}
+
 // The transpose between the column and the row passes: block q
 // of every source slab p goes to block p of slab q.  inv: column-phase calcN
 // inputs -> row phase; fwd: row outputs -> column phase.  The blocks are
@@ -364,6 +389,7 @@ int transpose_fields(sw_ctx* c, bool inv, const int* fields, int nfl, hipStream_
       return fail(c, SW_E_INVALID, "row-chunked transpose: row-major tiles, device transports, rows in 4s");
   }
   const size_t off = (size_t)r0 * g0.kcl, cnt = (size_t)(r1 - r0) * g0.kcl;  // within each block
+  c->xbytes += (double)nfl * (c->P - 1) * cnt * sizeof(double2);  // one slab's sends to the others
   if (!c->dist) {
     for (int i = 0; i < nfl; ++i) {
       const int o = fields[i];
@@ -418,7 +444,14 @@ int transpose(sw_ctx* c, bool inv, int nfields) {
   Timer tm(c, K_XCHG);
   int f[16];
   for (int i = 0; i < nfields; ++i) f[i] = i;
-  return transpose_fields(c, inv, f, nfields, c->stream);
+  const bool tw = c->time_waits && c->nwait + 2 <= (int)c->wev.size();  // exposed in full
+  if (tw) HIPCHK(c, hipEventRecord(c->wev[c->nwait], c->stream));
+  if (int rc = transpose_fields(c, inv, f, nfields, c->stream)) return rc;
+  if (tw) {
+    HIPCHK(c, hipEventRecord(c->wev[c->nwait + 1], c->stream));
+    c->nwait += 2;
+  }
+  return 0;
 }
 
 // --- pipelined exchange (P > 1, RCCL or in-process copies) ------------------
@@ -478,8 +511,7 @@ int inv_group_async(sw_ctx* c, int g) {
 int join_comm(sw_ctx* c) {
   if (!c->comm) return 0;
   HIPCHK(c, hipEventRecord(c->ev_join, c->comm));
-  HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
-  return 0;
+  return wait_comm(c, c->ev_join);
 }
 
 // the row pass behind the inverse transposes: all at once after the side
@@ -492,7 +524,7 @@ int rows_pipelined(sw_ctx* c) {
   }
   const int per = c->sl[0].g.nyl / c->row_chunks;
   for (int k = 0; k < c->row_chunks; ++k) {
-    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_chunk[k], 0));
+    if (int rc = wait_comm(c, c->ev_chunk[k])) return rc;
     for (Slab& s : c->sl) sw::launch_row(c->kmodel, s.g, c->p, s.mir, s.mfr, c->tw_x, c->stream, k * per, per);
     HIPCHK(c, hipEventRecord(c->ev_rowc[k], c->stream));
   }
@@ -552,9 +584,14 @@ static void last_col_pass(sw_ctx* c, double2* Slab::*X, double2* Slab::*N, int o
 // op >= 0: the stepper update of `op` fused into the col_fwd pass (use_fwd_step)
 int calcN(sw_ctx* c, double2* Slab::*X, double2* Slab::*N, int op = -1, int stage = 0) {
   const int model = c->kmodel;
-  if (c->cfg.nop_calcN) {  // NOPcalcN!: N .= 0
-    for (Slab& s : c->sl)
+  if (c->cfg.nop_calcN) {  // NOPcalcN!: N .= 0 (the aliased modes' N too)
+    for (Slab& s : c->sl) {
       HIPCHK(c, hipMemsetAsync(s.*N, 0, (size_t)c->nf * s.g.cfield * sizeof(double2), c->stream));
+      if (c->alias)
+        for (int r = 0; r < 2; ++r)
+          if (s.a_nbuf[r] && c->ga[r].cfield > 0)
+            HIPCHK(c, hipMemsetAsync(s.a_nbuf[r], 0, (size_t)c->nf * c->ga[r].cfield * sizeof(double2), c->stream));
+    }
     return 0;
   }
   if (pipelined(c)) {
@@ -566,12 +603,13 @@ int calcN(sw_ctx* c, double2* Slab::*X, double2* Slab::*N, int op = -1, int stag
     if (int rc = rows_pipelined(c)) return rc;
     if (int rc = fwd_async(c)) return rc;
     if (op >= 0) {  // every field of a column in one block: all exchanges first
-      for (int f = 0; f < ps.nfc; ++f) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_fwd[f], 0));
+      for (int f = 0; f < ps.nfc; ++f)
+        if (int rc = wait_comm(c, c->ev_fwd[f])) return rc;
       for (Slab& s : c->sl) last_col_pass(c, X, N, op, stage, s);
       return 0;
     }
     for (int f = 0; f < ps.nfc; ++f) {
-      HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_fwd[f], 0));
+      if (int rc = wait_comm(c, c->ev_fwd[f])) return rc;
       for (Slab& s : c->sl) sw::launch_col_fwd(model, s.g, c->p, s.mfc, s.*N, s.*X, c->tw_y, c->stream, f, 1);
     }
     return 0;
@@ -610,8 +648,10 @@ int calcN(sw_ctx* c, double2* Slab::*X, double2* Slab::*N, int op = -1, int stag
 // re-evaluates the coupled update in every group measured slower at 2048²
 // than the separate kernels.
 bool use_fused(const sw_ctx* c) {
+  // aliased-state tracking runs the separate column passes (k_col_fwd_alias
+  // and the aliased updates follow k_col_fwd): never the fused pass
   if (c->cfg.unfused || c->cfg.nop_calcN || c->cfg.model == SW_MODEL_TY || c->cfg.model == SW_MODEL_MLQG ||
-      c->cfg.stepper == SW_STEP_FILTERED_RK4 || c->kmodel == sw::MODEL_RSWA)
+      c->cfg.stepper == SW_STEP_FILTERED_RK4 || c->kmodel == sw::MODEL_RSWA || c->alias)
     return false;
   if (c->fuse_all) return true;
   return c->kmodel == SW_MODEL_RSW && c->cfg.stepper == SW_STEP_FILTERED_AB3;
@@ -706,7 +746,7 @@ int run_stage(sw_ctx* c, int op, int stage, double2* Slab::*X) {
     if (int rc = rows_pipelined(c)) return rc;
     if (int rc = fwd_async(c)) return rc;
     for (int f = 0; f < ps.nfc; ++f) {  // column field f -> inverse group f
-      HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_fwd[f], 0));
+      if (int rc = wait_comm(c, c->ev_fwd[f])) return rc;
       for (Slab& s : c->sl) {
         sw::StepPtrs a = step_ptrs(c, s);
         a.stage = stage;
@@ -792,22 +832,33 @@ int alias_energy_cols(sw_ctx* c, bool post_step_state, int ncols) {
   return ncols;
 }
 
-void record_energy(sw_ctx* c, double2* Slab::*X) {
-  if (c->dist) {  // this rank's column sums; added over ranks at retrieval
+// one energy record of state X into dst: the sums [SW_NSUM], or (one slab per
+// process) this rank's column sums [kcl][SW_NSUM], added over ranks at retrieval
+void record_energy_to(sw_ctx* c, double2* Slab::*X, double* dst) {
+  if (c->dist) {
     const Slab& s = c->sl[0];
-    sw::launch_energy_cols(c->cfg.model, s.g, c->p, s.*X, c->erec + (size_t)c->diag_n * s.g.kcl * SW_NSUM, c->stream);
+    sw::launch_energy_cols(c->cfg.model, s.g, c->p, s.*X, dst, c->stream);
     return;
   }
   for (Slab& s : c->sl) sw::launch_energy_cols(c->cfg.model, s.g, c->p, s.*X, c->ecols + SW_NSUM * s.g.kr0, c->stream);
   const int ncols = alias_energy_cols(c, X == &Slab::sol, c->P * c->sl[0].g.kcl);
-  sw::launch_energy_final(c->ecols, ncols, c->erec + SW_NSUM * c->diag_n, c->stream);
+  sw::launch_energy_final(c->ecols, ncols, dst, c->stream);
+}
+
+// the records of this step: the scheduled one (sw_set_energy_diagnostics)
+// and/or the forced one (sw_step_record)
+void record_energy(sw_ctx* c, double2* Slab::*X, bool rec, bool frec) {
+  if (rec)
+    record_energy_to(c, X, c->erec + (c->dist ? (size_t)c->diag_n * c->sl[0].g.kcl * SW_NSUM : SW_NSUM * c->diag_n));
+  if (frec) record_energy_to(c, X, c->erec1);
 }
 
 int step_once(sw_ctx* c) {
   const int st = c->cfg.stepper;
   const bool rec = c->diag_freq > 0 && (c->step + 1) % c->diag_freq == 0 && c->diag_n < c->diag_cap;
+  const bool frec = c->force_rec;
   const bool rsw = c->cfg.model == SW_MODEL_RSW;
-  if (rec && rsw && st == SW_STEP_IFMAB3) record_energy(c, &Slab::sol);  // updated in place below
+  if ((rec || frec) && rsw && st == SW_STEP_IFMAB3) record_energy(c, &Slab::sol, rec, frec);  // updated in place below
   if (st == SW_STEP_FILTERED_AB3 || st == SW_STEP_IFMAB3) {
     if (int rc = run_stage(c, st == SW_STEP_FILTERED_AB3 ? sw::OP_FAB3 : sw::OP_IFMAB3, 0, &Slab::sol))
       return rc;
@@ -829,11 +880,11 @@ int step_once(sw_ctx* c) {
   c->t += c->cfg.dt;
   c->step += 1;
   if (c->euler_left > 0) c->euler_left -= 1;
+  if (rsw && st == SW_STEP_FILTERED_AB3) record_energy(c, &Slab::sol2, rec, frec);  // the pre-update buffer
+  else if (rsw && (st == SW_STEP_IFMRK4 || st == SW_STEP_FILTERED_RK4))
+    record_energy(c, &Slab::xs, rec, frec);  // stage-4 input
+  else if (!rsw) record_energy(c, &Slab::sol, rec, frec);
   if (rec) {
-    if (rsw && st == SW_STEP_FILTERED_AB3) record_energy(c, &Slab::sol2);  // the pre-update buffer
-    else if (rsw && (st == SW_STEP_IFMRK4 || st == SW_STEP_FILTERED_RK4))
-      record_energy(c, &Slab::xs);  // stage-4 input
-    else if (!rsw) record_energy(c, &Slab::sol);
     c->diag_steps.push_back(c->step);
     c->diag_t.push_back(c->t);
     c->diag_n += 1;
@@ -1273,7 +1324,8 @@ void sw_destroy(sw_ctx* c) {
   if (!c) return;
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (Slab& s : c->sl) free_slab(s);
-  void* ptrs[] = {c->tw_x, c->tw_y, c->stage, c->stage32, c->gbuf, c->dflt, c->flag, c->ecols, c->esum, c->erec};
+  void* ptrs[] = {c->tw_x, c->tw_y, c->stage, c->stage32, c->gbuf, c->dflt, c->flag, c->ecols, c->esum, c->erec,
+                  c->erec1};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   if (c->nccl) (void)ncclCommDestroy(c->nccl);
@@ -1290,6 +1342,7 @@ void sw_destroy(sw_ctx* c) {
   if (c->hrecv) (void)hipHostFree(c->hrecv);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
+  for (hipEvent_t e : c->wev) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -1594,6 +1647,107 @@ int sw_diag(sw_ctx* c, int32_t id, double* out) {
   return SW_OK;
 }
 
+// stepforward!(prob, n) whose last step also yields the energies FF's
+// Diagnostic functions read after it (the record semantics of
+// sw_set_energy_diagnostics), for a caller that steps lazily and needs them at
+// a diagnostic step (integration/julia/SWLib.jl, FF's increment!)
+int sw_step_record(sw_ctx* c, int64_t nsteps, sw_energy_record* out) {
+  if (!ready(c) || !out) return SW_E_STATE;
+  if (nsteps < 1) return fail(c, SW_E_INVALID, "sw_step_record: nsteps must be >= 1");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  const size_t per = c->dist ? (size_t)c->sl[0].g.kcl * SW_NSUM : SW_NSUM;
+  if (!c->erec1)
+    if (int rc = alloc(c, (void**)&c->erec1, per * sizeof(double))) return rc;
+  for (int64_t i = 0; i + 1 < nsteps; ++i)
+    if (int rc = step_once(c)) return rc;
+  c->force_rec = true;
+  const int rcs = step_once(c);
+  c->force_rec = false;
+  if (rcs) return rcs;
+  if (int rc = join_comm(c)) return rc;
+  HIPCHK(c, hipGetLastError());
+  std::vector<double> sums(SW_NSUM, 0.0);
+  if (c->dist) {  // collective: every rank's column sums, added in global column order
+    const size_t kcl = c->sl[0].g.kcl;
+    std::vector<double> all(per * c->P);
+    double* tmp = nullptr;
+    HIPCHK(c, hipMalloc((void**)&tmp, all.size() * sizeof(double)));
+    int rc = allgather(c, c->erec1, tmp, per * sizeof(double));
+    if (!rc && hipMemcpyAsync(all.data(), tmp, all.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream) !=
+                   hipSuccess)
+      rc = fail(c, SW_E_HIP, "energy record copy failed");
+    if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = fail(c, SW_E_HIP, "energy record sync failed");
+    (void)hipFree(tmp);
+    if (rc) return rc;
+    for (int k = 0; k < SW_NSUM; ++k)
+      for (int q = 0; q < c->P; ++q)
+        for (size_t col = 0; col < kcl; ++col) sums[k] += all[q * per + col * SW_NSUM + k];
+  } else {
+    HIPCHK(c, hipMemcpyAsync(sums.data(), c->erec1, SW_NSUM * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  out->step = c->step;
+  out->t = c->t;
+  energies_from_sums(c, sums.data(), out->ke, out->ke2, out->pe, out->wg);
+  if (c->cfg.check_nan) {
+    int h = 0;
+    if (int rc = nan_flag(c, h)) return rc;
+    if (h) return fail(c, SW_E_NAN, "Solution is NaN");
+  }
+  return SW_OK;
+}
+
+// The slab exchange explained (multi-GPU bench lines): nsteps steps of the
+// production schedule, each timed on the compute stream, with the time that
+// stream spent waiting for transposes (wait_comm; the sequential schedule's
+// transposes in full) and the bytes this slab sent.
+int sw_comm_profile(sw_ctx* c, int64_t nsteps, sw_comm_stats* out) {
+  if (!ready(c) || !out) return SW_E_STATE;
+  if (nsteps < 1) return fail(c, SW_E_INVALID, "sw_comm_profile: nsteps must be >= 1");
+  HIPCHK(c, hipSetDevice(c->cfg.device));
+  if (c->wev.empty()) {
+    c->wev.resize(256);
+    for (hipEvent_t& e : c->wev) HIPCHK(c, hipEventCreate(&e));
+  }
+  if (int rc = join_comm(c)) return rc;
+  double step_ms = 0.0, wait_ms = 0.0;
+  c->xbytes = 0.0;
+  int rc = 0;
+  for (int64_t i = 0; i < nsteps && !rc; ++i) {
+    c->time_waits = true;
+    c->nwait = 0;
+    if (hipEventRecord(c->ev0, c->stream) != hipSuccess) rc = fail(c, SW_E_HIP, "event record failed");
+    if (!rc) rc = step_once(c);
+    if (!rc) rc = join_comm(c);
+    c->time_waits = false;
+    if (rc) break;
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    HIPCHK(c, hipEventSynchronize(c->ev1));
+    float ms = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    step_ms += ms;
+    for (int k = 0; k + 1 < c->nwait; k += 2) {
+      HIPCHK(c, hipEventElapsedTime(&ms, c->wev[k], c->wev[k + 1]));
+      wait_ms += ms;
+    }
+  }
+  c->time_waits = false;
+  if (rc) return rc;
+  HIPCHK(c, hipGetLastError());
+  out->nranks = c->P;
+  out->transport = c->P == 1 ? SW_XPORT_NONE : (!c->dist ? SW_XPORT_LOCAL : (c->hostx ? SW_XPORT_HOST : SW_XPORT_RCCL));
+  int cnt = 0;
+  if (c->nccl) NCCLCHK(c, ncclCommCount(c->nccl, &cnt));
+  out->rccl_ranks = cnt;
+  out->pipelined = pipelined(c) ? 1 : 0;
+  out->row_chunks = pipelined(c) ? c->row_chunks : 1;
+  out->reserved = 0;
+  out->step_us = step_ms * 1e3 / nsteps;
+  out->exposed_us = wait_ms * 1e3 / nsteps;
+  out->bytes_sent = c->xbytes / nsteps;
+  return SW_OK;
+}
+
 int sw_set_energy_diagnostics(sw_ctx* c, int64_t freq, int64_t capacity) {
   if (!ready(c)) return SW_E_STATE;
   if (freq < 0 || capacity < 0) return fail(c, SW_E_INVALID, "freq and capacity must be >= 0");
@@ -1729,7 +1883,7 @@ struct CkptHeader {
   int32_t abi, model, stepper, nx, ny, nf, nslots, euler_left;
   double t;
   int64_t step;
-  int64_t reserved;
+  int64_t aliased_state;                // the context's sw_config.aliased_state (ABI 9; 0 before)
 };
 static_assert(sizeof(CkptHeader) == 64, "checkpoint header is 64 bytes");
 const char kCkptMagic[8] = {'S', 'W', 'C', 'K', 'P', 'T', '0', '1'};
@@ -1765,6 +1919,7 @@ int sw_get_checkpoint(const sw_ctx* cc, void* buf, size_t bytes) {
   h.euler_left = c->euler_left;
   h.t = c->t;
   h.step = c->step;
+  h.aliased_state = c->alias ? 1 : 0;
   char* out = static_cast<char*>(buf);
   std::memcpy(out, &h, sizeof(h));
   const size_t fb = full_bytes(c);
@@ -1790,6 +1945,12 @@ int sw_set_checkpoint(sw_ctx* c, const void* buf, size_t bytes) {
   CkptHeader h;
   std::memcpy(&h, buf, sizeof(h));
   if (std::memcmp(h.magic, kCkptMagic, 8) != 0) return fail(c, SW_E_INVALID, "sw_set_checkpoint: not a libsw checkpoint");
+  // the blob layout is that of ABI 7 (its introduction) up to this one
+  if (h.abi < 7 || h.abi > SW_ABI_VERSION) return fail(c, SW_E_INVALID, "sw_set_checkpoint: unknown checkpoint ABI");
+  // an aliased-state blob carries modes a default context drops, and the
+  // reverse lacks them: neither continues bitwise
+  if (h.aliased_state != (c->alias ? 1 : 0))
+    return fail(c, SW_E_INVALID, "sw_set_checkpoint: aliased_state differs from the checkpoint's");
   if (h.model != c->cfg.model || h.stepper != c->cfg.stepper || h.nx != c->cfg.nx || h.ny != c->cfg.ny ||
       h.nf != c->nf || h.nslots != ckpt_slots(c) || h.step < 0 || h.euler_left < 0 || h.euler_left > 3)
     return fail(c, SW_E_INVALID, "sw_set_checkpoint: checkpoint of a different problem or stepper");

@@ -1103,6 +1103,45 @@ __device__ __forceinline__ void load_real_h(double2 (&v)[8], const Geom& g, int 
   }
 }
 
+// RSW half row: the c2r inputs of v and of ζ = ik V̂ − Ûy from ONE read of V
+// (with Uy), the same arithmetic as load_real_h with SrcField{V} and
+// SrcZeta{V, Uy} (bitwise)
+template <int LOG2N>
+__device__ __forceinline__ void load_v_zeta_h(double2 (&v)[8], double2 (&z)[8], const Geom& g, int t, int y,
+                                              const double2* __restrict__ V, const double2* __restrict__ Uy,
+                                              double2 wt) {
+  using H = RowH<LOG2N>;
+  asm volatile("" : "+v"(t), "+v"(wt.x), "+v"(wt.y));
+  const SrcZeta sz{V, Uy};
+  auto comb = [&](double2 x, double2 xm, int s) {
+    const double2 S = cadd(x, cconj(xm)), D = csub(x, cconj(xm));
+    const double2 T = cmul(D, cconj(H::wk(wt, s)));
+    return make_double2(S.x - T.y, S.y + T.x);
+  };
+#pragma unroll
+  for (int hb = 0; hb < 2; ++hb) {
+    SrcZeta::Raw a[4], b[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int s = 4 * hb + j, k = t + s * H::NTH, km = H::M - k;
+      a[j] = b[j] = SrcZeta::zero();
+      if (s * H::NTH < g.kc) a[j] = sz.ld(H::inv(g, k < g.kc ? k : 0, y));
+      if (H::M - (s + 1) * H::NTH < g.kc) b[j] = sz.ld(H::inv(g, km < g.kc ? km : 0, y));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int s = 4 * hb + j, k = t + s * H::NTH, km = H::M - k;
+      double2 x = k < g.kc ? a[j].v : zero2(), xm = km < g.kc ? b[j].v : zero2();
+      if (k == 0) x.y = 0.0;
+      v[s] = comb(x, xm, s);
+      x = k < g.kc ? sz.val(a[j], k, g) : zero2();
+      xm = km < g.kc ? sz.val(b[j], km, g) : zero2();
+      if (k == 0) x.y = 0.0;
+      z[s] = comb(x, xm, s);
+    }
+  }
+}
+
 // r2c output of one real field from v[s] = Z[t + s NTH]: emit(k, s, X[k]) for
 // live k (one LDS round trip for the mirrors Z[M - k])
 template <int LOG2N, typename Emit>
@@ -1133,14 +1172,34 @@ __device__ __forceinline__ void split_real_h(const double2 (&v)[8], int t, const
 #ifndef SW_ROW_H_FLY
 #define SW_ROW_H_FLY true
 #endif
+// rows per block of the half-length rows (experiment knob; NB = 2: the two
+// rows of a block write the two 32-B halves of each 64-B half-line of a 2×4
+// forward tile in lockstep, and blocks b, b + 8 (one XCD) the tile's other
+// two rows — row0_of_block)
+#ifndef SW_ROWH_NB
+#define SW_ROWH_NB 1
+#endif
+#ifndef SW_RSW_ROWH_NB
+#define SW_RSW_ROWH_NB 1
+#endif
+template <int LOG2N, bool RSW = false>
+__host__ __device__ constexpr int rowh_nb();
+// local row of line ln of block b (NB rows per block)
+template <int NB>
+__device__ __forceinline__ int rowh_row(int b, int nb, int ln) {
+  return NB == 1 ? col_of_block(b, nb) : row0_of_block<NB>(b, nb) + ln;
+}
 template <int LOG2N>
-static __global__ void __launch_bounds__(RowH<LOG2N>::NTH, SW_MINW_ROW_H)
+static __global__ void __launch_bounds__(RowH<LOG2N>::NTH * rowh_nb<LOG2N>(), SW_MINW_ROW_H)
     k_row_qg_h(Geom g, Phys p, const double2* __restrict__ Mi, double2* __restrict__ Mo,
                const double2* __restrict__ tw, int yoff) {
   using H = RowH<LOG2N>;
-  extern __shared__ double2 smem[];
-  const int t = threadIdx.x;
-  const int y = yoff + col_of_block(blockIdx.x, gridDim.x);
+  constexpr int NB = rowh_nb<LOG2N>();
+  extern __shared__ double2 smem_all[];
+  const int ln = NB == 1 ? 0 : (int)threadIdx.x / H::NTH;
+  const int t = threadIdx.x - ln * H::NTH;
+  double2* smem = smem_all + ln * FftPlan<H::LM>::LDS;
+  const int y = yoff + rowh_row<NB>(blockIdx.x, gridDim.x, ln);
   Twiddles<H::LM, SW_ROW_H_FLY> tws;  // stage twiddles read per stage: register room
   tws.load(t, tw, 1);                    // W_M^j = W_N^(2j)
   const double2 wt = tw[t];
@@ -1188,14 +1247,32 @@ static __global__ void __launch_bounds__(RowH<LOG2N>::NTH, SW_MINW_ROW_H)
 #ifndef SW_MINW_ROW_RSW_H
 #define SW_MINW_ROW_RSW_H 2
 #endif
+// ζ's c2r input formed from the same read of V as v's and parked in a second
+// line buffer of LDS until η's registers are free (0: V read twice)
+#ifndef SW_RSW_ROWH_ZPARK
+#define SW_RSW_ROWH_ZPARK 1
+#endif
 template <int LOG2N>
-static __global__ void __launch_bounds__(RowH<LOG2N>::NTH, SW_MINW_ROW_RSW_H)
+__host__ __device__ constexpr int rsw_rowh_lines() { return SW_RSW_ROWH_ZPARK ? 2 : 1; }
+template <int LOG2N, bool RSW>
+__host__ __device__ constexpr int rowh_nb() {
+  if constexpr (RSW)
+    return (SW_RSW_ROWH_NB == 2 && 2 * rsw_rowh_lines<LOG2N>() * FftPlan<LOG2N - 1>::LDS * 16 <= 160 * 1024) ? 2 : 1;
+  else
+    return SW_ROWH_NB;
+}
+template <int LOG2N>
+static __global__ void __launch_bounds__((RowH<LOG2N>::NTH * rowh_nb<LOG2N, true>()), SW_MINW_ROW_RSW_H)
     k_row_rsw_h(Geom g, Phys p, const double2* __restrict__ Mi, double2* __restrict__ Mo,
                 const double2* __restrict__ tw, int yoff) {
   using H = RowH<LOG2N>;
-  extern __shared__ double2 smem[];
-  const int t = threadIdx.x;
-  const int y = yoff + col_of_block(blockIdx.x, gridDim.x);
+  constexpr int NB = rowh_nb<LOG2N, true>();
+  extern __shared__ double2 smem_all[];
+  const int ln = NB == 1 ? 0 : (int)threadIdx.x / H::NTH;
+  const int t = threadIdx.x - ln * H::NTH;
+  double2* smem = smem_all + ln * rsw_rowh_lines<LOG2N>() * FftPlan<H::LM>::LDS;
+  double2* park = smem + FftPlan<H::LM>::LDS;  // ZPARK: ζ's c2r input, slots t + s NTH
+  const int y = yoff + rowh_row<NB>(blockIdx.x, gridDim.x, ln);
   Twiddles<H::LM> tws;
   tws.load(t, tw, 1);  // W_M^j = W_N^(2j)
   const double2 wt = tw[t];
@@ -1224,7 +1301,13 @@ static __global__ void __launch_bounds__(RowH<LOG2N>::NTH, SW_MINW_ROW_RSW_H)
   double2 u[8], v[8], e[8], w[8];
   load_real_h<LOG2N>(u, g, t, y, SrcField{U, false}, wt);
   inv(u);
-  load_real_h<LOG2N>(v, g, t, y, SrcField{V, false}, wt);
+  if constexpr (SW_RSW_ROWH_ZPARK) {
+    load_v_zeta_h<LOG2N>(v, e, g, t, y, V, Uy, wt);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) park[t + s * H::NTH] = e[s];  // read back by this thread only
+  } else {
+    load_real_h<LOG2N>(v, g, t, y, SrcField{V, false}, wt);
+  }
   inv(v);
   load_real_h<LOG2N>(e, g, t, y, SrcField{Hh, false}, wt);
   inv(e);
@@ -1242,7 +1325,12 @@ static __global__ void __launch_bounds__(RowH<LOG2N>::NTH, SW_MINW_ROW_RSW_H)
   split_real_h<LOG2N>(w, t, g, smem, wt,
                       [&](int k, int, double2 X) { Mo[3 * MF + H::fwd(g, k, y)] = cmul_i(X, -(k * g.mk)); });
   // ζ = vx - uy in η's registers
-  load_real_h<LOG2N>(e, g, t, y, SrcZeta{V, Uy}, wt);
+  if constexpr (SW_RSW_ROWH_ZPARK) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) e[s] = park[t + s * H::NTH];
+  } else {
+    load_real_h<LOG2N>(e, g, t, y, SrcZeta{V, Uy}, wt);
+  }
   inv(e);
   // 2: (ζu)^
   prod(e, u);
@@ -2662,9 +2750,11 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
   constexpr size_t sh_qg2 = FftPlan<L>::LDS * BQ::NB * sizeof(double2);
   constexpr size_t sh_ty = FftPlan<L>::LDS * BT::NB * sizeof(double2);
   if (model == MODEL_RSW) {
+    constexpr int nbr = rowh_nb<L, true>();
     if constexpr (rsw_row_half<L>())
-      hipLaunchKernelGGL((k_row_rsw_h<L>), dim3(nrows), dim3(RowH<L>::NTH), FftPlan<L - 1>::LDS * sizeof(double2), s,
-                         g, p, Mi, Mo, tw, y0);
+      hipLaunchKernelGGL((k_row_rsw_h<L>), dim3(nrows / nbr), dim3(RowH<L>::NTH * nbr),
+                         nbr * rsw_rowh_lines<L>() * FftPlan<L - 1>::LDS * sizeof(double2), s, g, p, Mi, Mo,
+                         tw, y0);
     else
       hipLaunchKernelGGL((k_row<MODEL_RSW, L>), dim3(nrows / BR::NB), dim3(BR::THREADS), sh_rsw, s, g, p, Mi, Mo,
                          tw, y0, nullptr);
@@ -2685,8 +2775,8 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
       hipLaunchKernelGGL((k_row<MODEL_QG2, L, true>), dim3(nrows / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p, Mi,
                          Mo, tw, y0, Ma);
   } else if constexpr (qg_row_half<L>()) {
-    hipLaunchKernelGGL((k_row_qg_h<L>), dim3(nrows), dim3(RowH<L>::NTH), FftPlan<L - 1>::LDS * sizeof(double2), s, g,
-                       p, Mi, Mo, tw, y0);
+    hipLaunchKernelGGL((k_row_qg_h<L>), dim3(nrows / rowh_nb<L>()), dim3(RowH<L>::NTH * rowh_nb<L>()),
+                       rowh_nb<L>() * FftPlan<L - 1>::LDS * sizeof(double2), s, g, p, Mi, Mo, tw, y0);
   } else {
     hipLaunchKernelGGL((k_row<MODEL_QG2, L>), dim3(nrows / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p, Mi, Mo, tw,
                        y0, nullptr);
@@ -2856,9 +2946,9 @@ int row_lines_per_block(int model, int log2nx) {
   by_len(log2nx, [&](auto L) {
     constexpr int l = decltype(L)::value;
     nb = model == MODEL_RSWA ? BlkRow<MODEL_RSWA, l>::NB
-       : model == MODEL_RSW ? (rsw_row_half<l>() ? 1 : BlkRow<MODEL_RSW, l>::NB)
+       : model == MODEL_RSW ? (rsw_row_half<l>() ? rowh_nb<l, true>() : BlkRow<MODEL_RSW, l>::NB)
                             : (model == MODEL_TY ? BlkRow<MODEL_TY, l>::NB
-                                                 : (qg_row_half<l>() ? 1 : BlkRow<MODEL_QG2, l>::NB));
+                                                 : (qg_row_half<l>() ? rowh_nb<l>() : BlkRow<MODEL_QG2, l>::NB));
   });
   return nb;
 }

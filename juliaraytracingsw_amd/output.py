@@ -184,6 +184,17 @@ def restart(prob, filename, field="sol"):
         if "checkpoint/blob" in d.files:
             prob.ctx.set_checkpoint(d["checkpoint/blob"])
             return int(d["checkpoint/step"])
+        if "checkpoint/sol" in d.files:  # a checkpoint written before the blob (round 2 format)
+            prob.sol = d["checkpoint/sol"]
+            step = int(d["checkpoint/step"])
+            prob.clock.set(float(d["checkpoint/t"]), step)
+            k = 1
+            while f"checkpoint/history/{k}" in d.files:
+                prob.ctx.set_history(k, d[f"checkpoint/history/{k}"])
+                k += 1
+            if k == 1 and prob.ctx.history_slots() > 0:
+                prob.ctx.reset_history()
+            return step
     key = snapshot_keys(filename, field)[-1]
     step = int(key.rsplit("/", 1)[1])
     with np.load(filename) as d:

@@ -3,7 +3,7 @@ three drivers the north star names, through include/sw.h.
 
 Julia is not installed here, so the Julia shim cannot run.  This module is
 its Python twin: every SWLib.jl function that reaches libsw has a function
-of the same name here (``run_steps!`` -> ``run_steps`` …) issuing the same C
+of the same name here (``flush!`` -> ``flush`` …) issuing the same C
 entry points in the same order (tests/test_julia_shim.py checks that by
 text), plus host stand-ins for the FourierFlows objects the drivers touch
 (Problem, Clock, Diagnostic, vars).  The replays transcribe the drivers'
@@ -71,11 +71,45 @@ class Diagnostic:
         self.i = 1
 
 
+def increment(diags):
+    """FF increment!(diags): each Diagnostic whose freq divides clock.step
+    stores calc(prob) (a full one is left as it is)."""
+    for d in diags:
+        clock = d.prob.clock
+        if clock.step % d.freq == 0 and d.i < len(d.t):
+            d.value = d.calc(d.prob)
+            d.data[d.i], d.t[d.i], d.steps[d.i] = d.value, float(clock.t), clock.step
+            d.i += 1
+
+
+def ff_stepforward(tw, prob, diags, nsteps):
+    """FourierFlows' own stepforward!(prob, diags, nsteps), which SWLib does
+    not redefine: stepforward!(prob) (-> the per-step seam, dispatched on the
+    SWStepper) and increment!(diags) per step."""
+    for _ in range(nsteps):
+        tw.stepforward_seam(prob.sol, prob.clock, prob.timestepper, prob.eqn, prob.vars, prob.params, prob.grid)
+        increment(diags)
+
+
 # ------------------------------------------------------------------- the twin
 class SWStepper:
     def __init__(self, ctx, filt, model):
         self.ctx, self.filter, self.model = ctx, filt, model
-        self.freq, self.seen, self.record_t, self.blewup = 0, 0, [], False
+        self.pending, self.synced, self.rec, self.rec_step, self.blewup = 0, True, None, -1, False
+
+
+def is_sw(prob):
+    return isinstance(prob.timestepper, SWStepper)
+
+
+def as_T(T, x):
+    """SWLib.as_T: the energy in the Problem's real type (FF's Diagnostic
+    holds what the reference's function returns for T)"""
+    if isinstance(x, tuple):
+        return tuple(as_T(T, y) for y in x)
+    if isinstance(x, list):
+        return [T(y) for y in x]
+    return T(x)
 
 
 class Twin:
@@ -84,7 +118,6 @@ class Twin:
     def __init__(self):
         self.lib = _lib.load()
         self.calls = []
-        self.RECORD = {}
 
     def c(self, name, *args):
         self.calls.append(name)
@@ -144,9 +177,11 @@ class Twin:
 
     def load_solution(self, prob):
         ts = prob.timestepper
+        ts.pending = 0
         self.upload(ts, prob.sol)
         self.download(prob.sol, ts)
         self.push_clock(ts, prob.clock)
+        ts.synced, ts.rec_step, ts.blewup = True, -1, False
 
     def physical(self, dst, ts, fid):
         """dst: a host [ny][nx] array (Julia (nx, ny)) or one layer of one"""
@@ -154,67 +189,75 @@ class Twin:
         return dst
 
     # -- stepping and records --------------------------------------------------
-    def run_steps(self, sol, clock, ts, n):
+    def stepforward_seam(self, sol, clock, ts, equation, vars_, params, grid):
+        """FourierFlows.stepforward!(sol, clock, ts::SWStepper, …): counts the
+        step, advances the clock in the Problem's arithmetic; no C call."""
+        ts.pending += 1
+        ts.synced = False
+        clock.t = clock.T(clock.t + clock.dt)
+        clock.step += 1
+
+    def flush(self, prob):
+        ts = prob.timestepper
+        if ts.pending == 0:
+            return
+        n, ts.pending = ts.pending, 0
         rc = self.c("sw_step", ts.ctx, int(n))
         ts.blewup = rc == SW_E_NAN
         if not ts.blewup:
             self.check(ts, rc, "sw_step")
-        for _ in range(n):
-            clock.t = clock.T(clock.t + clock.dt)
-            clock.step += 1
-            if ts.freq > 0 and clock.step % ts.freq == 0:
-                ts.record_t.append(float(clock.t))
-        self.download(sol, ts)
-
-    def attach_diagnostics(self, prob, diags):
-        ts = prob.timestepper
-        if not diags:
-            return
-        freq = diags[0].freq
-        if any(d.freq != freq for d in diags):
-            raise _lib.LibSWError("libsw records one diagnostics frequency per problem")
-        if any(d.calc not in self.RECORD for d in diags):
-            raise _lib.LibSWError("libsw records the models' energy diagnostics only")
-        cap = max(len(d.t) for d in diags)
-        self.check(ts, self.c("sw_set_energy_diagnostics", ts.ctx, int(freq), int(cap)), "sw_set_energy_diagnostics")
-        ts.freq, ts.seen = freq, 0
-        ts.record_t.clear()
-
-    def take_records(self, prob, diags):
-        ts = prob.timestepper
-        n = C.c_int64()
-        self.check(ts, self.c("sw_get_energy_diagnostics", ts.ctx, None, 0, C.byref(n)), "sw_get_energy_diagnostics")
-        if n.value <= ts.seen:
-            return
-        recs = (_lib.SwEnergyRecord * n.value)()
-        self.check(ts, self.c("sw_get_energy_diagnostics", ts.ctx, recs, n.value, C.byref(n)),
-                   "sw_get_energy_diagnostics")
-        for k, r in enumerate(recs[ts.seen:n.value]):
-            for d in diags:
-                if d.i >= len(d.t):
-                    continue
-                d.data[d.i] = self.RECORD[d.calc](r, d.value)
-                d.t[d.i] = ts.record_t[ts.seen + k]
-                d.steps[d.i] = r.step
-                d.value = d.data[d.i]
-                d.i += 1
-        ts.seen = n.value
-
-    def stepforward(self, prob, diags, nsteps):
-        """FourierFlows.stepforward!(prob, diags, nsteps) for a libsw problem."""
-        ts = prob.timestepper
-        if ts.freq == 0:
-            self.attach_diagnostics(prob, diags)
-        self.run_steps(prob.sol, prob.clock, ts, nsteps)
-        self.take_records(prob, diags)
         if ts.blewup:
-            blowup(prob)
+            self.blowup(prob)
 
+    def sync(self, prob):
+        ts = prob.timestepper
+        self.flush(prob)
+        if not ts.synced:
+            self.download(prob.sol, ts)
+        ts.synced = True
 
-def blowup(prob):
-    for name in ("η", "q", "u", "v"):
-        if hasattr(prob.vars, name):
-            getattr(prob.vars, name)[...] = np.nan
+    def device_energy(self, prob, pick):
+        ts = prob.timestepper
+        if ts.pending > 0:
+            n, ts.pending = ts.pending, 0
+            r = _lib.SwEnergyRecord()
+            rc = self.c("sw_step_record", ts.ctx, int(n), C.byref(r))
+            ts.blewup = rc == SW_E_NAN
+            if not ts.blewup:
+                self.check(ts, rc, "sw_step_record")
+            ts.rec, ts.rec_step = r, prob.clock.step
+            if ts.blewup:
+                self.blowup(prob)
+        elif ts.rec_step != prob.clock.step:
+            ts.rec, ts.rec_step = self.diag_record(ts, prob.clock), prob.clock.step
+        return as_T(np.float32 if prob.sol.dtype == np.complex64 else np.float64, pick(ts.rec))
+
+    def diag_record(self, ts, clock):
+        def d(i):
+            x = C.c_double()
+            self.check(ts, self.c("sw_diag", ts.ctx, int(i), C.byref(x)), "sw_diag")
+            return x.value
+
+        r = _lib.SwEnergyRecord()
+        r.step, r.t = clock.step, float(clock.t)
+        if ts.model == _lib.SW_MODEL_TY:
+            r.ke, r.ke2, r.pe = d(1), d(6), d(2)  # SW_DIAG_KE, BT, PE
+            for k in range(4):
+                r.wg[k] = d(7 + k)  # SW_DIAG_WAVE_KE ..
+        else:
+            r.ke, r.ke2, r.pe = d(5), d(4), d(2)  # SW_DIAG_KE1, KE2, PE
+        return r
+
+    @staticmethod
+    def blowup(prob):
+        for name in ("η", "q", "u", "v"):
+            if hasattr(prob.vars, name):
+                getattr(prob.vars, name)[...] = np.nan
+
+    def energy_method(self, host_fn, pick):
+        """SWLib.energy_methods!: the model's energy function with the libsw
+        method in front (device value for a libsw problem, else the host's)"""
+        return lambda pr: self.device_energy(pr, pick) if is_sw(pr) else host_fn(pr)
 
 
 def _host_vars(grid, T, spec, phys, nlayers=None):
@@ -294,6 +337,8 @@ def mlqg_problem(tw, nlayers, *, nx, Lx, f0, H, b, U, mu, beta, dt, stepper="Fil
 # -------------------------------------------------- updatevars! on the device
 def rsw_updatevars(tw, prob):
     v, g, sol, ts = prob.vars, prob.grid, prob.sol, prob.timestepper
+    tw.sync(prob)
+    g.dealias(sol)  # :104
     v.uh[...], v.vh[...], v.ηh[...] = sol[0], sol[1], sol[2]
     v.ζh[...] = 1j * g.kr[None, :] * v.vh - 1j * g.l[:, None] * v.uh - prob.params.f * v.ηh
     tw.physical(v.u, ts, 0)
@@ -304,6 +349,7 @@ def rsw_updatevars(tw, prob):
 
 def ty_updatevars(tw, prob, all_=True):
     v, g, sol, ts = prob.vars, prob.grid, prob.sol, prob.timestepper
+    tw.sync(prob)
     v.ζth[...], v.uch[...], v.vch[...], v.pch[...] = sol[0], sol[1], sol[2], sol[3]
     tw.physical(v.ζt, ts, 3)
     tw.physical(v.uc, ts, 0)
@@ -323,6 +369,7 @@ def ty_updatevars(tw, prob, all_=True):
 
 def mlqg_updatevars(tw, prob):
     v, g, sol, p, ts = prob.vars, prob.grid, prob.sol, prob.params, prob.timestepper
+    tw.sync(prob)
     v.qh[...] = sol
     v.ψh[...] = O.mlqg_streamfunction(v.qh.astype(np.complex128), g, p)
     v.uh[...] = -1j * g.l[:, None] * v.ψh
@@ -382,15 +429,16 @@ def rsw_driver_start(tw, nx=128, nsteps=240, output_freq=20, diags_freq=10, spin
     # start! (:184-226)
     outputs = [("problem",)]
 
-    def kinetic_energy(pr):  # rsw/RotatingShallowWater.jl:323-327 on the host vars
+    def host_kinetic_energy(pr):  # rsw/RotatingShallowWater.jl:323-327 on the host vars
         v = pr.vars
         return (O.parsevalsum2(v.uh, grid) + O.parsevalsum2(v.vh, grid)) / (2 * grid.Lx * grid.Ly)
 
-    def potential_energy(pr):  # :329-333
+    def host_potential_energy(pr):  # :329-333
         return 0.5 * float(params.Cg2) * O.parsevalsum2(pr.vars.ηh, grid) / (grid.Lx * grid.Ly)
 
-    tw.RECORD[kinetic_energy] = lambda r, v: r.ke
-    tw.RECORD[potential_energy] = lambda r, v: r.pe
+    # RotatingShallowWater.kinetic_energy / potential_energy after SWLib.attach!
+    kinetic_energy = tw.energy_method(host_kinetic_energy, lambda r: r.ke)
+    potential_energy = tw.energy_method(host_potential_energy, lambda r: r.pe)
     diags = [Diagnostic(kinetic_energy, prob, nsteps=nsteps, freq=diags_freq),
              Diagnostic(potential_energy, prob, nsteps=nsteps, freq=diags_freq)]
     # enforce_reality_condition! (:118-133): the reference's method; its
@@ -405,7 +453,7 @@ def rsw_driver_start(tw, nx=128, nsteps=240, output_freq=20, diags_freq=10, spin
         if step % 100 == 0:
             v = prob.vars
             cfls.append(float(prob.clock.dt) * max(np.max(np.abs(v.u)) / grid.dx, np.max(np.abs(v.v)) / grid.dy))
-        tw.stepforward(prob, diags, output_freq)
+        ff_stepforward(tw, prob, diags, output_freq)
         if np.any(np.isnan(prob.vars.η)):
             raise RuntimeError("Solution is NaN")
         rsw_updatevars(tw, prob)
@@ -431,14 +479,15 @@ def ty_driver_start(tw, nx=64, startup_dt=3e-2, dt=5e-3, startup_nsteps=200, sta
     ty_set_solution(tw, sp, *ic)
     ic = sp.sol.copy()
 
-    def wave_geostrophic_energy(pr):
+    def host_wave_geostrophic_energy(pr):
         return O.ty_energies(pr.sol.copy(), grid)[2]
 
-    def barotropic_energy(pr):
+    def host_barotropic_energy(pr):
         return O.ty_energies(pr.sol.copy(), grid)[0]
 
-    tw.RECORD[wave_geostrophic_energy] = lambda r, v: ((r.wg[0], r.wg[1]), (r.wg[2], r.wg[3]))
-    tw.RECORD[barotropic_energy] = lambda r, v: r.ke2
+    wave_geostrophic_energy = tw.energy_method(host_wave_geostrophic_energy,
+                                               lambda r: ((r.wg[0], r.wg[1]), (r.wg[2], r.wg[3])))
+    barotropic_energy = tw.energy_method(host_barotropic_energy, lambda r: r.ke2)
     diags = [Diagnostic(wave_geostrophic_energy, sp, nsteps=startup_nsteps, freq=25),
              Diagnostic(barotropic_energy, sp, nsteps=startup_nsteps, freq=25)]
     outputs = [("startup",)]
@@ -450,7 +499,7 @@ def ty_driver_start(tw, nx=64, startup_dt=3e-2, dt=5e-3, startup_nsteps=200, sta
             v = sp.vars
             _ = float(sp.clock.dt) * max(v.uc.max() / grid.dx, v.vc.max() / grid.dy, v.ut.max() / grid.dx,
                                          v.vt.max() / grid.dy)
-        tw.stepforward(sp, diags, startup_nsubs)
+        ff_stepforward(tw, sp, diags, startup_nsubs)
         startup_steps += startup_nsubs
         ty_updatevars(tw, sp, all_=False)  # enforce_reality_condition!
         ty_updatevars(tw, sp)
@@ -467,7 +516,7 @@ def ty_driver_start(tw, nx=64, startup_dt=3e-2, dt=5e-3, startup_nsteps=200, sta
     ty_updatevars(tw, prob)
     outputs.append((prob.clock.step, prob.sol.copy()))
     for j in range(0, round(nsteps / nsubs) + 1):
-        tw.stepforward(prob, diags, nsubs)
+        ff_stepforward(tw, prob, diags, nsubs)
         ty_updatevars(tw, prob, all_=False)
         ty_updatevars(tw, prob)
         outputs.append((prob.clock.step, prob.sol.copy()))
@@ -500,18 +549,19 @@ def mlqg_simulation_start(tw, nx=64, nsteps=100, nsubs=25, seed=1234, amplitude_
     mlqg_set_q(tw, prob, q0)
     ic = prob.sol.copy()
 
-    def energies(pr):
+    def host_energies(pr):
         KE, PE = O.mlqg_energies(pr.sol.copy(), grid, pr.params)
-        return (tuple(KE), (PE,))
+        return (list(KE), [PE])
 
-    tw.RECORD[energies] = lambda r, v: ((r.ke, r.ke2), (r.pe,))
+    # GF MultiLayerQG.energies: per-layer KE vector, PE vector
+    energies = tw.energy_method(host_energies, lambda r: ([r.ke, r.ke2], [r.pe]))
     diags = [Diagnostic(energies, prob, nsteps=nsteps)]
     outputs = [("problem",)]
     for j in range(0, round(nsteps / nsubs) + 1):
         if j % (1000 / nsubs) == 0:
             v = prob.vars
             _ = float(prob.clock.dt) * max(v.u.max() / grid.dx, v.v.max() / grid.dy)
-        tw.stepforward(prob, diags, nsubs)
+        ff_stepforward(tw, prob, diags, nsubs)
         mlqg_updatevars(tw, prob)
         outputs.append((prob.clock.step, prob.vars.ψh.copy()))
     return prob, diags, outputs, ic

@@ -197,3 +197,32 @@ def test_rejected_where_not_built(bad):
         cfg.nranks = cfg.local_slabs = 2
     with pytest.raises(LibSWError, match="aliased_state"):
         _lib.Context(cfg)
+
+
+@pytest.mark.parametrize("stepper", ["IFMAB3", "IFMRK4"])
+def test_nop_calcN_zeroes_the_aliased_N(stepper):
+    """With NOPcalcN! (rsw/RotatingShallowWater.jl:135) N is zero on every
+    mode, the aliased ones included (their N buffers were left as
+    they were): the IF steppers then propagate the full state linearly,
+    exp(n dt L)·sol0 per mode, at the aliased modes too."""
+    from juliaraytracingsw_amd import rotating_shallow_water as RSW
+
+    n, dt, steps = 64, 0.01, 7
+    g = O.TwoDGrid(n)
+    prob = RSW.Problem("gpu", nx=n, dt=dt, nu=1e-9, f=3.0, Cg=1.0, stepper=stepper, nop_calcN=True,
+                       aliased_state=True)
+    rng = np.random.default_rng(7)
+    ic = rng.standard_normal((3, n, n // 2 + 1)) + 1j * rng.standard_normal((3, n, n // 2 + 1))
+    c0 = ic[:, :, 0]
+    ic[:, :, 0] = 0.5 * (c0 + np.conj(c0[:, (-np.arange(n)) % n]))  # a real field's kr = 0 column
+    ic[:, :, -1] = 0.0  # the Nyquist column is not carried
+    prob.ctx.set_state(ic)
+    x = prob.ctx.get_state()
+    mask = _aliased_mask(g)
+    assert np.max(np.abs(x[:, mask])) > 0.1  # the aliased modes are held
+    assert np.max(np.abs(prob.calcN(x))) == 0.0
+    prob.ctx.step(steps)
+    L = O.rsw_L(g, O.RSWParams(1e-9, 4, 3.0, 1.0))
+    exact = O.mvmul(O.expm_batched(L * (steps * dt)), x)
+    assert _full_err(prob.ctx.get_state(), exact) < 1e-12
+    prob.close()

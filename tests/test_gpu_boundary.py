@@ -211,3 +211,74 @@ def test_step_alg_bytes_counts_every_stage(name):
     per_step = sum(s["alg_bytes"] * s["launches"] for s in stats if s["name"] != "transpose") / nst
     assert prob.ctx.step_alg_bytes() == pytest.approx(per_step, rel=1e-12)
     prob.close()
+
+
+def test_legacy_checkpoint_file_restarts(tmp_path):
+    """A checkpoint file written before the fp64 blob (round-2 layout:
+    checkpoint/sol, t, step, history/k) still restarts: state, clock and
+    history are set from it, bitwise for fp64 buffers."""
+    import zipfile
+
+    p = sw_cases.case_params("rsw_fab3", 64)
+    g = O.TwoDGrid(64, aliased_fraction=p.get("af", 1 / 3))
+    a = sw_cases.libsw_problem(p)
+    a.sol = sw_cases.initial_condition(p, g)
+    a.stepforward(9)
+    fn = str(tmp_path / "old.jld2")
+    t, step = a.ctx.get_clock()
+    with zipfile.ZipFile(fn, "w") as zf:
+        output._put(zf, "checkpoint/sol", a.ctx.get_state())
+        output._put(zf, "checkpoint/t", t)
+        output._put(zf, "checkpoint/step", step)
+        for k in (1, 2):
+            output._put(zf, f"checkpoint/history/{k}", a.ctx.get_history(k))
+    a.stepforward(6)
+    b = sw_cases.libsw_problem(p)
+    assert output.restart(b, fn) == 9
+    b.stepforward(6)
+    assert np.array_equal(a.sol, b.sol) and b.ctx.get_clock() == a.ctx.get_clock()
+    a.close()
+    b.close()
+
+
+def test_checkpoint_aliased_state_must_match():
+    """An aliased_state blob carries modes a default context would drop (and
+    the reverse lacks them): sw_set_checkpoint refuses the mismatch instead of
+    continuing non-bitwise."""
+    p = sw_cases.case_params("qg2_ifmab3", 64)
+    a = sw_cases.libsw_problem(p, aliased_state=True)
+    b = sw_cases.libsw_problem(p)
+    a.stepforward(3)
+    b.stepforward(3)
+    with pytest.raises(_lib.LibSWError, match="aliased_state"):
+        b.ctx.set_checkpoint(a.ctx.get_checkpoint())
+    with pytest.raises(_lib.LibSWError, match="aliased_state"):
+        a.ctx.set_checkpoint(b.ctx.get_checkpoint())
+    a.ctx.set_checkpoint(a.ctx.get_checkpoint())
+    a.close()
+    b.close()
+
+
+@pytest.mark.parametrize("name", ["rsw_fab3", "rsw_ifmab3", "rsw_ifmrk4", "qg2_ifmab3", "ty_etdrk4", "mlqg_frk4"])
+def test_step_record_matches_the_recorded_diagnostics(name):
+    """sw_step_record(n) (ABI 9, the lazy Julia seam's energy at a
+    Diagnostic step) steps n times and returns exactly the record
+    sw_set_energy_diagnostics keeps for that step, on the same state."""
+    p = sw_cases.case_params(name, 64)
+    g = O.TwoDGrid(64, Lx=p.get("Lx", 2 * np.pi), aliased_fraction=p.get("af", 1 / 3))
+    ic = sw_cases.initial_condition(p, g)
+    a, b = sw_cases.libsw_problem(p), sw_cases.libsw_problem(p)
+    a.sol = ic
+    b.sol = ic
+    a.ctx.set_energy_diagnostics(5, 10)
+    a.ctx.step(15)
+    recs = a.ctx.energy_diagnostics()
+    got = [b.ctx.step_record(5) for _ in range(3)]
+    assert [r[0] for r in got] == [r[0] for r in recs] == [5, 10, 15]
+    for r, q in zip(got, recs):
+        assert r[1:5] == q[1:5] and r[5] == q[5]  # bitwise: the same reduction
+    assert np.array_equal(a.sol, b.sol)
+    with pytest.raises(_lib.LibSWError):
+        b.ctx.step_record(0)
+    a.close()
+    b.close()
