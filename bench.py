@@ -28,6 +28,10 @@ Extra keys on the same JSON line (never `value`):
       GPUs (one GPU at N = 1), steps/s (--no-config4 to skip);
   `host_boundary` — one state download/upload through the C ABI over PCIe,
       and the rate with the driver's per-frame download;
+  `comm` (N > 1, slab) — the exchange explained (sw_comm_profile): transport,
+      RCCL rank count, schedule (pipelined / sequential, row chunks) and per
+      rank the compute-stream µs per step spent waiting for transposes, the
+      step's µs and the bytes sent per step (also in `config5` / `config4`);
   `cpu_baseline` — rank 0 at N = 1 only.
 """
 import argparse
@@ -243,6 +247,20 @@ def main():
 
     from juliaraytracingsw_amd import slab_comm
 
+    def comm_report(prob, nsteps=10):
+        """sw_comm_profile on every rank (collective), gathered to every rank"""
+        if world == 1:
+            return None
+        st = prob.ctx.comm_profile(nsteps)
+        per = [None] * world
+        dist.all_gather_object(per, dict(rank=rank, exposed_transpose_us_per_step=st["exposed_transpose_us"],
+                                         step_us=st["step_us"], sent_MB_per_step=st["sent_bytes_per_step"] / 1e6))
+        ex = max(r["exposed_transpose_us_per_step"] for r in per)
+        return {"transport": st["transport"], "rccl_ranks": st["rccl_ranks"], "nranks": st["nranks"],
+                "schedule": st["schedule"], "row_chunks": st["row_chunks"], "profiled_steps": nsteps,
+                "exposed_transpose_us_per_step_max": ex,
+                "exposed_fraction_of_step": ex / max(r["step_us"] for r in per), "per_rank": per}
+
     def decomposition():
         if world == 1:
             return None
@@ -329,6 +347,7 @@ def main():
         prob, P = make_problem(args.model, args.n, args.stepper, local, None, over)
         elapsed = timed(prob, args.warmup, args.steps)
 
+    comm = comm_report(prob) if slab else None
     # roofline: per-kernel HIP-event durations on libsw's stream
     stats = prob.ctx.profile(args.profile_steps)
     step_alg = prob.ctx.step_alg_bytes()
@@ -364,6 +383,7 @@ def main():
     def extra_config(model, n, stepper, steps, warmup, label):
         ex, _ = make_problem(model, n, stepper, local, decomposition())
         te = timed(ex, warmup, steps, label)
+        cx = comm_report(ex, 3)
         sx = ex.ctx.profile(3)
         ex.close()
         del ex
@@ -371,7 +391,7 @@ def main():
                 "ms_per_step": te / steps * 1e3, "scaling": "strong" if world > 1 else None,
                 "workload": f"{label} fp64, " + (f"slab{world}" if world > 1 else "single-gpu"),
                 "kernels": [{"name": s["name"], "avg_us": s["avg_ms"] * 1e3, "per_step": s["launches"] / 3}
-                            for s in sx]}
+                            for s in sx], "comm": cx}
 
     headline_cfg = (args.model, args.n, args.stepper) == ("rsw", 2048, "FilteredAB3")
     config5 = config4 = None
@@ -454,6 +474,7 @@ def main():
                      "alg_bytes": s["alg_bytes"]} for s in stats],
         "ensemble": ensemble,
         "slab_error": slab_error,
+        "comm": comm,
         "config5": config5,
         "config4": config4,
         "cpu_baseline": cpu,

@@ -185,6 +185,37 @@ def expm_batched(A):
     return out.reshape(sh)
 
 
+def expm_2x2(A):
+    """exp of a batch of 2×2 matrices in closed form (the 2LQG/MLQG operators;
+    utils/IFMAB3.jl:26-30 takes Julia's Padé ``exp`` per mode): with m the
+    half trace and B = A − m I (traceless, B² = δ² I, δ² = p² + b c),
+    exp(A) = e^m (cosh δ I + sinh(δ)/δ B), both even in δ (no branch), series
+    for small |δ|.  Checked against scipy's expm per mode in
+    tests/test_oracle.py; it makes the 8192² oracle run affordable (scipy's
+    expm over 33.5 M matrices is not)."""
+    a, b, c, d = A[..., 0, 0], A[..., 0, 1], A[..., 1, 0], A[..., 1, 1]
+    m = 0.5 * (a + d)
+    p = 0.5 * (a - d)
+    d2 = p * p + b * c
+    dl = np.sqrt(d2)
+    small = np.abs(d2) < 1e-6
+    with np.errstate(invalid="ignore", divide="ignore"):
+        ch = np.where(small, 1 + d2 / 2 + d2 * d2 / 24 + d2 ** 3 / 720, np.cosh(dl))
+        sh = np.where(small, 1 + d2 / 6 + d2 * d2 / 120 + d2 ** 3 / 5040, np.sinh(dl) / np.where(small, 1, dl))
+    em = np.exp(m)
+    out = np.empty(A.shape, np.complex128)
+    out[..., 0, 0] = em * (ch + sh * p)
+    out[..., 1, 1] = em * (ch - sh * p)
+    out[..., 0, 1] = em * (sh * b)
+    out[..., 1, 0] = em * (sh * c)
+    return out
+
+
+def expm_modes(A):
+    """Per-mode exp: the closed form for 2×2 operators, scipy's expm otherwise."""
+    return expm_2x2(A) if A.shape[-2:] == (2, 2) else expm_batched(A)
+
+
 def mvmul(A, x):
     """``mvmul!`` (utils/IFMAB3.jl:90-100, 124-127): y[…,r] = Σ_c A[…,r,c] x[…,c].
 
@@ -739,8 +770,8 @@ class IFMRK4:
     """
 
     def __init__(self, L, dt, grid, nf, use_filter=False, **filter_kw):
-        self.expLdt = expm_batched(L * dt)
-        self.expLhdt = expm_batched(L * 0.5 * dt)
+        self.expLdt = expm_modes(L * dt)
+        self.expLhdt = expm_modes(L * 0.5 * dt)
         if use_filter:
             self.filter = makefilter(grid, **filter_kw)[None]
         else:

@@ -17,6 +17,10 @@
 
 What the RCCL transport itself adds (the same blocks moved by grouped
 ncclSend/ncclRecv between processes) runs on the driver's multi-GPU node."""
+import json
+import os
+import sys
+
 import numpy as np
 import pytest
 
@@ -97,3 +101,44 @@ def test_config5_qg2_8192_ifmrk4():
     assert np.isfinite(a.sol).all()
     a.close()
     b.close()
+
+
+@pytest.mark.timeout(600)
+def test_config5_stepped_state_matches_the_oracle():
+    """BASELINE config 5 at full size, nonlinear: TwoLayerQG
+    8192² IFMRK4 from the seeded driver IC, two full steps, libsw on one slab
+    and on eight (in-process) against the oracle's two steps
+    (tests/golden/make_qg2_8192.py; its fixture keeps 24 l rows of the
+    state, every live kr, both layers).  Within 1e-10 of the sample's
+    magnitude, where the nonlinear part of the sample is far larger; the
+    eight-slab state bitwise the one-slab state; the full per-layer sums of
+    |q̂|² within 1e-12."""
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import make_qg2_8192 as M
+
+    fx = np.load(os.path.join(os.path.dirname(__file__), "golden", "qg2_ifmrk4_8192_rows.npz"))
+    rows, kc, steps = fx["rows"], int(fx["kc"]), int(fx["steps"])
+    p = sw_cases.case_params("qg2_ifmrk4", 8192)
+    assert json.loads(str(fx["params"])) == json.loads(json.dumps(p))
+    g = O.TwoDGrid(8192)
+    ic = g.dealias(sw_cases.initial_condition(p, g))
+    # the box's seeded IC is the generator's (numpy's PCG64 + pocketfft)
+    assert np.allclose(M.ic_check(ic[:, rows, :kc]), fx["ic_check"], rtol=1e-12, atol=0)
+    ref = fx["sol_rows"]
+    scale = np.max(np.abs(ref))
+    nonlinear = float(fx["nonlinear_part"])
+    assert nonlinear > 1e-6  # the nonlinear term moved the sample (2.0e-5 of it), 1e5 x the tolerance
+    got = {}
+    for P in (1, 8):
+        kw = {} if P == 1 else dict(decomposition=dict(nranks=8, local_slabs=8))
+        a = sw_cases.libsw_problem(p, **kw)
+        a.sol = ic
+        a.stepforward(steps)
+        got[P] = a.sol
+        a.close()
+    assert np.array_equal(got[1], got[8])
+    e = np.max(np.abs(got[1][:, rows, :kc] - ref)) / scale
+    print(f"[config5] 8192² IFMRK4, {steps} steps: sample error {e:.2e} of its max; nonlinear part {nonlinear:.2e}")
+    assert e < 1e-10, e
+    ss = np.array([np.sum(np.abs(got[1][f]) ** 2) for f in range(2)])
+    assert np.allclose(ss, fx["sumsq"], rtol=1e-12, atol=0), (ss, fx["sumsq"])

@@ -4,6 +4,7 @@ the committed golden fixtures against it."""
 import glob
 import json
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -380,7 +381,7 @@ def test_fab3_driver_params_stability_boundary(n, unstable):
 
 
 # --- golden fixtures -----------------------------------------------------------
-GOLDEN_FILES = sorted(glob.glob(os.path.join(GOLDEN, "*.npz")))
+GOLDEN_FILES = sorted(f for f in glob.glob(os.path.join(GOLDEN, "*.npz")) if not f.endswith("_rows.npz"))
 
 
 def test_golden_present():
@@ -403,3 +404,43 @@ def test_oracle_reproduces_golden(fn):
         pr.stepforward(s - done)
         done = s
         assert O.parity_error(pr.sol, d[key], pr.grid) < 1e-12, key
+
+
+# --- closed-form 2×2 integrating factors (the 8192² oracle) -------------------
+@pytest.mark.parametrize("model", ["qg2", "mlqg"])
+@pytest.mark.parametrize("tau", [1e-4, 0.05, 0.5, 5.0])
+def test_expm_2x2_matches_scipy(model, tau):
+    """sw_oracle.expm_2x2 (cosh/sinh of the traceless part) equals scipy's
+    expm mode by mode (≤ 1e-11 of each mode's matrix norm), for the 2LQG
+    (with its Float32 literals) and MultiLayerQG operators."""
+    g = O.TwoDGrid(64, aliased_fraction=0.0 if model == "mlqg" else 1 / 3)
+    if model == "qg2":
+        L = O.qg2_L(g, O.QG2Params(0.5, 1e-2, 1e-6, 4))
+    else:
+        P = O.mlqg_simulation_params(64)
+        L = O.mlqg_L(g, O.MLQGParams(P["f0"], P["H"], P["b"], P["U"], P["mu"], P["beta"], 1e-6, 4))
+        if L.ndim == 3:  # a diagonal operator: promote
+            L = np.stack([np.stack([L[0], 0 * L[0]], -1), np.stack([0 * L[1], L[1]], -1)], -2)
+    a, b = O.expm_batched(L * tau), O.expm_2x2(L * tau)
+    na = np.linalg.norm(a, axis=(-2, -1))
+    # worst modes: the strongly damped ones (norms ~1e-100, where the
+    # scaling-and-squaring of expm loses digits) and, at dt·L ~ 200i, the
+    # cancellation in δ² = p² + bc (≈ 1e4·eps); the median mode to < 1e-14
+    r = np.linalg.norm(a - b, axis=(-2, -1)) / np.maximum(na, 1e-300)  # (underflowed modes: both 0)
+    assert np.max(r) < 1e-11
+    assert np.median(r) < 1e-14
+
+
+def test_config5_fixture_ic_is_the_seeded_driver_ic():
+    """tests/golden/qg2_ifmrk4_8192_rows.npz was generated from the seeded
+    driver IC that the GPU test regenerates (numpy PCG64 + pocketfft)."""
+    fx = np.load(os.path.join(GOLDEN, "qg2_ifmrk4_8192_rows.npz"))
+    p = sw_cases.case_params("qg2_ifmrk4", 8192)
+    assert json.loads(str(fx["params"])) == json.loads(json.dumps(p))
+    g = O.TwoDGrid(8192)
+    ic = g.dealias(sw_cases.initial_condition(p, g))
+    sys.path.insert(0, GOLDEN)
+    import make_qg2_8192 as M
+
+    rows, kc = fx["rows"], int(fx["kc"])
+    assert np.allclose(M.ic_check(ic[:, rows, :kc]), fx["ic_check"], rtol=1e-12, atol=0)
