@@ -417,6 +417,61 @@ __device__ __forceinline__ void dft_w(double2 (&a)[W]) {
   else dft8<DIR>(a);
 }
 
+// Pruned radix-W butterflies of the decimated transforms (PRUNE): the
+// row transforms' inputs are zero, and their outputs unused, at the natural
+// positions [3N/8, 5N/8) — slots s = 3 and 4 of every thread — whenever the
+// live band kc <= 3N/8 (the 2/3 rule: kc = N/3): the inverse inputs there are
+// the dealiased modes kc <= k <= N - kc, the forward outputs k there are
+// neither live (k < kc) nor a live mirror (N - k < kc).  ZM: bit q set ->
+// a[q] is zero (inputs, DIF) or not needed (outputs, DIT).
+__host__ __device__ constexpr bool prune_slot(int s) { return s == 3 || s == 4; }
+template <int W, int HN, int H>
+__host__ __device__ constexpr unsigned prune_mask() {
+  unsigned m = 0;
+  for (int q = 0; q < W; ++q)
+    if (prune_slot(H + HN * q)) m |= 1u << q;
+  return m;
+}
+__device__ __forceinline__ double2 cneg(double2 a) { return make_double2(-a.x, -a.y); }
+// a + b, a - b with compile-time zeros (no rounding of x ± 0: the sign of a
+// zero result may differ from the unpruned form, the values do not)
+template <bool ZA, bool ZB>
+__device__ __forceinline__ double2 zadd(double2 a, double2 b) {
+  if constexpr (ZA && ZB) return make_double2(0.0, 0.0);
+  else if constexpr (ZA) return b;
+  else if constexpr (ZB) return a;
+  else return cadd(a, b);
+}
+template <bool ZA, bool ZB>
+__device__ __forceinline__ double2 zsub(double2 a, double2 b) {
+  if constexpr (ZA && ZB) return make_double2(0.0, 0.0);
+  else if constexpr (ZA) return cneg(b);
+  else if constexpr (ZB) return a;
+  else return csub(a, b);
+}
+// dft_w with the inputs of ZM known zero (DIF)
+template <int W, int DIR, unsigned ZM>
+__device__ __forceinline__ void dft_w_zin(double2 (&a)[W]) {
+  if constexpr (ZM == 0) {
+    dft_w<W, DIR>(a);
+  } else if constexpr (W == 2) {
+    const double2 x0 = a[0], x1 = a[1];
+    a[0] = zadd<(ZM & 1) != 0, (ZM & 2) != 0>(x0, x1);
+    a[1] = zsub<(ZM & 1) != 0, (ZM & 2) != 0>(x0, x1);
+  } else if constexpr (W == 4) {
+    constexpr bool z0 = ZM & 1, z1 = ZM & 2, z2 = ZM & 4, z3 = ZM & 8;
+    const double2 s0 = zadd<z0, z2>(a[0], a[2]), s1 = zsub<z0, z2>(a[0], a[2]);
+    const double2 s2 = zadd<z1, z3>(a[1], a[3]), d = zsub<z1, z3>(a[1], a[3]);
+    const double2 s3 = (DIR < 0) ? make_double2(d.y, -d.x) : make_double2(-d.y, d.x);
+    a[0] = cadd(s0, s2);
+    a[2] = csub(s0, s2);
+    a[1] = cadd(s1, s3);
+    a[3] = csub(s1, s3);
+  } else {
+    dft_w<W, DIR>(a);  // W = 8 (4096-point lines): unpruned
+  }
+}
+
 // pw[c] = ω^(c t), c < W (pw[0] unused)
 template <int W, int DIR>
 __device__ __forceinline__ void tw_powers(double2 wt, double2 (&pw)[W]) {
@@ -434,25 +489,35 @@ __device__ __forceinline__ void tw_powers(double2 wt, double2 (&pw)[W]) {
   }
 }
 
-template <int W, int DIR, int C, bool PRE = true, bool FLY = false, bool SHARE = false>
+// the DIF's radix-W over q for h = H (then H + 1 …): pruned inputs per H
+template <int W, int DIR, int C, bool PRUNE, int H>
+__device__ __forceinline__ void dif_radix(double2 (&v)[C][8], const double2 (&pw)[W]) {
+  constexpr int HN = 8 / W;
+  if constexpr (H < HN) {
+    constexpr unsigned ZM = PRUNE ? prune_mask<W, HN, H>() : 0u;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      double2 a[W];
+#pragma unroll
+      for (int q = 0; q < W; ++q) a[q] = v[c][H + HN * q];
+      dft_w_zin<W, DIR, ZM>(a);
+      v[c][H] = a[0];
+#pragma unroll
+      for (int q = 1; q < W; ++q) v[c][H + HN * q] = w8_mul<DIR>(cmul(a[q], pw[q]), H * q);
+    }
+    dif_radix<W, DIR, C, PRUNE, H + 1>(v, pw);
+  }
+}
+
+// PRUNE: slots 3 and 4 hold zeros (prune_slot: a live band kc <= 3N/8)
+template <int W, int DIR, int C, bool PRE = true, bool FLY = false, bool SHARE = false, bool PRUNE = false>
 __device__ __forceinline__ void fftw_dif(double2 (&v)[C][8], int t, double2 wt,
                                          const Twiddles<9, FLY>& tq, double2* __restrict__ line, int stride) {
   constexpr int Q = 512, NT = 64 * W, HN = 8 / W;
   static_assert(W == 2 || W == 4 || W == 8, "1024-, 2048- or 4096-point lines");
   double2 pw[W];
   tw_powers<W, DIR>(wt, pw);
-#pragma unroll
-  for (int c = 0; c < C; ++c)
-#pragma unroll
-    for (int h = 0; h < HN; ++h) {
-      double2 a[W];
-#pragma unroll
-      for (int q = 0; q < W; ++q) a[q] = v[c][h + HN * q];
-      dft_w<W, DIR>(a);
-      v[c][h] = a[0];
-#pragma unroll
-      for (int q = 1; q < W; ++q) v[c][h + HN * q] = w8_mul<DIR>(cmul(a[q], pw[q]), h * q);
-    }
+  dif_radix<W, DIR, C, PRUNE && W != 8, 0>(v, pw);
   if constexpr (PRE) lds_barrier();
   const int b = LPs<true>(t);
 #pragma unroll
@@ -469,7 +534,8 @@ __device__ __forceinline__ void fftw_dif(double2 (&v)[C][8], int t, double2 wt,
   fft_lines<9, DIR, C, FLY, true, SHARE>(v, j, tq, reg, stride);
 }
 
-template <int W, int DIR, int C, bool FLY = false, bool PRE = false, bool SHARE = false>
+// PRUNE: slots 3 and 4 of the result are not needed (left zero)
+template <int W, int DIR, int C, bool FLY = false, bool PRE = false, bool SHARE = false, bool PRUNE = false>
 __device__ __forceinline__ void fftw_dit(double2 (&v)[C][8], int t, double2 wt,
                                          const Twiddles<9, FLY>& tq, double2* __restrict__ line, int stride) {
   constexpr int Q = 512, NT = 64 * W, HN = 8 / W;
@@ -498,7 +564,8 @@ __device__ __forceinline__ void fftw_dit(double2 (&v)[C][8], int t, double2 wt,
       for (int q = 1; q < W; ++q) a[q] = w8_mul<DIR>(cmul(a[q], pw[q]), h * q);
       dft_w<W, DIR>(a);
 #pragma unroll
-      for (int p = 0; p < W; ++p) v[c][h + HN * p] = a[p];
+      for (int p = 0; p < W; ++p)  // (an unused output's arithmetic is dead code)
+        v[c][h + HN * p] = (PRUNE && prune_slot(h + HN * p)) ? make_double2(0.0, 0.0) : a[p];
     }
 }
 

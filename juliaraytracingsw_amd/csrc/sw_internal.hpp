@@ -5,6 +5,17 @@
 #include <stdint.h>
 #include <stddef.h>
 
+// The SW_EXP_* knobs time the cost of one resource by removing it and give
+// wrong results by design: only experiment builds (-DSW_EXPERIMENTS,
+// tools/build_variants.sh) may define them; a production translation unit
+// cannot compile them in.
+#if !defined(SW_EXPERIMENTS) &&                                                                   \
+    (defined(SW_EXP_NOHBM) || defined(SW_EXP_NOLOAD) || defined(SW_EXP_NOSTORE) ||                \
+     defined(SW_EXP_CS_NOMIX) || defined(SW_EXP_CS_NOUPD) || defined(SW_EXP_NOBAR) ||             \
+     defined(SW_EXP_NOTW) || defined(SW_EXP_NOLDS) || defined(SW_EXP_NOFILT))
+#error "SW_EXP_* knobs give wrong results: experiment builds only (-DSW_EXPERIMENTS)"
+#endif
+
 // No implicit FMA contraction in libsw: the same formula rounds the same way
 // in every kernel (and on the host), so kernel fusion never changes results.
 #pragma clang fp contract(off)

@@ -533,14 +533,17 @@ __device__ __forceinline__ void load_uv_eta_zeta(double2 (&w)[2][8], const RowId
 // After a forward FFT of z = a + i b (Z[t + s*NT] in v), hand Â[k], B̂[k] for
 // k = t + s NT < kc to emit(k, s, Â, B̂).  Needs Z[nx-k] from a mirror
 // thread: one LDS round trip.
-template <int LOG2N, bool LEAN = false, typename Emit>
+// PRUNE: slots 3 and 4 are never read as a mirror (sw_fft.hpp prune_slot):
+// not written
+template <int LOG2N, bool LEAN = false, bool PRUNE = false, typename Emit>
 __device__ __forceinline__ void split_pair(const double2 (&v)[8], int t, const Geom& g,
                                            double2* line, Emit emit) {
   if constexpr (LOG2N >= SW_OPAQUE_LOG2 || LEAN) asm volatile("" : "+v"(t));
   constexpr int N = 1 << LOG2N, NT = N / 8;
   lds_barrier();  // previous LDS readers are done
 #pragma unroll
-  for (int s = 0; s < 8; ++s) line[LP<LOG2N>(t + s * NT)] = v[s];
+  for (int s = 0; s < 8; ++s)
+    if (!(PRUNE && prune_slot(s))) line[LP<LOG2N>(t + s * NT)] = v[s];
   lds_barrier();
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
@@ -557,7 +560,7 @@ __device__ __forceinline__ void split_pair(const double2 (&v)[8], int t, const G
 
 // split_pair for C transforms at once (C line buffers `stride` apart, one
 // barrier pair): emit(c, k, s, Â, B̂).
-template <int LOG2N, int C, typename Emit>
+template <int LOG2N, int C, bool PRUNE = false, typename Emit>
 __device__ __forceinline__ void split_pairs(const double2 (&v)[C][8], int t, const Geom& g,
                                             double2* line, int stride, Emit emit) {
   SW_OPAQUE_T(t);
@@ -566,7 +569,8 @@ __device__ __forceinline__ void split_pairs(const double2 (&v)[C][8], int t, con
 #pragma unroll
   for (int c = 0; c < C; ++c)
 #pragma unroll
-    for (int s = 0; s < 8; ++s) line[c * stride + LP<LOG2N>(t + s * NT)] = v[c][s];
+    for (int s = 0; s < 8; ++s)
+      if (!(PRUNE && prune_slot(s))) line[c * stride + LP<LOG2N>(t + s * NT)] = v[c][s];
   lds_barrier();
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
@@ -583,11 +587,11 @@ __device__ __forceinline__ void split_pairs(const double2 (&v)[C][8], int t, con
   }
 }
 
-template <int LOG2N, bool LEAN = false>
+template <int LOG2N, bool LEAN = false, bool PRUNE = false>
 __device__ __forceinline__ void store_pair(const double2 (&v)[8], const RowIdx<LOG2N, LEAN>& ri, const Geom& g,
                                            double2* line, double2* __restrict__ A,
                                            double2* __restrict__ B) {
-  split_pair<LOG2N, LEAN>(v, ri.t, g, line, [&](int, int s, double2 a, double2 b) {
+  split_pair<LOG2N, LEAN, PRUNE>(v, ri.t, g, line, [&](int, int s, double2 a, double2 b) {
     const int o = ri.ofwd(g, s);
     A[o] = a;
     B[o] = b;
@@ -700,7 +704,9 @@ template <int MODEL, int LOG2N>
 __host__ __device__ constexpr bool row_fly() {
   return LOG2N >= SW_TWFLY_LOG2 || (MODEL == MODEL_QG2 && LOG2N >= SW_QG_ROW_FLY_MIN);
 }
-template <int MODEL, int LOG2N, bool ALIAS = false>
+// PRUNE: a live band kc <= 3N/8 (row_prunable): the decimated transforms
+// skip the zero inputs and unused outputs of slots 3 and 4 (sw_fft.hpp)
+template <int MODEL, int LOG2N, bool ALIAS = false, bool PRUNE = false>
 static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
                                          (BlkRow<MODEL, LOG2N>::THREADS >= 1024 ? 4
                                           : (MODEL == MODEL_QG2 ? (row_fly<MODEL, LOG2N>() ? 4 : SW_MINW_ROW_QG)
@@ -746,7 +752,7 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
     // u + i v and η + i ζ, transformed together (fft_lines leaves z[x = t + s*NT])
     if constexpr (W > 0) {
       load_uv_eta_zeta<LOG2N>(w, ri, g, U, V, H, Uy);  // V read once (row 74.9 -> 73.5 µs)
-      fftw_dif<W, +1, 2, false, false, SW_ROW_TW_SHARE>(w, c.t, wt, tq, line, LS);
+      fftw_dif<W, +1, 2, false, false, SW_ROW_TW_SHARE, PRUNE>(w, c.t, wt, tq, line, LS);
     } else if constexpr (CB == 2) {
       load_pair<LOG2N>(w[0], ri, g, U, V, false);
       load_eta_zeta<LOG2N>(w[1], ri, g, H, V, Uy);
@@ -769,7 +775,7 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
       w[1][s] = make_double2(zeta * u, u * eta);                   // ζu + i uη
     }
     if constexpr (W == 0 || !SW_SPLIT_FOLD) {
-      if constexpr (W > 0) fftw_dit<W, -1, 2, false, false, SW_ROW_TW_SHARE>(w, c.t, wt, tq, line, LS);
+      if constexpr (W > 0) fftw_dit<W, -1, 2, false, false, SW_ROW_TW_SHARE, PRUNE>(w, c.t, wt, tq, line, LS);
       else fft_pair<LOG2N, -1, CB>(w, c.t, tws, line, LS);
     }
     auto emit = [&](int cc, int k, int s, double2 a, double2 b) {
@@ -785,7 +791,7 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
     if constexpr (W > 0 && SW_SPLIT_FOLD) {
       fftw_dit_split<W, 2>(w, c.t, g.kc, wt, tq, line, LS, emit);
     } else if constexpr (CB == 2) {
-      split_pairs<LOG2N, 2>(w, c.t, g, line, LS, emit);
+      split_pairs<LOG2N, 2, PRUNE && (W > 0)>(w, c.t, g, line, LS, emit);
     } else {
       split_pairs<LOG2N, 1>(reinterpret_cast<const double2(&)[1][8]>(w[0]), c.t, g, line, LS, emit);
       split_pairs<LOG2N, 1>(reinterpret_cast<const double2(&)[1][8]>(w[1]), c.t, g, line, LS,
@@ -796,7 +802,8 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
     for (int s = 0; s < 8; ++s) v[s] = make_double2(pc[s], 0.0);
     lds_barrier();  // split_pairs' mirror reads are done
     if constexpr (W > 0)
-      fftw_dit<W, -1, 1, false, false, SW_ROW_TW_SHARE>(reinterpret_cast<double2(&)[1][8]>(v), c.t, wt, tq, line, LS);
+      fftw_dit<W, -1, 1, false, false, SW_ROW_TW_SHARE, PRUNE>(reinterpret_cast<double2(&)[1][8]>(v), c.t, wt, tq,
+                                                                line, LS);
     else fft_line<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
@@ -952,12 +959,13 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
     }
     auto wnt = [&]() { return FL ? tw[c.t] : wt; };
     using V1 = double2(&)[1][8];
+    constexpr bool PR = PRUNE && W > 0 && !ALIAS;  // (ALIAS reads the slots kc <= k <= N/2)
     auto inv = [&](double2(&x)[8]) {
-      if constexpr (W > 0) fftw_dif<W, +1, 1, true, FL>(reinterpret_cast<V1>(x), c.t, wnt(), tq, line, 0);
+      if constexpr (W > 0) fftw_dif<W, +1, 1, true, FL, false, PR>(reinterpret_cast<V1>(x), c.t, wnt(), tq, line, 0);
       else fft_line<LOG2N, +1>(x, c.t, tws, line);
     };
     auto fwd = [&](double2(&x)[8]) {
-      if constexpr (W > 0) fftw_dit<W, -1, 1, FL>(reinterpret_cast<V1>(x), c.t, wnt(), tq, line, 0);
+      if constexpr (W > 0) fftw_dit<W, -1, 1, FL, false, false, PR>(reinterpret_cast<V1>(x), c.t, wnt(), tq, line, 0);
       else fft_line<LOG2N, -1>(x, c.t, tws, line);
     };
     double2 q[8];
@@ -977,7 +985,7 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
                                  });
       } else {
         fwd(v);
-        store_pair<LOG2N>(v, ri, g, line, A, B);
+        store_pair<LOG2N, row_fly<MODEL, LOG2N>(), PR>(v, ri, g, line, A, B);
       }
     };
     // ψx1 + i ψx2;  ψx q per layer (swqg/TwoLayerQG.jl:169)
@@ -2739,6 +2747,18 @@ void LenOps<L>::col_inv(int model, const Geom& g, const Phys& p, const double2* 
     hipLaunchKernelGGL((k_col_inv<MODEL_QG2, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
 }
 
+// the pruned row transforms (k_row PRUNE) where they apply: the decimated
+// transforms (roww) and a live band kc <= 3N/8 (every 2/3-rule grid;
+// MultiLayerQG's aliased_fraction = 0 keeps the full ones).  SW_ROW_PRUNE=0:
+// never (A/B builds)
+#ifndef SW_ROW_PRUNE
+#define SW_ROW_PRUNE 1
+#endif
+template <int L>
+static bool row_prunable(const Geom& g) {
+  return SW_ROW_PRUNE && roww<L>() > 0 && 8 * g.kc <= 3 * g.nx;
+}
+
 template <int L>
 void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, double2* Mo, const double2* tw,
                     hipStream_t s, int y0, int nrows, double2* Ma) {
@@ -2755,6 +2775,9 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
       hipLaunchKernelGGL((k_row_rsw_h<L>), dim3(nrows / nbr), dim3(RowH<L>::NTH * nbr),
                          nbr * rsw_rowh_lines<L>() * FftPlan<L - 1>::LDS * sizeof(double2), s, g, p, Mi, Mo,
                          tw, y0);
+    else if (row_prunable<L>(g))
+      hipLaunchKernelGGL((k_row<MODEL_RSW, L, false, true>), dim3(nrows / BR::NB), dim3(BR::THREADS), sh_rsw, s, g,
+                         p, Mi, Mo, tw, y0, nullptr);
     else
       hipLaunchKernelGGL((k_row<MODEL_RSW, L>), dim3(nrows / BR::NB), dim3(BR::THREADS), sh_rsw, s, g, p, Mi, Mo,
                          tw, y0, nullptr);
@@ -2777,6 +2800,9 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
   } else if constexpr (qg_row_half<L>()) {
     hipLaunchKernelGGL((k_row_qg_h<L>), dim3(nrows / rowh_nb<L>()), dim3(RowH<L>::NTH * rowh_nb<L>()),
                        rowh_nb<L>() * FftPlan<L - 1>::LDS * sizeof(double2), s, g, p, Mi, Mo, tw, y0);
+  } else if (row_prunable<L>(g)) {
+    hipLaunchKernelGGL((k_row<MODEL_QG2, L, false, true>), dim3(nrows / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p,
+                       Mi, Mo, tw, y0, nullptr);
   } else {
     hipLaunchKernelGGL((k_row<MODEL_QG2, L>), dim3(nrows / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p, Mi, Mo, tw,
                        y0, nullptr);
