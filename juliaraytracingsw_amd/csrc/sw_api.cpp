@@ -54,6 +54,8 @@ struct Slab {
   double2* a_xs[2] = {};                     // stage-input scratch (discarded: calcN dealiases)
   double2* a_nbuf[2] = {};                   // this calcN's output there (aliases a_hist or a_n)
   double2* a_mrow = nullptr;                 // row-pass x-spectra kr >= kc of the forward fields
+                                             // (slab 0 owns it; every slab's row pass writes its rows)
+  Geom ga[2]{};                              // this slab's aliased regions (alias_geom; region 0 on slab 0)
 };
 
 struct sw_ctx {
@@ -116,7 +118,6 @@ struct sw_ctx {
   int euler_left = 0;                        // sw_reset_history: forward-Euler start-up steps still to run
                                              // (cleared by sw_set_history; the clock does not move it)
   bool alias = false;                        // sw_config.aliased_state
-  Geom ga[2]{};                              // its two regions (alias_geom)
   std::string err;
   // profiling
   bool prof = false;
@@ -248,19 +249,21 @@ std::vector<double2> twiddles(int N) {
 
 // The aliased modes FF's dealias! zeroes as two compact regions
 // the mode-wise kernels (k_step_elem, k_energy_cols, k_scatter_modes) walk
-// like the live set: r = 0 the columns kr in [kc, nx/2], every row; r = 1 the
-// live columns, rows l in [lc, lr2) (lrow_of(j) = lc + j).  One slab.
+// like the live set: r = 0 the columns kr in [kc, nx/2], every row (held by
+// slab 0: its y-transforms need every row, which all slabs of this process
+// write); r = 1 the slab's own live columns, rows l in [lc, lr2)
+// (lrow_of(j) = lc + j).  Slabs of one process (local_slabs = nranks).
 Geom alias_geom(const Geom& g, int r) {
   Geom a = g;
   if (r == 0) {
     a.kr0 = g.kc;
-    a.kcn = g.nkr - g.kc;
+    a.kcn = g.slab == 0 ? g.nkr - g.kc : 0;
     a.lc = g.ny;
     a.lr2 = g.ny;
     a.Lr = g.ny;
   } else {
-    a.kr0 = 0;
-    a.kcn = g.kc;
+    a.kr0 = g.kr0;
+    a.kcn = g.kcn;
     a.lc = 0;
     a.lr2 = g.lc;
     a.Lr = g.lr2 - g.lc;
@@ -485,7 +488,9 @@ const PipeSpec& pipe_spec(int model) {
   return model == SW_MODEL_RSW ? rsw : (model == SW_MODEL_TY ? ty : qg2);
 }
 
-bool pipelined(const sw_ctx* c) { return c->P > 1 && !c->hostx && c->overlap && !c->prof; }
+// (aliased-state tracking runs the sequential calcN, whose last step is the
+// aliased modes' column pass)
+bool pipelined(const sw_ctx* c) { return c->P > 1 && !c->hostx && c->overlap && !c->prof && !c->alias; }
 
 // after the compute stream has launched the producer of inverse group g.
 // The last group goes over in row_chunks chunks of rows, each followed by
@@ -589,8 +594,8 @@ int calcN(sw_ctx* c, double2* Slab::*X, double2* Slab::*N, int op = -1, int stag
       HIPCHK(c, hipMemsetAsync(s.*N, 0, (size_t)c->nf * s.g.cfield * sizeof(double2), c->stream));
       if (c->alias)
         for (int r = 0; r < 2; ++r)
-          if (s.a_nbuf[r] && c->ga[r].cfield > 0)
-            HIPCHK(c, hipMemsetAsync(s.a_nbuf[r], 0, (size_t)c->nf * c->ga[r].cfield * sizeof(double2), c->stream));
+          if (s.a_nbuf[r] && s.ga[r].kcn > 0)
+            HIPCHK(c, hipMemsetAsync(s.a_nbuf[r], 0, (size_t)c->nf * s.ga[r].cfield * sizeof(double2), c->stream));
     }
     return 0;
   }
@@ -622,7 +627,7 @@ int calcN(sw_ctx* c, double2* Slab::*X, double2* Slab::*N, int op = -1, int stag
   {
     Timer tm(c, K_ROW);
     for (Slab& s : c->sl)
-      sw::launch_row(model, s.g, c->p, s.mir, s.mfr, c->tw_x, c->stream, 0, -1, c->alias ? s.a_mrow : nullptr);
+      sw::launch_row(model, s.g, c->p, s.mir, s.mfr, c->tw_x, c->stream, 0, -1, c->alias ? c->sl[0].a_mrow : nullptr);
   }
   if (int rc = transpose(c, false, c->nfwd)) return rc;
   {
@@ -632,7 +637,7 @@ int calcN(sw_ctx* c, double2* Slab::*X, double2* Slab::*N, int op = -1, int stag
   if (c->alias)  // N at the aliased modes (the reference's calcN! writes them: swqg/TwoLayerQG.jl:171,179)
     for (Slab& s : c->sl)
       for (int r = 0; r < 2; ++r)
-        sw::launch_col_fwd_alias(c->kmodel, s.g, c->ga[r], r, c->p, s.mfc, s.a_mrow, s.a_nbuf[r], c->tw_y,
+        sw::launch_col_fwd_alias(c->kmodel, s.g, s.ga[r], r, c->p, s.mfc, c->sl[0].a_mrow, s.a_nbuf[r], c->tw_y,
                                  c->stream);
   return 0;
 }
@@ -801,9 +806,10 @@ int run_stage(sw_ctx* c, int op, int stage, double2* Slab::*X) {
       // the post-step values the reference's update writes there
       // (utils/IFMAB3.jl:142-160; filter after)
       for (int r = 0; c->alias && r < 2; ++r) {
+        if (s.ga[r].kcn <= 0) continue;
         sw::StepPtrs b = alias_step_ptrs(c, s, r);
         b.stage = stage;
-        sw::launch_step_elem(c->nf, op, c->ga[r], c->p, b, s.a_nbuf[r], s.a_xs[r], c->stream);
+        sw::launch_step_elem(c->nf, op, s.ga[r], c->p, b, s.a_nbuf[r], s.a_xs[r], c->stream);
       }
     }
     c->mixed_valid = false;
@@ -824,11 +830,14 @@ int alias_energy_cols(sw_ctx* c, bool post_step_state, int ncols) {
   // 2LQG energies read prob.sol (the post-step state); RSW's read vars.uh,
   // the dealiased calcN input (rsw/RotatingShallowWater.jl:323-333)
   if (!c->alias || !post_step_state || c->cfg.model != SW_MODEL_QG2) return ncols;
-  for (int r = 0; r < 2; ++r) {
-    sw::launch_energy_cols(c->cfg.model, c->ga[r], c->p, c->sl[0].a_sol[r], c->ecols + SW_NSUM * (size_t)ncols,
-                           c->stream);
-    ncols += c->ga[r].kcn;
-  }
+  // region 0 (slab 0), then every slab's region 1 in slab order: the global
+  // column order, whatever the decomposition (bitwise the same sums)
+  for (int r = 0; r < 2; ++r)
+    for (Slab& s : c->sl) {
+      if (s.ga[r].kcn <= 0) continue;
+      sw::launch_energy_cols(c->cfg.model, s.ga[r], c->p, s.a_sol[r], c->ecols + SW_NSUM * (size_t)ncols, c->stream);
+      ncols += s.ga[r].kcn;
+    }
   return ncols;
 }
 
@@ -1011,17 +1020,27 @@ void free_slab(Slab& s) {
     for (void* q : a)
       if (q) (void)hipFree(q);
   }
-  if (s.a_mrow) (void)hipFree(s.a_mrow);
+  if (s.a_mrow && s.ga[0].kcn > 0) (void)hipFree(s.a_mrow);  // (slab 0's; the others point to it)
 }
 
-// aliased-state tracking: a compact aliased pair <-> c->stage (the full array)
-void alias_scatter(sw_ctx* c, double2* const (&a)[2]) {
+// aliased-state tracking: every slab's compact aliased pair (arr(s)[r]) <->
+// c->stage (the full array)
+template <typename Arr>
+void alias_scatter(sw_ctx* c, Arr arr) {
   if (!c->alias) return;
-  for (int r = 0; r < 2; ++r) sw::launch_scatter_modes(c->nf, c->ga[r], a[r], c->stage, c->stream);
+  for (Slab& s : c->sl)
+    for (int r = 0; r < 2; ++r) sw::launch_scatter_modes(c->nf, s.ga[r], arr(s)[r], c->stage, c->stream);
 }
-void alias_gather(sw_ctx* c, double2* const (&a)[2]) {
+template <typename Arr>
+void alias_gather(sw_ctx* c, Arr arr) {
   if (!c->alias) return;
-  for (int r = 0; r < 2; ++r) sw::launch_gather_modes(c->nf, c->ga[r], c->stage, a[r], c->stream);
+  for (Slab& s : c->sl)
+    for (int r = 0; r < 2; ++r) sw::launch_gather_modes(c->nf, s.ga[r], c->stage, arr(s)[r], c->stream);
+}
+auto A_SOL = [](Slab& s) -> double2** { return s.a_sol; };
+auto A_NBUF = [](Slab& s) -> double2** { return s.a_nbuf; };
+inline auto a_hist(int h) {
+  return [h](Slab& s) -> double2** { return s.a_hist[h]; };
 }
 
 }  // namespace
@@ -1087,9 +1106,12 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
     if ((k.model != SW_MODEL_QG2 && k.model != SW_MODEL_RSW) ||
         (k.stepper != SW_STEP_IFMAB3 && k.stepper != SW_STEP_IFMRK4 && k.stepper != SW_STEP_FILTERED_AB3))
       return fail(c, SW_E_INVALID, "aliased_state: RSW or 2LQG with IFMAB3, IFMRK4 or FilteredAB3");
-    if (k.nranks > 1) return fail(c, SW_E_INVALID, "aliased_state: one slab (nranks = 1)");
+    // region 0's y-transforms need every row of the row pass's aliased
+    // x-spectra: all slabs in this process (not one slab per process)
+    if (k.nranks > 1 && k.local_slabs != k.nranks)
+      return fail(c, SW_E_INVALID, "aliased_state: every slab in one process (local_slabs = nranks)");
     if (!sw::row_alias_built(k.model == SW_MODEL_RSW ? sw::MODEL_RSWA : SW_MODEL_QG2, ilog2(k.nx)))
-      return fail(c, SW_E_INVALID, "aliased_state: 2LQG nx <= 4096 (the full-length 2LQG row pass)");
+      return fail(c, SW_E_INVALID, "aliased_state: the row pass's aliased output is not built at this nx");
   }
   const int P = k.nranks;
   if (!pow2(P) || k.ny / P < 32)
@@ -1228,11 +1250,14 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
     }
   }
   c->alias = k.aliased_state != 0;
-  if (c->alias) {
-    Slab& s = c->sl[0];
+  size_t alias_cols = 0;
+  for (Slab& s : c->sl) {
+    if (!c->alias) break;
     for (int r = 0; r < 2; ++r) {
-      c->ga[r] = alias_geom(s.g, r);
-      const size_t cb = (size_t)c->nf * c->ga[r].cfield * sizeof(double2);
+      s.ga[r] = alias_geom(s.g, r);
+      if (s.ga[r].kcn <= 0) continue;
+      alias_cols += s.ga[r].kcn;
+      const size_t cb = (size_t)c->nf * s.ga[r].cfield * sizeof(double2);
       for (double2** q : {&s.a_sol[r], &s.a_zero[r], &s.a_xs[r]})
         if ((rc = alloc(c, (void**)q, cb))) return rc;
       if (k.stepper == SW_STEP_IFMRK4) {
@@ -1243,8 +1268,12 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
           if ((rc = alloc(c, (void**)&s.a_hist[i][r], cb))) return rc;
       }
     }
-    const size_t mrow = (size_t)c->nfwd * (s.g.nkr - s.g.kc) * s.g.ny * sizeof(double2);
-    if ((rc = alloc(c, (void**)&s.a_mrow, mrow))) return rc;
+    if (s.ga[0].kcn > 0) {
+      const size_t mrow = (size_t)c->nfwd * (s.g.nkr - s.g.kc) * s.g.ny * sizeof(double2);
+      if ((rc = alloc(c, (void**)&s.a_mrow, mrow))) return rc;
+    } else {
+      s.a_mrow = c->sl[0].a_mrow;
+    }
   }
   const Geom& g = c->sl[0].g;
   if ((rc = alloc(c, (void**)&c->stage, full_bytes(c)))) return rc;
@@ -1252,7 +1281,7 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
     if ((rc = alloc(c, (void**)&c->stage32, full_bytes(c) / 2))) return rc;
   if ((rc = alloc(c, (void**)&c->dflt, (size_t)g.nx * g.ny * sizeof(double)))) return rc;
   if ((rc = alloc(c, (void**)&c->flag, 1024 * sizeof(int)))) return rc;
-  const size_t ecols = (size_t)P * g.kcl + (c->alias ? (size_t)c->ga[0].kcn + c->ga[1].kcn : 0);
+  const size_t ecols = (size_t)P * g.kcl + alias_cols;
   if ((rc = alloc(c, (void**)&c->ecols, SW_NSUM * ecols * sizeof(double)))) return rc;
   if ((rc = alloc(c, (void**)&c->esum, (SW_NSUM + 2 * (size_t)P) * sizeof(double)))) return rc;
   if (c->dist) {
@@ -1363,7 +1392,7 @@ int sw_set_state(sw_ctx* c, const void* sol, size_t bytes) {
   HIPCHK(c, hipSetDevice(c->cfg.device));
   if (int rc = upload(c, sol, c->stage, full_bytes(c))) return rc;
   for (Slab& s : c->sl) sw::launch_gather(c->nf, s.g, c->stage, s.sol, c->stream);
-  alias_gather(c, c->sl[0].a_sol);  // sol .= q0h keeps them until updatevars!/calcN! dealias
+  alias_gather(c, A_SOL);  // sol .= q0h keeps them until updatevars!/calcN! dealias
   c->mixed_valid = false;
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1376,7 +1405,7 @@ int sw_get_state(const sw_ctx* cc, void* sol, size_t bytes) {
   if (!sol || bytes != caller_bytes(c, full_bytes(c))) return fail(c, SW_E_INVALID, "sw_get_state: size mismatch");
   HIPCHK(c, hipSetDevice(c->cfg.device));
   if (int rc = collect_full(c, &Slab::sol)) return rc;
-  alias_scatter(c, c->sl[0].a_sol);
+  alias_scatter(c, A_SOL);
   if (int rc = download(c, c->stage, sol, full_bytes(c))) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return SW_OK;
@@ -1431,7 +1460,7 @@ int sw_calcN(sw_ctx* c, const void* sol, void* N, size_t bytes) {
   set_alias_nbuf(c, c->cfg.stepper == SW_STEP_IFMRK4);
   if (int rc = calcN(c, &Slab::xs, &Slab::nbuf)) return rc;
   if (int rc = collect_full(c, &Slab::nbuf)) return rc;
-  alias_scatter(c, c->sl[0].a_nbuf);
+  alias_scatter(c, A_NBUF);
   if (int rc = download(c, c->stage, N, full_bytes(c))) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return SW_OK;
@@ -1470,7 +1499,9 @@ int sw_get_physical(sw_ctx* c, int32_t fid, void* out, size_t bytes) {
   HIPCHK(c, hipSetDevice(c->cfg.device));
   // updatevars! begins with dealias!(sol, grid) (swqg/TwoLayerQG.jl:115)
   for (int r = 0; c->alias && r < 2; ++r)
-    HIPCHK(c, hipMemsetAsync(c->sl[0].a_sol[r], 0, (size_t)c->nf * c->ga[r].cfield * sizeof(double2), c->stream));
+    for (Slab& s : c->sl)
+      if (s.ga[r].kcn > 0)
+        HIPCHK(c, hipMemsetAsync(s.a_sol[r], 0, (size_t)c->nf * s.ga[r].cfield * sizeof(double2), c->stream));
   if (int rc = physical_to_dflt(c, fid)) return rc;
   if (c->dist) {
     const size_t rows = (size_t)g0.nyl * g0.nx;
@@ -1848,7 +1879,7 @@ int sw_get_history(const sw_ctx* cc, int32_t slot, void* buf, size_t bytes) {
   if (int rc = join_comm(c)) return rc;
   for (Slab& s : c->sl) s.view = s.hist[h];
   if (int rc = collect_full(c, &Slab::view)) return rc;
-  alias_scatter(c, c->sl[0].a_hist[h]);
+  alias_scatter(c, a_hist(h));
   if (int rc = download(c, c->stage, buf, full_bytes(c))) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return SW_OK;
@@ -1863,7 +1894,7 @@ int sw_set_history(sw_ctx* c, int32_t slot, const void* buf, size_t bytes) {
   if (int rc = join_comm(c)) return rc;
   if (int rc = upload(c, buf, c->stage, full_bytes(c))) return rc;
   for (Slab& s : c->sl) sw::launch_gather(c->nf, s.g, c->stage, s.hist[h], c->stream);
-  alias_gather(c, c->sl[0].a_hist[h]);
+  alias_gather(c, a_hist(h));
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->euler_left = 0;  // the history is valid again: AB3 from the next step (clock.step >= 3)
@@ -1926,12 +1957,12 @@ int sw_get_checkpoint(const sw_ctx* cc, void* buf, size_t bytes) {
   for (int k = 0; k <= h.nslots; ++k) {  // fp64 always: no narrowing to the caller precision
     if (k == 0) {
       if (int rc = collect_full(c, &Slab::sol)) return rc;
-      alias_scatter(c, c->sl[0].a_sol);
+      alias_scatter(c, A_SOL);
     } else {
       const int hi = hist_index(c, k);
       for (Slab& s : c->sl) s.view = s.hist[hi];
       if (int rc = collect_full(c, &Slab::view)) return rc;
-      alias_scatter(c, c->sl[0].a_hist[hi]);
+      alias_scatter(c, a_hist(hi));
     }
     HIPCHK(c, hipMemcpyAsync(out + sizeof(h) + k * fb, c->stage, fb, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1961,7 +1992,8 @@ int sw_set_checkpoint(sw_ctx* c, const void* buf, size_t bytes) {
   for (int k = 0; k <= h.nslots; ++k) {
     HIPCHK(c, hipMemcpyAsync(c->stage, in + sizeof(h) + k * fb, fb, hipMemcpyHostToDevice, c->stream));
     for (Slab& s : c->sl) sw::launch_gather(c->nf, s.g, c->stage, k == 0 ? s.sol : s.hist[hist_index(c, k)], c->stream);
-    alias_gather(c, k == 0 ? c->sl[0].a_sol : c->sl[0].a_hist[hist_index(c, k)]);
+    if (k == 0) alias_gather(c, A_SOL);
+    else alias_gather(c, a_hist(hist_index(c, k)));
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipStreamSynchronize(c->stream));  // the staging buffer is reused
   }

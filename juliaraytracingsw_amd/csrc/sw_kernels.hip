@@ -832,7 +832,7 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
     fft_line<LOG2N, -1>(pr, c.t, tws, line);
     store_pair<LOG2N>(pr, ri, g, line, Mo, Mo + MF);
     const long long MA = (long long)(g.nkr - g.kc) * g.ny;  // aliased columns × rows per field
-    if constexpr (ALIAS) store_alias_pair<LOG2N>(pr, c.t, g, line, Ma, Ma + MA, y);
+    if constexpr (ALIAS) store_alias_pair<LOG2N>(pr, c.t, g, line, Ma, Ma + MA, y + g.y0);
     load_pair<LOG2N>(v, ri, g, H, nullptr, false);  // η
     fft_line<LOG2N, +1>(v, c.t, tws, line);
 #pragma unroll
@@ -843,7 +843,7 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
       Mo[2 * MF + o] = cmul_i(a, -(k * g.mk));
       Mo[3 * MF + o] = b;
     });
-    if constexpr (ALIAS) store_alias_pair<LOG2N, true>(v, c.t, g, line, Ma + 2 * MA, Ma + 3 * MA, y);
+    if constexpr (ALIAS) store_alias_pair<LOG2N, true>(v, c.t, g, line, Ma + 2 * MA, Ma + 3 * MA, y + g.y0);
   } else if constexpr (MODEL == MODEL_TY) {
     // thomasyamada/ThomasYamada.jl:129-262.  Inputs (k_col_inv): 0 ζ, 1 ψ,
     // 2 ût, 3 ∂y ut, 4 uc, 5 ∂y uc, 6 vc, 7 pc, 8 ∂y pc.  Physical fields in
@@ -995,14 +995,14 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
     for (int s = 0; s < 8; ++s) v[s] = make_double2(v[s].x * q[s].x, v[s].y * q[s].y);
     fwd_store(Mo, Mo + MF);
     const long long MA = (long long)(g.nkr - g.kc) * g.ny;  // aliased columns × rows per field
-    if constexpr (ALIAS) store_alias_pair<LOG2N>(v, c.t, g, line, Ma, Ma + MA, y);
+    if constexpr (ALIAS) store_alias_pair<LOG2N>(v, c.t, g, line, Ma, Ma + MA, y + g.y0);
     // ψy q per layer (:177)
     load_pair<LOG2N>(v, ri, g, Py1, Py2, false);
     inv(v);
 #pragma unroll
     for (int s = 0; s < 8; ++s) v[s] = make_double2(v[s].x * q[s].x, v[s].y * q[s].y);
     fwd_store(Mo + 2 * MF, Mo + 3 * MF);
-    if constexpr (ALIAS) store_alias_pair<LOG2N>(v, c.t, g, line, Ma + 2 * MA, Ma + 3 * MA, y);
+    if constexpr (ALIAS) store_alias_pair<LOG2N>(v, c.t, g, line, Ma + 2 * MA, Ma + 3 * MA, y + g.y0);
   }
 }
 
@@ -2793,10 +2793,9 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
       hipLaunchKernelGGL((k_row<MODEL_RSWA, L>), dim3(nrows / BA::NB), dim3(BA::THREADS),
                          FftPlan<L>::LDS * BA::NB * sizeof(double2), s, g, p, Mi, Mo, tw, y0, nullptr);
   }
-  else if (Ma) {  // aliased-state tracking: the full-length row (row_alias_built: lines up to 4096)
-    if constexpr (L <= 12)
-      hipLaunchKernelGGL((k_row<MODEL_QG2, L, true>), dim3(nrows / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p, Mi,
-                         Mo, tw, y0, Ma);
+  else if (Ma) {  // aliased-state tracking: the full-length row (it writes the aliased x-spectra)
+    hipLaunchKernelGGL((k_row<MODEL_QG2, L, true>), dim3(nrows / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p, Mi,
+                       Mo, tw, y0, Ma);
   } else if constexpr (qg_row_half<L>()) {
     hipLaunchKernelGGL((k_row_qg_h<L>), dim3(nrows / rowh_nb<L>()), dim3(RowH<L>::NTH * rowh_nb<L>()),
                        rowh_nb<L>() * FftPlan<L - 1>::LDS * sizeof(double2), s, g, p, Mi, Mo, tw, y0);
@@ -2948,7 +2947,7 @@ void launch_row(int model, const Geom& g, const Phys& p, const double2* Minv, do
 bool row_alias_built(int model, int log2nx) {
   bool ok = false;
   by_len(log2nx, [&](auto L) {
-    ok = model == MODEL_RSWA || (model == MODEL_QG2 && decltype(L)::value <= 12);
+    ok = model == MODEL_RSWA || model == MODEL_QG2;
   });
   return ok;
 }

@@ -733,8 +733,8 @@ class IFMAB3:
     """utils/IFMAB3.jl:68-88, 128-169 (CPU method)."""
 
     def __init__(self, L, dt, grid, nf, use_filter=False, diagonal=False, **filter_kw):
-        self.expLdt = expm_batched(L * dt)
-        self.exp2Ldt = expm_batched(L * 2 * dt)
+        self.expLdt = expm_modes(L * dt)
+        self.exp2Ldt = expm_modes(L * 2 * dt)
         shape = (nf, grid.nl, grid.nkr)
         self.N = np.zeros(shape, np.complex128)
         self.Nm1 = np.zeros(shape, np.complex128)
