@@ -74,7 +74,7 @@ class Problem:
         cfg.check_nan = 1 if check_nan else 0
         cfg.nop_calcN = 1 if nop_calcN else 0
         cfg.unfused = 1 if unfused else 0
-        # carry the modes the 2/3 rule removes (2LQG, one slab: include/sw.h)
+        # carry the modes the 2/3 rule removes (RSW / 2LQG, slabs in one process: include/sw.h)
         cfg.aliased_state = 1 if aliased_state else 0
         # slab decomposition: nranks slabs; local_slabs == nranks
         # holds them all on this GPU, else this process holds slab `rank` and

@@ -24,7 +24,7 @@ def Problem(dev="gpu", *, nx=128, ny=None, Lx=2 * np.pi, Ly=None, U=0.5, mu=1e-2
     fp64 either way (BASELINE parity precision) and rounds once on output.
     ``aliased_state=True`` also carries the modes the 2/3 rule removes, so
     ``prob.sol``, calcN and the energy diagnostics cover the full array as
-    the reference's do (one slab, nx <= 4096; include/sw.h).
+    the reference's do (slabs of one process; include/sw.h).
     """
     if dev not in ("gpu", "GPU", "GPU()"):
         raise _lib.LibSWError("libsw runs on the GPU only (dev='gpu')")

@@ -6,8 +6,9 @@ every mode (swqg/TwoLayerQG.jl:152-182: rfft of the products, no dealias of
 N), and the IF/AB3 update writes E·dt·(…N…) into prob.sol there
 (utils/IFMAB3.jl:142-160), so between steps prob.sol holds aliased modes,
 which its energies (:230-252) count and the next calcN!/updatevars!
-discards.  With aliased_state = 1 libsw carries them too (one slab, 2LQG,
-nx <= 4096); the oracle keeps the full arrays, so every comparison here is
+discards.  With aliased_state = 1 libsw carries them too (RSW and 2LQG, any
+nx up to 8192, one slab or several in one process); the oracle keeps the
+full arrays, so every comparison here is
 over ALL modes of the full (nkr, nl) array, at the strongly nonlinear 64²
 cases of tests/sw_cases.py.  RSW (whose update writes those modes into
 prob.sol too) carries them with its calcN in the reference's advective form
