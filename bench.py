@@ -119,7 +119,21 @@ def cpu_baseline(model, stepper, n, grids=(128, 1024, 2048), samples=5, warm_ste
         by_grid[str(g)] = {"steps_per_s": statistics.median(rates), "steps_per_sample": counts,
                            "warmup_steps": warm_steps, "samples": samples, "min": min(rates), "max": max(rates)}
     O.set_fft_workers(None)
+    # BASELINE.md §3's optional extra: the reference's own CPU path if the box
+    # has it (`julia -e 'using FourierFlows'`); recorded either way
+    import shutil
+
+    jl = shutil.which("julia")
+    probe = "julia not on PATH: the reference's FourierFlows/FFTW path cannot run on this box"
+    if jl:
+        try:
+            r = subprocess.run([jl, "-e", "using FourierFlows"], capture_output=True, text=True, timeout=120)
+            probe = ("julia found, `using FourierFlows` succeeded (not timed by this script)" if r.returncode == 0
+                     else f"julia found, `using FourierFlows` failed: {r.stderr.strip()[-200:]}")
+        except Exception as exc:  # noqa: BLE001 - recorded
+            probe = f"julia found, probe failed: {exc}"
     return dict(value=by_grid[str(n)]["steps_per_s"], unit="timesteps/s", cores=cores, kind="port",
+                reference_probe=probe,
                 nproc=os.cpu_count(), affinity_cores=affinity, cpu_model=_cpu_model(), by_grid=by_grid,
                 sample=f"{stepper} steps of the {model.upper()} oracle: the repo's fp64 numpy/scipy restatement of "
                        f"the reference op sequence (numpy elementwise + scipy.fft workers={cores}), not "

@@ -472,11 +472,17 @@ __device__ __forceinline__ void dft_w_zin(double2 (&a)[W]) {
   }
 }
 
-// pw[c] = ω^(c t), c < W (pw[0] unused)
+// the radix-8 decimations (4096-point lines: the 128-VGPR half rows) form
+// the powers of ω^t as a chain, two live at a time (for_twiddles)
+template <int W>
+__host__ __device__ constexpr bool tw_chain() { return W == 8; }
+
+// pw[c] = ω^(c t), c < W (pw[0] unused; tw_chain: pw[1] only)
 template <int W, int DIR>
 __device__ __forceinline__ void tw_powers(double2 wt, double2 (&pw)[W]) {
   pw[0] = make_double2(1.0, 0.0);
   if constexpr (W > 1) pw[1] = DIR < 0 ? wt : cconj(wt);
+  if constexpr (tw_chain<W>()) return;
   if constexpr (W > 2) {
     pw[2] = cmul(pw[1], pw[1]);
     pw[3] = cmul(pw[2], pw[1]);
@@ -489,6 +495,22 @@ __device__ __forceinline__ void tw_powers(double2 wt, double2 (&pw)[W]) {
   }
 }
 
+// ω^(q t) for q = 1 … W−1: the table pw, or (CHAIN: the 4096-point lines
+// of the 128-VGPR half rows) a chain from pw[1], two powers live at a time
+template <int W, int DIR, bool CHAIN, typename F>
+__device__ __forceinline__ void for_twiddles(const double2 (&pw)[W], F f) {
+  if constexpr (CHAIN) {
+    double2 wq = pw[1];
+#pragma unroll
+    for (int q = 1; q < W; ++q) {
+      f(q, wq);
+      if (q + 1 < W) wq = cmul(wq, pw[1]);
+    }
+  } else {
+#pragma unroll
+    for (int q = 1; q < W; ++q) f(q, pw[q]);
+  }
+}
 // the DIF's radix-W over q for h = H (then H + 1 …): pruned inputs per H
 template <int W, int DIR, int C, bool PRUNE, int H>
 __device__ __forceinline__ void dif_radix(double2 (&v)[C][8], const double2 (&pw)[W]) {
@@ -502,8 +524,9 @@ __device__ __forceinline__ void dif_radix(double2 (&v)[C][8], const double2 (&pw
       for (int q = 0; q < W; ++q) a[q] = v[c][H + HN * q];
       dft_w_zin<W, DIR, ZM>(a);
       v[c][H] = a[0];
-#pragma unroll
-      for (int q = 1; q < W; ++q) v[c][H + HN * q] = w8_mul<DIR>(cmul(a[q], pw[q]), H * q);
+      for_twiddles<W, DIR, tw_chain<W>()>(pw, [&](int q, double2 wq) {
+        v[c][H + HN * q] = w8_mul<DIR>(cmul(a[q], wq), H * q);
+      });
     }
     dif_radix<W, DIR, C, PRUNE, H + 1>(v, pw);
   }
@@ -560,8 +583,7 @@ __device__ __forceinline__ void fftw_dit(double2 (&v)[C][8], int t, double2 wt,
       double2 a[W];
 #pragma unroll
       for (int q = 0; q < W; ++q) a[q] = line[c * stride + q * Q + b + NT * h];
-#pragma unroll
-      for (int q = 1; q < W; ++q) a[q] = w8_mul<DIR>(cmul(a[q], pw[q]), h * q);
+      for_twiddles<W, DIR, tw_chain<W>()>(pw, [&](int q, double2 wq) { a[q] = w8_mul<DIR>(cmul(a[q], wq), h * q); });
       dft_w<W, DIR>(a);
 #pragma unroll
       for (int p = 0; p < W; ++p)  // (an unused output's arithmetic is dead code)
@@ -611,11 +633,10 @@ __device__ __forceinline__ void fftw_dit_split(double2 (&v)[C][8], int t, int kc
         A[q] = make_double2(0.5 * (y.x + ym.x), 0.5 * (y.y - ym.y));
         B[q] = make_double2(0.5 * (y.y + ym.y), -0.5 * (y.x - ym.x));
       }
-#pragma unroll
-      for (int q = 1; q < W; ++q) {
-        A[q] = w8_mul<DIR>(cmul(A[q], pw[q]), h * q);
-        B[q] = w8_mul<DIR>(cmul(B[q], pw[q]), h * q);
-      }
+      for_twiddles<W, DIR, tw_chain<W>()>(pw, [&](int q, double2 wq) {
+        A[q] = w8_mul<DIR>(cmul(A[q], wq), h * q);
+        B[q] = w8_mul<DIR>(cmul(B[q], wq), h * q);
+      });
       dft_w<W, DIR>(A);
       dft_w<W, DIR>(B);
 #pragma unroll
