@@ -162,13 +162,14 @@ typedef struct sw_config {
   /* caller-buffer element type (SW_PREC_*), the reference's `T`            */
   int32_t precision;
   /* 1: also carry the modes the 2/3 rule removes (RSW or 2LQG with IFMAB3,
-   * IFMRK4 or FilteredAB3, nx up to 8192; one slab, or several slabs in one
+   * IFMRK4 or FilteredAB3, Thomas-Yamada with ETDRK4, nx up to 8192; one
+   * slab, or several slabs in one
    * process (local_slabs = nranks) — not one slab per process; RSW then runs
    * its calcN in the reference's advective form).  The reference's calcN!
    * returns N there (swqg/TwoLayerQG.jl:171,179; rsw/RotatingShallowWater.jl
    * :140-230) and its update writes them into prob.sol (utils/IFMAB3.jl
    * :142-160) until the next calcN!/updatevars! dealiases: sw_calcN,
-   * sw_get_state, the history/checkpoint I/O and the 2LQG energy
+   * sw_get_state, the history/checkpoint I/O and the 2LQG/TY energy
    * diagnostics (records and sw_diag; RSW's read the dealiased vars.uh) then
    * cover the full array, as the reference's do.  Off (0, the default): live
    * modes only, zeros elsewhere.  sw_get_physical

@@ -134,10 +134,10 @@ function config(model, stepper::AbstractString; nx, ny, Lx, Ly, aliased_fraction
     cfg.aliased_fraction, cfg.dt = aliased_fraction, T(dt)
     cfg.precision = T == Float32 ? SW_PREC_F32 : SW_PREC_F64
     cfg.device = parse(Int32, get(ENV, "LIBSW_DEVICE", "0"))
-    # LIBSW_ALIASED_STATE=1: RotatingShallowWater's / TwoLayerQG's prob.sol,
+    # LIBSW_ALIASED_STATE=1: RotatingShallowWater's / TwoLayerQG's / ThomasYamada's prob.sol,
     # calcN! and energies on the full array, the modes the 2/3 rule removes
     # included (include/sw.h)
-    model in (SW_MODEL_RSW, SW_MODEL_QG2) &&
+    model in (SW_MODEL_RSW, SW_MODEL_QG2, SW_MODEL_TY) &&
         (cfg.aliased_state = get(ENV, "LIBSW_ALIASED_STATE", "0") == "1" ? 1 : 0)
     return cfg
 end

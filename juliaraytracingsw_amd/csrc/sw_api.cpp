@@ -52,6 +52,8 @@ struct Slab {
   double2* a_acc[2] = {};                    // IFMRK4: running combination there
   double2* a_n[2] = {};                      // IFMRK4: calcN output there
   double2* a_xs[2] = {};                     // stage-input scratch (discarded: calcN dealiases)
+  double2* a_xs2[2] = {};                    // ETDRK4: s₂ there
+  double* a_etd[2] = {};                     // ETDRK4: the coefficient table there
   double2* a_nbuf[2] = {};                   // this calcN's output there (aliases a_hist or a_n)
   double2* a_mrow = nullptr;                 // row-pass x-spectra kr >= kc of the forward fields
                                              // (slab 0 owns it; every slab's row pass writes its rows)
@@ -691,10 +693,12 @@ bool fwd_step_lds(const sw_ctx* c) {
 }
 
 // aliased-state tracking: this calcN's output at the aliased modes
-void set_alias_nbuf(sw_ctx* c, bool rk4) {
+void set_alias_nbuf(sw_ctx* c) {
   if (!c->alias) return;
+  const int st = c->cfg.stepper;
+  const bool sep = st == SW_STEP_IFMRK4 || st == SW_STEP_ETDRK4;  // N into its own buffer
   for (Slab& s : c->sl)
-    for (int r = 0; r < 2; ++r) s.a_nbuf[r] = rk4 ? s.a_n[r] : s.a_hist[c->head][r];
+    for (int r = 0; r < 2; ++r) s.a_nbuf[r] = sep ? s.a_n[r] : s.a_hist[c->head][r];
 }
 
 sw::StepPtrs alias_step_ptrs(const sw_ctx* c, const Slab& s, int r) {
@@ -706,6 +710,12 @@ sw::StepPtrs alias_step_ptrs(const sw_ctx* c, const Slab& s, int r) {
   a.stream = 0;
   if (c->cfg.stepper == SW_STEP_IFMRK4) {
     a.h0 = s.a_acc[r];
+  } else if (c->cfg.stepper == SW_STEP_ETDRK4) {
+    a.h0 = s.a_acc[r];
+    a.n1 = s.a_hist[0][r];
+    a.n2 = s.a_hist[1][r];
+    a.xs2 = s.a_xs2[r];
+    a.etd = s.a_etd[r];
   } else {
     a.h0 = s.a_hist[c->head][r];
     a.h1 = s.a_hist[(c->head + 2) % 3][r];
@@ -790,7 +800,7 @@ int run_stage(sw_ctx* c, int op, int stage, double2* Slab::*X) {
     // the update then overwrites in place (N -> RHS or N); nbuf aliases it
     if (op != sw::OP_RK4 && op != sw::OP_ETDRK4 && op != sw::OP_FRK4)
       for (Slab& s : c->sl) s.nbuf = s.hist[c->head];
-    set_alias_nbuf(c, op == sw::OP_RK4);
+    set_alias_nbuf(c);
     if (use_fwd_step(c)) {
       if (int rc = calcN(c, X, &Slab::nbuf, op, stage)) return rc;
       c->mixed_valid = false;
@@ -829,7 +839,8 @@ int run_stage(sw_ctx* c, int op, int stage, double2* Slab::*X) {
 int alias_energy_cols(sw_ctx* c, bool post_step_state, int ncols) {
   // 2LQG energies read prob.sol (the post-step state); RSW's read vars.uh,
   // the dealiased calcN input (rsw/RotatingShallowWater.jl:323-333)
-  if (!c->alias || !post_step_state || c->cfg.model != SW_MODEL_QG2) return ncols;
+  // (Thomas–Yamada's read prob.sol too: thomasyamada/ThomasYamada.jl:333-360)
+  if (!c->alias || !post_step_state || (c->cfg.model != SW_MODEL_QG2 && c->cfg.model != SW_MODEL_TY)) return ncols;
   // region 0 (slab 0), then every slab's region 1 in slab order: the global
   // column order, whatever the decomposition (bitwise the same sums)
   for (int r = 0; r < 2; ++r)
@@ -1016,7 +1027,7 @@ void free_slab(Slab& s) {
   if (s.mfc && s.mfc != s.mfr) (void)hipFree(s.mfc);
   for (int r = 0; r < 2; ++r) {
     void* a[] = {s.a_sol[r], s.a_zero[r], s.a_hist[0][r], s.a_hist[1][r], s.a_hist[2][r], s.a_acc[r], s.a_n[r],
-                 s.a_xs[r]};
+                 s.a_xs[r],  s.a_xs2[r],  s.a_etd[r]};
     for (void* q : a)
       if (q) (void)hipFree(q);
   }
@@ -1103,14 +1114,17 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   if (k.precision != SW_PREC_F64 && k.precision != SW_PREC_F32)
     return fail(c, SW_E_INVALID, "precision must be SW_PREC_F64 or SW_PREC_F32");
   if (k.aliased_state) {
-    if ((k.model != SW_MODEL_QG2 && k.model != SW_MODEL_RSW) ||
-        (k.stepper != SW_STEP_IFMAB3 && k.stepper != SW_STEP_IFMRK4 && k.stepper != SW_STEP_FILTERED_AB3))
-      return fail(c, SW_E_INVALID, "aliased_state: RSW or 2LQG with IFMAB3, IFMRK4 or FilteredAB3");
+    const bool ab_or_if = k.stepper == SW_STEP_IFMAB3 || k.stepper == SW_STEP_IFMRK4 ||
+                          k.stepper == SW_STEP_FILTERED_AB3;
+    if (!(((k.model == SW_MODEL_QG2 || k.model == SW_MODEL_RSW) && ab_or_if) ||
+          (k.model == SW_MODEL_TY && k.stepper == SW_STEP_ETDRK4)))
+      return fail(c, SW_E_INVALID,
+                  "aliased_state: RSW or 2LQG with IFMAB3, IFMRK4 or FilteredAB3, or Thomas-Yamada with ETDRK4");
     // region 0's y-transforms need every row of the row pass's aliased
     // x-spectra: all slabs in this process (not one slab per process)
     if (k.nranks > 1 && k.local_slabs != k.nranks)
       return fail(c, SW_E_INVALID, "aliased_state: every slab in one process (local_slabs = nranks)");
-    if (!sw::row_alias_built(k.model == SW_MODEL_RSW ? sw::MODEL_RSWA : SW_MODEL_QG2, ilog2(k.nx)))
+    if (!sw::row_alias_built(k.model == SW_MODEL_RSW ? sw::MODEL_RSWA : k.model, ilog2(k.nx)))
       return fail(c, SW_E_INVALID, "aliased_state: the row pass's aliased output is not built at this nx");
   }
   const int P = k.nranks;
@@ -1260,10 +1274,17 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
       const size_t cb = (size_t)c->nf * s.ga[r].cfield * sizeof(double2);
       for (double2** q : {&s.a_sol[r], &s.a_zero[r], &s.a_xs[r]})
         if ((rc = alloc(c, (void**)q, cb))) return rc;
-      if (k.stepper == SW_STEP_IFMRK4) {
+      if (k.stepper == SW_STEP_IFMRK4 || k.stepper == SW_STEP_ETDRK4) {
         if ((rc = alloc(c, (void**)&s.a_acc[r], cb))) return rc;
         if ((rc = alloc(c, (void**)&s.a_n[r], cb))) return rc;
-      } else {
+      }
+      if (k.stepper == SW_STEP_ETDRK4) {  // N₁, N₂, s₂ and the coefficients at the aliased modes
+        for (double2** q : {&s.a_hist[0][r], &s.a_hist[1][r], &s.a_xs2[r]})
+          if ((rc = alloc(c, (void**)q, cb))) return rc;
+        if ((rc = alloc(c, (void**)&s.a_etd[r], (size_t)sw::ETD_N * s.ga[r].cfield * sizeof(double)))) return rc;
+        sw::launch_etd_coeffs(s.ga[r], c->p, s.a_etd[r], c->stream);
+        HIPCHK(c, hipGetLastError());
+      } else if (k.stepper != SW_STEP_IFMRK4) {
         for (int i = 0; i < 3; ++i)
           if ((rc = alloc(c, (void**)&s.a_hist[i][r], cb))) return rc;
       }
@@ -1457,7 +1478,7 @@ int sw_calcN(sw_ctx* c, const void* sol, void* N, size_t bytes) {
         c->cfg.stepper != SW_STEP_FILTERED_RK4)
       s.nbuf = s.hist[c->head];
   }
-  set_alias_nbuf(c, c->cfg.stepper == SW_STEP_IFMRK4);
+  set_alias_nbuf(c);
   if (int rc = calcN(c, &Slab::xs, &Slab::nbuf)) return rc;
   if (int rc = collect_full(c, &Slab::nbuf)) return rc;
   alias_scatter(c, A_NBUF);

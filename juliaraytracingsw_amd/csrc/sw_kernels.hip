@@ -654,6 +654,25 @@ __device__ __forceinline__ void store_alias_pair(const double2 (&v)[8], int t, c
   }
 }
 
+// store_alias_pair with the outputs formed by the caller: emit(o, k, Â, B̂)
+// for the aliased kc <= k <= nx/2 of the pair in LDS, o = the offset of
+// [k - kc][y] in one aliased field (Thomas–Yamada's seven outputs)
+template <int LOG2N, typename Emit>
+__device__ __forceinline__ void store_alias_with(const double2 (&v)[8], int t, const Geom& g, const double2* line,
+                                                 int y, Emit emit) {
+  constexpr int N = 1 << LOG2N, NT = N / 8;
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const int k = t + s * NT;
+    if (k >= g.kc && k <= N / 2) {
+      const double2 zk = v[s];
+      const double2 zn = line[LP<LOG2N>((N - k) & (N - 1))];
+      emit((long long)(k - g.kc) * g.ny + y, k, make_double2(0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y)),
+           make_double2(0.5 * (zk.y + zn.y), -0.5 * (zk.x - zn.x)));
+    }
+  }
+}
+
 // The 2LQG row from 2048-point lines (SW_QG_ROW_FLY_MIN): stage twiddles read
 // per stage and the thread index opaque per transform (Twiddles<…, FLY>), 116
 // VGPRs, 4 waves per SIMD — 2048²: 85 -> 76 µs, config 3 +2-3 %
@@ -890,6 +909,10 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
       w[s] = make_double2(ut[s] * zt[s], uc[s] * vc[s]);          // p2 + i p3
       v[s] = make_double2(vt[s] * zt[s], uc[s] * uc[s] - vc[s] * vc[s]);  // p1 + i p4
     }
+    // aliased-state tracking: the x-spectra kc <= k <= nx/2 of every output
+    // into Ma [field][k - kc][global row] (k_col_fwd_alias), as the live ones
+    const long long MA = (long long)(g.nkr - g.kc) * g.ny;
+    const int yg = y + g.y0;
     fft_line<LOG2N, -1>(w, c.t, tws, line);
     split_pair<LOG2N>(w, c.t, g, line, [&](int k, int s, double2 a, double2 b) {
       const double kw = k * g.mk;
@@ -897,11 +920,21 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
       Mo[o] = cscale(csub(cmul_i(a, kw), cscale(b, kw * kw)), nRo);
       Mo[2 * MF + o] = cscale(b, nRo);
     });
+    if constexpr (ALIAS)
+      store_alias_with<LOG2N>(w, c.t, g, line, yg, [&](long long o, int k, double2 a, double2 b) {
+        const double kw = k * g.mk;
+        Ma[o] = cscale(csub(cmul_i(a, kw), cscale(b, kw * kw)), nRo);
+        Ma[2 * MA + o] = cscale(b, nRo);
+      });
     fft_line<LOG2N, -1>(v, c.t, tws, line);
     split_pair<LOG2N>(v, c.t, g, line, [&](int k, int s, double2 a, double2 b) {
       const double kw = k * g.mk;
       Mo[MF + ri.ofwd(g, s)] = cscale(cadd(cmul_i(a, 1.0), cscale(b, kw)), nRo);
     });
+    if constexpr (ALIAS)
+      store_alias_with<LOG2N>(v, c.t, g, line, yg, [&](long long o, int k, double2 a, double2 b) {
+        Ma[MA + o] = cscale(cadd(cmul_i(a, 1.0), cscale(b, k * g.mk)), nRo);
+      });
     // ∂y ut + i ∂x vc
     load_pair_m<LOG2N>(v, ri, g, F[3], 0, F[6], 1);
     fft_line<LOG2N, +1>(v, c.t, tws, line);
@@ -915,6 +948,10 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
     split_pair<LOG2N>(v, c.t, g, line, [&](int k, int s, double2 a, double2 b) {
       Mo[3 * MF + ri.ofwd(g, s)] = cscale(cadd(cmul_i(a, k * g.mk), b), nRo);
     });
+    if constexpr (ALIAS)
+      store_alias_with<LOG2N>(v, c.t, g, line, yg, [&](long long o, int k, double2 a, double2 b) {
+        Ma[3 * MA + o] = cscale(cadd(cmul_i(a, k * g.mk), b), nRo);
+      });
     // ∂x vt + i ∂x pc
     load_pair_m<LOG2N>(v, ri, g, F[1], 2, F[7], 1);
     fft_line<LOG2N, +1>(v, c.t, tws, line);
@@ -930,6 +967,11 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
       Mo[4 * MF + o] = cscale(a, nRo);
       Mo[5 * MF + o] = cscale(b, nRo);
     });
+    if constexpr (ALIAS)
+      store_alias_with<LOG2N>(v, c.t, g, line, yg, [&](long long o, int, double2 a, double2 b) {
+        Ma[4 * MA + o] = cscale(a, nRo);
+        Ma[5 * MA + o] = cscale(b, nRo);
+      });
     // ∂y pc
     load_pair_m<LOG2N>(v, ri, g, F[8], 0, nullptr, 0);
     fft_line<LOG2N, +1>(v, c.t, tws, line);
@@ -940,6 +982,8 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
     for (int s = 0; s < 8; ++s) {
       const int k = c.t + s * Bk::NT;
       if (RowIdx<LOG2N>::fwd_any(g, s) && k < g.kc) Mo[6 * MF + ri.ofwd(g, s)] = cscale(v[s], nRo);
+      if constexpr (ALIAS)  // (a real line: its transform is the spectrum itself)
+        if (k >= g.kc && k <= Bk::NT * 4) Ma[6 * MA + (long long)(k - g.kc) * g.ny + yg] = cscale(v[s], nRo);
     }
   } else {
     const double2 *Q1 = Mi, *Q2 = Mi + MF, *P1 = Mi + 2 * MF, *P2 = Mi + 3 * MF,
@@ -1562,6 +1606,12 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
     fft_line<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) acc[s] = cadd(acc[s], apply_mul(v[s], nt.mb, k, lwav(g, c.t + s * NT)));
+  }
+  if (nt.fc >= 0) {  // Thomas–Yamada's N_ζ (the linear terms vanish here: calcN! dealiases its input)
+    load_col(nt.fc);
+    fft_line<LOG2N, -1>(v, c.t, tws, line);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) acc[s] = cadd(acc[s], apply_mul(v[s], nt.mc, k, lwav(g, c.t + s * NT)));
   }
   if (live) {
     double2* Nf = N + (long long)f * ga.cfield + (long long)col * ga.LrP;
@@ -2782,8 +2832,12 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
       hipLaunchKernelGGL((k_row<MODEL_RSW, L>), dim3(nrows / BR::NB), dim3(BR::THREADS), sh_rsw, s, g, p, Mi, Mo,
                          tw, y0, nullptr);
   } else if (model == MODEL_TY) {
-    hipLaunchKernelGGL((k_row<MODEL_TY, L>), dim3(nrows / BT::NB), dim3(BT::THREADS), sh_ty, s, g, p, Mi, Mo, tw, y0,
-                       nullptr);
+    if (Ma)
+      hipLaunchKernelGGL((k_row<MODEL_TY, L, true>), dim3(nrows / BT::NB), dim3(BT::THREADS), sh_ty, s, g, p, Mi,
+                         Mo, tw, y0, Ma);
+    else
+      hipLaunchKernelGGL((k_row<MODEL_TY, L>), dim3(nrows / BT::NB), dim3(BT::THREADS), sh_ty, s, g, p, Mi, Mo, tw,
+                         y0, nullptr);
   } else if (model == MODEL_RSWA) {
     using BA = BlkRow<MODEL_RSWA, L>;
     if (Ma)
@@ -2814,6 +2868,9 @@ void LenOps<L>::col_fwd_alias(int model, const Geom& g, const Geom& ga, int regi
   const int nb = (ga.kcn + Blk<L>::NB - 1) / Blk<L>::NB;
   if (model == MODEL_RSWA)
     hipLaunchKernelGGL((k_col_fwd_alias<MODEL_RSWA, L>), dim3(nb, 3), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g,
+                       ga, region, p, Mf, Ma, N, tw);
+  else if (model == MODEL_TY)
+    hipLaunchKernelGGL((k_col_fwd_alias<MODEL_TY, L>), dim3(nb, 4), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g,
                        ga, region, p, Mf, Ma, N, tw);
   else
     hipLaunchKernelGGL((k_col_fwd_alias<MODEL_QG2, L>), dim3(nb, 2), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g,
@@ -2947,7 +3004,7 @@ void launch_row(int model, const Geom& g, const Phys& p, const double2* Minv, do
 bool row_alias_built(int model, int log2nx) {
   bool ok = false;
   by_len(log2nx, [&](auto L) {
-    ok = model == MODEL_RSWA || model == MODEL_QG2;
+    ok = model == MODEL_RSWA || model == MODEL_QG2 || model == MODEL_TY;
   });
   return ok;
 }

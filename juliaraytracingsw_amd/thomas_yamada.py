@@ -16,10 +16,17 @@ from .problem import Diagnostic, Problem as _Problem, increment, stepforward  # 
 
 def Problem(dev="gpu", *, nx=128, ny=None, Lx=2 * np.pi, Ly=None, nu=3.5e-25, nnu=8, Ro=0.2,
             stepper="ETDRK4", dt=5e-2, aliased_fraction=1 / 3, T=np.float64, device=0,
-            check_nan=True, unfused=False, decomposition=None):
+            check_nan=True, unfused=False, decomposition=None, aliased_state=False):
     """``ThomasYamada.Problem(dev; nx, ny, Lx, Ly, ν, nν, Ro, stepper, dt,
     aliased_fraction, T)`` (:55-74).  ``stepper`` must be "ETDRK4" (the only
-    stepper the reference runs this model with, cpu-setup/Parameters.jl:12)."""
+    stepper the reference runs this model with, cpu-setup/Parameters.jl:12).
+
+    ``aliased_state=True`` also carries the modes the 2/3 rule removes, as
+    the reference's prob.sol holds them between steps: calcN! dealiases its
+    input in place (:130) but returns N on every mode, and the ETDRK4 update
+    writes α N₁ + 2β (N₂ + N₃) + Γ N₄ there (the energies, :333-360, count
+    them; the next calcN!/updatevars! discards them).  Off by default: the
+    modes never reach a dealiased quantity."""
     if dev not in ("gpu", "GPU", "GPU()"):
         raise _lib.LibSWError("libsw runs on the GPU only (dev='gpu')")
     if stepper != "ETDRK4":
@@ -30,7 +37,7 @@ def Problem(dev="gpu", *, nx=128, ny=None, Lx=2 * np.pi, Ly=None, nu=3.5e-25, nn
     return _Problem(_lib.SW_MODEL_TY, nx=nx, ny=ny, Lx=Lx, Ly=Ly, dt=dt,
                     aliased_fraction=aliased_fraction, stepper=stepper, params=params,
                     device=device, check_nan=check_nan, T=T, unfused=unfused,
-                    **(decomposition or {}))
+                    aliased_state=aliased_state, **(decomposition or {}))
 
 
 def set_solution(prob, zeta0h, u0h, v0h, p0h):
@@ -52,7 +59,8 @@ def enforce_reality_condition(prob):
     for each field.  In Julia ``sol[:,:,k]`` (no ``@views``) is a copy, so
     those r2c's write into temporaries and the state is left as it is: the
     function amounts to ``dealias!`` + ``updatevars!`` — which is what this
-    does (the libsw state is dealiased already).  Returns the physical vars."""
+    does (libsw's updatevars! dealiases an aliased_state problem's state
+    first).  Returns the physical vars."""
     return updatevars(prob)
 
 

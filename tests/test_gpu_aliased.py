@@ -6,7 +6,9 @@ every mode (swqg/TwoLayerQG.jl:152-182: rfft of the products, no dealias of
 N), and the IF/AB3 update writes E·dt·(…N…) into prob.sol there
 (utils/IFMAB3.jl:142-160), so between steps prob.sol holds aliased modes,
 which its energies (:230-252) count and the next calcN!/updatevars!
-discards.  With aliased_state = 1 libsw carries them too (RSW and 2LQG, any
+discards.  Thomas–Yamada's calcN! and ETDRK4 update do the same
+(thomasyamada/ThomasYamada.jl:130; its energies read prob.sol).  With
+aliased_state = 1 libsw carries them too (RSW, 2LQG and TY, any
 nx up to 8192, one slab or several in one process); the oracle keeps the
 full arrays, so every comparison here is
 over ALL modes of the full (nkr, nl) array, at the strongly nonlinear 64²
@@ -53,7 +55,7 @@ def _full_err(a, b):
     return float(np.max(np.abs(a - b)) / np.max(np.abs(b)))
 
 
-@pytest.mark.parametrize("name", QG_CASES + ["rsw_fab3", "rsw_ifmab3", "rsw_ifmrk4"])
+@pytest.mark.parametrize("name", QG_CASES + ["rsw_fab3", "rsw_ifmab3", "rsw_ifmrk4", "ty_etdrk4"])
 def test_full_state_matches_the_reference_array(name):
     """prob.sol after each of 12 steps equals the oracle's un-dealiased
     post-step state on every mode, the aliased ones included (nonzero)."""
@@ -118,7 +120,7 @@ def test_energy_records_of_the_undealiased_state(name):
     prob.close()
 
 
-@pytest.mark.parametrize("name", ["qg2_ifmab3", "qg2_ifmrk4", "rsw_ifmab3"])
+@pytest.mark.parametrize("name", ["qg2_ifmab3", "qg2_ifmrk4", "rsw_ifmab3", "ty_etdrk4"])
 def test_calcN_on_every_mode(name):
     """sw_calcN returns N on the full array, as the reference's calcN!."""
     p, pr, prob = _setup(name)
@@ -132,6 +134,29 @@ def test_calcN_on_every_mode(name):
     assert amax > 1e-7 * np.max(np.abs(ref))
     assert _full_err(got, ref) < RTOL
     assert np.max(np.abs(got[:, mask] - ref[:, mask])) < 1e-8 * amax  # on the aliased modes' own scale
+    prob.close()
+
+
+def test_ty_energies_of_the_undealiased_state():
+    """Thomas–Yamada's energies read prob.sol (thomasyamada/ThomasYamada.jl
+    :333-367), whose aliased modes the ETDRK4 update sets (α N₁ + 2β (N₂ +
+    N₃) + Γ N₄ there, calcN! returning N on every mode): barotropic,
+    baroclinic and the wave/geostrophic split of the full array within 1e-10."""
+    from juliaraytracingsw_amd import thomas_yamada as TY
+
+    p, pr, prob = _setup("ty_etdrk4")
+    for _ in range(3):
+        pr.stepforward(2)
+        prob.stepforward(2)
+        bt, bc, wg = O.ty_energies(pr.sol.copy(), pr.grid)
+        deal = O.ty_energies(pr.grid.dealias(pr.sol.copy()), pr.grid)
+        assert abs(TY.barotropic_energy(prob) / bt - 1) < RTOL
+        assert np.allclose(TY.baroclinic_energy(prob), bc, rtol=RTOL, atol=0)
+        got = TY.wave_geostrophic_energy(prob)
+        assert np.allclose(np.ravel(got), np.ravel(wg), rtol=RTOL, atol=0), (got, wg)
+    gap = abs(bc[0] / deal[1][0] - 1)
+    print(f"[aliased] ty_etdrk4: full-array vs dealiased baroclinic KE differ by {gap:.2e} (relative)")
+    assert gap > 1e-14  # the aliased modes count
     prob.close()
 
 
@@ -179,18 +204,17 @@ def test_default_mode_unchanged():
     prob.close()
 
 
-@pytest.mark.parametrize("bad", ["ty", "frk4", "one_slab_per_process"])
+@pytest.mark.parametrize("bad", ["frk4", "one_slab_per_process"])
 def test_rejected_where_not_built(bad):
-    """Only where it is built: RSW / 2LQG with IFMAB3/IFMRK4/FilteredAB3, every
-    slab in one process (the aliased columns' y-transforms need every row)."""
+    """Only where it is built: RSW / 2LQG with IFMAB3/IFMRK4/FilteredAB3 or
+    Thomas–Yamada with ETDRK4 (not GeophysicalFlows' FilteredRK4), every slab
+    in one process (the aliased columns' y-transforms need every row)."""
     from juliaraytracingsw_amd import _lib
 
     cfg = _lib.default_config()
     cfg.model, cfg.stepper, cfg.nx, cfg.ny = _lib.SW_MODEL_QG2, _lib.STEPPERS["IFMAB3"], 64, 64
     cfg.aliased_state = 1
-    if bad == "ty":
-        cfg.model, cfg.stepper = _lib.SW_MODEL_TY, _lib.STEPPERS["ETDRK4"]
-    elif bad == "frk4":
+    if bad == "frk4":
         cfg.stepper = _lib.STEPPERS["FilteredRK4"]
     else:
         cfg.nranks, cfg.local_slabs, cfg.rank = 2, 1, 0
@@ -202,9 +226,19 @@ def _alias_case(name, nx, ny, amp, seed=11):
     """Oracle problem on an nx × ny grid with a random IC spread over the live
     band (products then reach the aliased modes), and a libsw builder."""
     from juliaraytracingsw_amd import rotating_shallow_water as RSW
+    from juliaraytracingsw_amd import thomas_yamada as TY
 
     p = sw_cases.case_params(name, 256)
     dt = 1e-3
+    if p["model"] == "ty":  # (ν K^16 negligible: every mode, the aliased ones, stays active)
+        pr = O.Problem("ty", "ETDRK4", nx, dt, Lx=p["Lx"], ny=ny, params=O.TYParams(1e-50, 8, p["Ro"]))
+        pr.set_solution(pr.grid.rfft(amp * np.random.default_rng(seed).standard_normal((4, ny, nx))))
+
+        def make_ty(P):
+            dec = None if P == 1 else dict(nranks=P, local_slabs=P)
+            return TY.Problem("gpu", nx=nx, ny=ny, Lx=p["Lx"], dt=dt, nu=1e-50, nnu=8, Ro=p["Ro"],
+                              aliased_state=True, decomposition=dec)
+        return pr, make_ty
     if p["model"] == "rsw":
         params = O.RSWParams(1e-30, 4, p["f"], p["Cg"])
     else:
@@ -233,6 +267,8 @@ def _alias_case(name, nx, ny, amp, seed=11):
     ("qg2_ifmrk4", 8192, 32, (1,), 3, 2.0),      # an 8192-point row (the full-length row with ALIAS)
     ("rsw_ifmab3", 256, 256, (1, 2, 4), 6, 0.3),  # RSW's advective form on 2 and 4 slabs
     ("qg2_fab3", 512, 512, (1, 2, 8), 6, 2.0),
+    ("ty_etdrk4", 256, 256, (1, 2, 4), 3, 0.5),    # Thomas–Yamada's ETDRK4 on slabs
+    ("ty_etdrk4", 8192, 32, (1,), 2, 0.5),         # and an 8192-point row
 ])
 def test_full_state_on_slabs_and_long_rows(name, nx, ny, slabs, steps, amp):
     """prob.sol on every mode of the full array, the aliased ones included,
