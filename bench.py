@@ -32,6 +32,12 @@ Extra keys on the same JSON line (never `value`):
       RCCL rank count, schedule (pipelined / sequential, row chunks) and per
       rank the compute-stream µs per step spent waiting for transposes, the
       step's µs and the bytes sent per step (also in `config5` / `config4`);
+  `kernels_cold`, `roofline.hbm_only` — the per-kernel table again with L2
+      and the 256 MiB Infinity Cache evicted before every launch (libsw's
+      SW_PROF_COLD), i.e. each kernel's inputs from HBM alone; the warm table
+      (`kernels`, `roofline.achieved`) is the step as it runs, where a kernel
+      reads part of what the previous one wrote from the Infinity Cache
+      (--no-cold-profile to skip);
   `cpu_baseline` — rank 0 at N = 1 only.
 """
 import argparse
@@ -184,6 +190,8 @@ def main():
     ap.add_argument("--stepper", default="FilteredAB3",
                     choices=["FilteredAB3", "IFMAB3", "IFMRK4", "ETDRK4", "FilteredRK4"])
     ap.add_argument("--profile-steps", type=int, default=50)
+    ap.add_argument("--no-cold-profile", action="store_true",
+                    help="skip the per-kernel table with caches evicted before each launch")
     ap.add_argument("--min-warmup-s", type=float, default=0.1,
                     help="untimed steps after the W warm-up steps until this much stepping has run (steady state)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -364,6 +372,18 @@ def main():
     comm = comm_report(prob) if slab else None
     # roofline: per-kernel HIP-event durations on libsw's stream
     stats = prob.ctx.profile(args.profile_steps)
+    # the same kernels with L2 and the 256 MiB Infinity Cache evicted before
+    # each launch (SW_PROF_COLD): every input from HBM.  In the step a kernel
+    # reads what the previous one wrote, partly from the Infinity Cache, so
+    # the warm table above is the step's rate and this one the HBM-only rate
+    stats_cold = None
+    if not args.no_cold_profile:
+        os.environ["SW_PROF_COLD"] = "1"
+        try:
+            stats_cold = prob.ctx.profile(max(3, args.profile_steps // 5))
+        finally:
+            os.environ.pop("SW_PROF_COLD", None)
+            prob.ctx.profile(1)  # (frees the eviction buffer)
     step_alg = prob.ctx.step_alg_bytes()
     # the boundary's host-buffer cost: one state download and
     # upload through the C ABI, i.e. over PCIe (after the timed region)
@@ -424,6 +444,8 @@ def main():
     kern = [s for s in stats if s["name"] != "transpose"]
     dom = max(kern, key=lambda s: s["avg_ms"] * s["launches"])
     achieved = dom["alg_bytes"] / (dom["avg_ms"] * 1e-3) / 1e9
+    dom_cold = next((s for s in stats_cold or [] if s["name"] == dom["name"]), None)
+    achieved_cold = dom_cold["alg_bytes"] / (dom_cold["avg_ms"] * 1e-3) / 1e9 if dom_cold else None
     traffic = None
     try:
         tj = json.load(open(args.traffic_json))
@@ -483,9 +505,17 @@ def main():
         "reference_byte_model": {"bytes_per_step": balg, "equivalent_GBps_per_gpu": balg * per_gpu_rate / 1e9},
         "roofline": {"bound": "hbm", "kernel": dom["name"], "achieved": achieved, "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
-                     "alg_bytes_per_launch": dom["alg_bytes"], "avg_us_per_launch": dom["avg_ms"] * 1e3},
+                     "alg_bytes_per_launch": dom["alg_bytes"], "avg_us_per_launch": dom["avg_ms"] * 1e3,
+                     # in the step some of its input comes from the Infinity
+                     # Cache; with L2 and that cache evicted before the launch
+                     # (SW_PROF_COLD) every byte comes from HBM:
+                     "hbm_only": None if dom_cold is None else {
+                         "achieved": achieved_cold, "frac": achieved_cold / HBM_PEAK_GBPS,
+                         "avg_us_per_launch": dom_cold["avg_ms"] * 1e3}},
         "kernels": [{"name": s["name"], "avg_us": s["avg_ms"] * 1e3, "per_step": s["launches"] / args.profile_steps,
                      "alg_bytes": s["alg_bytes"]} for s in stats],
+        "kernels_cold": None if stats_cold is None else [
+            {"name": s["name"], "avg_us": s["avg_ms"] * 1e3, "alg_bytes": s["alg_bytes"]} for s in stats_cold],
         "ensemble": ensemble,
         "slab_error": slab_error,
         "comm": comm,

@@ -313,7 +313,9 @@ typedef struct sw_comm_stats {
 int sw_comm_profile(sw_ctx* ctx, int64_t nsteps, sw_comm_stats* out);
 
 /* Per-kernel HIP-event timing of `nsteps` steps (the state advances).
- * Fills up to max_stats entries; *n_stats receives the count. */
+ * Fills up to max_stats entries; *n_stats receives the count.  With
+ * SW_PROF_COLD=1 in the environment a read of a 512 MiB buffer precedes each
+ * timed kernel (L2 and Infinity Cache evicted: inputs from HBM alone). */
 int sw_profile_steps(sw_ctx* ctx, int64_t nsteps, sw_kernel_stat* stats,
                      int32_t max_stats, int32_t* n_stats);
 

@@ -125,6 +125,11 @@ struct sw_ctx {
   bool prof = false;
   std::vector<KStat> stats;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // SW_PROF_COLD=1: before each profiled kernel a read of this 512 MiB buffer
+  // evicts L2 and the 256 MiB Infinity Cache, so each kernel reads its inputs
+  // from HBM (the cold per-kernel table in bench.py)
+  double* cold = nullptr;
+  unsigned long long* cold_out = nullptr;
 };
 
 namespace {
@@ -339,10 +344,12 @@ static double step_bytes(const sw_ctx* c) {
   return nstage * (kernel_bytes(c, K_ROW) + kernel_bytes(c, K_COLSTEP));  // primed pipeline
 }
 
+constexpr size_t kColdBytes = size_t(512) << 20;
 struct Timer {
   sw_ctx* c;
   int kid;
   Timer(sw_ctx* c_, int k) : c(c_), kid(k) {
+    if (c->prof && c->cold) sw::launch_absmax(c->cold, kColdBytes / sizeof(double), c->cold_out, 0, c->stream);
     if (c->prof) (void)hipEventRecord(c->ev0, c->stream);
   }
   ~Timer() {
@@ -1375,7 +1382,7 @@ void sw_destroy(sw_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (Slab& s : c->sl) free_slab(s);
   void* ptrs[] = {c->tw_x, c->tw_y, c->stage, c->stage32, c->gbuf, c->dflt, c->flag, c->ecols, c->esum, c->erec,
-                  c->erec1};
+                  c->erec1, c->cold, c->cold_out};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   if (c->nccl) (void)ncclCommDestroy(c->nccl);
@@ -1850,6 +1857,18 @@ int sw_profile_steps(sw_ctx* c, int64_t nsteps, sw_kernel_stat* out, int32_t max
     s.ms = 0.0;
   }
   if (int rc = join_comm(c)) return rc;
+  const char* ce = std::getenv("SW_PROF_COLD");
+  if (ce && ce[0] == '1' && !c->cold) {
+    if (int rc = alloc(c, (void**)&c->cold, kColdBytes)) return rc;
+    if (int rc = alloc(c, (void**)&c->cold_out, 64)) return rc;
+  }
+  if (!(ce && ce[0] == '1') && c->cold) {
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipFree(c->cold);
+    (void)hipFree(c->cold_out);
+    c->cold = nullptr;
+    c->cold_out = nullptr;
+  }
   c->prof = true;
   int rc = 0;
   for (int64_t i = 0; i < nsteps && !rc; ++i) rc = step_once(c);
