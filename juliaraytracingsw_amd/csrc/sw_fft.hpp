@@ -646,4 +646,101 @@ __device__ __forceinline__ void fftw_dit_split(double2 (&v)[C][8], int t, int kc
   }
 }
 
+// ---------------------------------------------------------------------------
+// 8192-point lines over 1024 threads (16 waves) decimated by 16 across the
+// waves, as fftw_dif/fftw_dit above (Q = 512, one wave per sub-transform):
+// the radix-16 split as a radix-8 in each thread's registers (spacing 1024)
+// and a radix-2 on the way out of the one workgroup-wide exchange.  With
+// ω = exp(DIR 2πi/N), N = 8192, wave w = 8e + c, lane j:
+//   DIF (natural in: v[s] = x[t + 1024 s] → decimated out):
+//     y_c[n] = ω^(nc) Σ_q x[n + 1024 q] ω_8^(qc)            (registers)
+//     z_w[m] = (y_c[m] + (-1)^e y_c[m + 512]) ω_1024^(m e)  (after the exchange)
+//     X[16 m + w] = DFT_512(z_w)[m]                          (wave-local)
+//     on exit lane j of wave w holds X[16 (j + 64 r) + w] in v[r];
+//   DIT (that order in → natural out): Y_w = DFT_512(x[16 m + w]),
+//     Z_c[k] = Y_c[k mod 512] + ω_1024^k Y_(c+8)[k mod 512], k < 1024,
+//     X[k + 1024 q] = Σ_c ω_8^(qc) ω^(kc) Z_c[k]: on exit v[q] = X[t + 1024 q].
+// Three workgroup barriers per transform (Stockham: ten).  tab: the
+// forward-sign table of length N (W_N^t read per transform, not held);
+// tq = Twiddles<9, true>::load(t & 63, tab, 4).  PRE: a barrier before the
+// first LDS write.
+// ---------------------------------------------------------------------------
+// ω_16^u (u < 8), ω_16 = exp(DIR 2πi/16), times a (u a constant once unrolled)
+template <int DIR>
+__device__ __forceinline__ double2 w16_mul(double2 a, int u) {
+  constexpr double c1 = 0.92387953251128675613, s1 = 0.38268343236508977173;
+  if (u == 0) return a;
+  if (u == 4) return (DIR < 0) ? make_double2(a.y, -a.x) : make_double2(-a.y, a.x);
+  if (u == 2 || u == 6) return w8_mul<DIR>(a, u / 2);
+  const double cs[8] = {1.0, c1, 0.0, s1, 0.0, -s1, 0.0, -c1};
+  const double sn[8] = {0.0, s1, 0.0, c1, 0.0, c1, 0.0, s1};
+  return cmul(a, make_double2(cs[u], DIR * sn[u]));
+}
+
+template <int DIR, bool PRE = true>
+__device__ __forceinline__ void fft16_dif(double2 (&v)[8], int t, const Twiddles<9, true>& tq,
+                                          const double2* __restrict__ tab, double2* __restrict__ line) {
+  constexpr int NT = 1024, Q = 512;
+  asm volatile("" : "+v"(t));
+  const double2 wt = tab[t];
+  const double2 t8 = tab[8 * (t & 63)];  // ω_1024^j (waves 8-15), issued early
+  dft8<DIR>(v);
+  {  // ω^(t c), a chain (two powers live)
+    const double2 w1 = DIR < 0 ? wt : cconj(wt);
+    double2 wp = w1;
+#pragma unroll
+    for (int c = 1; c < 8; ++c) {
+      v[c] = cmul(v[c], wp);
+      if (c < 7) wp = cmul(wp, w1);
+    }
+  }
+  if constexpr (PRE) lds_barrier();
+  const int b = LPs<true>(t);
+#pragma unroll
+  for (int c = 0; c < 8; ++c) line[c * NT + b] = v[c];
+  lds_barrier();
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6), j = t & 63;
+  const double2* src = line + (w & 7) * NT + LPs<true>(j);
+  if (w < 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = cadd(src[64 * u], src[64 * u + Q]);
+  } else {
+    const double2 wj = DIR < 0 ? t8 : cconj(t8);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = w16_mul<DIR>(cmul(csub(src[64 * u], src[64 * u + Q]), wj), u);
+  }
+  lds_barrier();  // every wave has read its sub-line: the regions are free
+  fft_lines<9, DIR, 1, true, true>(reinterpret_cast<double2(&)[1][8]>(v), j, tq, line + w * Q, 0);
+}
+
+template <int DIR, bool PRE = true>
+__device__ __forceinline__ void fft16_dit(double2 (&v)[8], int t, const Twiddles<9, true>& tq,
+                                          const double2* __restrict__ tab, double2* __restrict__ line) {
+  constexpr int Q = 512;
+  if constexpr (PRE) lds_barrier();
+  asm volatile("" : "+v"(t));
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6), j = t & 63;
+  double2* reg = line + w * Q;
+  fft_lines<9, DIR, 1, true, true>(reinterpret_cast<double2(&)[1][8]>(v), j, tq, reg, 0);  // Y_w[j + 64 r]
+  const int bj = LPs<true>(j);
+#pragma unroll
+  for (int r = 0; r < 8; ++r) reg[bj + 64 * r] = v[r];
+  const double2 t8 = tab[8 * t], wt = tab[t];  // ω_1024^t (t < 1024), W_N^t: in flight over the barrier
+  lds_barrier();
+  const double2 wk = DIR < 0 ? t8 : cconj(t8);
+  const double2* src = line + LPs<true>(t & (Q - 1));
+#pragma unroll
+  for (int c = 0; c < 8; ++c) v[c] = cadd(src[c * Q], cmul(src[(c + 8) * Q], wk));
+  {
+    const double2 w1 = DIR < 0 ? wt : cconj(wt);
+    double2 wp = w1;
+#pragma unroll
+    for (int c = 1; c < 8; ++c) {
+      v[c] = cmul(v[c], wp);
+      if (c < 7) wp = cmul(wp, w1);
+    }
+  }
+  dft8<DIR>(v);
+}
+
 }  // namespace sw

@@ -155,6 +155,85 @@ __device__ __forceinline__ LineCtx line_ctx() {
 
 __device__ __forceinline__ double2 zero2() { return make_double2(0.0, 0.0); }
 
+// ---------------------------------------------------------------------------
+// Decimated column transforms (round 4).  From 2^SW_COL_DEC_MIN points the
+// column passes' y-transforms are the wave-decimated ones (sw_fft.hpp:
+// fftw_dif/fftw_dit for W = N/512 <= 8, fft16_dif/fft16_dit at 8192): one
+// workgroup exchange per transform, the rest inside each wave.  Their
+// physical-space side is in the decimated order, and the mixed fields keep it:
+// slot s of thread t (wave w = t/64, lane j) is the stored row
+//   p = 512 w + j + 64 s,   physical row y = (N/512) (p mod 512) + p / 512,
+// contiguous across the lanes as the natural order's p = t + s NT.  The row
+// pass is order-blind (it transforms whole stored rows; the slab exchange
+// moves blocks of stored rows), so nothing else changes: k_col_inv writes
+// that order (DIF: natural spectrum in), k_col_fwd / k_col_step read it (DIT:
+// natural spectrum out); the physical-space output (k_col_inv1, k_row_c2r1)
+// keeps the natural order.  Aliased-state tracking's row-pass x-spectra
+// (Ma, indexed by the stored row) follow the same order.
+// ---------------------------------------------------------------------------
+#ifndef SW_COL_DEC_MIN
+#define SW_COL_DEC_MIN 12
+#endif
+template <int LOG2N>
+__host__ __device__ constexpr bool col_dec() {
+  return LOG2N >= SW_COL_DEC_MIN && LOG2N >= 10 && LOG2N <= 13;
+}
+// stored row of slot s of thread t
+template <int LOG2N>
+__device__ __forceinline__ int cpos(int t, int s) {
+  if constexpr (col_dec<LOG2N>()) return ((t >> 6) << 9) + (t & 63) + (s << 6);
+  else return t + s * FftPlan<LOG2N>::NT;
+}
+template <int LOG2N, bool DEC = col_dec<LOG2N>()>
+struct ColTw {
+  Twiddles<LOG2N> tws;
+  __device__ __forceinline__ void load(int t, const double2* __restrict__ tw) { tws.load(t, tw); }
+};
+template <int LOG2N>
+struct ColTw<LOG2N, true> {
+  static constexpr bool FLY = LOG2N >= 12;
+  Twiddles<9, FLY> tq;
+  const double2* tab;
+  __device__ __forceinline__ void load(int t, const double2* __restrict__ tw) {
+    tq.load(t & 63, tw, LOG2N - 9);
+    tab = tw;
+  }
+};
+// the column passes' y-transform: DIR = +1 natural spectrum -> stored rows,
+// DIR = -1 stored rows -> natural spectrum (v[s] = X[t + s NT])
+template <int LOG2N, int DIR>
+__device__ __forceinline__ void col_fft(double2 (&v)[8], int t, const ColTw<LOG2N>& c, double2* __restrict__ line) {
+  if constexpr (!col_dec<LOG2N>()) {
+    fft_line<LOG2N, DIR>(v, t, c.tws, line);
+  } else if constexpr (LOG2N == 13) {
+    if constexpr (DIR > 0) fft16_dif<DIR>(v, t, c.tq, c.tab, line);
+    else fft16_dit<DIR>(v, t, c.tq, c.tab, line);
+  } else {
+    constexpr int W = 1 << (LOG2N - 9);
+    constexpr bool FLY = ColTw<LOG2N>::FLY;
+    using V1 = double2(&)[1][8];
+    const double2 wt = c.tab[t];  // W_N^t, read per transform (not held)
+    if constexpr (DIR > 0) fftw_dif<W, DIR, 1, true, FLY>(reinterpret_cast<V1>(v), t, wt, c.tq, line, 0);
+    else fftw_dit<W, DIR, 1, FLY, true>(reinterpret_cast<V1>(v), t, wt, c.tq, line, 0);
+  }
+}
+// the inverse-field stores of a column line at the stored rows cpos (as
+// store_col_i: closed form with one slab)
+template <int LOG2N, typename F>
+__device__ __forceinline__ void store_col_p(const Geom& g, int krl, int t, F put) {
+  constexpr bool DEC = col_dec<LOG2N>();
+  constexpr int PS = DEC ? 64 : FftPlan<LOG2N>::NT;  // stored-row stride of the slots
+  if (SW_TILE_I == 2 && SW_LORD_I == 0 && PS % 4 == 0 && g.nslab == 1) {
+    const int b = midc_i_col_base<PS>(g, krl, cpos<LOG2N>(t, 0));
+#pragma unroll
+    for (int s = 0; s < 8; ++s) put(s, b + s * (PS >> 2) * (g.kcl >> 1) * 8);
+  } else {
+    asm volatile("" : "+v"(t));
+#pragma unroll
+    for (int s = 0; s < 8; ++s) put(s, midc_i(g, krl, cpos<LOG2N>(t, s)));
+  }
+}
+
 // ===========================================================================
 // col_inv: for column kr, build the y-spectra the row pass needs, inverse FFT
 // along y (scaled by 1/(nx ny), FF's normalised c2r), store to mixed space.
@@ -188,7 +267,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
   const bool live = krl < g.kcn;
   if (B::NB == 1 && !live) return;  // padding column: nobody reads it
   double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
-  Twiddles<LOG2N> tws;
+  ColTw<LOG2N> tws;
   tws.load(c.t, tw);
   const double scale = 1.0 / ((double)g.nx * (double)g.ny);
   const double k = (g.kr0 + krl) * g.mk;
@@ -197,7 +276,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
   auto store = [&](int o) {  // fft_line leaves Y[t + s*NT] in v[s]
     if (live) {
       double2* Mo = M + (long long)o * g.mfield;
-      store_col_i<NT>(g, krl, c.t, [&](int s, int o) { Mo[o] = v[s]; });
+      store_col_p<LOG2N>(g, krl, c.t, [&](int s, int o) { Mo[o] = v[s]; });
     }
   };
 
@@ -215,12 +294,12 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
       x[s] = (live && j >= 0) ? t : zero2();
       v[s] = cscale(x[s], scale);
     }
-    fft_line<LOG2N, +1>(v, c.t, tws, line);
+    col_fft<LOG2N, +1>(v, c.t, tws, line);
     store(grp);
     if (grp == 0 || (MODEL == MODEL_RSWA && grp == 1)) {  // ∂y u: Uy (advective form: and ∂y v: Vy)
 #pragma unroll
       for (int s = 0; s < 8; ++s) v[s] = cmul_i(x[s], lwav(g, c.t + s * NT) * scale);
-      fft_line<LOG2N, +1>(v, c.t, tws, line);
+      col_fft<LOG2N, +1>(v, c.t, tws, line);
       store(3 + grp);
     }
   } else if constexpr (MODEL == MODEL_TY) {
@@ -254,34 +333,34 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
         psi[s] = v[s];
         v[s] = cscale(x[s], scale);
       }
-      fft_line<LOG2N, +1>(v, c.t, tws, line);
+      col_fft<LOG2N, +1>(v, c.t, tws, line);
       store(0);
 #pragma unroll
       for (int s = 0; s < 8; ++s) v[s] = cscale(psi[s], scale);
-      fft_line<LOG2N, +1>(v, c.t, tws, line);
+      col_fft<LOG2N, +1>(v, c.t, tws, line);
       store(1);
     } else if (grp == 1) {  // x = ψ
 #pragma unroll
       for (int s = 0; s < 8; ++s) v[s] = cmul_i(x[s], -lwav(g, c.t + s * NT) * scale);
-      fft_line<LOG2N, +1>(v, c.t, tws, line);
+      col_fft<LOG2N, +1>(v, c.t, tws, line);
       store(2);
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
         const double l = lwav(g, c.t + s * NT);
         v[s] = cscale(x[s], (l * l) * scale);
       }
-      fft_line<LOG2N, +1>(v, c.t, tws, line);
+      col_fft<LOG2N, +1>(v, c.t, tws, line);
       store(3);
     } else {
       const int o = grp == 2 ? 4 : (grp == 3 ? 6 : 7);
 #pragma unroll
       for (int s = 0; s < 8; ++s) v[s] = cscale(x[s], scale);
-      fft_line<LOG2N, +1>(v, c.t, tws, line);
+      col_fft<LOG2N, +1>(v, c.t, tws, line);
       store(o);
       if (grp != 3) {  // ∂y uc, ∂y pc
 #pragma unroll
         for (int s = 0; s < 8; ++s) v[s] = cmul_i(x[s], lwav(g, c.t + s * NT) * scale);
-        fft_line<LOG2N, +1>(v, c.t, tws, line);
+        col_fft<LOG2N, +1>(v, c.t, tws, line);
         store(o + 1);
       }
     }
@@ -306,15 +385,15 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
       qg_psi(p, K2, q1.x, q1.y, q2.x, q2.y, grp, psi[s].x, psi[s].y);
       v[s] = cscale(qg, scale);
     }
-    fft_line<LOG2N, +1>(v, c.t, tws, line);
+    col_fft<LOG2N, +1>(v, c.t, tws, line);
     store(grp);
 #pragma unroll
     for (int s = 0; s < 8; ++s) v[s] = cscale(psi[s], scale);
-    fft_line<LOG2N, +1>(v, c.t, tws, line);
+    col_fft<LOG2N, +1>(v, c.t, tws, line);
     store(2 + grp);
 #pragma unroll
     for (int s = 0; s < 8; ++s) v[s] = cmul_i(psi[s], lwav(g, c.t + s * NT) * scale);
-    fft_line<LOG2N, +1>(v, c.t, tws, line);
+    col_fft<LOG2N, +1>(v, c.t, tws, line);
     store(4 + grp);
   }
 }
@@ -1487,7 +1566,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
   if (B::NB == 1 && !live) return;
   const int krA = krl < g.kcl ? krl : g.kcl - 1;  // in-bounds address
   double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
-  Twiddles<LOG2N> tws;
+  ColTw<LOG2N> tws;
   tws.load(c.t, tw);
   const double k = (g.kr0 + krl) * g.mk;
   const long long MF = g.mfield;
@@ -1496,7 +1575,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
   auto load_col = [&](const double2* Mfield) {
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      const double2 t = mix_ld_col(Mfield + midc(g, krA, c.t + s * NT));
+      const double2 t = mix_ld_col(Mfield + midc(g, krA, cpos<LOG2N>(c.t, s)));
       v[s] = live ? t : zero2();
     }
   };
@@ -1504,18 +1583,18 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
   const NTerms nt = nterms<MODEL>(grp);
   // fft_line leaves F[m = t + s*NT] in v[s]; only live rows are written
   load_col(Mf + nt.fa * MF);
-  fft_line<LOG2N, -1>(v, c.t, tws, line);
+  col_fft<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
   for (int s = 0; s < 8; ++s) acc[s] = apply_mul(v[s], nt.ma, k, lwav(g, c.t + s * NT));
   if (nt.fb >= 0) {
     load_col(Mf + nt.fb * MF);
-    fft_line<LOG2N, -1>(v, c.t, tws, line);
+    col_fft<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) acc[s] = cadd(acc[s], apply_mul(v[s], nt.mb, k, lwav(g, c.t + s * NT)));
   }
   if (MODEL == MODEL_TY && nt.fc >= 0) {
     load_col(Mf + nt.fc * MF);
-    fft_line<LOG2N, -1>(v, c.t, tws, line);
+    col_fft<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) acc[s] = cadd(acc[s], apply_mul(v[s], nt.mc, k, lwav(g, c.t + s * NT)));
   }
@@ -1583,7 +1662,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
   const bool live = col < ga.kcn;
   const int colA = live ? col : 0;
   double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
-  Twiddles<LOG2N> tws;
+  ColTw<LOG2N> tws;
   tws.load(c.t, tw);
   const double k = (ga.kr0 + colA) * g.mk;
   const long long MA = (long long)(g.nkr - g.kc) * g.ny;
@@ -1591,25 +1670,25 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
   auto load_col = [&](int fi) {
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      const int m = c.t + s * NT;
+      const int m = cpos<LOG2N>(c.t, s);  // stored row
       const double2 t = region == 0 ? Ma[fi * MA + (long long)colA * g.ny + m] : Mf[fi * g.mfield + midc(g, colA, m)];
       v[s] = live ? t : zero2();
     }
   };
   const NTerms nt = nterms<MODEL>(f);
   load_col(nt.fa);
-  fft_line<LOG2N, -1>(v, c.t, tws, line);
+  col_fft<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
   for (int s = 0; s < 8; ++s) acc[s] = apply_mul(v[s], nt.ma, k, lwav(g, c.t + s * NT));
   if (nt.fb >= 0) {
     load_col(nt.fb);
-    fft_line<LOG2N, -1>(v, c.t, tws, line);
+    col_fft<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) acc[s] = cadd(acc[s], apply_mul(v[s], nt.mb, k, lwav(g, c.t + s * NT)));
   }
   if (nt.fc >= 0) {  // Thomas–Yamada's N_ζ (the linear terms vanish here: calcN! dealiases its input)
     load_col(nt.fc);
-    fft_line<LOG2N, -1>(v, c.t, tws, line);
+    col_fft<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) acc[s] = cadd(acc[s], apply_mul(v[s], nt.mc, k, lwav(g, c.t + s * NT)));
   }
@@ -2065,7 +2144,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   if (B::NB == 1 && !live) return;
   const int krA = krl < g.kcl ? krl : g.kcl - 1;
   double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
-  Twiddles<LOG2N> tws;
+  ColTw<LOG2N> tws;
   tws.load(c.t, tw);
   const double k = (g.kr0 + krl) * g.mk;
   const long long MF = g.mfield;
@@ -2074,7 +2153,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   auto load_col = [&](const double2* Mfield) {
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      const double2 t = mix_ld_col(Mfield + midc(g, krA, c.t + s * NT));
+      const double2 t = mix_ld_col(Mfield + midc(g, krA, cpos<LOG2N>(c.t, s)));
       v[s] = live ? t : zero2();
     }
   };
@@ -2083,12 +2162,12 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   auto compute_N = [&](double2 (&n)[8], int f) {
     const NTerms nt = nterms<MODEL>(f);
     load_col(Mf + nt.fa * MF);
-    fft_line<LOG2N, -1>(v, c.t, tws, line);
+    col_fft<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) n[s] = apply_mul(v[s], nt.ma, k, lwav(g, c.t + s * NT));
     if (nt.fb >= 0) {
       load_col(Mf + nt.fb * MF);
-      fft_line<LOG2N, -1>(v, c.t, tws, line);
+      col_fft<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
       for (int s = 0; s < 8; ++s) n[s] = cadd(n[s], apply_mul(v[s], nt.mb, k, lwav(g, c.t + s * NT)));
     }
@@ -2153,7 +2232,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   auto store = [&](int o) {
     if (live) {
       double2* Mo = Minv + (long long)o * MF;
-      store_col_i<NT>(g, krl, c.t, [&](int s, int o) { Mo[o] = v[s]; });
+      store_col_p<LOG2N>(g, krl, c.t, [&](int s, int o) { Mo[o] = v[s]; });
     }
   };
   if constexpr (MODEL == MODEL_RSW) {
@@ -2163,12 +2242,12 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
       load_x(f, x);
 #pragma unroll
       for (int s = 0; s < 8; ++s) v[s] = cscale(x[s], scale);
-      fft_line<LOG2N, +1>(v, c.t, tws, line);
+      col_fft<LOG2N, +1>(v, c.t, tws, line);
       store(f);
       if (f == 0) {  // Uy
 #pragma unroll
         for (int s = 0; s < 8; ++s) v[s] = cmul_i(x[s], lwav(g, c.t + s * NT) * scale);
-        fft_line<LOG2N, +1>(v, c.t, tws, line);
+        col_fft<LOG2N, +1>(v, c.t, tws, line);
         store(3);
       }
     }
@@ -2180,7 +2259,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     for (int f = 0; f < 2; ++f) {
 #pragma unroll
       for (int s = 0; s < 8; ++s) v[s] = cscale(f ? q2[s] : q1[s], scale);
-      fft_line<LOG2N, +1>(v, c.t, tws, line);
+      col_fft<LOG2N, +1>(v, c.t, tws, line);
       store(f);
       double2 psi[8];
 #pragma unroll
@@ -2190,11 +2269,11 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
         qg_psi(p, K2, q1[s].x, q1[s].y, q2[s].x, q2[s].y, f, psi[s].x, psi[s].y);
         v[s] = cscale(psi[s], scale);
       }
-      fft_line<LOG2N, +1>(v, c.t, tws, line);
+      col_fft<LOG2N, +1>(v, c.t, tws, line);
       store(2 + f);
 #pragma unroll
       for (int s = 0; s < 8; ++s) v[s] = cmul_i(psi[s], lwav(g, c.t + s * NT) * scale);
-      fft_line<LOG2N, +1>(v, c.t, tws, line);
+      col_fft<LOG2N, +1>(v, c.t, tws, line);
       store(4 + f);
     }
   }
@@ -2227,7 +2306,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   const int krA = krl < g.kcl ? krl : g.kcl - 1;
   double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
   double2* park = smem + B::NB * FftPlan<LOG2N>::LDS + (long long)c.ln * NF * g.Lr;
-  Twiddles<LOG2N> tws;
+  ColTw<LOG2N> tws;
   tws.load(c.t, tw);
   const double k = (g.kr0 + krl) * g.mk;
   const long long MF = g.mfield;
@@ -2235,7 +2314,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   auto load_col = [&](const double2* Mfield) {
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      const double2 t = mix_ld_col(Mfield + midc(g, krA, c.t + s * NT));
+      const double2 t = mix_ld_col(Mfield + midc(g, krA, cpos<LOG2N>(c.t, s)));
       v[s] = live ? t : zero2();
     }
   };
@@ -2244,12 +2323,12 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   for (int f = 0; f < NF; ++f) {
     const NTerms nt = nterms<MODEL>(f);
     load_col(Mf + nt.fa * MF);
-    fft_line<LOG2N, -1>(v, c.t, tws, line);
+    col_fft<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) n[s] = apply_mul(v[s], nt.ma, k, lwav(g, c.t + s * NT));
     if (nt.fb >= 0) {
       load_col(Mf + nt.fb * MF);
-      fft_line<LOG2N, -1>(v, c.t, tws, line);
+      col_fft<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
       for (int s = 0; s < 8; ++s) n[s] = cadd(n[s], apply_mul(v[s], nt.mb, k, lwav(g, c.t + s * NT)));
     }
@@ -2322,7 +2401,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, (Blk<LOG2N>::THREA
   if (B::NB == 1 && !live) return;
   const int krA = krl < g.kcl ? krl : g.kcl - 1;
   double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
-  Twiddles<LOG2N> tws;
+  ColTw<LOG2N> tws;
   tws.load(c.t, tw);
   const double k = (g.kr0 + krl) * g.mk;
   const long long MF = g.mfield;
@@ -2334,7 +2413,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, (Blk<LOG2N>::THREA
 #ifdef SW_EXP_CS_NOMIX  // experiment: mixed-field loads from one line (wrong results)
       const double2 t = Mfield[c.t & 7];
 #else
-      const double2 t = mix_ld_col(Mfield + midc(g, krA, c.t + s * NT));
+      const double2 t = mix_ld_col(Mfield + midc(g, krA, cpos<LOG2N>(c.t, s)));
 #endif
       dst[s] = live ? t : zero2();
     }
@@ -2342,12 +2421,12 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, (Blk<LOG2N>::THREA
   const NTerms nt = nterms<MODEL_RSW>(f);
   // ---- N_f (rsw/RotatingShallowWater.jl:174-226; nterms)
   load_col(v, Mf + nt.fa * MF);
-  fft_line<LOG2N, -1>(v, c.t, tws, line);
+  col_fft<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
   for (int s = 0; s < 8; ++s) n[s] = apply_mul(v[s], nt.ma, k, lwav(g, c.t + s * NT));
   if (nt.fb >= 0) {
     load_col(v, Mf + nt.fb * MF);
-    fft_line<LOG2N, -1>(v, c.t, tws, line);
+    col_fft<LOG2N, -1>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) n[s] = cadd(n[s], apply_mul(v[s], nt.mb, k, lwav(g, c.t + s * NT)));
   }
@@ -2429,17 +2508,17 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, (Blk<LOG2N>::THREA
   auto store = [&](int o) {
     if (live) {
       double2* Mo = Minv + (long long)o * MF;
-      store_col_i<NT>(g, krl, c.t, [&](int s, int o) { Mo[o] = v[s]; });
+      store_col_p<LOG2N>(g, krl, c.t, [&](int s, int o) { Mo[o] = v[s]; });
     }
   };
 #pragma unroll
   for (int s = 0; s < 8; ++s) v[s] = cscale(x[s], scale);
-  fft_line<LOG2N, +1>(v, c.t, tws, line);
+  col_fft<LOG2N, +1>(v, c.t, tws, line);
   store(f);
   if (f == 0) {  // ∂y u: Uy
 #pragma unroll
     for (int s = 0; s < 8; ++s) v[s] = cmul_i(x[s], lwav(g, c.t + s * NT) * scale);
-    fft_line<LOG2N, +1>(v, c.t, tws, line);
+    col_fft<LOG2N, +1>(v, c.t, tws, line);
     store(3);
   }
 }
