@@ -821,12 +821,18 @@ int run_stage(sw_ctx* c, int op, int stage, double2* Slab::*X) {
       sw::launch_step_elem(c->nf, op, s.g, c->p, a, s.nbuf, s.xs, c->stream);
       // the same update at the aliased modes, from the zero (dealiased) state:
       // the post-step values the reference's update writes there
-      // (utils/IFMAB3.jl:142-160; filter after)
+      // (utils/IFMAB3.jl:142-160; filter after).  NOPcalcN!
+      // (rsw/RotatingShallowWater.jl:135) dealiases nothing, so there the
+      // update starts from the aliased modes' own values: a copy of them in
+      // the zero buffer (not in place: the FilteredAB3 matvec couples fields)
       for (int r = 0; c->alias && r < 2; ++r) {
         if (s.ga[r].kcn <= 0) continue;
+        const size_t cb = (size_t)c->nf * s.ga[r].cfield * sizeof(double2);
+        if (c->cfg.nop_calcN) HIPCHK(c, hipMemcpyAsync(s.a_zero[r], s.a_sol[r], cb, hipMemcpyDeviceToDevice, c->stream));
         sw::StepPtrs b = alias_step_ptrs(c, s, r);
         b.stage = stage;
         sw::launch_step_elem(c->nf, op, s.ga[r], c->p, b, s.a_nbuf[r], s.a_xs[r], c->stream);
+        if (c->cfg.nop_calcN) HIPCHK(c, hipMemsetAsync(s.a_zero[r], 0, cb, c->stream));
       }
     }
     c->mixed_valid = false;

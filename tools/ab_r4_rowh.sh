@@ -16,6 +16,6 @@ for r in $(seq $R); do
   for v in $(ls sweep_var | grep '^q13' | sed 's/.so$//'); do run $v qg2 8192 IFMRK4 12 3 || exit 1; done
   for v in $(ls sweep_var | grep '^r12' | sed 's/.so$//'); do run $v rsw 4096 FilteredAB3 100 20 || exit 1; done
 done
-for v in $(ls sweep_var | grep "^q13[ab]" | sed "s/.so$//"); do bash tools/traffic_at.sh $PWD/sweep_var/$v.so $v qg2 IFMRK4 8192 4 || exit 2; done
+for v in $(ls sweep_var | grep "^q13" | sed "s/.so$//"); do bash tools/traffic_at.sh $PWD/sweep_var/$v.so $v qg2 IFMRK4 8192 4 || exit 2; done
 for v in $(ls sweep_var | grep '^r12' | sed 's/.so$//'); do bash tools/traffic_at.sh $PWD/sweep_var/$v.so $v rsw FilteredAB3 4096 10 || exit 3; done
 for f in gpurun_out/tr/*/t.json; do python -c "import json,sys; d=json.load(open('$f')); print('$f', {k: (round(d['fetch_bytes'].get(k,0)/1e6,1), round(d['write_bytes'].get(k,0)/1e6,1)) for k in d['kernels']})"; done
