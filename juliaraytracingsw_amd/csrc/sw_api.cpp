@@ -174,6 +174,9 @@ int col_lines_per_block(int ny) {
   return NT >= SW_BLK_THREADS ? 1 : std::min(SW_BLK_THREADS / NT, 32);
 }
 
+#ifndef SW_TILE_F4_QG
+#define SW_TILE_F4_QG 13
+#endif
 // geometry of slab s of P
 Geom make_geom(const sw_config& k, int P, int s) {
   Geom g{};
@@ -231,8 +234,18 @@ Geom make_geom(const sw_config& k, int P, int s) {
     ford = 0;
     if (const char* e = std::getenv("SW_FWD_ORD")) ford = e[0] == '1';
   }
-  g.fsy = ford ? 1 : g.kcl / 2;
-  g.fsk = ford ? g.nyl / 4 : 1;
+  // forward tiles of 4 columns × 2 rows (fa = 2) where the 2LQG/MultiLayerQG
+  // row is the half-length one at 2^SW_TILE_F4_QG points and up: its forward
+  // stores then fill 64 B of each line per row, and partial 2×4 lines no
+  // longer leave L2 before their four rows meet (config 5: row writes 1.54×
+  // -> 1.13× of their bytes, row 1838 -> 1617 µs, the column pass reading
+  // them 479 -> 625 µs, +2 % per step; profiles/r04/ab_rowh.md).
+  // SW_TILE_FA=1/2 overrides.
+  g.fa = 1;
+  if ((k.model == SW_MODEL_QG2 || k.model == SW_MODEL_MLQG) && g.log2nx >= SW_TILE_F4_QG) g.fa = 2;
+  if (const char* e = std::getenv("SW_TILE_FA")) g.fa = (e[0] == '2') ? 2 : 1;
+  g.fsy = ford ? 1 : g.kcl >> g.fa;
+  g.fsk = ford ? g.nyl >> (3 - g.fa) : 1;
   return g;
 }
 

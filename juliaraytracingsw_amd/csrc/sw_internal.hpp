@@ -67,11 +67,13 @@ struct Geom {
   long long cfield;   // elements per compact field  = max(kcn,1)*LrP
   long long mfield;   // elements per mixed field    = kcl*ny = (P*kcl)*nyl
   int tcm;            // inverse mixed fields: column-major tiles (mtile_local)
-  // forward mixed fields (A = 2, B = 4 tiles): line stride per 4 rows and per
-  // 2 columns — (1, nyl/4): lines in column order (one slab); (kcl/2, 1):
-  // in row order (several slabs: a chunk of rows is contiguous per block, so
-  // the forward transposes can follow the row pass chunk by chunk)
-  int fsy, fsk;
+  // forward mixed fields (A = 2^fa columns × B = 8/A rows per tile): line
+  // stride per B rows and per A columns — (1, nyl/B): lines in column order
+  // (one slab); (kcl/A, 1): in row order (several slabs: a chunk of rows is
+  // contiguous per block, so the forward transposes can follow the row pass
+  // chunk by chunk).  fa = 1 (2×4 tiles) but for the 2LQG half-length rows
+  // at 8192 points (fa = 2: 4×2, sw_api.cpp make_geom)
+  int fsy, fsk, fa;
 };
 
 struct Phys {
@@ -156,10 +158,13 @@ __host__ __device__ inline int mtile_x(const Geom& g, int kr, int yl, int cm = 0
   }
   return p * g.nyl * g.kcl + mtile_local<A, ORD>(g, krl, yl, cm);
 }
-// forward fields: row phase / column phase (A = 2: the line order from Geom)
+// forward fields: row phase / column phase (A = 2^fa: tile and line order
+// from Geom)
 #if SW_TILE_F == 2
 __host__ __device__ inline int mtile_f_local(const Geom& g, int krl, int yl) {
-  return ((yl >> 2) * g.fsy + (krl >> 1) * g.fsk) * 8 + (yl & 3) * 2 + (krl & 1);
+  const int fb = 3 - g.fa;
+  return ((yl >> fb) * g.fsy + (krl >> g.fa) * g.fsk) * 8 + ((yl & ((1 << fb) - 1)) << g.fa) +
+         (krl & ((1 << g.fa) - 1));
 }
 __host__ __device__ inline int midx(const Geom& g, int kr, int yl) {
   int p = 0, krl = kr;

@@ -174,14 +174,23 @@ __device__ __forceinline__ double2 zero2() { return make_double2(0.0, 0.0); }
 #ifndef SW_COL_DEC_MIN
 #define SW_COL_DEC_MIN 12
 #endif
-template <int LOG2N>
+// the 2LQG/MultiLayerQG column kernels from 2048 points (config 3, 2LQG
+// 2048² IFMAB3: col_fwd 30.0 -> 28.0 µs, 5332-5358 -> 5435-5583 steps/s; the
+// RSW fused column step there: 82.4 -> 83.8 µs, so RSW keeps SW_COL_DEC_MIN;
+// profiles/r04/ab_coldec.md)
+#ifndef SW_COL_DEC_MIN_QG
+#define SW_COL_DEC_MIN_QG 11
+#endif
+// MODEL: the kernel family whose column passes write and read the mixed
+// fields (one order per family: its col_inv, col_fwd, col_step, alias pass)
+template <int LOG2N, int MODEL = -1>
 __host__ __device__ constexpr bool col_dec() {
-  return LOG2N >= SW_COL_DEC_MIN && LOG2N >= 10 && LOG2N <= 13;
+  return LOG2N >= (MODEL == MODEL_QG2 ? SW_COL_DEC_MIN_QG : SW_COL_DEC_MIN) && LOG2N >= 10 && LOG2N <= 13;
 }
 // stored row of slot s of thread t
-template <int LOG2N>
+template <int LOG2N, bool DEC = col_dec<LOG2N>()>
 __device__ __forceinline__ int cpos(int t, int s) {
-  if constexpr (col_dec<LOG2N>()) return ((t >> 6) << 9) + (t & 63) + (s << 6);
+  if constexpr (DEC) return ((t >> 6) << 9) + (t & 63) + (s << 6);
   else return t + s * FftPlan<LOG2N>::NT;
 }
 template <int LOG2N, bool DEC = col_dec<LOG2N>()>
@@ -201,16 +210,16 @@ struct ColTw<LOG2N, true> {
 };
 // the column passes' y-transform: DIR = +1 natural spectrum -> stored rows,
 // DIR = -1 stored rows -> natural spectrum (v[s] = X[t + s NT])
-template <int LOG2N, int DIR>
-__device__ __forceinline__ void col_fft(double2 (&v)[8], int t, const ColTw<LOG2N>& c, double2* __restrict__ line) {
-  if constexpr (!col_dec<LOG2N>()) {
+template <int LOG2N, int DIR, bool DEC = col_dec<LOG2N>()>
+__device__ __forceinline__ void col_fft(double2 (&v)[8], int t, const ColTw<LOG2N, DEC>& c, double2* __restrict__ line) {
+  if constexpr (!DEC) {
     fft_line<LOG2N, DIR>(v, t, c.tws, line);
   } else if constexpr (LOG2N == 13) {
     if constexpr (DIR > 0) fft16_dif<DIR>(v, t, c.tq, c.tab, line);
     else fft16_dit<DIR>(v, t, c.tq, c.tab, line);
   } else {
     constexpr int W = 1 << (LOG2N - 9);
-    constexpr bool FLY = ColTw<LOG2N>::FLY;
+    constexpr bool FLY = ColTw<LOG2N, true>::FLY;
     using V1 = double2(&)[1][8];
     const double2 wt = c.tab[t];  // W_N^t, read per transform (not held)
     if constexpr (DIR > 0) fftw_dif<W, DIR, 1, true, FLY>(reinterpret_cast<V1>(v), t, wt, c.tq, line, 0);
@@ -219,18 +228,17 @@ __device__ __forceinline__ void col_fft(double2 (&v)[8], int t, const ColTw<LOG2
 }
 // the inverse-field stores of a column line at the stored rows cpos (as
 // store_col_i: closed form with one slab)
-template <int LOG2N, typename F>
+template <int LOG2N, bool DEC = col_dec<LOG2N>(), typename F>
 __device__ __forceinline__ void store_col_p(const Geom& g, int krl, int t, F put) {
-  constexpr bool DEC = col_dec<LOG2N>();
   constexpr int PS = DEC ? 64 : FftPlan<LOG2N>::NT;  // stored-row stride of the slots
   if (SW_TILE_I == 2 && SW_LORD_I == 0 && PS % 4 == 0 && g.nslab == 1) {
-    const int b = midc_i_col_base<PS>(g, krl, cpos<LOG2N>(t, 0));
+    const int b = midc_i_col_base<PS>(g, krl, cpos<LOG2N, DEC>(t, 0));
 #pragma unroll
     for (int s = 0; s < 8; ++s) put(s, b + s * (PS >> 2) * (g.kcl >> 1) * 8);
   } else {
     asm volatile("" : "+v"(t));
 #pragma unroll
-    for (int s = 0; s < 8; ++s) put(s, midc_i(g, krl, cpos<LOG2N>(t, s)));
+    for (int s = 0; s < 8; ++s) put(s, midc_i(g, krl, cpos<LOG2N, DEC>(t, s)));
   }
 }
 
@@ -267,7 +275,8 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
   const bool live = krl < g.kcn;
   if (B::NB == 1 && !live) return;  // padding column: nobody reads it
   double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
-  ColTw<LOG2N> tws;
+  constexpr bool CD = col_dec<LOG2N, MODEL>();  // the family's stored-row order
+  ColTw<LOG2N, CD> tws;
   tws.load(c.t, tw);
   const double scale = 1.0 / ((double)g.nx * (double)g.ny);
   const double k = (g.kr0 + krl) * g.mk;
@@ -276,7 +285,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
   auto store = [&](int o) {  // fft_line leaves Y[t + s*NT] in v[s]
     if (live) {
       double2* Mo = M + (long long)o * g.mfield;
-      store_col_p<LOG2N>(g, krl, c.t, [&](int s, int o) { Mo[o] = v[s]; });
+      store_col_p<LOG2N, CD>(g, krl, c.t, [&](int s, int o) { Mo[o] = v[s]; });
     }
   };
 
@@ -294,12 +303,12 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
       x[s] = (live && j >= 0) ? t : zero2();
       v[s] = cscale(x[s], scale);
     }
-    col_fft<LOG2N, +1>(v, c.t, tws, line);
+    col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
     store(grp);
     if (grp == 0 || (MODEL == MODEL_RSWA && grp == 1)) {  // ∂y u: Uy (advective form: and ∂y v: Vy)
 #pragma unroll
       for (int s = 0; s < 8; ++s) v[s] = cmul_i(x[s], lwav(g, c.t + s * NT) * scale);
-      col_fft<LOG2N, +1>(v, c.t, tws, line);
+      col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
       store(3 + grp);
     }
   } else if constexpr (MODEL == MODEL_TY) {
@@ -333,34 +342,34 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
         psi[s] = v[s];
         v[s] = cscale(x[s], scale);
       }
-      col_fft<LOG2N, +1>(v, c.t, tws, line);
+      col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
       store(0);
 #pragma unroll
       for (int s = 0; s < 8; ++s) v[s] = cscale(psi[s], scale);
-      col_fft<LOG2N, +1>(v, c.t, tws, line);
+      col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
       store(1);
     } else if (grp == 1) {  // x = ψ
 #pragma unroll
       for (int s = 0; s < 8; ++s) v[s] = cmul_i(x[s], -lwav(g, c.t + s * NT) * scale);
-      col_fft<LOG2N, +1>(v, c.t, tws, line);
+      col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
       store(2);
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
         const double l = lwav(g, c.t + s * NT);
         v[s] = cscale(x[s], (l * l) * scale);
       }
-      col_fft<LOG2N, +1>(v, c.t, tws, line);
+      col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
       store(3);
     } else {
       const int o = grp == 2 ? 4 : (grp == 3 ? 6 : 7);
 #pragma unroll
       for (int s = 0; s < 8; ++s) v[s] = cscale(x[s], scale);
-      col_fft<LOG2N, +1>(v, c.t, tws, line);
+      col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
       store(o);
       if (grp != 3) {  // ∂y uc, ∂y pc
 #pragma unroll
         for (int s = 0; s < 8; ++s) v[s] = cmul_i(x[s], lwav(g, c.t + s * NT) * scale);
-        col_fft<LOG2N, +1>(v, c.t, tws, line);
+        col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
         store(o + 1);
       }
     }
@@ -385,15 +394,15 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
       qg_psi(p, K2, q1.x, q1.y, q2.x, q2.y, grp, psi[s].x, psi[s].y);
       v[s] = cscale(qg, scale);
     }
-    col_fft<LOG2N, +1>(v, c.t, tws, line);
+    col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
     store(grp);
 #pragma unroll
     for (int s = 0; s < 8; ++s) v[s] = cscale(psi[s], scale);
-    col_fft<LOG2N, +1>(v, c.t, tws, line);
+    col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
     store(2 + grp);
 #pragma unroll
     for (int s = 0; s < 8; ++s) v[s] = cmul_i(psi[s], lwav(g, c.t + s * NT) * scale);
-    col_fft<LOG2N, +1>(v, c.t, tws, line);
+    col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
     store(4 + grp);
   }
 }
@@ -441,8 +450,11 @@ struct RowIdx {
   __device__ __forceinline__ static int row_inv(const Geom& g, int y) {
     return (y >> 2) * (g.kcl >> 1) * 8 + (y & 3) * (g.tcm ? 1 : 2);
   }
+  // (A = 2^fa columns per tile: k = t + s NT adds s NT nyl, NT a multiple of A)
   __device__ __forceinline__ static int fwd0(const Geom& g, int t, int y) {
-    return (y >> 2) * 8 + (y & 3) * 2 + 2 * g.nyl * (t >> 1) + (t & 1);
+    const int fb = 3 - g.fa;
+    return (y >> fb) * 8 + ((y & ((1 << fb) - 1)) << g.fa) + (((t >> g.fa) * g.nyl) << g.fa) +
+           (t & ((1 << g.fa) - 1));
   }
   __device__ __forceinline__ int oinv_calc(const Geom& g, int s) const {
     int tt = t;
@@ -692,12 +704,29 @@ __host__ __device__ constexpr int row_tgt() {
 template <int MODEL, int LOG2N>
 using BlkRow = Blk<LOG2N, row_tgt<MODEL>()>;
 
+// The lean RSW row (SW_RSW_ROW_LEAN): one line buffer per row, the
+// transforms one at a time, stage twiddles and row offsets formed per use
+// (the 2LQG row's measures), 128 VGPRs: four rows per CU (4 waves per SIMD)
+// instead of two.  The decimated-transform lengths whose RSW row is
+// full-length (1024, 2048).
+#ifndef SW_RSW_ROW_LEAN
+#define SW_RSW_ROW_LEAN 0
+#endif
+template <int LOG2N>
+__host__ __device__ constexpr int roww();
+template <int MODEL, int LOG2N>
+__host__ __device__ constexpr bool rsw_row_lean() {
+  return MODEL == MODEL_RSW && SW_RSW_ROW_LEAN && LOG2N >= 10 && LOG2N <= 11 && roww<LOG2N>() > 0;
+}
 template <int MODEL, int LOG2N>
 __host__ __device__ constexpr int row_lds_lines() {
 #ifdef SW_ROW_CB1  // sweep knob: one line buffer per row
   return 1;
 #else
-  return (MODEL == MODEL_RSW && 2 * BlkRow<MODEL, LOG2N>::NB * FftPlan<LOG2N>::LDS * 16 <= 160 * 1024) ? 2 : 1;
+  return (MODEL == MODEL_RSW && !rsw_row_lean<MODEL, LOG2N>() &&
+          2 * BlkRow<MODEL, LOG2N>::NB * FftPlan<LOG2N>::LDS * 16 <= 160 * 1024)
+             ? 2
+             : 1;
 #endif
 }
 // C = 2: both transforms per barrier; C = 1: one after the other
@@ -784,6 +813,11 @@ __host__ __device__ constexpr int roww() {
 // (sw_fft.hpp fftw_dit_split): bitwise-tested (GPU parity at 2048) but
 // measured slower — RSW row 73.7 -> 74.7, 2LQG row 74.3 -> 76.7 µs (the
 // radix-W combination done twice costs more VALU than the second exchange)
+// the full-length 2LQG row at 8192 points on the 16-wave decimated
+// transforms (experiment knob; the half-length row k_row_qg_h is the default)
+#ifndef SW_ROW16
+#define SW_ROW16 0
+#endif
 #ifndef SW_SPLIT_FOLD
 #define SW_SPLIT_FOLD 0
 #endif
@@ -800,7 +834,7 @@ __host__ __device__ constexpr int roww_h() {
 }
 template <int MODEL, int LOG2N>
 __host__ __device__ constexpr bool row_fly() {
-  return LOG2N >= SW_TWFLY_LOG2 || (MODEL == MODEL_QG2 && LOG2N >= SW_QG_ROW_FLY_MIN);
+  return LOG2N >= SW_TWFLY_LOG2 || (MODEL == MODEL_QG2 && LOG2N >= SW_QG_ROW_FLY_MIN) || rsw_row_lean<MODEL, LOG2N>();
 }
 // PRUNE: a live band kc <= 3N/8 (row_prunable): the decimated transforms
 // skip the zero inputs and unused outputs of slots 3 and 4 (sw_fft.hpp)
@@ -808,7 +842,7 @@ template <int MODEL, int LOG2N, bool ALIAS = false, bool PRUNE = false>
 static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
                                          (BlkRow<MODEL, LOG2N>::THREADS >= 1024 ? 4
                                           : (MODEL == MODEL_QG2 ? (row_fly<MODEL, LOG2N>() ? 4 : SW_MINW_ROW_QG)
-                                                                : SW_MINW_ROW)))
+                                                                : (rsw_row_lean<MODEL, LOG2N>() ? 4 : SW_MINW_ROW))))
     k_row(Geom g, Phys p, const double2* __restrict__ Mi, double2* __restrict__ Mo,
           const double2* __restrict__ tw, int yoff, double2* __restrict__ Ma) {
   using Bk = BlkRow<MODEL, LOG2N>;
@@ -827,7 +861,52 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
   const long long MF = g.mfield;
   double2 v[8];
 
-  if constexpr (MODEL == MODEL_RSW) {
+  if constexpr (rsw_row_lean<MODEL, LOG2N>()) {
+    // the vorticity-form RSW row below (same outputs, same arithmetic per
+    // line), one transform at a time through one line buffer: every product
+    // formed as soon as u, v, η, ζ exist, then K + iζv, ζu + iuη and the real
+    // vη line transformed in turn (the live set shrinks as they go)
+    const double2 *U = Mi, *V = Mi + MF, *H = Mi + 2 * MF, *Uy = Mi + 3 * MF;
+    constexpr int W = roww<LOG2N>();
+    Twiddles<9, true> tq;
+    tq.load(c.t & 63, tw, LOG2N - 9);
+    auto wnt = [&]() { return tw[c.t]; };  // W_N^t per transform (not held)
+    using V1 = double2(&)[1][8];
+    double2 w[2][8];
+    load_uv_eta_zeta<LOG2N, true>(w, ri, g, U, V, H, Uy);
+    fftw_dif<W, +1, 1, true, true, false, PRUNE>(reinterpret_cast<V1>(w[0]), c.t, wnt(), tq, line, 0);
+    fftw_dif<W, +1, 1, true, true, false, PRUNE>(reinterpret_cast<V1>(w[1]), c.t, wnt(), tq, line, 0);
+    double pc[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const double u = w[0][s].x, vv = w[0][s].y, eta = w[1][s].x, zeta = w[1][s].y;
+      pc[s] = vv * eta;
+      w[0][s] = make_double2(0.5 * (u * u + vv * vv), zeta * vv);  // K + i ζv
+      w[1][s] = make_double2(zeta * u, u * eta);                   // ζu + i uη
+    }
+    fftw_dit<W, -1, 1, true, false, false, PRUNE>(reinterpret_cast<V1>(w[0]), c.t, wnt(), tq, line, 0);
+    split_pair<LOG2N, true, PRUNE>(w[0], c.t, g, line, [&](int k, int s, double2 a, double2 b) {
+      const int o = ri.ofwd(g, s);
+      Mo[o] = cadd(cmul_i(a, -(k * g.mk)), b);  // P = -ik K̂ + (ζv)^
+      Mo[MF + o] = a;                            // K̂
+    });
+    // PRE: the split's mirror reads span every wave's region
+    fftw_dit<W, -1, 1, true, true, false, PRUNE>(reinterpret_cast<V1>(w[1]), c.t, wnt(), tq, line, 0);
+    split_pair<LOG2N, true, PRUNE>(w[1], c.t, g, line, [&](int k, int s, double2 a, double2 b) {
+      const int o = ri.ofwd(g, s);
+      Mo[2 * MF + o] = a;                       // (ζu)^
+      Mo[3 * MF + o] = cmul_i(b, -(k * g.mk));  // Q = -ik (uη)^
+    });
+    // 4: (vη)^ (real input: the transform is the spectrum itself)
+#pragma unroll
+    for (int s = 0; s < 8; ++s) v[s] = make_double2(pc[s], 0.0);
+    fftw_dit<W, -1, 1, true, true, false, PRUNE>(reinterpret_cast<V1>(v), c.t, wnt(), tq, line, 0);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int k = c.t + s * Bk::NT;
+      if (RowIdx<LOG2N>::fwd_any(g, s) && k < g.kc) Mo[4 * MF + ri.ofwd(g, s)] = v[s];
+    }
+  } else if constexpr (MODEL == MODEL_RSW) {
     // rsw/RotatingShallowWater.jl:140-230 in vorticity form:
     //   u ux + v uy = ∂x K - ζ v,  u vx + v vy = ∂y K + ζ u,
     //   K = (u² + v²)/2, ζ = vx - uy.
@@ -1074,21 +1153,27 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
     // at 128); a 64-entry LDS table of the stage twiddles spilled 26 and read
     // 88-91 against 74.5-75 µs (round 3, interleaved A/B)
     constexpr bool FL = row_fly<MODEL, LOG2N>();
-    Twiddles<9, FL> tq;
+    // 8192 points (SW_ROW16): the 16-wave decimated transforms of the
+    // column passes (sw_fft.hpp fft16_dif / fft16_dit: three barriers per
+    // transform, Stockham's ten)
+    constexpr bool W16 = LOG2N == 13 && SW_ROW16;
+    Twiddles<9, FL || W16> tq;
     double2 wt = zero2();
-    if constexpr (W > 0) {
+    if constexpr (W > 0 || W16) {
       tq.load(c.t & 63, tw, LOG2N - 9);
-      if constexpr (!FL) wt = tw[c.t];
+      if constexpr (!FL && !W16) wt = tw[c.t];
     }
     auto wnt = [&]() { return FL ? tw[c.t] : wt; };
     using V1 = double2(&)[1][8];
     constexpr bool PR = PRUNE && W > 0 && !ALIAS;  // (ALIAS reads the slots kc <= k <= N/2)
     auto inv = [&](double2(&x)[8]) {
-      if constexpr (W > 0) fftw_dif<W, +1, 1, true, FL, false, PR>(reinterpret_cast<V1>(x), c.t, wnt(), tq, line, 0);
+      if constexpr (W16) fft16_dif<+1>(x, c.t, tq, tw, line);
+      else if constexpr (W > 0) fftw_dif<W, +1, 1, true, FL, false, PR>(reinterpret_cast<V1>(x), c.t, wnt(), tq, line, 0);
       else fft_line<LOG2N, +1>(x, c.t, tws, line);
     };
     auto fwd = [&](double2(&x)[8]) {
-      if constexpr (W > 0) fftw_dit<W, -1, 1, FL, false, false, PR>(reinterpret_cast<V1>(x), c.t, wnt(), tq, line, 0);
+      if constexpr (W16) fft16_dit<-1>(x, c.t, tq, tw, line);
+      else if constexpr (W > 0) fftw_dit<W, -1, 1, FL, false, false, PR>(reinterpret_cast<V1>(x), c.t, wnt(), tq, line, 0);
       else fft_line<LOG2N, -1>(x, c.t, tws, line);
     };
     double2 q[8];
@@ -1566,7 +1651,8 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
   if (B::NB == 1 && !live) return;
   const int krA = krl < g.kcl ? krl : g.kcl - 1;  // in-bounds address
   double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
-  ColTw<LOG2N> tws;
+  constexpr bool CD = col_dec<LOG2N, MODEL>();  // the family's stored-row order
+  ColTw<LOG2N, CD> tws;
   tws.load(c.t, tw);
   const double k = (g.kr0 + krl) * g.mk;
   const long long MF = g.mfield;
@@ -1575,7 +1661,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
   auto load_col = [&](const double2* Mfield) {
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      const double2 t = mix_ld_col(Mfield + midc(g, krA, cpos<LOG2N>(c.t, s)));
+      const double2 t = mix_ld_col(Mfield + midc(g, krA, cpos<LOG2N, CD>(c.t, s)));
       v[s] = live ? t : zero2();
     }
   };
@@ -1583,18 +1669,18 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
   const NTerms nt = nterms<MODEL>(grp);
   // fft_line leaves F[m = t + s*NT] in v[s]; only live rows are written
   load_col(Mf + nt.fa * MF);
-  col_fft<LOG2N, -1>(v, c.t, tws, line);
+  col_fft<LOG2N, -1, CD>(v, c.t, tws, line);
 #pragma unroll
   for (int s = 0; s < 8; ++s) acc[s] = apply_mul(v[s], nt.ma, k, lwav(g, c.t + s * NT));
   if (nt.fb >= 0) {
     load_col(Mf + nt.fb * MF);
-    col_fft<LOG2N, -1>(v, c.t, tws, line);
+    col_fft<LOG2N, -1, CD>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) acc[s] = cadd(acc[s], apply_mul(v[s], nt.mb, k, lwav(g, c.t + s * NT)));
   }
   if (MODEL == MODEL_TY && nt.fc >= 0) {
     load_col(Mf + nt.fc * MF);
-    col_fft<LOG2N, -1>(v, c.t, tws, line);
+    col_fft<LOG2N, -1, CD>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) acc[s] = cadd(acc[s], apply_mul(v[s], nt.mc, k, lwav(g, c.t + s * NT)));
   }
@@ -1662,7 +1748,8 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
   const bool live = col < ga.kcn;
   const int colA = live ? col : 0;
   double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
-  ColTw<LOG2N> tws;
+  constexpr bool CD = col_dec<LOG2N, MODEL>();  // the family's stored-row order
+  ColTw<LOG2N, CD> tws;
   tws.load(c.t, tw);
   const double k = (ga.kr0 + colA) * g.mk;
   const long long MA = (long long)(g.nkr - g.kc) * g.ny;
@@ -1670,25 +1757,25 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
   auto load_col = [&](int fi) {
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      const int m = cpos<LOG2N>(c.t, s);  // stored row
+      const int m = cpos<LOG2N, CD>(c.t, s);  // stored row
       const double2 t = region == 0 ? Ma[fi * MA + (long long)colA * g.ny + m] : Mf[fi * g.mfield + midc(g, colA, m)];
       v[s] = live ? t : zero2();
     }
   };
   const NTerms nt = nterms<MODEL>(f);
   load_col(nt.fa);
-  col_fft<LOG2N, -1>(v, c.t, tws, line);
+  col_fft<LOG2N, -1, CD>(v, c.t, tws, line);
 #pragma unroll
   for (int s = 0; s < 8; ++s) acc[s] = apply_mul(v[s], nt.ma, k, lwav(g, c.t + s * NT));
   if (nt.fb >= 0) {
     load_col(nt.fb);
-    col_fft<LOG2N, -1>(v, c.t, tws, line);
+    col_fft<LOG2N, -1, CD>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) acc[s] = cadd(acc[s], apply_mul(v[s], nt.mb, k, lwav(g, c.t + s * NT)));
   }
   if (nt.fc >= 0) {  // Thomas–Yamada's N_ζ (the linear terms vanish here: calcN! dealiases its input)
     load_col(nt.fc);
-    col_fft<LOG2N, -1>(v, c.t, tws, line);
+    col_fft<LOG2N, -1, CD>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) acc[s] = cadd(acc[s], apply_mul(v[s], nt.mc, k, lwav(g, c.t + s * NT)));
   }
@@ -2144,7 +2231,8 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   if (B::NB == 1 && !live) return;
   const int krA = krl < g.kcl ? krl : g.kcl - 1;
   double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
-  ColTw<LOG2N> tws;
+  constexpr bool CD = col_dec<LOG2N, MODEL>();  // the family's stored-row order
+  ColTw<LOG2N, CD> tws;
   tws.load(c.t, tw);
   const double k = (g.kr0 + krl) * g.mk;
   const long long MF = g.mfield;
@@ -2153,7 +2241,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   auto load_col = [&](const double2* Mfield) {
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      const double2 t = mix_ld_col(Mfield + midc(g, krA, cpos<LOG2N>(c.t, s)));
+      const double2 t = mix_ld_col(Mfield + midc(g, krA, cpos<LOG2N, CD>(c.t, s)));
       v[s] = live ? t : zero2();
     }
   };
@@ -2162,12 +2250,12 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   auto compute_N = [&](double2 (&n)[8], int f) {
     const NTerms nt = nterms<MODEL>(f);
     load_col(Mf + nt.fa * MF);
-    col_fft<LOG2N, -1>(v, c.t, tws, line);
+    col_fft<LOG2N, -1, CD>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) n[s] = apply_mul(v[s], nt.ma, k, lwav(g, c.t + s * NT));
     if (nt.fb >= 0) {
       load_col(Mf + nt.fb * MF);
-      col_fft<LOG2N, -1>(v, c.t, tws, line);
+      col_fft<LOG2N, -1, CD>(v, c.t, tws, line);
 #pragma unroll
       for (int s = 0; s < 8; ++s) n[s] = cadd(n[s], apply_mul(v[s], nt.mb, k, lwav(g, c.t + s * NT)));
     }
@@ -2232,7 +2320,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   auto store = [&](int o) {
     if (live) {
       double2* Mo = Minv + (long long)o * MF;
-      store_col_p<LOG2N>(g, krl, c.t, [&](int s, int o) { Mo[o] = v[s]; });
+      store_col_p<LOG2N, CD>(g, krl, c.t, [&](int s, int o) { Mo[o] = v[s]; });
     }
   };
   if constexpr (MODEL == MODEL_RSW) {
@@ -2242,12 +2330,12 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
       load_x(f, x);
 #pragma unroll
       for (int s = 0; s < 8; ++s) v[s] = cscale(x[s], scale);
-      col_fft<LOG2N, +1>(v, c.t, tws, line);
+      col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
       store(f);
       if (f == 0) {  // Uy
 #pragma unroll
         for (int s = 0; s < 8; ++s) v[s] = cmul_i(x[s], lwav(g, c.t + s * NT) * scale);
-        col_fft<LOG2N, +1>(v, c.t, tws, line);
+        col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
         store(3);
       }
     }
@@ -2259,7 +2347,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     for (int f = 0; f < 2; ++f) {
 #pragma unroll
       for (int s = 0; s < 8; ++s) v[s] = cscale(f ? q2[s] : q1[s], scale);
-      col_fft<LOG2N, +1>(v, c.t, tws, line);
+      col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
       store(f);
       double2 psi[8];
 #pragma unroll
@@ -2269,11 +2357,11 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
         qg_psi(p, K2, q1[s].x, q1[s].y, q2[s].x, q2[s].y, f, psi[s].x, psi[s].y);
         v[s] = cscale(psi[s], scale);
       }
-      col_fft<LOG2N, +1>(v, c.t, tws, line);
+      col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
       store(2 + f);
 #pragma unroll
       for (int s = 0; s < 8; ++s) v[s] = cmul_i(psi[s], lwav(g, c.t + s * NT) * scale);
-      col_fft<LOG2N, +1>(v, c.t, tws, line);
+      col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
       store(4 + f);
     }
   }
@@ -2306,7 +2394,8 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   const int krA = krl < g.kcl ? krl : g.kcl - 1;
   double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
   double2* park = smem + B::NB * FftPlan<LOG2N>::LDS + (long long)c.ln * NF * g.Lr;
-  ColTw<LOG2N> tws;
+  constexpr bool CD = col_dec<LOG2N, MODEL>();  // the family's stored-row order
+  ColTw<LOG2N, CD> tws;
   tws.load(c.t, tw);
   const double k = (g.kr0 + krl) * g.mk;
   const long long MF = g.mfield;
@@ -2314,7 +2403,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   auto load_col = [&](const double2* Mfield) {
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      const double2 t = mix_ld_col(Mfield + midc(g, krA, cpos<LOG2N>(c.t, s)));
+      const double2 t = mix_ld_col(Mfield + midc(g, krA, cpos<LOG2N, CD>(c.t, s)));
       v[s] = live ? t : zero2();
     }
   };
@@ -2323,12 +2412,12 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
   for (int f = 0; f < NF; ++f) {
     const NTerms nt = nterms<MODEL>(f);
     load_col(Mf + nt.fa * MF);
-    col_fft<LOG2N, -1>(v, c.t, tws, line);
+    col_fft<LOG2N, -1, CD>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) n[s] = apply_mul(v[s], nt.ma, k, lwav(g, c.t + s * NT));
     if (nt.fb >= 0) {
       load_col(Mf + nt.fb * MF);
-      col_fft<LOG2N, -1>(v, c.t, tws, line);
+      col_fft<LOG2N, -1, CD>(v, c.t, tws, line);
 #pragma unroll
       for (int s = 0; s < 8; ++s) n[s] = cadd(n[s], apply_mul(v[s], nt.mb, k, lwav(g, c.t + s * NT)));
     }
@@ -2401,7 +2490,8 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, (Blk<LOG2N>::THREA
   if (B::NB == 1 && !live) return;
   const int krA = krl < g.kcl ? krl : g.kcl - 1;
   double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
-  ColTw<LOG2N> tws;
+  constexpr bool CD = col_dec<LOG2N, MODEL_RSW>();  // the family's stored-row order
+  ColTw<LOG2N, CD> tws;
   tws.load(c.t, tw);
   const double k = (g.kr0 + krl) * g.mk;
   const long long MF = g.mfield;
@@ -2413,7 +2503,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, (Blk<LOG2N>::THREA
 #ifdef SW_EXP_CS_NOMIX  // experiment: mixed-field loads from one line (wrong results)
       const double2 t = Mfield[c.t & 7];
 #else
-      const double2 t = mix_ld_col(Mfield + midc(g, krA, cpos<LOG2N>(c.t, s)));
+      const double2 t = mix_ld_col(Mfield + midc(g, krA, cpos<LOG2N, CD>(c.t, s)));
 #endif
       dst[s] = live ? t : zero2();
     }
@@ -2421,12 +2511,12 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, (Blk<LOG2N>::THREA
   const NTerms nt = nterms<MODEL_RSW>(f);
   // ---- N_f (rsw/RotatingShallowWater.jl:174-226; nterms)
   load_col(v, Mf + nt.fa * MF);
-  col_fft<LOG2N, -1>(v, c.t, tws, line);
+  col_fft<LOG2N, -1, CD>(v, c.t, tws, line);
 #pragma unroll
   for (int s = 0; s < 8; ++s) n[s] = apply_mul(v[s], nt.ma, k, lwav(g, c.t + s * NT));
   if (nt.fb >= 0) {
     load_col(v, Mf + nt.fb * MF);
-    col_fft<LOG2N, -1>(v, c.t, tws, line);
+    col_fft<LOG2N, -1, CD>(v, c.t, tws, line);
 #pragma unroll
     for (int s = 0; s < 8; ++s) n[s] = cadd(n[s], apply_mul(v[s], nt.mb, k, lwav(g, c.t + s * NT)));
   }
@@ -2508,17 +2598,17 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, (Blk<LOG2N>::THREA
   auto store = [&](int o) {
     if (live) {
       double2* Mo = Minv + (long long)o * MF;
-      store_col_p<LOG2N>(g, krl, c.t, [&](int s, int o) { Mo[o] = v[s]; });
+      store_col_p<LOG2N, CD>(g, krl, c.t, [&](int s, int o) { Mo[o] = v[s]; });
     }
   };
 #pragma unroll
   for (int s = 0; s < 8; ++s) v[s] = cscale(x[s], scale);
-  col_fft<LOG2N, +1>(v, c.t, tws, line);
+  col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
   store(f);
   if (f == 0) {  // ∂y u: Uy
 #pragma unroll
     for (int s = 0; s < 8; ++s) v[s] = cmul_i(x[s], lwav(g, c.t + s * NT) * scale);
-    col_fft<LOG2N, +1>(v, c.t, tws, line);
+    col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
     store(3);
   }
 }
