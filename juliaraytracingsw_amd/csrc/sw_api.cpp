@@ -689,7 +689,7 @@ bool use_fused(const sw_ctx* c) {
 // mode, no N in HBM); the next calcN's col_inv runs separately.  Built for
 // RSW IFMAB3/IFMRK4 and 2LQG FilteredAB3/IFMAB3/IFMRK4 (not MultiLayerQG,
 // whose N adds terms from the calcN input in k_col_fwd), bitwise equal to the
-// two kernels; used where it wins (tools/fwdstep_ab.sh): 2LQG
+// two kernels; used where it wins (tools/ab/fwdstep_ab.sh): 2LQG
 // FilteredAB3 on lines up to 2048 points (0 spills; 5409 -> 5601 steps/s at
 // 2048²).  The coupled IF/RK4 updates hold every field's N next to the
 // per-mode exponential and spill (82-180 VGPRs at 2048, 350+ at 8192): 2LQG

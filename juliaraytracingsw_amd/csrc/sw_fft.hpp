@@ -120,7 +120,7 @@ __device__ __forceinline__ void lds_barrier() {
 // 4096-point lines too, with the per-stage twiddles below and 4 waves per
 // SIMD for their 512-thread blocks (two blocks per CU instead of one): RSW
 // 4096² col_step 405 -> 382 µs, 2LQG 4096² row 533 -> 440, col_fwd 140 -> 126
-// (tools/ab_lean.sh).
+// (tools/ab/ab_lean.sh).
 #ifndef SW_OPAQUE_LOG2
 #define SW_OPAQUE_LOG2 12
 #endif

@@ -101,7 +101,7 @@ __host__ __device__ inline double lwav(const Geom& g, int m) {
 // 128-B line holds a tile of A columns kr × B = 8/A rows y (16-B elements, kr
 // fastest).  The row pass touches 16·A bytes of a line, the column pass
 // 16·B; the blocks that share a line are placed on one XCD (col_of_block),
-// where L2 stitches the line.  Measured on MI355X at 2048² (tools/sweep.sh,
+// where L2 stitches the line.  Measured on MI355X at 2048² (tools/ab/sweep.sh,
 // DESIGN.md §2): 2×4 tiles in both directions beat whole-line rows (8×1) or
 // whole-line columns (1×8) by 11 % per step, because a pass that touches
 // 16 B of each line pays for the whole line in L1 fills and L2 requests.

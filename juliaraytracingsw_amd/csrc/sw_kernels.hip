@@ -691,7 +691,7 @@ __device__ __forceinline__ void store_pair(const double2 (&v)[8], const RowIdx<L
 
 // LDS line buffers per row of k_row: RSW transforms pairs of lines together
 // where two buffers per row fit the 160 KB of LDS (nx <= 4096)
-// Threads per block of the row pass.  Measured (tools/sweep_sizes.sh): the
+// Threads per block of the row pass.  Measured (tools/ab/sweep_sizes.sh): the
 // RSW row (two line buffers) runs best with up to 256 threads per block
 // (1024²: 29 vs 36 µs at 128), every other kernel with one line per block
 // down to 64 threads (512² TY / MultiLayerQG steps +11-14 %, 1024² RSW
@@ -704,29 +704,12 @@ __host__ __device__ constexpr int row_tgt() {
 template <int MODEL, int LOG2N>
 using BlkRow = Blk<LOG2N, row_tgt<MODEL>()>;
 
-// The lean RSW row (SW_RSW_ROW_LEAN): one line buffer per row, the
-// transforms one at a time, stage twiddles and row offsets formed per use
-// (the 2LQG row's measures), 128 VGPRs: four rows per CU (4 waves per SIMD)
-// instead of two.  The decimated-transform lengths whose RSW row is
-// full-length (1024, 2048).
-#ifndef SW_RSW_ROW_LEAN
-#define SW_RSW_ROW_LEAN 0
-#endif
-template <int LOG2N>
-__host__ __device__ constexpr int roww();
-template <int MODEL, int LOG2N>
-__host__ __device__ constexpr bool rsw_row_lean() {
-  return MODEL == MODEL_RSW && SW_RSW_ROW_LEAN && LOG2N >= 10 && LOG2N <= 11 && roww<LOG2N>() > 0;
-}
 template <int MODEL, int LOG2N>
 __host__ __device__ constexpr int row_lds_lines() {
 #ifdef SW_ROW_CB1  // sweep knob: one line buffer per row
   return 1;
 #else
-  return (MODEL == MODEL_RSW && !rsw_row_lean<MODEL, LOG2N>() &&
-          2 * BlkRow<MODEL, LOG2N>::NB * FftPlan<LOG2N>::LDS * 16 <= 160 * 1024)
-             ? 2
-             : 1;
+  return (MODEL == MODEL_RSW && 2 * BlkRow<MODEL, LOG2N>::NB * FftPlan<LOG2N>::LDS * 16 <= 160 * 1024) ? 2 : 1;
 #endif
 }
 // C = 2: both transforms per barrier; C = 1: one after the other
@@ -784,7 +767,7 @@ __device__ __forceinline__ void store_alias_with(const double2 (&v)[8], int t, c
 // The 2LQG row from 2048-point lines (SW_QG_ROW_FLY_MIN): stage twiddles read
 // per stage and the thread index opaque per transform (Twiddles<…, FLY>), 116
 // VGPRs, 4 waves per SIMD — 2048²: 85 -> 76 µs, config 3 +2-3 %
-// (tools/ab_lean11.sh); the same measures slow the RSW kernels there (row
+// (tools/ab/ab_lean11.sh); the same measures slow the RSW kernels there (row
 // 77 -> 82, col_step 85 -> 92 µs), which keep theirs.
 #ifndef SW_QG_ROW_FLY_MIN
 #define SW_QG_ROW_FLY_MIN 11
@@ -834,7 +817,7 @@ __host__ __device__ constexpr int roww_h() {
 }
 template <int MODEL, int LOG2N>
 __host__ __device__ constexpr bool row_fly() {
-  return LOG2N >= SW_TWFLY_LOG2 || (MODEL == MODEL_QG2 && LOG2N >= SW_QG_ROW_FLY_MIN) || rsw_row_lean<MODEL, LOG2N>();
+  return LOG2N >= SW_TWFLY_LOG2 || (MODEL == MODEL_QG2 && LOG2N >= SW_QG_ROW_FLY_MIN);
 }
 // PRUNE: a live band kc <= 3N/8 (row_prunable): the decimated transforms
 // skip the zero inputs and unused outputs of slots 3 and 4 (sw_fft.hpp)
@@ -842,7 +825,7 @@ template <int MODEL, int LOG2N, bool ALIAS = false, bool PRUNE = false>
 static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
                                          (BlkRow<MODEL, LOG2N>::THREADS >= 1024 ? 4
                                           : (MODEL == MODEL_QG2 ? (row_fly<MODEL, LOG2N>() ? 4 : SW_MINW_ROW_QG)
-                                                                : (rsw_row_lean<MODEL, LOG2N>() ? 4 : SW_MINW_ROW))))
+                                                                : SW_MINW_ROW)))
     k_row(Geom g, Phys p, const double2* __restrict__ Mi, double2* __restrict__ Mo,
           const double2* __restrict__ tw, int yoff, double2* __restrict__ Ma) {
   using Bk = BlkRow<MODEL, LOG2N>;
@@ -861,52 +844,7 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
   const long long MF = g.mfield;
   double2 v[8];
 
-  if constexpr (rsw_row_lean<MODEL, LOG2N>()) {
-    // the vorticity-form RSW row below (same outputs, same arithmetic per
-    // line), one transform at a time through one line buffer: every product
-    // formed as soon as u, v, η, ζ exist, then K + iζv, ζu + iuη and the real
-    // vη line transformed in turn (the live set shrinks as they go)
-    const double2 *U = Mi, *V = Mi + MF, *H = Mi + 2 * MF, *Uy = Mi + 3 * MF;
-    constexpr int W = roww<LOG2N>();
-    Twiddles<9, true> tq;
-    tq.load(c.t & 63, tw, LOG2N - 9);
-    auto wnt = [&]() { return tw[c.t]; };  // W_N^t per transform (not held)
-    using V1 = double2(&)[1][8];
-    double2 w[2][8];
-    load_uv_eta_zeta<LOG2N, true>(w, ri, g, U, V, H, Uy);
-    fftw_dif<W, +1, 1, true, true, false, PRUNE>(reinterpret_cast<V1>(w[0]), c.t, wnt(), tq, line, 0);
-    fftw_dif<W, +1, 1, true, true, false, PRUNE>(reinterpret_cast<V1>(w[1]), c.t, wnt(), tq, line, 0);
-    double pc[8];
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const double u = w[0][s].x, vv = w[0][s].y, eta = w[1][s].x, zeta = w[1][s].y;
-      pc[s] = vv * eta;
-      w[0][s] = make_double2(0.5 * (u * u + vv * vv), zeta * vv);  // K + i ζv
-      w[1][s] = make_double2(zeta * u, u * eta);                   // ζu + i uη
-    }
-    fftw_dit<W, -1, 1, true, false, false, PRUNE>(reinterpret_cast<V1>(w[0]), c.t, wnt(), tq, line, 0);
-    split_pair<LOG2N, true, PRUNE>(w[0], c.t, g, line, [&](int k, int s, double2 a, double2 b) {
-      const int o = ri.ofwd(g, s);
-      Mo[o] = cadd(cmul_i(a, -(k * g.mk)), b);  // P = -ik K̂ + (ζv)^
-      Mo[MF + o] = a;                            // K̂
-    });
-    // PRE: the split's mirror reads span every wave's region
-    fftw_dit<W, -1, 1, true, true, false, PRUNE>(reinterpret_cast<V1>(w[1]), c.t, wnt(), tq, line, 0);
-    split_pair<LOG2N, true, PRUNE>(w[1], c.t, g, line, [&](int k, int s, double2 a, double2 b) {
-      const int o = ri.ofwd(g, s);
-      Mo[2 * MF + o] = a;                       // (ζu)^
-      Mo[3 * MF + o] = cmul_i(b, -(k * g.mk));  // Q = -ik (uη)^
-    });
-    // 4: (vη)^ (real input: the transform is the spectrum itself)
-#pragma unroll
-    for (int s = 0; s < 8; ++s) v[s] = make_double2(pc[s], 0.0);
-    fftw_dit<W, -1, 1, true, true, false, PRUNE>(reinterpret_cast<V1>(v), c.t, wnt(), tq, line, 0);
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const int k = c.t + s * Bk::NT;
-      if (RowIdx<LOG2N>::fwd_any(g, s) && k < g.kc) Mo[4 * MF + ri.ofwd(g, s)] = v[s];
-    }
-  } else if constexpr (MODEL == MODEL_RSW) {
+  if constexpr (MODEL == MODEL_RSW) {
     // rsw/RotatingShallowWater.jl:140-230 in vorticity form:
     //   u ux + v uy = ∂x K - ζ v,  u vx + v vy = ∂y K + ζ u,
     //   K = (u² + v²)/2, ζ = vx - uy.
@@ -2941,7 +2879,7 @@ static size_t lds_bytes() {
 }
 
 // 2LQG col_inv with the two layer blocks of a column paired on one XCD
-// (k_col_inv, gbase < 0), measured (tools/qg_inv_pair_ab.sh): 8192-point
+// (k_col_inv, gbase < 0), measured (tools/ab/qg_inv_pair_ab.sh): 8192-point
 // columns 949.7 -> 881.3 µs (config 5 61.2 -> 61.9 steps/s); 2048-point
 // columns 47-48 -> 48-50 µs (not used there).  1: on 8192-point lines,
 // 2: every length, 0: never (experiments).

@@ -1,7 +1,7 @@
 #!/bin/bash
 # On the GPU box: A/B of sweep_var/*.so — optional GPU parity tests per
 # variant, then R rounds of the default bench (variants interleaved per round,
-# so box drift hits all alike).  usage: bash tools/ab.sh [--check "pytest -k expr"] [R] [extra bench args]
+# so box drift hits all alike).  usage: bash tools/ab/ab.sh [--check "pytest -k expr"] [R] [extra bench args]
 mkdir -p gpurun_out/ab
 CHECK=""
 if [ "$1" = "--check" ]; then CHECK=$2; shift 2; fi

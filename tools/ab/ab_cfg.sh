@@ -1,7 +1,7 @@
 #!/bin/bash
 # On the GPU box: A/B of full-build variants (every transform length) over the
 # BASELINE configurations, variants interleaved per round so box drift hits
-# all alike.  usage: bash tools/ab_cfg.sh R so1 so2 ... [-- CONFIGS]
+# all alike.  usage: bash tools/ab/ab_cfg.sh R so1 so2 ... [-- CONFIGS]
 #   CONFIGS: model:grid:stepper:steps[:nutune:cfltune] (default: configs 2-5 + the metric)
 mkdir -p gpurun_out/abc
 R=$1; shift

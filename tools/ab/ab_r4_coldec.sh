@@ -3,7 +3,7 @@
 # interleaved benches of sweep_var/c14.so (natural-order Stockham columns),
 # c12.so (decimated from 4096: the default) and c11.so (from 2048) on
 # config 5, config 4, the 2048² metric and 2LQG 2048² IFMAB3.
-# usage: bash tools/ab_r4_coldec.sh [R]
+# usage: bash tools/ab/ab_r4_coldec.sh [R]
 mkdir -p gpurun_out/ab
 R=${1:-2}
 run() {  # variant tag model grid stepper steps warmup

@@ -3,7 +3,7 @@
 # SW_RSW_ROWH_NB) and the RSW half row's single read of V (SW_RSW_ROWH_ZPARK):
 # interleaved benches of sweep_var/q13*.so (config 5) and r12*.so (config 4),
 # then PMC traffic per variant (tools/traffic_at.sh).
-# usage: bash tools/ab_r4_rowh.sh [R]
+# usage: bash tools/ab/ab_r4_rowh.sh [R]
 mkdir -p gpurun_out/ab
 R=${1:-2}
 run() {  # name model grid stepper steps warmup

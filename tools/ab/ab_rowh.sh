@@ -2,7 +2,7 @@
 # On the GPU box: the half-length 2LQG row (k_row_qg_h) against the
 # full-length pair row, interleaved: config 5 (8192² IFMRK4, --len 13
 # builds h13/f13) and config 3 (2048² IFMAB3, --len 11 builds h11/f11).
-# usage: bash tools/ab_rowh.sh [R]
+# usage: bash tools/ab/ab_rowh.sh [R]
 mkdir -p gpurun_out/ab
 R=${1:-2}
 run() {  # name grid stepper steps warmup

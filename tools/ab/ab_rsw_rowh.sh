@@ -2,7 +2,7 @@
 # On the GPU box: the half-length RSW row (k_row_rsw_h) against k_row.
 # Parity first with the all-length build (sweep_var/rall.so), then interleaved
 # benches of the --len builds r11*/r12*/r13* (RSW FilteredAB3 2048²/4096²/8192²).
-# usage: bash tools/ab_rsw_rowh.sh [R]
+# usage: bash tools/ab/ab_rsw_rowh.sh [R]
 mkdir -p gpurun_out/ab
 R=${1:-2}
 LIBSW_PATH=$PWD/sweep_var/rall.so timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \

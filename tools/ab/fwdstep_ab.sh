@@ -2,7 +2,7 @@
 # A/B of the fused forward+update column pass (SW_FWD_STEP=1, default) against
 # separate col_fwd + update kernels (SW_FWD_STEP=0) on the coupled-update pairs;
 # SW_FWD_STEP=2: the variant with N parked in LDS. FS="0 2" picks the modes.
-# Usage (via gpurun): bash tools/fwdstep_ab.sh [OUTDIR]
+# Usage (via gpurun): bash tools/ab/fwdstep_ab.sh [OUTDIR]
 set -o pipefail
 O=${1:-gpurun_out/fwdstep}
 mkdir -p $O

@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of the XCD-paired 2LQG col_inv grid (SW_QG_INV_PAIR) on variant builds
 # (tools/build_variants.sh --len 11 pair0:-DSW_QG_INV_PAIR=0 pair1:-DSW_QG_INV_PAIR=2; --len 13 pair0_13/pair1_13),
-# after the 2LQG GPU parity tests.  Usage (via gpurun): bash tools/qg_inv_pair_ab.sh
+# after the 2LQG GPU parity tests.  Usage (via gpurun): bash tools/ab/qg_inv_pair_ab.sh
 set -o pipefail
 r() { n=$1; shift; LIBSW_PATH=$PWD/sweep_var/$n.so timeout -k 10 200 python bench.py --no-cpu-baseline --no-config5 --model qg2 "$@" > gpurun_out/pair/$n.json 2> gpurun_out/pair/$n.err && python -c "import json; d=json.load(open('gpurun_out/pair/$n.json')); print('$n', round(d['value'],2), [(k['name'], round(k['avg_us'],1)) for k in d['kernels']])"; }
 mkdir -p gpurun_out/pair

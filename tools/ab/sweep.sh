@@ -1,6 +1,6 @@
 #!/bin/bash
 # On the GPU box: short bench of every sweep_var/*.so (per-kernel HIP-event times).
-# usage: bash tools/sweep.sh [--check] [extra bench args]
+# usage: bash tools/ab/sweep.sh [--check] [extra bench args]
 #   --check: first run the RSW FilteredAB3 parity/slab GPU tests against each variant
 mkdir -p gpurun_out/sweep
 CHECK=0

@@ -1,6 +1,6 @@
 #!/bin/bash
 # On the GPU box: short bench of every sweep_var/*.so under each value of an
-# environment knob.  usage: bash tools/sweep_env.sh [VAR "v1 v2 ..."]
+# environment knob.  usage: bash tools/ab/sweep_env.sh [VAR "v1 v2 ..."]
 mkdir -p gpurun_out/sweep
 VAR=${1:-NONE}; VALS=${2:-0}
 for so in sweep_var/*.so; do n=$(basename $so .so); for v in $VALS; do

@@ -1,6 +1,6 @@
 #!/bin/bash
 # On the GPU box: per-model bench lines for sweep_var/<name><len>.so builds
-# (tools/build_variants.sh --len L).  usage: bash tools/sweep_models.sh
+# (tools/build_variants.sh --len L).  usage: bash tools/ab/sweep_models.sh
 mkdir -p gpurun_out/sweep
 run() {  # so model grid stepper
   SW_CHECK_NAN=0 LIBSW_PATH=$PWD/sweep_var/$1.so timeout -k 10 120 python bench.py --no-cpu-baseline --no-config5 \

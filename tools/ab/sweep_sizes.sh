@@ -1,6 +1,6 @@
 #!/bin/bash
 # On the GPU box: per-kernel times of every sweep_var/*.so at the large
-# configurations.  usage: bash tools/sweep_sizes.sh "model stepper n steps" ...
+# configurations.  usage: bash tools/ab/sweep_sizes.sh "model stepper n steps" ...
 mkdir -p gpurun_out/sizes
 CFGS=("$@")
 for so in sweep_var/*.so; do
