@@ -55,6 +55,11 @@ int main(int argc, char** argv) {
   run<9, 4>(n, in, out);
   run<3, 2>(n, in, out);
   run<12, 6>(n, in, out);
+  // write-heavy mixes (the 8192-point column inverse: 2 compact reads, 6 mixed writes)
+  run<0, 6>(n, in, out);
+  run<1, 3>(n, in, out);
+  run<2, 6>(n, in, out);
+  run<1, 6>(n, in, out);
   CK(hipFree(in));
   CK(hipFree(out));
   return 0;
