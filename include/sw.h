@@ -163,9 +163,9 @@ typedef struct sw_config {
   int32_t precision;
   /* 1: also carry the modes the 2/3 rule removes (RSW or 2LQG with IFMAB3,
    * IFMRK4 or FilteredAB3, Thomas-Yamada with ETDRK4, nx up to 8192; one
-   * slab, or several slabs in one
-   * process (local_slabs = nranks) — not one slab per process; RSW then runs
-   * its calcN in the reference's advective form).  The reference's calcN!
+   * slab, several slabs in one process, or one slab per process (the aliased
+   * columns' row-pass x-spectra all-gathered per calcN); RSW then runs its
+   * calcN in the reference's advective form).  The reference's calcN!
    * returns N there (swqg/TwoLayerQG.jl:171,179; rsw/RotatingShallowWater.jl
    * :140-230) and its update writes them into prob.sol (utils/IFMAB3.jl
    * :142-160) until the next calcN!/updatevars! dealiases: sw_calcN,

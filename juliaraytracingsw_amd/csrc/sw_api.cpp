@@ -91,6 +91,7 @@ struct sw_ctx {
   double2* stage = nullptr;                  // full (nkr,nl,nf) staging
   float* stage32 = nullptr;                  // SW_PREC_F32: the caller-precision copy of stage / dflt
   double2* gbuf = nullptr;                   // dist: all-gathered compact slabs
+  double2* abuf = nullptr;                   // dist + aliased_state: all-gathered aliased regions
   double* dflt = nullptr;                    // physical staging / reductions
   double* ecols = nullptr;                   // per-column energy sums [global column][SW_NSUM]
   double* esum = nullptr;                    // energy sums / gathered maxima (sw_diag)
@@ -270,9 +271,10 @@ std::vector<double2> twiddles(int N) {
 // The aliased modes FF's dealias! zeroes as two compact regions
 // the mode-wise kernels (k_step_elem, k_energy_cols, k_scatter_modes) walk
 // like the live set: r = 0 the columns kr in [kc, nx/2], every row (held by
-// slab 0: its y-transforms need every row, which all slabs of this process
-// write); r = 1 the slab's own live columns, rows l in [lc, lr2)
-// (lrow_of(j) = lc + j).  Slabs of one process (local_slabs = nranks).
+// slab 0: its y-transforms need every row, which every slab's row pass
+// writes into its block of the x-spectra — in one process directly, one slab
+// per process through an all-gather per calcN); r = 1 the slab's own live
+// columns, rows l in [lc, lr2) (lrow_of(j) = lc + j).
 Geom alias_geom(const Geom& g, int r) {
   Geom a = g;
   if (r == 0) {
@@ -607,6 +609,7 @@ static void last_col_pass(sw_ctx* c, double2* Slab::*X, double2* Slab::*N, int o
   sw::launch_col_fwd_step(c->kmodel, op, s.g, c->p, a, s.mfc, c->tw_y, c->stream, fwd_step_lds(c));
 }
 
+int allgather(sw_ctx* c, const void* mine, void* dst, size_t bytes);
 // equation.calcN!(N, X, …): col_inv -> transpose -> row -> transpose -> col_fwd;
 // op >= 0: the stepper update of `op` fused into the col_fwd pass (use_fwd_step)
 int calcN(sw_ctx* c, double2* Slab::*X, double2* Slab::*N, int op = -1, int stage = 0) {
@@ -650,6 +653,11 @@ int calcN(sw_ctx* c, double2* Slab::*X, double2* Slab::*N, int op = -1, int stag
     Timer tm(c, K_ROW);
     for (Slab& s : c->sl)
       sw::launch_row(model, s.g, c->p, s.mir, s.mfr, c->tw_x, c->stream, 0, -1, c->alias ? c->sl[0].a_mrow : nullptr);
+  }
+  if (c->alias && c->dist) {  // every rank's block of the aliased x-spectra, for slab 0's region 0 (ma_off)
+    const Slab& s = c->sl[0];
+    const size_t B = (size_t)c->nfwd * sw::ma_field(s.g);
+    if (int rc = allgather(c, s.a_mrow + (size_t)s.g.slab * B, s.a_mrow, B * sizeof(double2))) return rc;
   }
   if (int rc = transpose(c, false, c->nfwd)) return rc;
   {
@@ -878,12 +886,54 @@ int alias_energy_cols(sw_ctx* c, bool post_step_state, int ncols) {
   return ncols;
 }
 
+// aliased-state energies: 2LQG's and Thomas–Yamada's energy functions read
+// the full post-step array (RSW's the dealiased vars.uh)
+bool alias_energy(const sw_ctx* c) {
+  return c->alias && (c->cfg.model == SW_MODEL_QG2 || c->cfg.model == SW_MODEL_TY);
+}
+// energy columns of one rank's record (one slab per process): the kcl live
+// columns, then (alias_energy) region 0's nkr - kc columns (slab 0; zeros on
+// the others) and the slab's region 1 padded to kcl columns
+size_t rank_cols(const sw_ctx* c) {
+  const Geom& g = c->sl[0].g;
+  return (size_t)g.kcl + (alias_energy(c) ? (size_t)(g.nkr - g.kc) + g.kcl : 0);
+}
+// one record's sums from every rank's columns (rank q's at all + q * per +
+// off), added in the undecomposed run's global column order — the live
+// columns, region 0, every slab's region 1 — so bitwise the same for any
+// decomposition (padding columns hold zeros)
+void sum_rank_cols(const sw_ctx* c, const double* all, size_t per, size_t off, double* sums) {
+  const Geom& g = c->sl[0].g;
+  const size_t kcl = g.kcl, na = (size_t)(g.nkr - g.kc);
+  for (int k = 0; k < SW_NSUM; ++k) {
+    double acc = 0.0;
+    for (int q = 0; q < c->P; ++q)
+      for (size_t col = 0; col < kcl; ++col) acc += all[q * per + off + col * SW_NSUM + k];
+    if (alias_energy(c)) {
+      for (size_t col = 0; col < na; ++col) acc += all[off + (kcl + col) * SW_NSUM + k];
+      for (int q = 0; q < c->P; ++q)
+        for (size_t col = 0; col < kcl; ++col) acc += all[q * per + off + (kcl + na + col) * SW_NSUM + k];
+    }
+    sums[k] = acc;
+  }
+}
+
 // one energy record of state X into dst: the sums [SW_NSUM], or (one slab per
-// process) this rank's column sums [kcl][SW_NSUM], added over ranks at retrieval
+// process) this rank's column sums [rank_cols][SW_NSUM], added over ranks at
+// retrieval
 void record_energy_to(sw_ctx* c, double2* Slab::*X, double* dst) {
   if (c->dist) {
     const Slab& s = c->sl[0];
     sw::launch_energy_cols(c->cfg.model, s.g, c->p, s.*X, dst, c->stream);
+    if (alias_energy(c)) {
+      const size_t na = (size_t)(s.g.nkr - s.g.kc);
+      double* d0 = dst + SW_NSUM * (size_t)s.g.kcl;
+      (void)hipMemsetAsync(d0, 0, SW_NSUM * (na + s.g.kcl) * sizeof(double), c->stream);
+      if (X == &Slab::sol)  // (the post-step state, as alias_energy_cols)
+        for (int r = 0; r < 2; ++r)
+          if (s.ga[r].kcn > 0)
+            sw::launch_energy_cols(c->cfg.model, s.ga[r], c->p, s.a_sol[r], d0 + (r ? SW_NSUM * na : 0), c->stream);
+    }
     return;
   }
   for (Slab& s : c->sl) sw::launch_energy_cols(c->cfg.model, s.g, c->p, s.*X, c->ecols + SW_NSUM * s.g.kr0, c->stream);
@@ -895,7 +945,7 @@ void record_energy_to(sw_ctx* c, double2* Slab::*X, double* dst) {
 // and/or the forced one (sw_step_record)
 void record_energy(sw_ctx* c, double2* Slab::*X, bool rec, bool frec) {
   if (rec)
-    record_energy_to(c, X, c->erec + (c->dist ? (size_t)c->diag_n * c->sl[0].g.kcl * SW_NSUM : SW_NSUM * c->diag_n));
+    record_energy_to(c, X, c->erec + (c->dist ? (size_t)c->diag_n * rank_cols(c) * SW_NSUM : SW_NSUM * c->diag_n));
   if (frec) record_energy_to(c, X, c->erec1);
 }
 
@@ -1044,7 +1094,7 @@ int nan_flag(sw_ctx* c, int& h) {
   return 0;
 }
 
-void free_slab(Slab& s) {
+void free_slab(Slab& s, bool own_mrow) {
   void* ptrs[] = {s.sol, s.sol2, s.hist[0], s.hist[1], s.hist[2], s.acc, s.xs, s.mic, s.mfr, s.etd};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
@@ -1057,16 +1107,54 @@ void free_slab(Slab& s) {
     for (void* q : a)
       if (q) (void)hipFree(q);
   }
-  if (s.a_mrow && s.ga[0].kcn > 0) (void)hipFree(s.a_mrow);  // (slab 0's; the others point to it)
+  if (s.a_mrow && (s.ga[0].kcn > 0 || own_mrow)) (void)hipFree(s.a_mrow);  // (slab 0's; the others point to it)
 }
 
 // aliased-state tracking: every slab's compact aliased pair (arr(s)[r]) <->
 // c->stage (the full array)
+// One slab per process: every rank's regions, all-gathered (region 1 padded
+// to kcl columns; region 0 from slab 0), then scattered into every rank's
+// full array, as collect_full does for the live modes.
+int alias_slot(const sw_ctx* c, size_t& r1pad, size_t& r0sz) {
+  const Geom& g = c->sl[0].g;
+  r1pad = (size_t)g.kcl * alias_geom(g, 1).LrP;
+  r0sz = (size_t)(g.nkr - g.kc) * alias_geom(g, 0).LrP;
+  return c->nf;
+}
 template <typename Arr>
-void alias_scatter(sw_ctx* c, Arr arr) {
-  if (!c->alias) return;
-  for (Slab& s : c->sl)
-    for (int r = 0; r < 2; ++r) sw::launch_scatter_modes(c->nf, s.ga[r], arr(s)[r], c->stage, c->stream);
+int alias_scatter(sw_ctx* c, Arr arr) {
+  if (!c->alias) return 0;
+  if (!c->dist) {
+    for (Slab& s : c->sl)
+      for (int r = 0; r < 2; ++r) sw::launch_scatter_modes(c->nf, s.ga[r], arr(s)[r], c->stage, c->stream);
+    return 0;
+  }
+  Slab& s = c->sl[0];
+  size_t r1pad, r0sz;
+  const int nf = alias_slot(c, r1pad, r0sz);
+  const size_t slot = (size_t)nf * (r1pad + r0sz);
+  double2* mine = c->abuf + (size_t)s.g.slab * slot;
+  for (int r = 0; r < 2; ++r) {
+    if (s.ga[r].kcn <= 0) continue;
+    double2* dst = mine + (r == 1 ? 0 : (size_t)nf * r1pad);
+    const size_t stride = r == 1 ? r1pad : r0sz;
+    for (int f = 0; f < nf; ++f)
+      HIPCHK(c, hipMemcpyAsync(dst + f * stride, arr(s)[r] + f * s.ga[r].cfield, s.ga[r].cfield * sizeof(double2),
+                               hipMemcpyDeviceToDevice, c->stream));
+  }
+  if (int rc = allgather(c, mine, c->abuf, slot * sizeof(double2))) return rc;
+  for (int q = 0; q < c->P; ++q) {
+    const Geom gq = make_geom(c->cfg, c->P, q);
+    for (int r = 0; r < 2; ++r) {
+      Geom ga = alias_geom(gq, r);
+      if (ga.kcn <= 0) continue;
+      ga.cfield = (long long)(r == 1 ? r1pad : r0sz);
+      sw::launch_scatter_modes(nf, ga, c->abuf + (size_t)q * slot + (r == 1 ? 0 : (size_t)nf * r1pad), c->stage,
+                               c->stream);
+    }
+  }
+  HIPCHK(c, hipGetLastError());
+  return 0;
 }
 template <typename Arr>
 void alias_gather(sw_ctx* c, Arr arr) {
@@ -1146,10 +1234,8 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
           (k.model == SW_MODEL_TY && k.stepper == SW_STEP_ETDRK4)))
       return fail(c, SW_E_INVALID,
                   "aliased_state: RSW or 2LQG with IFMAB3, IFMRK4 or FilteredAB3, or Thomas-Yamada with ETDRK4");
-    // region 0's y-transforms need every row of the row pass's aliased
-    // x-spectra: all slabs in this process (not one slab per process)
-    if (k.nranks > 1 && k.local_slabs != k.nranks)
-      return fail(c, SW_E_INVALID, "aliased_state: every slab in one process (local_slabs = nranks)");
+    // (one slab per process: region 0's y-transforms need every row of the
+    // row pass's aliased x-spectra, all-gathered per calcN)
     if (!sw::row_alias_built(k.model == SW_MODEL_RSW ? sw::MODEL_RSWA : k.model, ilog2(k.nx)))
       return fail(c, SW_E_INVALID, "aliased_state: the row pass's aliased output is not built at this nx");
   }
@@ -1315,7 +1401,7 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
           if ((rc = alloc(c, (void**)&s.a_hist[i][r], cb))) return rc;
       }
     }
-    if (s.ga[0].kcn > 0) {
+    if (s.ga[0].kcn > 0 || c->dist) {  // (one slab per process: every rank's rows, all-gathered)
       const size_t mrow = (size_t)c->nfwd * (s.g.nkr - s.g.kc) * s.g.ny * sizeof(double2);
       if ((rc = alloc(c, (void**)&s.a_mrow, mrow))) return rc;
     } else {
@@ -1328,17 +1414,28 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
     if ((rc = alloc(c, (void**)&c->stage32, full_bytes(c) / 2))) return rc;
   if ((rc = alloc(c, (void**)&c->dflt, (size_t)g.nx * g.ny * sizeof(double)))) return rc;
   if ((rc = alloc(c, (void**)&c->flag, 1024 * sizeof(int)))) return rc;
-  const size_t ecols = (size_t)P * g.kcl + alias_cols;
+  size_t ecols = (size_t)P * g.kcl + alias_cols;
+  if (c->dist && alias_energy(c))  // + region 0, every slab's region 1 and their gather scratch (sw_diag)
+    ecols = (size_t)P * g.kcl + ((size_t)(g.nkr - g.kc) + (size_t)P * g.kcl) +
+            (size_t)P * ((size_t)(g.nkr - g.kc) + g.kcl);
   if ((rc = alloc(c, (void**)&c->ecols, SW_NSUM * ecols * sizeof(double)))) return rc;
   if ((rc = alloc(c, (void**)&c->esum, (SW_NSUM + 2 * (size_t)P) * sizeof(double)))) return rc;
   if (c->dist) {
     const size_t gb = (size_t)P * c->nf * g.kcl * g.LrP * sizeof(double2);
     if ((rc = alloc(c, (void**)&c->gbuf, gb))) return rc;
+    size_t ab = 0, mb = 0;  // aliased state: the regions' and the row pass's x-spectra all-gathers
+    if (c->alias) {
+      size_t r1pad, r0sz;
+      const int nf = alias_slot(c, r1pad, r0sz);
+      ab = (size_t)P * nf * (r1pad + r0sz) * sizeof(double2);
+      if ((rc = alloc(c, (void**)&c->abuf, ab))) return rc;
+      mb = (size_t)c->nfwd * (g.nkr - g.kc) * g.ny * sizeof(double2);
+    }
     if (c->hostx) {
       // largest message set: a transpose, the compact all-gather or the physical rows
       const size_t tb = (size_t)std::max(c->ninv, c->nfwd) * (size_t)g.mfield * sizeof(double2);
       const size_t pb = (size_t)g.nx * g.ny * sizeof(double);
-      c->hbytes = std::max(tb, std::max(gb, pb));
+      c->hbytes = std::max(std::max(tb, std::max(gb, pb)), std::max(ab, mb));
       HIPCHK(c, hipHostMalloc((void**)&c->hsend, c->hbytes, hipHostMallocDefault));
       HIPCHK(c, hipHostMalloc((void**)&c->hrecv, c->hbytes, hipHostMallocDefault));
     }
@@ -1399,8 +1496,8 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
 void sw_destroy(sw_ctx* c) {
   if (!c) return;
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (Slab& s : c->sl) free_slab(s);
-  void* ptrs[] = {c->tw_x, c->tw_y, c->stage, c->stage32, c->gbuf, c->dflt, c->flag, c->ecols, c->esum, c->erec,
+  for (Slab& s : c->sl) free_slab(s, c->dist);
+  void* ptrs[] = {c->tw_x, c->tw_y, c->stage, c->stage32, c->gbuf, c->abuf, c->dflt, c->flag, c->ecols, c->esum, c->erec,
                   c->erec1, c->cold, c->cold_out};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
@@ -1452,7 +1549,7 @@ int sw_get_state(const sw_ctx* cc, void* sol, size_t bytes) {
   if (!sol || bytes != caller_bytes(c, full_bytes(c))) return fail(c, SW_E_INVALID, "sw_get_state: size mismatch");
   HIPCHK(c, hipSetDevice(c->cfg.device));
   if (int rc = collect_full(c, &Slab::sol)) return rc;
-  alias_scatter(c, A_SOL);
+  if (int rc = alias_scatter(c, A_SOL)) return rc;
   if (int rc = download(c, c->stage, sol, full_bytes(c))) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return SW_OK;
@@ -1507,7 +1604,7 @@ int sw_calcN(sw_ctx* c, const void* sol, void* N, size_t bytes) {
   set_alias_nbuf(c);
   if (int rc = calcN(c, &Slab::xs, &Slab::nbuf)) return rc;
   if (int rc = collect_full(c, &Slab::nbuf)) return rc;
-  alias_scatter(c, A_NBUF);
+  if (int rc = alias_scatter(c, A_NBUF)) return rc;
   if (int rc = download(c, c->stage, N, full_bytes(c))) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return SW_OK;
@@ -1618,7 +1715,7 @@ static int gather_new_energy_sums(sw_ctx* c) {
     c->esums_n = n1;
     return 0;
   }
-  const size_t kcl = c->sl[0].g.kcl, rec = kcl * SW_NSUM;  // doubles per record and rank
+  const size_t rec = rank_cols(c) * SW_NSUM;  // doubles per record and rank
   int64_t chunk = n1 - n0;
   if (c->hostx) chunk = std::max<int64_t>(1, std::min<int64_t>(chunk, c->hbytes / (c->P * rec * sizeof(double))));
   std::vector<double> all((size_t)chunk * rec * c->P);
@@ -1634,12 +1731,7 @@ static int gather_new_energy_sums(sw_ctx* c) {
       rc = fail(c, SW_E_HIP, "energy gather copy failed");
     if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = fail(c, SW_E_HIP, "energy gather sync failed");
     for (int64_t r = 0; r < m && !rc; ++r)
-      for (int k = 0; k < SW_NSUM; ++k) {
-        double acc = 0.0;
-        for (int q = 0; q < c->P; ++q)
-          for (size_t col = 0; col < kcl; ++col) acc += all[q * per + ((size_t)r * kcl + col) * SW_NSUM + k];
-        c->esums_host[(size_t)(r0 + r) * SW_NSUM + k] = acc;
-      }
+      sum_rank_cols(c, all.data(), per, (size_t)r * rec, c->esums_host.data() + (size_t)(r0 + r) * SW_NSUM);
   }
   (void)hipStreamSynchronize(c->stream);
   (void)hipFree(tmp);
@@ -1700,11 +1792,33 @@ int sw_diag(sw_ctx* c, int32_t id, double* out) {
       ((id == SW_DIAG_KE1 || id == SW_DIAG_KE2) && c->cfg.model == SW_MODEL_TY))
     return fail(c, SW_E_INVALID, "diagnostic not defined for this model");
   for (Slab& s : c->sl) sw::launch_energy_cols(c->cfg.model, s.g, c->p, s.sol, c->ecols + SW_NSUM * s.g.kr0, c->stream);
+  int ncols = c->P * c->sl[0].g.kcl;
   if (c->dist) {
-    const Geom& g0 = c->sl[0].g;
+    const Slab& s = c->sl[0];
+    const Geom& g0 = s.g;
     if (int rc = allgather(c, c->ecols + SW_NSUM * g0.kr0, c->ecols, SW_NSUM * (size_t)g0.kcl * sizeof(double))) return rc;
+    if (alias_energy(c)) {
+      // every rank's aliased columns, in the undecomposed order: region 0
+      // (slab 0), then every slab's region 1 (padded to kcl: zeros)
+      const size_t na = (size_t)(g0.nkr - g0.kc), kcl = g0.kcl, slot = (na + kcl) * SW_NSUM;
+      double* ord = c->ecols + SW_NSUM * (size_t)ncols;
+      double* scr = ord + SW_NSUM * (na + c->P * kcl);
+      double* mine = scr + (size_t)g0.slab * slot;
+      HIPCHK(c, hipMemsetAsync(mine, 0, slot * sizeof(double), c->stream));
+      for (int r = 0; r < 2; ++r)
+        if (s.ga[r].kcn > 0)
+          sw::launch_energy_cols(c->cfg.model, s.ga[r], c->p, s.a_sol[r], mine + (r ? SW_NSUM * na : 0), c->stream);
+      if (int rc = allgather(c, mine, scr, slot * sizeof(double))) return rc;
+      HIPCHK(c, hipMemcpyAsync(ord, scr, SW_NSUM * na * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+      for (int q = 0; q < c->P; ++q)
+        HIPCHK(c, hipMemcpyAsync(ord + SW_NSUM * (na + q * kcl), scr + q * slot + SW_NSUM * na,
+                                 SW_NSUM * kcl * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+      ncols += (int)(na + c->P * kcl);
+    }
+  } else {
+    ncols = alias_energy_cols(c, true, ncols);
   }
-  sw::launch_energy_final(c->ecols, alias_energy_cols(c, true, c->P * c->sl[0].g.kcl), c->esum, c->stream);
+  sw::launch_energy_final(c->ecols, ncols, c->esum, c->stream);
   HIPCHK(c, hipGetLastError());
   std::vector<double> sums(SW_NSUM);
   HIPCHK(c, hipMemcpyAsync(sums.data(), c->esum, SW_NSUM * sizeof(double), hipMemcpyDeviceToHost, c->stream));
@@ -1733,7 +1847,7 @@ int sw_step_record(sw_ctx* c, int64_t nsteps, sw_energy_record* out) {
   if (!ready(c) || !out) return SW_E_STATE;
   if (nsteps < 1) return fail(c, SW_E_INVALID, "sw_step_record: nsteps must be >= 1");
   HIPCHK(c, hipSetDevice(c->cfg.device));
-  const size_t per = c->dist ? (size_t)c->sl[0].g.kcl * SW_NSUM : SW_NSUM;
+  const size_t per = c->dist ? rank_cols(c) * SW_NSUM : SW_NSUM;
   if (!c->erec1)
     if (int rc = alloc(c, (void**)&c->erec1, per * sizeof(double))) return rc;
   for (int64_t i = 0; i + 1 < nsteps; ++i)
@@ -1746,7 +1860,6 @@ int sw_step_record(sw_ctx* c, int64_t nsteps, sw_energy_record* out) {
   HIPCHK(c, hipGetLastError());
   std::vector<double> sums(SW_NSUM, 0.0);
   if (c->dist) {  // collective: every rank's column sums, added in global column order
-    const size_t kcl = c->sl[0].g.kcl;
     std::vector<double> all(per * c->P);
     double* tmp = nullptr;
     HIPCHK(c, hipMalloc((void**)&tmp, all.size() * sizeof(double)));
@@ -1757,9 +1870,7 @@ int sw_step_record(sw_ctx* c, int64_t nsteps, sw_energy_record* out) {
     if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = fail(c, SW_E_HIP, "energy record sync failed");
     (void)hipFree(tmp);
     if (rc) return rc;
-    for (int k = 0; k < SW_NSUM; ++k)
-      for (int q = 0; q < c->P; ++q)
-        for (size_t col = 0; col < kcl; ++col) sums[k] += all[q * per + col * SW_NSUM + k];
+    sum_rank_cols(c, all.data(), per, 0, sums.data());
   } else {
     HIPCHK(c, hipMemcpyAsync(sums.data(), c->erec1, SW_NSUM * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1841,7 +1952,7 @@ int sw_set_energy_diagnostics(sw_ctx* c, int64_t freq, int64_t capacity) {
   c->esums_host.clear();
   c->esums_n = 0;
   if (c->diag_cap > 0) {
-    const size_t per = c->dist ? (size_t)c->sl[0].g.kcl * SW_NSUM : SW_NSUM;
+    const size_t per = c->dist ? rank_cols(c) * SW_NSUM : SW_NSUM;
     if (int rc = alloc(c, (void**)&c->erec, (size_t)c->diag_cap * per * sizeof(double))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
   }
@@ -1938,7 +2049,7 @@ int sw_get_history(const sw_ctx* cc, int32_t slot, void* buf, size_t bytes) {
   if (int rc = join_comm(c)) return rc;
   for (Slab& s : c->sl) s.view = s.hist[h];
   if (int rc = collect_full(c, &Slab::view)) return rc;
-  alias_scatter(c, a_hist(h));
+  if (int rc = alias_scatter(c, a_hist(h))) return rc;
   if (int rc = download(c, c->stage, buf, full_bytes(c))) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return SW_OK;
@@ -2016,12 +2127,12 @@ int sw_get_checkpoint(const sw_ctx* cc, void* buf, size_t bytes) {
   for (int k = 0; k <= h.nslots; ++k) {  // fp64 always: no narrowing to the caller precision
     if (k == 0) {
       if (int rc = collect_full(c, &Slab::sol)) return rc;
-      alias_scatter(c, A_SOL);
+      if (int rc = alias_scatter(c, A_SOL)) return rc;
     } else {
       const int hi = hist_index(c, k);
       for (Slab& s : c->sl) s.view = s.hist[hi];
       if (int rc = collect_full(c, &Slab::view)) return rc;
-      alias_scatter(c, a_hist(hi));
+      if (int rc = alias_scatter(c, a_hist(hi))) return rc;
     }
     HIPCHK(c, hipMemcpyAsync(out + sizeof(h) + k * fb, c->stage, fb, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));

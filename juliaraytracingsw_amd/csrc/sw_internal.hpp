@@ -181,6 +181,20 @@ __host__ __device__ inline int midc(const Geom& g, int krl, int y) {
 __host__ __device__ inline int midx(const Geom& g, int kr, int yl) { return mtile_x<SW_TILE_F, SW_LORD_F>(g, kr, yl); }
 __host__ __device__ inline int midc(const Geom& g, int krl, int y) { return mtile_c<SW_TILE_F, SW_LORD_F>(g, krl, y); }
 #endif
+// Aliased-state tracking: the row pass's x-spectra kr in [kc, nx/2] of its
+// NFA forward outputs (Ma).  One block per slab q of the stored rows,
+// [q][f][kr - kc][yl] (stored row m = q nyl + yl), so that one slab's rows
+// are one contiguous piece (one all-gather assembles them on the slab holding
+// the aliased columns, sw_api.cpp); one slab: [f][kr - kc][y].  Field f of
+// block q starts at Ma + ma_off(g, NFA, 0, q nyl) + f · ma_field(g).
+__host__ __device__ inline long long ma_field(const Geom& g) { return (long long)(g.nkr - g.kc) * g.nyl; }
+__host__ __device__ inline long long ma_off(const Geom& g, int nfa, int col, int m) {
+  const int q = m >> g.log2nyl, yl = m & (g.nyl - 1);
+  return ((long long)q * nfa * (g.nkr - g.kc) + col) * g.nyl + yl;
+}
+// fields of Ma per kernel family (the row pass's forward outputs)
+__host__ __device__ constexpr int ma_nfa(int model) { return model == MODEL_TY ? 7 : 4; }
+
 // inverse fields: column phase / row phase
 __host__ __device__ inline int midc_i(const Geom& g, int krl, int y) { return mtile_c<SW_TILE_I, SW_LORD_I>(g, krl, y, g.tcm); }
 __host__ __device__ inline int midx_i(const Geom& g, int kr, int yl) { return mtile_x<SW_TILE_I, SW_LORD_I>(g, kr, yl, g.tcm); }

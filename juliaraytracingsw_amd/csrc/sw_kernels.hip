@@ -725,9 +725,9 @@ __device__ __forceinline__ void fft_pair(double2 (&w)[2][8], int t, const Twiddl
 }
 
 // After split_pair (LDS still holds Z): the aliased x-spectra kc <= k <= nx/2
-// of the pair, A[k] and B[k], into [k - kc][y] of A and B (aliased-state
-// tracking, sw_config.aliased_state)
-template <int LOG2N, bool NIK_A = false>
+// of the pair, A[k] and B[k], into (k - kc, stored row y) of the Ma fields A
+// and B (aliased-state tracking, sw_config.aliased_state; ma_off)
+template <int LOG2N, int NFA, bool NIK_A = false>
 __device__ __forceinline__ void store_alias_pair(const double2 (&v)[8], int t, const Geom& g, const double2* line,
                                                  double2* __restrict__ A, double2* __restrict__ B, int y) {
   constexpr int N = 1 << LOG2N, NT = N / 8;
@@ -737,7 +737,7 @@ __device__ __forceinline__ void store_alias_pair(const double2 (&v)[8], int t, c
     if (k >= g.kc && k <= N / 2) {
       const double2 zk = v[s];
       const double2 zn = line[LP<LOG2N>((N - k) & (N - 1))];
-      const long long o = (long long)(k - g.kc) * g.ny + y;
+      const long long o = ma_off(g, NFA, k - g.kc, y);
       const double2 a = make_double2(0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y));
       A[o] = NIK_A ? cmul_i(a, -(k * g.mk)) : a;  // as the live outputs: Q = -ik (uη)^ (RSW)
       B[o] = make_double2(0.5 * (zk.y + zn.y), -0.5 * (zk.x - zn.x));
@@ -747,8 +747,8 @@ __device__ __forceinline__ void store_alias_pair(const double2 (&v)[8], int t, c
 
 // store_alias_pair with the outputs formed by the caller: emit(o, k, Â, B̂)
 // for the aliased kc <= k <= nx/2 of the pair in LDS, o = the offset of
-// [k - kc][y] in one aliased field (Thomas–Yamada's seven outputs)
-template <int LOG2N, typename Emit>
+// (k - kc, y) in one Ma field (Thomas–Yamada's seven outputs)
+template <int LOG2N, int NFA, typename Emit>
 __device__ __forceinline__ void store_alias_with(const double2 (&v)[8], int t, const Geom& g, const double2* line,
                                                  int y, Emit emit) {
   constexpr int N = 1 << LOG2N, NT = N / 8;
@@ -758,7 +758,7 @@ __device__ __forceinline__ void store_alias_with(const double2 (&v)[8], int t, c
     if (k >= g.kc && k <= N / 2) {
       const double2 zk = v[s];
       const double2 zn = line[LP<LOG2N>((N - k) & (N - 1))];
-      emit((long long)(k - g.kc) * g.ny + y, k, make_double2(0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y)),
+      emit(ma_off(g, NFA, k - g.kc, y), k, make_double2(0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y)),
            make_double2(0.5 * (zk.y + zn.y), -0.5 * (zk.x - zn.x)));
     }
   }
@@ -946,8 +946,8 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
     for (int s = 0; s < 8; ++s) pr[s] = make_double2(pr[s].x + uv[s].y * v[s].x, pr[s].y + uv[s].y * v[s].y);
     fft_line<LOG2N, -1>(pr, c.t, tws, line);
     store_pair<LOG2N>(pr, ri, g, line, Mo, Mo + MF);
-    const long long MA = (long long)(g.nkr - g.kc) * g.ny;  // aliased columns × rows per field
-    if constexpr (ALIAS) store_alias_pair<LOG2N>(pr, c.t, g, line, Ma, Ma + MA, y + g.y0);
+    const long long MA = ma_field(g);  // aliased columns × rows per field
+    if constexpr (ALIAS) store_alias_pair<LOG2N, ma_nfa(MODEL)>(pr, c.t, g, line, Ma, Ma + MA, y + g.y0);
     load_pair<LOG2N>(v, ri, g, H, nullptr, false);  // η
     fft_line<LOG2N, +1>(v, c.t, tws, line);
 #pragma unroll
@@ -958,7 +958,7 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
       Mo[2 * MF + o] = cmul_i(a, -(k * g.mk));
       Mo[3 * MF + o] = b;
     });
-    if constexpr (ALIAS) store_alias_pair<LOG2N, true>(v, c.t, g, line, Ma + 2 * MA, Ma + 3 * MA, y + g.y0);
+    if constexpr (ALIAS) store_alias_pair<LOG2N, ma_nfa(MODEL), true>(v, c.t, g, line, Ma + 2 * MA, Ma + 3 * MA, y + g.y0);
   } else if constexpr (MODEL == MODEL_TY) {
     // thomasyamada/ThomasYamada.jl:129-262.  Inputs (k_col_inv): 0 ζ, 1 ψ,
     // 2 ût, 3 ∂y ut, 4 uc, 5 ∂y uc, 6 vc, 7 pc, 8 ∂y pc.  Physical fields in
@@ -1006,8 +1006,8 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
       v[s] = make_double2(vt[s] * zt[s], uc[s] * uc[s] - vc[s] * vc[s]);  // p1 + i p4
     }
     // aliased-state tracking: the x-spectra kc <= k <= nx/2 of every output
-    // into Ma [field][k - kc][global row] (k_col_fwd_alias), as the live ones
-    const long long MA = (long long)(g.nkr - g.kc) * g.ny;
+    // into Ma (ma_off: field, k - kc, stored row; k_col_fwd_alias), as the live ones
+    const long long MA = ma_field(g);
     const int yg = y + g.y0;
     fft_line<LOG2N, -1>(w, c.t, tws, line);
     split_pair<LOG2N>(w, c.t, g, line, [&](int k, int s, double2 a, double2 b) {
@@ -1017,7 +1017,7 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
       Mo[2 * MF + o] = cscale(b, nRo);
     });
     if constexpr (ALIAS)
-      store_alias_with<LOG2N>(w, c.t, g, line, yg, [&](long long o, int k, double2 a, double2 b) {
+      store_alias_with<LOG2N, ma_nfa(MODEL)>(w, c.t, g, line, yg, [&](long long o, int k, double2 a, double2 b) {
         const double kw = k * g.mk;
         Ma[o] = cscale(csub(cmul_i(a, kw), cscale(b, kw * kw)), nRo);
         Ma[2 * MA + o] = cscale(b, nRo);
@@ -1028,7 +1028,7 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
       Mo[MF + ri.ofwd(g, s)] = cscale(cadd(cmul_i(a, 1.0), cscale(b, kw)), nRo);
     });
     if constexpr (ALIAS)
-      store_alias_with<LOG2N>(v, c.t, g, line, yg, [&](long long o, int k, double2 a, double2 b) {
+      store_alias_with<LOG2N, ma_nfa(MODEL)>(v, c.t, g, line, yg, [&](long long o, int k, double2 a, double2 b) {
         Ma[MA + o] = cscale(cadd(cmul_i(a, 1.0), cscale(b, k * g.mk)), nRo);
       });
     // ∂y ut + i ∂x vc
@@ -1045,7 +1045,7 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
       Mo[3 * MF + ri.ofwd(g, s)] = cscale(cadd(cmul_i(a, k * g.mk), b), nRo);
     });
     if constexpr (ALIAS)
-      store_alias_with<LOG2N>(v, c.t, g, line, yg, [&](long long o, int k, double2 a, double2 b) {
+      store_alias_with<LOG2N, ma_nfa(MODEL)>(v, c.t, g, line, yg, [&](long long o, int k, double2 a, double2 b) {
         Ma[3 * MA + o] = cscale(cadd(cmul_i(a, k * g.mk), b), nRo);
       });
     // ∂x vt + i ∂x pc
@@ -1064,7 +1064,7 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
       Mo[5 * MF + o] = cscale(b, nRo);
     });
     if constexpr (ALIAS)
-      store_alias_with<LOG2N>(v, c.t, g, line, yg, [&](long long o, int, double2 a, double2 b) {
+      store_alias_with<LOG2N, ma_nfa(MODEL)>(v, c.t, g, line, yg, [&](long long o, int, double2 a, double2 b) {
         Ma[4 * MA + o] = cscale(a, nRo);
         Ma[5 * MA + o] = cscale(b, nRo);
       });
@@ -1079,7 +1079,7 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
       const int k = c.t + s * Bk::NT;
       if (RowIdx<LOG2N>::fwd_any(g, s) && k < g.kc) Mo[6 * MF + ri.ofwd(g, s)] = cscale(v[s], nRo);
       if constexpr (ALIAS)  // (a real line: its transform is the spectrum itself)
-        if (k >= g.kc && k <= Bk::NT * 4) Ma[6 * MA + (long long)(k - g.kc) * g.ny + yg] = cscale(v[s], nRo);
+        if (k >= g.kc && k <= Bk::NT * 4) Ma[6 * MA + ma_off(g, ma_nfa(MODEL), k - g.kc, yg)] = cscale(v[s], nRo);
     }
   } else {
     const double2 *Q1 = Mi, *Q2 = Mi + MF, *P1 = Mi + 2 * MF, *P2 = Mi + 3 * MF,
@@ -1140,15 +1140,15 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
 #pragma unroll
     for (int s = 0; s < 8; ++s) v[s] = make_double2(v[s].x * q[s].x, v[s].y * q[s].y);
     fwd_store(Mo, Mo + MF);
-    const long long MA = (long long)(g.nkr - g.kc) * g.ny;  // aliased columns × rows per field
-    if constexpr (ALIAS) store_alias_pair<LOG2N>(v, c.t, g, line, Ma, Ma + MA, y + g.y0);
+    const long long MA = ma_field(g);  // aliased columns × rows per field
+    if constexpr (ALIAS) store_alias_pair<LOG2N, ma_nfa(MODEL)>(v, c.t, g, line, Ma, Ma + MA, y + g.y0);
     // ψy q per layer (:177)
     load_pair<LOG2N>(v, ri, g, Py1, Py2, false);
     inv(v);
 #pragma unroll
     for (int s = 0; s < 8; ++s) v[s] = make_double2(v[s].x * q[s].x, v[s].y * q[s].y);
     fwd_store(Mo + 2 * MF, Mo + 3 * MF);
-    if constexpr (ALIAS) store_alias_pair<LOG2N>(v, c.t, g, line, Ma + 2 * MA, Ma + 3 * MA, y + g.y0);
+    if constexpr (ALIAS) store_alias_pair<LOG2N, ma_nfa(MODEL)>(v, c.t, g, line, Ma + 2 * MA, Ma + 3 * MA, y + g.y0);
   }
 }
 
@@ -1690,13 +1690,13 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
   ColTw<LOG2N, CD> tws;
   tws.load(c.t, tw);
   const double k = (ga.kr0 + colA) * g.mk;
-  const long long MA = (long long)(g.nkr - g.kc) * g.ny;
+  const long long MA = ma_field(g);
   double2 v[8], acc[8];
   auto load_col = [&](int fi) {
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       const int m = cpos<LOG2N, CD>(c.t, s);  // stored row
-      const double2 t = region == 0 ? Ma[fi * MA + (long long)colA * g.ny + m] : Mf[fi * g.mfield + midc(g, colA, m)];
+      const double2 t = region == 0 ? Ma[fi * MA + ma_off(g, ma_nfa(MODEL), colA, m)] : Mf[fi * g.mfield + midc(g, colA, m)];
       v[s] = live ? t : zero2();
     }
   };

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--steps", type=int, default=6)
     ap.add_argument("--freq", type=int, default=2)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--aliased", action="store_true", help="aliased_state: the full (nkr, nl) array")
     a = ap.parse_args()
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
@@ -35,7 +36,8 @@ def main():
     p = sw_cases.case_params(a.case, a.n)
     grid = O.TwoDGrid(a.n)
     ic = sw_cases.initial_condition(p, grid)
-    prob = sw_cases.libsw_problem(p, decomposition=slab_comm.host_decomposition(rank, world))
+    kw = dict(aliased_state=True) if a.aliased else {}
+    prob = sw_cases.libsw_problem(p, decomposition=slab_comm.host_decomposition(rank, world), **kw)
     prob.sol = ic
     N = prob.calcN(ic)
     cap = a.steps // a.freq + 1
@@ -45,28 +47,34 @@ def main():
     mid = prob.ctx.energy_diagnostics()  # gathered once; the rest incrementally below
     prob.stepforward(a.steps - half)
     sol = prob.sol
-    phys = M.updatevars(prob)
+    # (energies of prob.sol before updatevars!, which dealiases it: with
+    # aliased_state they include the aliased modes)
     ke, pe = np.sum(M.kinetic_energy(prob)), M.potential_energy(prob)
+    phys = M.updatevars(prob)
     recs, cfl = prob.ctx.energy_diagnostics(), M.cfl(prob)
     res = {}
     if rank == 0:
-        ref = sw_cases.libsw_problem(p)
+        ref = sw_cases.libsw_problem(p, **kw)
         ref.sol = ic
         Nr = ref.calcN(ic)
         ref.ctx.set_energy_diagnostics(a.freq, cap)
         ref.stepforward(a.steps)
+        rsol = ref.sol
+        rke, rpe = np.sum(M.kinetic_energy(ref)), M.potential_energy(ref)
         pr = M.updatevars(ref)
         res = dict(
-            state_equal=bool(np.array_equal(sol, ref.sol)),
+            state_equal=bool(np.array_equal(sol, rsol)),
             calcN_equal=bool(np.array_equal(N, Nr)),
             physical_equal=bool(all(np.array_equal(phys[k], pr[k]) for k in pr)),
-            ke_rel=abs(ke / np.sum(M.kinetic_energy(ref)) - 1),
-            pe_rel=abs(pe / M.potential_energy(ref) - 1),
+            ke_rel=abs(ke / rke - 1),
+            pe_rel=abs(pe / rpe - 1),
             records_equal=bool(recs == ref.ctx.energy_diagnostics() and len(recs) == a.steps // a.freq
                                and mid == recs[:len(mid)] and len(mid) == half // a.freq),
             n_records=len(recs),
             cfl_equal=bool(cfl == M.cfl(ref)),
             world=world,
+            # the largest aliased mode of the state (aliased_state: nonzero)
+            aliased_max=float(np.max(np.abs(np.where(O.TwoDGrid(a.n).dealias(np.ones_like(sol)) == 0, sol, 0)))),
         )
         ref.close()
     prob.close()

@@ -204,20 +204,16 @@ def test_default_mode_unchanged():
     prob.close()
 
 
-@pytest.mark.parametrize("bad", ["frk4", "one_slab_per_process"])
-def test_rejected_where_not_built(bad):
+def test_rejected_where_not_built():
     """Only where it is built: RSW / 2LQG with IFMAB3/IFMRK4/FilteredAB3 or
-    Thomas–Yamada with ETDRK4 (not GeophysicalFlows' FilteredRK4), every slab
-    in one process (the aliased columns' y-transforms need every row)."""
+    Thomas–Yamada with ETDRK4 (not GeophysicalFlows' FilteredRK4).  (One slab
+    per process is built: tests/test_gpu_multiprocess.py.)"""
     from juliaraytracingsw_amd import _lib
 
     cfg = _lib.default_config()
     cfg.model, cfg.stepper, cfg.nx, cfg.ny = _lib.SW_MODEL_QG2, _lib.STEPPERS["IFMAB3"], 64, 64
     cfg.aliased_state = 1
-    if bad == "frk4":
-        cfg.stepper = _lib.STEPPERS["FilteredRK4"]
-    else:
-        cfg.nranks, cfg.local_slabs, cfg.rank = 2, 1, 0
+    cfg.stepper = _lib.STEPPERS["FilteredRK4"]
     with pytest.raises(LibSWError, match="aliased_state"):
         _lib.Context(cfg)
 

@@ -23,17 +23,22 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("case,world,steps,freq", [("rsw_fab3", 2, 6, 2), ("qg2_ifmrk4", 2, 6, 2),
-                                                   ("rsw_ifmab3", 4, 6, 2),
-                                                   # more records than one host-staged gather holds
-                                                   # before the chunked, incremental gather
-                                                   ("rsw_fab3", 2, 240, 1)])
-def test_one_process_per_slab(case, world, steps, freq, tmp_path):
+@pytest.mark.parametrize("case,world,steps,freq,aliased", [("rsw_fab3", 2, 6, 2, False), ("qg2_ifmrk4", 2, 6, 2, False),
+                                                           ("rsw_ifmab3", 4, 6, 2, False),
+                                                           # more records than one host-staged gather holds
+                                                           # before the chunked, incremental gather
+                                                           ("rsw_fab3", 2, 240, 1, False),
+                                                           # aliased_state on one slab per process: the aliased
+                                                           # columns' x-spectra all-gathered per calcN, the
+                                                           # full-array state/calcN/energies gathered
+                                                           ("qg2_ifmrk4", 2, 6, 2, True), ("qg2_ifmab3", 4, 6, 2, True),
+                                                           ("rsw_fab3", 2, 6, 2, True)])
+def test_one_process_per_slab(case, world, steps, freq, aliased, tmp_path):
     out = tmp_path / "res.json"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
            os.path.join(HERE, "mp_slab_worker.py"), "--case", case, "--out", str(out),
-           "--steps", str(steps), "--freq", str(freq)]
+           "--steps", str(steps), "--freq", str(freq)] + (["--aliased"] if aliased else [])
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     res = json.loads(out.read_text())
@@ -41,6 +46,7 @@ def test_one_process_per_slab(case, world, steps, freq, tmp_path):
     assert res["state_equal"] and res["calcN_equal"] and res["physical_equal"], res
     assert res["ke_rel"] == 0 and res["pe_rel"] == 0, res
     assert res["records_equal"] and res["cfl_equal"], res
+    assert (res["aliased_max"] > 0) == aliased, res
 
 
 def test_bench_line_explains_the_exchange():
