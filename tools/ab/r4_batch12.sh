@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 4 GPU batch 12: pruned decimated row transforms on/off at 2048
-# (m11base / m11np, -DSW_ROW_PRUNE=0), then the N=2 bench line rehearsed on
+# (m11base / m11np, -DSW_ROW_PRUNE=0), the paired 2LQG col_inv at 2048
+# (m11pair, -DSW_QG_INV_PAIR=2), then the N=2 bench line rehearsed on
 # one GPU over gloo (host-staged slab transport).
 mkdir -p gpurun_out/ab
 run() {  # tag so model grid stepper steps warmup
@@ -14,6 +15,7 @@ for r in 1 2 3; do
   run p_np_m m11np rsw 2048 FilteredAB3 2000 200 || exit 1
   run p_base_q m11base qg2 2048 IFMAB3 2000 200 || exit 1
   run p_np_q m11np qg2 2048 IFMAB3 2000 200 || exit 1
+  run p_pair_q m11pair qg2 2048 IFMAB3 2000 200 || exit 1
 done
 SW_BENCH_BACKEND=gloo timeout -k 10 600 python bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu-baseline \
   > gpurun_out/bench_gloo2.json 2> gpurun_out/bench_gloo2.err || { echo "gloo2 failed"; tail -20 gpurun_out/bench_gloo2.err; exit 2; }
