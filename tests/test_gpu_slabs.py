@@ -127,3 +127,40 @@ def test_slab_config_errors():
         RSW.Problem("gpu", nx=64, decomposition=dict(nranks=4, local_slabs=4))
     with pytest.raises(LibSWError):  # RCCL slab without a unique id
         RSW.Problem("gpu", nx=128, decomposition=dict(nranks=2, rank=0, local_slabs=1))
+
+
+@pytest.mark.parametrize("overlap", [False, "chunks"])
+def test_slabs_bitwise_8192_rows_forward_tiles(overlap, monkeypatch):
+    """8192-point rows of the 2LQG family write their forward fields as 4×2
+    tiles (Geom::fa = 2, config 5's layout); on several slabs those tiles' lines
+    are in row order, so a chunk of rows stays one contiguous piece per peer
+    block and the forward transposes can follow the row pass chunk by chunk.
+    2LQG IFMRK4 on an 8192 × 512 grid over 2 slabs, sequential and pipelined in
+    4 row chunks: bitwise equal to one slab."""
+    from juliaraytracingsw_amd import two_layer_qg as QG2
+
+    p = sw_cases.case_params("qg2_ifmrk4", 64)
+
+    def make(dec=None):
+        return QG2.Problem("gpu", nx=8192, ny=512, dt=1e-3, nu=1e-30, nnu=4, U=p["U"], mu=p["mu"], f0=p["f0"],
+                           Cg=p["Cg"], drhorho0=p["drhorho0"], stepper="IFMRK4", T=np.float64,
+                           decomposition=dec)
+
+    a = make()
+    rng = np.random.default_rng(5)
+    shape = a.sol.shape
+    ic = 1e-3 * (rng.standard_normal(shape) + 1j * rng.standard_normal(shape))
+    a.sol = ic
+    monkeypatch.setenv("SW_OVERLAP", "0" if overlap is False else "1")
+    if overlap == "chunks":
+        monkeypatch.setenv("SW_ROW_CHUNKS", "4")
+    b = make(dict(nranks=2, local_slabs=2))
+    monkeypatch.delenv("SW_OVERLAP", raising=False)
+    monkeypatch.delenv("SW_ROW_CHUNKS", raising=False)
+    b.sol = ic
+    a.stepforward(2)
+    b.stepforward(2)
+    assert np.array_equal(a.sol, b.sol)
+    assert np.max(np.abs(a.sol)) > 0
+    a.close()
+    b.close()
