@@ -796,11 +796,6 @@ __host__ __device__ constexpr int roww() {
 // (sw_fft.hpp fftw_dit_split): bitwise-tested (GPU parity at 2048) but
 // measured slower — RSW row 73.7 -> 74.7, 2LQG row 74.3 -> 76.7 µs (the
 // radix-W combination done twice costs more VALU than the second exchange)
-// the full-length 2LQG row at 8192 points on the 16-wave decimated
-// transforms (experiment knob; the half-length row k_row_qg_h is the default)
-#ifndef SW_ROW16
-#define SW_ROW16 0
-#endif
 #ifndef SW_SPLIT_FOLD
 #define SW_SPLIT_FOLD 0
 #endif
@@ -1091,27 +1086,21 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
     // at 128); a 64-entry LDS table of the stage twiddles spilled 26 and read
     // 88-91 against 74.5-75 µs (round 3, interleaved A/B)
     constexpr bool FL = row_fly<MODEL, LOG2N>();
-    // 8192 points (SW_ROW16): the 16-wave decimated transforms of the
-    // column passes (sw_fft.hpp fft16_dif / fft16_dit: three barriers per
-    // transform, Stockham's ten)
-    constexpr bool W16 = LOG2N == 13 && SW_ROW16;
-    Twiddles<9, FL || W16> tq;
+    Twiddles<9, FL> tq;
     double2 wt = zero2();
-    if constexpr (W > 0 || W16) {
+    if constexpr (W > 0) {
       tq.load(c.t & 63, tw, LOG2N - 9);
-      if constexpr (!FL && !W16) wt = tw[c.t];
+      if constexpr (!FL) wt = tw[c.t];
     }
     auto wnt = [&]() { return FL ? tw[c.t] : wt; };
     using V1 = double2(&)[1][8];
     constexpr bool PR = PRUNE && W > 0 && !ALIAS;  // (ALIAS reads the slots kc <= k <= N/2)
     auto inv = [&](double2(&x)[8]) {
-      if constexpr (W16) fft16_dif<+1>(x, c.t, tq, tw, line);
-      else if constexpr (W > 0) fftw_dif<W, +1, 1, true, FL, false, PR>(reinterpret_cast<V1>(x), c.t, wnt(), tq, line, 0);
+      if constexpr (W > 0) fftw_dif<W, +1, 1, true, FL, false, PR>(reinterpret_cast<V1>(x), c.t, wnt(), tq, line, 0);
       else fft_line<LOG2N, +1>(x, c.t, tws, line);
     };
     auto fwd = [&](double2(&x)[8]) {
-      if constexpr (W16) fft16_dit<-1>(x, c.t, tq, tw, line);
-      else if constexpr (W > 0) fftw_dit<W, -1, 1, FL, false, false, PR>(reinterpret_cast<V1>(x), c.t, wnt(), tq, line, 0);
+      if constexpr (W > 0) fftw_dit<W, -1, 1, FL, false, false, PR>(reinterpret_cast<V1>(x), c.t, wnt(), tq, line, 0);
       else fft_line<LOG2N, -1>(x, c.t, tws, line);
     };
     double2 q[8];
