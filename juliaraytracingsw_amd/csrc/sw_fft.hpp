@@ -477,9 +477,13 @@ __device__ __forceinline__ void dft_w_zin(double2 (&a)[W]) {
 template <int W>
 __host__ __device__ constexpr bool tw_chain() { return W == 8; }
 
-// pw[c] = ω^(c t), c < W (pw[0] unused; tw_chain: pw[1] only)
+// pw[c] = ω^(c t), c < W (pw[0] unused; tw_chain: pw[1] only).  tw_chain:
+// ω^t made opaque per call, so that its powers (formed per transform) are not
+// hoisted out of the caller's loops and kept for the kernel's life (the 2LQG
+// half row at 8192 spilled 54 VGPRs on them)
 template <int W, int DIR>
 __device__ __forceinline__ void tw_powers(double2 wt, double2 (&pw)[W]) {
+  if constexpr (tw_chain<W>()) asm volatile("" : "+v"(wt.x), "+v"(wt.y));
   pw[0] = make_double2(1.0, 0.0);
   if constexpr (W > 1) pw[1] = DIR < 0 ? wt : cconj(wt);
   if constexpr (tw_chain<W>()) return;

@@ -785,9 +785,10 @@ __host__ __device__ constexpr int roww() {
 }
 // the half-length rows' M-point lines: the RSW row (k_row_rsw_h, 2 waves
 // per SIMD) at 4096² (M = 2048, W = 4: row 401-407 -> 398 µs, config 4 one
-// GPU 1274 -> 1286 steps/s); the 2LQG row (k_row_qg_h, 128 VGPRs) spills
+// GPU 1274 -> 1286 steps/s); the 2LQG row (k_row_qg_h, 128 VGPRs) spilled
 // with them (4096²: row 426 -> 525 µs; 8192², W = 8: 1823 -> 3150 µs, 54
-// spills) and keeps Stockham, as does the RSW row at 8192² (unmeasured).
+// spills: the hoisted twiddle powers, round 4: 8) and keeps Stockham, as does
+// the RSW row at 8192² (unmeasured).
 // SW_ROWH_W=1: every half row.
 #ifndef SW_ROWH_W
 #define SW_ROWH_W 0
@@ -806,9 +807,17 @@ __host__ __device__ constexpr int roww() {
 #ifndef SW_ROW_TW_SHARE
 #define SW_ROW_TW_SHARE 0
 #endif
+// the 2LQG half row on the decimated transforms from 2^(SW_ROWH_W_QG_MIN + 1)
+// -point rows: at 8192 the radix-8 decimation (W = 8) fits 128 VGPRs (8
+// spilled) once its twiddle powers are formed per call (sw_fft.hpp
+// tw_powers), but measured neutral (row 1601-1603 against 1601-1606 µs,
+// tools/ab/r4_batch14.sh): the Stockham form stays (13: off)
+#ifndef SW_ROWH_W_QG_MIN
+#define SW_ROWH_W_QG_MIN 13
+#endif
 template <int LM, bool RSW = false>
 __host__ __device__ constexpr int roww_h() {
-  return (SW_ROWH_W || (RSW && LM == 11)) ? roww<LM>() : 0;
+  return (SW_ROWH_W || (RSW && LM == 11) || (!RSW && LM >= SW_ROWH_W_QG_MIN)) ? roww<LM>() : 0;
 }
 template <int MODEL, int LOG2N>
 __host__ __device__ constexpr bool row_fly() {
