@@ -885,40 +885,47 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
       load_pair<LOG2N>(w[0], ri, g, U, V, false);
       fft_line<LOG2N, +1>(w[0], c.t, tws, line);
     }
-    double pc[8];
+    // The forward pairs hold lines of one magnitude class: a pair's split
+    // leaves each half an absolute error ~ eps × the pair's norm, and ζu
+    // (~ k u² at wavenumber k) beside uη, K beside ζv put the larger line's
+    // roundoff into the smaller.  ζu + i ζv and uη + i vη pair; K, the real
+    // line, goes alone last, and P = -ik K̂ + (ζv)^ takes (ζv)^ from the
+    // registers (white-noise state, tests/test_gpu_invariants.py: the
+    // ⟨u, N_u⟩, ⟨v, N_v⟩ budgets 9e-18 -> 4e-19).  The inverse pair η + iζ
+    // keeps that roundoff in η (its budget ~1e-13 there, 1e-19 on the oracle).
+    double kk[8];
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       const double u = w[0][s].x, vv = w[0][s].y, eta = w[1][s].x, zeta = w[1][s].y;
-      pc[s] = vv * eta;
-      w[0][s] = make_double2(0.5 * (u * u + vv * vv), zeta * vv);  // K + i ζv
-      w[1][s] = make_double2(zeta * u, u * eta);                   // ζu + i uη
+      kk[s] = 0.5 * (u * u + vv * vv);
+      w[0][s] = make_double2(zeta * u, zeta * vv);  // ζu + i ζv
+      w[1][s] = make_double2(u * eta, vv * eta);    // uη + i vη
     }
-    if constexpr (W == 0 || !SW_SPLIT_FOLD) {
-      if constexpr (W > 0) fftw_dit<W, -1, 2, false, false, SW_ROW_TW_SHARE, PRUNE>(w, c.t, wt, tq, line, LS);
-      else fft_pair<LOG2N, -1, CB>(w, c.t, tws, line, LS);
-    }
+    if constexpr (W > 0) fftw_dit<W, -1, 2, false, false, SW_ROW_TW_SHARE, PRUNE>(w, c.t, wt, tq, line, LS);
+    else fft_pair<LOG2N, -1, CB>(w, c.t, tws, line, LS);
+    double2 zv[8];  // (ζv)^ of the live slots
+#pragma unroll
+    for (int s = 0; s < 8; ++s) zv[s] = zero2();
     auto emit = [&](int cc, int k, int s, double2 a, double2 b) {
       const int o = ri.ofwd(g, s);
       if (cc == 0) {
-        Mo[o] = cadd(cmul_i(a, -(k * g.mk)), b);
-        Mo[MF + o] = a;
-      } else {
         Mo[2 * MF + o] = a;
-        Mo[3 * MF + o] = cmul_i(b, -(k * g.mk));
+        zv[s] = b;
+      } else {
+        Mo[3 * MF + o] = cmul_i(a, -(k * g.mk));
+        Mo[4 * MF + o] = b;
       }
     };
-    if constexpr (W > 0 && SW_SPLIT_FOLD) {
-      fftw_dit_split<W, 2>(w, c.t, g.kc, wt, tq, line, LS, emit);
-    } else if constexpr (CB == 2) {
+    if constexpr (CB == 2) {
       split_pairs<LOG2N, 2, PRUNE && (W > 0)>(w, c.t, g, line, LS, emit);
     } else {
       split_pairs<LOG2N, 1>(reinterpret_cast<const double2(&)[1][8]>(w[0]), c.t, g, line, LS, emit);
       split_pairs<LOG2N, 1>(reinterpret_cast<const double2(&)[1][8]>(w[1]), c.t, g, line, LS,
                             [&](int, int k, int s, double2 a, double2 b) { emit(1, k, s, a, b); });
     }
-    // vη (real input: the transform is the spectrum itself)
+    // K (real input: the transform is the spectrum itself)
 #pragma unroll
-    for (int s = 0; s < 8; ++s) v[s] = make_double2(pc[s], 0.0);
+    for (int s = 0; s < 8; ++s) v[s] = make_double2(kk[s], 0.0);
     lds_barrier();  // split_pairs' mirror reads are done
     if constexpr (W > 0)
       fftw_dit<W, -1, 1, false, false, SW_ROW_TW_SHARE, PRUNE>(reinterpret_cast<double2(&)[1][8]>(v), c.t, wt, tq,
@@ -927,7 +934,11 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       const int k = c.t + s * Bk::NT;
-      if (RowIdx<LOG2N>::fwd_any(g, s) && k < g.kc) Mo[4 * MF + ri.ofwd(g, s)] = v[s];
+      if (RowIdx<LOG2N>::fwd_any(g, s) && k < g.kc) {
+        const int o = ri.ofwd(g, s);
+        Mo[o] = cadd(cmul_i(v[s], -(k * g.mk)), zv[s]);
+        Mo[MF + o] = v[s];
+      }
     }
   } else if constexpr (MODEL == MODEL_RSWA) {
     // rsw/RotatingShallowWater.jl:140-230 as written (advective form, the

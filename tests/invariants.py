@@ -10,7 +10,11 @@ obeys the continuous identities exactly (up to roundoff):
 * RotatingShallowWater (rsw/RotatingShallowWater.jl:140-230, advective form)
   for a divergence-free velocity (u, v) = (-∂y ψ, ∂x ψ) and any η:
   ⟨u, N_u⟩ = 0 and ⟨v, N_v⟩ = 0 (each is ∫ (u²/2) ∇·u, resp. v²),
-  ⟨ζ, ∂x N_v - ∂y N_u⟩ = 0 and ⟨η, N_η⟩ = 0.
+  ⟨ζ, ∂x N_v - ∂y N_u⟩ = 0 and ⟨η, N_η⟩ = 0;
+* ThomasYamada (thomasyamada/ThomasYamada.jl:129-262; N holds the rotation
+  and pressure terms too), any state: the total energy
+  ½∫(|∇ψ_T|² + u_c² + v_c² + p_c²) is conserved by N,
+  -⟨ψ_T, N_ζ⟩ + ⟨u_c, N_u⟩ + ⟨v_c, N_v⟩ + ⟨p_c, N_p⟩ = 0 (ψ_T = -ζ_T/K²).
 
 These identities are independent of the oracle (and of the reference): they
 pin the nonlinear transform chain against the equations themselves, at any
@@ -60,3 +64,10 @@ def qg2_residuals(grid, q, psi, N):
         out[f"enstrophy{j + 1}"] = rel(q[j], N[j])
         out[f"energy{j + 1}"] = rel(psi[j], N[j])
     return out
+
+
+def ty_residuals(grid, sol, N):
+    """the energy budget of N relative to the size of its terms"""
+    psi = -sol[0] * grid.invKrsq
+    t = [-inner(psi, N[0])] + [inner(sol[f], N[f]) for f in (1, 2, 3)]
+    return {"energy": abs(sum(t)) / sum(abs(x) for x in t)}

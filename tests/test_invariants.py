@@ -52,6 +52,19 @@ def test_oracle_qg2_invariants(n):
     assert min(I.qg2_residuals(grid, q, psi, bad).values()) > 1e-5
 
 
+@pytest.mark.parametrize("n", [64, 128])
+def test_oracle_ty_invariants(n):
+    p = sw_cases.case_params("ty_etdrk4", n)
+    grid = O.TwoDGrid(n, Lx=p["Lx"])
+    sol = I.random_real_spectrum(grid, 4, seed=13)
+    N = O.ty_calcN(sol.copy(), grid, O.TYParams(p["nu"], p["nnu"], p["Ro"]))
+    r = I.ty_residuals(grid, sol, N)
+    assert r["energy"] < TOL, r
+    bad = N.copy()
+    bad[3] *= 1.001  # 0.1 % on the pressure tendency
+    assert I.ty_residuals(grid, sol, bad)["energy"] > 1e-8
+
+
 def test_divergence_free_state():
     grid = O.TwoDGrid(64)
     s = I.rsw_state(grid, seed=3)
