@@ -9,6 +9,9 @@ forward) on the full arrays, one slab and several.
 * TwoLayerQG (swqg/TwoLayerQG.jl:152-182) at 2048² (config 3) and 8192²
   (config 5): ⟨q_j, N_j⟩ = ⟨ψ_j, N_j⟩ = 0 per layer, for white-noise q and
   for the stepped state of the parity case;
+* MultiLayerQG (GeophysicalFlows calcN_advection!, two layers) with
+  U = β = μ = 0 and the 2/3 rule at 512² (TwoLayerSimulation's grid) and
+  2048²: the TwoLayerQG identities per layer;
 * ThomasYamada (thomasyamada/ThomasYamada.jl:129-262) at 512² (its
   production size, thomasyamada/cpu-setup/Parameters.jl) and 2048²: the
   total-energy budget of N.
@@ -109,3 +112,17 @@ def test_ty_invariants(n, slabs):
     r = I.ty_residuals(grid, sol, N)
     print(f"ty {n}² slabs={slabs}: {r}")
     assert r["energy"] < TOL_TY, r
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("n,slabs", [(512, 1), (2048, 1), (2048, 2)])
+def test_mlqg_invariants(n, slabs):
+    p = dict(sw_cases.case_params("mlqg_frk4", n), U=[0.0, 0.0], beta=0.0, mu=0.0, af=1 / 3)
+    grid = O.TwoDGrid(n)
+    params = O.MLQGParams(p["f0"], p["H"], p["b"], p["U"], p["mu"], p["beta"], p["nu"], p["nnu"])
+    q = I.random_real_spectrum(grid, 2, seed=n + 4)
+    kw = dict(decomposition=dict(nranks=slabs, local_slabs=slabs)) if slabs > 1 else {}
+    N = _calcN(p, q, **kw)
+    r = I.qg2_residuals(grid, q, O.mlqg_streamfunction(q, grid, params), N)
+    print(f"mlqg {n}² slabs={slabs}: {r}")
+    assert max(r.values()) < TOL, r

@@ -65,6 +65,19 @@ def test_oracle_ty_invariants(n):
     assert I.ty_residuals(grid, sol, bad)["energy"] > 1e-8
 
 
+@pytest.mark.parametrize("n", [64, 128])
+def test_oracle_mlqg_invariants(n):
+    """MultiLayerQG with U = β = μ = 0 (no background PV gradient, no drag)
+    and the 2/3 rule: N_j = -J(ψ_j, q_j) per layer, as TwoLayerQG's."""
+    p = sw_cases.case_params("mlqg_frk4", n)
+    grid = O.TwoDGrid(n)
+    params = O.MLQGParams(p["f0"], p["H"], p["b"], [0.0, 0.0], 0.0, 0.0, p["nu"], p["nnu"])
+    q = I.random_real_spectrum(grid, 2, seed=14)
+    N = O.mlqg_calcN(q.copy(), grid, params)
+    r = I.qg2_residuals(grid, q, O.mlqg_streamfunction(q, grid, params), N)
+    assert max(r.values()) < TOL, r
+
+
 def test_divergence_free_state():
     grid = O.TwoDGrid(64)
     s = I.rsw_state(grid, seed=3)
