@@ -24,8 +24,10 @@ Extra keys on the same JSON line (never `value`):
   `ensemble` — the ensemble throughput of the same configuration on the N GPUs;
   `config5` — BASELINE config 5 (TwoLayerQG 8192² IFMRK4) decomposed over the
       N GPUs (one GPU at N = 1), steps/s (--no-config5 to skip);
-  `config4` — BASELINE config 4 (RSW 4096² FilteredAB3) decomposed over the N
-      GPUs (one GPU at N = 1), steps/s (--no-config4 to skip);
+  `config4` — BASELINE config 4 (RSW 4096² FilteredAB3) decomposed over
+      min(N, 4) GPUs, as BASELINE names it ("across 4 MI355X"; one GPU at
+      N = 1; at N = 8 ranks 4-7 only join the barriers), steps/s
+      (--no-config4 to skip);
   `host_boundary` — one state download/upload through the C ABI over PCIe,
       and the rate with the driver's per-frame download;
   `comm` (N > 1, slab) — the exchange explained (sw_comm_profile): transport,
@@ -38,9 +40,18 @@ Extra keys on the same JSON line (never `value`):
       (`kernels`, `roofline.achieved`) is the step as it runs, where a kernel
       reads part of what the previous one wrote from the Infinity Cache
       (--no-cold-profile to skip);
+  `box` — the GPU box's state (tools/box_state.py, amdsmi in-process):
+      product, serial, partition mode, power cap, clock ranges, and over each
+      timed region the sampled gfx / memory clocks, socket power, hotspot and
+      HBM temperatures, the energy-counter average power and the fraction of
+      the region spent power- or thermally-limited — per rank at N > 1 —
+      so a box-to-box swing can be attributed from the line itself;
+  `roofline.traffic` — PMC bytes per launch of the dominant kernel from the
+      newest round's profiles/rNN/traffic_<config>.json (`traffic_source`);
   `cpu_baseline` — rank 0 at N = 1 only.
 """
 import argparse
+import glob
 import json
 import math
 import os
@@ -53,6 +64,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+CONFIG4_MAX_RANKS = 4  # BASELINE config 4: "RSW 4096² slab-decomposed across 4 MI355X"
 SHORT = {'FilteredAB3': 'fab3', 'IFMAB3': 'ifmab3', 'IFMRK4': 'ifmrk4', 'ETDRK4': 'etdrk4',
          'FilteredRK4': 'frk4'}
 
@@ -148,6 +160,17 @@ def cpu_baseline(model, stepper, n, grids=(128, 1024, 2048), samples=5, warm_ste
                        f"or >= {sample_s:g} s each (BASELINE.md §3); value = the {n}² median")
 
 
+def latest_traffic_file(model, n, stepper):
+    """The newest round's PMC traffic file of this configuration
+    (profiles/rNN/traffic_<model><n>_<stepper>.json, tools/profile_round.sh)."""
+    def rnd(path):
+        d = os.path.basename(os.path.dirname(path))
+        return int(d[1:]) if d[1:].isdigit() else -1
+
+    c = glob.glob(os.path.join(ROOT, "profiles", "r*", f"traffic_{model}{n}_{stepper}.json"))
+    return max(c, key=rnd) if c else None
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -200,7 +223,10 @@ def main():
     ap.add_argument("--no-config4", action="store_true")
     ap.add_argument("--config4-steps", type=int, default=100)
     ap.add_argument("--mode", default="slab", choices=["ensemble", "slab"])
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_rsw2048_fab3.json"))
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC traffic file for roofline.traffic (default: the newest profiles/rNN/ file of the "
+                         "configuration)")
+    ap.add_argument("--no-box-state", action="store_true", help="skip the amdsmi box-state record")
     ap.add_argument("--nutune", type=float, default=None,
                     help="RSW: override RSWParameters' νtune (FilteredAB3 below 2048² is linearly unstable at the "
                          "driver's νtune = 20, DESIGN §4; the kernels' work does not depend on it)")
@@ -232,7 +258,8 @@ def main():
     if args.dry_run:
         if rank == 0:
             emit({"n_gpus": world, "parallelism": parallelism,
-                  "scaling": ("strong" if slab else "weak") if world > 1 else None, "rank0_of": world})
+                  "scaling": ("strong" if slab else "weak") if world > 1 else None, "rank0_of": world,
+                  "config5_ranks": world, "config4_ranks": min(world, CONFIG4_MAX_RANKS)})
         return
 
     import torch
@@ -269,14 +296,31 @@ def main():
 
     from juliaraytracingsw_amd import slab_comm
 
+    monitor = None
+    box_regions = {}
+    if not args.no_box_state:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        try:
+            import box_state
+
+            monitor = box_state.BoxMonitor(local)
+        except Exception as exc:  # noqa: BLE001 - the measurement never depends on it
+            print(f"[bench] box state unavailable: {exc}", file=sys.stderr)
+    box_static = monitor.static() if monitor is not None else None
+
     def comm_report(prob, nsteps=10):
-        """sw_comm_profile on every rank (collective), gathered to every rank"""
+        """sw_comm_profile on every rank of the problem (collective), gathered
+        to every rank; prob None on a rank outside the problem"""
         if world == 1:
             return None
-        st = prob.ctx.comm_profile(nsteps)
+        st = prob.ctx.comm_profile(nsteps) if prob is not None else None
         per = [None] * world
-        dist.all_gather_object(per, dict(rank=rank, exposed_transpose_us_per_step=st["exposed_transpose_us"],
-                                         step_us=st["step_us"], sent_MB_per_step=st["sent_bytes_per_step"] / 1e6))
+        dist.all_gather_object(per, None if st is None else dict(
+            rank=rank, exposed_transpose_us_per_step=st["exposed_transpose_us"], step_us=st["step_us"],
+            sent_MB_per_step=st["sent_bytes_per_step"] / 1e6))
+        per = [r for r in per if r is not None]
+        if st is None:
+            return None
         ex = max(r["exposed_transpose_us_per_step"] for r in per)
         return {"transport": st["transport"], "rccl_ranks": st["rccl_ranks"], "nranks": st["nranks"],
                 "schedule": st["schedule"], "row_chunks": st["row_chunks"], "profiled_steps": nsteps,
@@ -293,6 +337,8 @@ def main():
     extra_warmup = {}
 
     def timed(prob, warmup, steps, tag="headline"):
+        """max-over-ranks seconds of `steps` steps; prob None: a rank that
+        only joins the barriers (config 4 on 4 of 8 GPUs)"""
         # W warm-up steps, then — if they took less than --min-warmup-s of
         # stepping — more untimed steps until they have: the GPU's clocks and
         # caches reach their steady state only after tens of ms of load (K =
@@ -300,20 +346,28 @@ def main():
         # number (the slab transposes are collective); the count is reported.
         barrier_sync()
         t0 = time.perf_counter()
-        prob.stepforward(warmup)
+        if prob is not None:
+            prob.stepforward(warmup)
         barrier_sync()
         dt = max_over_ranks(time.perf_counter() - t0)
         extra = 0
         if args.min_warmup_s > 0 and dt < args.min_warmup_s:
             per = dt / warmup if warmup > 0 else 1e-3
             extra = int(min(100000, math.ceil((args.min_warmup_s - dt) / max(per, 1e-6))))
-            prob.stepforward(extra)
+            if prob is not None:
+                prob.stepforward(extra)
         extra_warmup[tag] = extra
         barrier_sync()
+        if monitor is not None:
+            monitor.start()
         t0 = time.perf_counter()
-        prob.stepforward(steps)  # sw_step returns when its stream is drained
+        if prob is not None:
+            prob.stepforward(steps)  # sw_step returns when its stream is drained
         barrier_sync()
-        return max_over_ranks(time.perf_counter() - t0)
+        el = time.perf_counter() - t0
+        if monitor is not None:
+            box_regions[tag] = monitor.stop()
+        return max_over_ranks(el)
 
     over = {k: v for k, v in (("nutune", args.nutune), ("cfltune", args.cfltune)) if v is not None}
     if args.model == "ty":
@@ -414,16 +468,33 @@ def main():
     # extras: BASELINE configs 5 (TwoLayerQG 8192² IFMRK4) and 4 (RSW 4096²
     # FilteredAB3), each one problem slab-decomposed over the N GPUs (one GPU
     # at N = 1)
-    def extra_config(model, n, stepper, steps, warmup, label):
-        ex, _ = make_problem(model, n, stepper, local, decomposition())
+    def extra_config(model, n, stepper, steps, warmup, label, max_ranks=None):
+        """one problem slab-decomposed over min(world, max_ranks) GPUs (ranks
+        [0, used)); the other ranks only join the barriers"""
+        used = world if max_ranks is None else min(world, max_ranks)
+        active = rank < used
+        dec = None
+        if world > 1:
+            if backend == "gloo":
+                # the host-staged all-to-all runs over a group of the used ranks
+                # (new_group is collective on every rank)
+                grp = dist.new_group(ranks=list(range(used))) if used < world else None
+                dec = slab_comm.host_decomposition(rank, used, grp) if active and used > 1 else None
+            else:
+                dec = slab_comm.rccl_decomposition(rank, world, used)
+                if used == 1:
+                    dec = None
+        ex = make_problem(model, n, stepper, local, dec)[0] if active else None
         te = timed(ex, warmup, steps, label)
-        cx = comm_report(ex, 3)
-        sx = ex.ctx.profile(3)
-        ex.close()
+        cx = comm_report(ex, 3) if used > 1 else None
+        sx = ex.ctx.profile(3) if active else []
+        if ex is not None:
+            ex.close()
         del ex
-        return {"value": steps / te, "unit": "timesteps/s", "n_gpus": world, "steps": steps,
-                "ms_per_step": te / steps * 1e3, "scaling": "strong" if world > 1 else None,
-                "workload": f"{label} fp64, " + (f"slab{world}" if world > 1 else "single-gpu"),
+        return {"value": steps / te, "unit": "timesteps/s", "n_gpus": used, "steps": steps,
+                "ms_per_step": te / steps * 1e3, "scaling": "strong" if used > 1 else None,
+                "ranks_idle": world - used,
+                "workload": f"{label} fp64, " + (f"slab{used}" if used > 1 else "single-gpu"),
                 "kernels": [{"name": s["name"], "avg_us": s["avg_ms"] * 1e3, "per_step": s["launches"] / 3}
                             for s in sx], "comm": cx}
 
@@ -434,7 +505,17 @@ def main():
                                "TwoLayerQG 8192^2 IFMRK4 (BASELINE config 5)")
     if not args.no_config4 and not slab_error and headline_cfg:
         config4 = extra_config("rsw", 4096, "FilteredAB3", args.config4_steps, 20,
-                               "RSW 4096^2 FilteredAB3 (BASELINE config 4)")
+                               "RSW 4096^2 FilteredAB3 (BASELINE config 4)", CONFIG4_MAX_RANKS)
+
+    box = None
+    if monitor is not None:
+        mine = {"rank": rank, "static": box_static, "regions": box_regions}
+        if dist is not None:
+            per = [None] * world
+            dist.all_gather_object(per, mine)
+        else:
+            per = [mine]
+        box = {"source": "amdsmi in-process (tools/box_state.py)", "per_rank": per}
 
     if rank != 0:
         if dist is not None:
@@ -447,12 +528,15 @@ def main():
     dom_cold = next((s for s in stats_cold or [] if s["name"] == dom["name"]), None)
     achieved_cold = dom_cold["alg_bytes"] / (dom_cold["avg_ms"] * 1e-3) / 1e9 if dom_cold else None
     traffic = None
+    traffic_src = args.traffic_json or latest_traffic_file(args.model, args.n, args.stepper)
     try:
-        tj = json.load(open(args.traffic_json))
+        tj = json.load(open(traffic_src))
         if tj.get("config") == f"{args.model}{args.n}_{args.stepper}" and world == 1:
             traffic = tj["kernels"].get(dom["name"])
     except Exception:
         traffic = None
+    if traffic is None:
+        traffic_src = None
     for s in stats:
         gbps = s["alg_bytes"] / (s["avg_ms"] * 1e-3) / 1e9
         print(f"[bench] {s['name']:>10s}: {s['avg_ms'] * 1e3:8.1f} us/launch  x{s['launches'] / args.profile_steps:.0f}/step"
@@ -505,6 +589,7 @@ def main():
         "reference_byte_model": {"bytes_per_step": balg, "equivalent_GBps_per_gpu": balg * per_gpu_rate / 1e9},
         "roofline": {"bound": "hbm", "kernel": dom["name"], "achieved": achieved, "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                     "traffic_source": None if traffic_src is None else os.path.relpath(traffic_src, ROOT),
                      "alg_bytes_per_launch": dom["alg_bytes"], "avg_us_per_launch": dom["avg_ms"] * 1e3,
                      # in the step some of its input comes from the Infinity
                      # Cache; with L2 and that cache evicted before the launch
@@ -522,6 +607,7 @@ def main():
         "config5": config5,
         "config4": config4,
         "cpu_baseline": cpu,
+        "box": box,
         # RSWDriver saves a frame every output_freq = floor(output_dt/dt) steps
         # (rsw/RSWDriver.jl:152, output_dt = 0.025/f): 81 steps at 2048²
         "host_boundary": {"state_bytes": int(st.nbytes), "get_state_ms": min(tg) * 1e3,

@@ -23,8 +23,11 @@
 #     utils/IFMAB3.jl:157 defines for its own stepper) only counts the step;
 #     the counted steps run on the device in one `sw_step` when the host next
 #     needs the state — an energy Diagnostic's value at FF's `increment!`
-#     (`sw_step_record`), `updatevars!`, `set_solution!` — and prob.sol is
-#     downloaded only there, never per step.
+#     (`sw_step_record`), `updatevars!`, `set_solution!`, or the first read
+#     of a physical field of `prob.vars` (`SWField`: the drivers' NaN scan
+#     right after the block, rsw/RSWDriver.jl:213, swqg/TwoLayerDriver.jl:106,
+#     so a blow-up throws on the frame it happened in) — and prob.sol is
+#     downloaded only at updatevars!/set_solution!, never per step.
 #   * `set_solution!` / `set_q!`, `updatevars!`, `enforce_reality_condition!`
 #     and the energy functions the Diagnostics call, of a libsw problem, go
 #     through the C ABI; for any other problem the reference's own method runs
@@ -83,6 +86,64 @@ end
 # struct sw_energy_record
 struct SWEnergyRecord
     step::Int64; t::Float64; ke::Float64; ke2::Float64; pe::Float64; wg::NTuple{4,Float64}
+end
+
+# ------------------------------------------------ physical fields of prob.vars
+# The reference's calcN! writes vars' physical fields at every step
+# (rsw/RotatingShallowWater.jl:147-149: u, v, η of the calcN input), and the
+# drivers scan one of them for NaN right after stepforward!(prob, diags, n)
+# (rsw/RSWDriver.jl:213 vars.η, swqg/TwoLayerDriver.jl:106 vars.q).  Here the
+# steps of that block may still be counted only (the per-step seam below).
+# So the physical fields of a libsw problem's vars are SWFields: host Arrays
+# whose first read runs the counted steps (flush!: one sw_step, no state
+# download) and, after SW_E_NAN, holds NaN (blowup!) — the driver's scan then
+# throws on the frame where the state went non-finite, and no NaN snapshot
+# is written.  Between updatevars! calls they hold the last updatevars!'s
+# fields (the reference's: the last calcN input), which no driver reads.
+mutable struct Owner
+    prob::Any          # the Problem these fields belong to (set once it is built)
+end
+
+struct SWField{T,N} <: AbstractArray{T,N}
+    data::Array{T,N}
+    owner::Owner
+end
+
+# run the problem's counted steps, if any, before the field is read
+function settle!(a::SWField)
+    prob = a.owner.prob
+    prob === nothing || prob.timestepper.pending == 0 || flush!(prob)
+    return a
+end
+Base.parent(a::SWField) = a.data
+Base.size(a::SWField) = size(a.data)
+Base.IndexStyle(::Type{<:SWField}) = IndexLinear()
+Base.@propagate_inbounds Base.getindex(a::SWField, i::Int) = (settle!(a); a.data[i])
+Base.@propagate_inbounds Base.setindex!(a::SWField, x, i::Int) = (a.data[i] = x; a)
+Base.similar(a::SWField, ::Type{S}, dims::Dims) where {S} = similar(a.data, S, dims)
+Base.fill!(a::SWField, x) = (fill!(a.data, x); a)
+# isnan.(vars.η), abs.(vars.u), @views … read the settled host array
+Base.Broadcast.broadcastable(a::SWField) = parent(settle!(a))
+# deepcopy(vars.u) before FFTW's mul! (rsw/RotatingShallowWater.jl:128-130,
+# swqg/TwoLayerQG.jl:147-148): a plain Array, which FFTW's plans accept
+Base.deepcopy_internal(a::SWField, d::IdDict) = Base.deepcopy_internal(parent(settle!(a)), d)
+host(a::SWField) = parent(a)
+host(a::Array) = a
+
+# the model's own Vars (rsw/RotatingShallowWater.jl:25-34, swqg/TwoLayerQG.jl:32-43,
+# thomasyamada/ThomasYamada.jl:26-43: Vars{Aphys, Atrans}) with every physical
+# (real) field an SWField of the same host array
+function device_vars(vars, owner::Owner)
+    V = typeof(vars).name.wrapper
+    wrap(x) = x isa Array && eltype(x) <: Real ? SWField(x, owner) : x
+    return V((wrap(getfield(vars, k)) for k in fieldnames(typeof(vars)))...)
+end
+
+# FourierFlows.Problem with the vars' owner set
+function owned_problem(owner::Owner, sol, clock, equation, grid, vars, params, ts)
+    prob = FourierFlows.Problem(sol, clock, equation, grid, vars, params, ts)
+    owner.prob = prob
+    return prob
 end
 
 # ------------------------------------------------------------- the time stepper
@@ -201,20 +262,23 @@ function load_solution!(prob)
     return nothing
 end
 
-# one physical field (updatevars!) into a host array or a layer of one
+# one physical field (updatevars!) into a host array (or SWField) or a layer of one
 function physical!(dst::AbstractArray, ts::SWStepper, id::Integer)
+    a = host(dst)
     check(ts, ccall((:sw_get_physical, libsw), Cint, (Ptr{Cvoid}, Int32, Ptr{Cvoid}, Csize_t),
-                    ts.ctx, id, dst, sizeof(dst)), "sw_get_physical")
+                    ts.ctx, id, a, sizeof(a)), "sw_get_physical")
     return dst
 end
-physical!(dst::Array{T,3}, ts::SWStepper, id::Integer, layer::Integer) where {T} =
-    GC.@preserve dst begin
-        n = size(dst, 1) * size(dst, 2)
-        p = pointer(dst, (layer - 1) * n + 1)
+function physical!(dst::AbstractArray{T,3}, ts::SWStepper, id::Integer, layer::Integer) where {T}
+    a = host(dst)
+    GC.@preserve a begin
+        n = size(a, 1) * size(a, 2)
+        p = pointer(a, (layer - 1) * n + 1)
         check(ts, ccall((:sw_get_physical, libsw), Cint, (Ptr{Cvoid}, Int32, Ptr{Cvoid}, Csize_t),
                         ts.ctx, id, p, n * sizeof(T)), "sw_get_physical")
-        dst
     end
+    return dst
+end
 
 # ------------------------------------------------------- stepping and records
 # FF's per-step seam (the method utils/IFMAB3.jl:157 defines for its own
@@ -296,9 +360,8 @@ const RECORD = IdDict{Any,Function}()
 # After SW_E_NAN the drivers' own test finds the NaN and throws "Solution is
 # NaN" (rsw/RSWDriver.jl:213-218 tests vars.η, swqg/TwoLayerDriver.jl:106-111
 # vars.q: in the reference calcN! leaves them NaN); prob.sol holds the
-# non-finite state.  (The device runs the counted steps at the next energy
-# Diagnostic step or updatevars!, so a blow-up shows at the first of those
-# after it.)
+# non-finite state.  The test's read of vars.η / vars.q itself runs the
+# block's counted steps (SWField), so it sees the blow-up of that block.
 function blowup!(prob)
     for name in (:η, :q, :u, :v)
         hasproperty(prob.vars, name) && fill!(getproperty(prob.vars, name), NaN)
@@ -319,7 +382,8 @@ function rsw_problem(M::Module; nx=128, ny=nx, Lx=2π, Ly=Lx, ν=1.0e-16, nν=4,
         error("libsw: the stochastic forcing calcF! is not on the libsw path")
     grid = TwoDGrid(CPU(); nx, Lx, ny, Ly, aliased_fraction, T)
     params = M.Params{T}(ν, nν, f, Cg^2)
-    vars = M.Vars(grid)
+    owner = Owner(nothing)
+    vars = device_vars(M.Vars(grid), owner)
     equation = M.Equation(params, grid)         # host L (populate_L!, CPU method :262-274)
     cfg = config(SW_MODEL_RSW, stepper; nx, ny, Lx, Ly, aliased_fraction, dt, T)
     cfg.f, cfg.Cg, cfg.nu, cfg.nnu = params.f, Cg, params.ν, nν   # libsw squares Cg as :88 does
@@ -329,7 +393,7 @@ function rsw_problem(M::Module; nx=128, ny=nx, Lx=2π, Ly=Lx, ν=1.0e-16, nν=4,
     ts = SWStepper(cfg, equation, stepper_filter(equation, filters, fkw))
     clock = FourierFlows.Clock{T}(dt, 0, 0)
     sol = zeros(CPU(), equation.T, equation.dims)
-    return FourierFlows.Problem(sol, clock, equation, grid, vars, params, ts)
+    return owned_problem(owner, sol, clock, equation, grid, vars, params, ts)
 end
 
 # swqg/TwoLayerQG.jl:55-90
@@ -339,7 +403,8 @@ function qg2_problem(M::Module; nx=128, ny=nx, Lx=2π, Ly=Lx, U=0.5, μ=1e-2, ν
     grid = TwoDGrid(CPU(); nx, Lx, ny, Ly, aliased_fraction, T)
     plan = FourierFlows.plan_flows_rfft(Array{T,3}(undef, grid.nx, grid.ny, 2), [1, 2])
     params = M.Params(T(U), T(μ), T(ν), nν, T(2 * f0^2 / Cg^2 / δρρ0), plan)
-    vars = M.Vars(grid)
+    owner = Owner(nothing)
+    vars = device_vars(M.Vars(grid), owner)
     equation = M.Equation(params, grid)         # host L (KernelAbstractions CPU backend)
     cfg = config(SW_MODEL_QG2, stepper; nx, ny, Lx, Ly, aliased_fraction, dt, T)
     # libsw rounds F, U, μ exactly as params holds them (T), and reproduces the
@@ -350,7 +415,7 @@ function qg2_problem(M::Module; nx=128, ny=nx, Lx=2π, Ly=Lx, U=0.5, μ=1e-2, ν
     ts = SWStepper(cfg, equation, stepper_filter(equation, filters, fkw))
     clock = FourierFlows.Clock{T}(dt, 0, 0)
     sol = zeros(CPU(), equation.T, equation.dims)
-    return FourierFlows.Problem(sol, clock, equation, grid, vars, params, ts)
+    return owned_problem(owner, sol, clock, equation, grid, vars, params, ts)
 end
 
 # thomasyamada/ThomasYamada.jl:55-74 (FF's ETDRK4 by default, :63)
@@ -359,14 +424,15 @@ function ty_problem(M::Module; nx=128, ny=nx, Lx=2π, Ly=Lx, ν=3.5e-25, nν=8, 
     stepper == "ETDRK4" || error("libsw: ThomasYamada steps with ETDRK4 (its diagonal L)")
     grid = TwoDGrid(CPU(); nx, Lx, ny, Ly, aliased_fraction, T)
     params = M.Params{T}(ν, nν, Ro)
-    vars = M.Vars(grid)
+    owner = Owner(nothing)
+    vars = device_vars(M.Vars(grid), owner)
     equation = M.Equation(params, grid)
     cfg = config(SW_MODEL_TY, stepper; nx, ny, Lx, Ly, aliased_fraction, dt, T)
     cfg.nu, cfg.nnu, cfg.Ro = params.ν, nν, params.Ro
     ts = SWStepper(cfg, equation, stepper_filter(equation, false, (;)))
     clock = FourierFlows.Clock{T}(dt, 0, 0)
     sol = zeros(CPU(), equation.T, equation.dims)
-    return FourierFlows.Problem(sol, clock, equation, grid, vars, params, ts)
+    return owned_problem(owner, sol, clock, equation, grid, vars, params, ts)
 end
 
 # GeophysicalFlows MultiLayerQG.Problem(nlayers, dev; nx, Lx, f₀, H, b, U, μ, β,
@@ -399,6 +465,7 @@ function rsw_updatevars!(prob)
     vars, grid, sol, ts = prob.vars, prob.grid, prob.sol, prob.timestepper
     sync!(prob)
     FourierFlows.dealias!(sol, grid)   # :104 (the device's copy is dealiased by sw_get_physical)
+    ts.rec_step = -1                   # energies read the updated vars.uh … from here (sw_diag)
     @. vars.uh = @view sol[:, :, 1]
     @. vars.vh = @view sol[:, :, 2]
     @. vars.ηh = @view sol[:, :, 3]
@@ -413,6 +480,7 @@ function qg2_updatevars!(M, prob)
     vars, grid, sol, params, ts = prob.vars, prob.grid, prob.sol, prob.params, prob.timestepper
     sync!(prob)
     FourierFlows.dealias!(sol, grid)   # :115 (the device's copy is dealiased by sw_get_physical)
+    ts.rec_step = -1
     @. vars.qh = sol
     M.streamfunctionfrompv!(vars.ψh, vars.qh, grid, params)
     @. vars.ζh = -grid.Krsq * vars.ψh
@@ -426,10 +494,13 @@ function qg2_updatevars!(M, prob)
 end
 
 # thomasyamada/ThomasYamada.jl:76-101 (all = true) and enforce_reality_condition!
-# :103-123 (all = false: its mul! into the copies sol[:,:,k] leave sol as it is)
+# :103-123 (all = false: its mul! into the copies sol[:,:,k] leave sol as it is);
+# both dealias sol in place first (:79, :106)
 function ty_updatevars!(prob; all=true)
     vars, grid, sol, ts = prob.vars, prob.grid, prob.sol, prob.timestepper
     sync!(prob)
+    FourierFlows.dealias!(sol, grid)   # :79 / :106 (the device's copy is dealiased by sw_get_physical)
+    ts.rec_step = -1
     @. vars.ζth = sol[:, :, 1]; @. vars.uch = sol[:, :, 2]
     @. vars.vch = sol[:, :, 3]; @. vars.pch = sol[:, :, 4]
     physical!(vars.ζt, ts, 3); physical!(vars.uc, ts, 0); physical!(vars.vc, ts, 1); physical!(vars.pc, ts, 2)
@@ -447,6 +518,7 @@ end
 function mlqg_updatevars!(M, prob)
     vars, grid, sol, params, ts = prob.vars, prob.grid, prob.sol, prob.params, prob.timestepper
     sync!(prob)
+    ts.rec_step = -1
     @. vars.qh = sol
     M.streamfunctionfrompv!(vars.ψh, vars.qh, params, grid)
     @. vars.uh = -im * grid.l * vars.ψh

@@ -18,14 +18,19 @@ import traceback
 from . import _lib
 
 
-def rccl_decomposition(rank: int, world: int) -> dict:
+def rccl_decomposition(rank: int, world: int, nranks: int | None = None) -> dict | None:
     """Problem(decomposition=...) kwargs for slab `rank` of `world`, one GPU
-    per process, RCCL transposes.  Collective: every rank must call it."""
+    per process, RCCL transposes.  Collective: every rank of the default
+    group must call it.  With `nranks` < world only ranks [0, nranks) form
+    the problem (BASELINE config 4 on 4 of 8 GPUs); the others get None."""
     import torch.distributed as dist
 
+    n = world if nranks is None else nranks
     box = [_lib.comm_unique_id() if rank == 0 else None]
     dist.broadcast_object_list(box, src=0)
-    return dict(nranks=world, rank=rank, local_slabs=1, comm_unique_id=box[0])
+    if rank >= n:
+        return None
+    return dict(nranks=n, rank=rank, local_slabs=1, comm_unique_id=box[0])
 
 
 def _as_tensor(addr: int, nbytes: int):

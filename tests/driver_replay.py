@@ -102,6 +102,27 @@ def is_sw(prob):
     return isinstance(prob.timestepper, SWStepper)
 
 
+class Owner:
+    """SWLib.Owner: the Problem a device_vars' SWFields belong to."""
+
+    def __init__(self, tw):
+        self.tw, self.prob = tw, None
+
+
+class DeviceVars(types.SimpleNamespace):
+    """SWLib.device_vars: the model's vars with every physical (real) field an
+    SWField — reading one first runs the problem's counted steps
+    (``settle!`` -> ``flush!``), as the drivers' NaN scan right after
+    stepforward!(prob, diags, n) does (rsw/RSWDriver.jl:213)."""
+
+    def __getattribute__(self, name):
+        d = object.__getattribute__(self, "__dict__")
+        if name in d.get("_phys", ()):
+            owner = d["_owner"]
+            owner.tw.settle(owner.prob)
+        return object.__getattribute__(self, name)
+
+
 def as_T(T, x):
     """SWLib.as_T: the energy in the Problem's real type (FF's Diagnostic
     holds what the reference's function returns for T)"""
@@ -188,6 +209,11 @@ class Twin:
         self.check(ts, self.c("sw_get_physical", ts.ctx, int(fid), dst.ctypes.data, dst.nbytes), "sw_get_physical")
         return dst
 
+    def settle(self, prob):
+        """SWLib.settle!(a::SWField): a physical field of prob.vars is read"""
+        if prob is not None and prob.timestepper.pending != 0:
+            self.flush(prob)
+
     # -- stepping and records --------------------------------------------------
     def stepforward_seam(self, sol, clock, ts, equation, vars_, params, grid):
         """FourierFlows.stepforward!(sol, clock, ts::SWStepper, …): counts the
@@ -260,16 +286,24 @@ class Twin:
         return lambda pr: self.device_energy(pr, pick) if is_sw(pr) else host_fn(pr)
 
 
-def _host_vars(grid, T, spec, phys, nlayers=None):
+def _host_vars(grid, T, spec, phys, nlayers=None, owner=None):
+    """the model's Vars(grid); with `owner`, SWLib.device_vars of it"""
     shape_p = (grid.ny, grid.nx) if nlayers is None else (nlayers, grid.ny, grid.nx)
     shape_s = (grid.nl, grid.nkr) if nlayers is None else (nlayers, grid.nl, grid.nkr)
     ct = np.complex64 if T == np.float32 else np.complex128
-    v = types.SimpleNamespace()
+    v = types.SimpleNamespace() if owner is None else DeviceVars(_phys=tuple(phys), _owner=owner)
     for n in phys:
         setattr(v, n, np.zeros(shape_p, T))
     for n in spec:
         setattr(v, n, np.zeros(shape_s, ct))
     return v
+
+
+def owned_problem(owner, sol, clock, eq, grid, vars_, params, ts):
+    """SWLib.owned_problem: FourierFlows.Problem with the vars' owner set"""
+    prob = Problem(sol, clock, eq, grid, vars_, params, ts)
+    owner.prob = prob
+    return prob
 
 
 def _filter(grid, nf, filters, T, **fkw):
@@ -285,7 +319,8 @@ def rsw_problem(tw, *, nx=128, ny=None, Lx=2 * np.pi, Ly=None, nu=1.0e-16, nnu=4
     Ly = Lx if Ly is None else Ly
     grid = O.TwoDGrid(nx, Lx, ny=ny, Ly=Ly, aliased_fraction=aliased_fraction)
     params = types.SimpleNamespace(ν=T(nu), nν=nnu, f=T(f), Cg2=T(Cg ** 2))
-    vars_ = _host_vars(grid, T, ("uh", "vh", "ηh", "ζh"), ("u", "v", "η", "ζ"))
+    owner = Owner(tw)
+    vars_ = _host_vars(grid, T, ("uh", "vh", "ηh", "ζh"), ("u", "v", "η", "ζ"), owner=owner)
     eq = Equation(T, (3, grid.nl, grid.nkr))
     cfg = tw.config(_lib.SW_MODEL_RSW, stepper, nx=nx, ny=ny, Lx=Lx, Ly=Ly, aliased_fraction=aliased_fraction,
                     dt=dt, T=T)
@@ -293,7 +328,7 @@ def rsw_problem(tw, *, nx=128, ny=None, Lx=2 * np.pi, Ly=None, nu=1.0e-16, nnu=4
     filters = stepper in ("FilteredAB3", "FilteredRK4") or use_filter
     fkw = tw.set_filter(cfg, use_filter, **skw)
     ts = tw.SWStepper(cfg, eq, _filter(grid, 3, filters, T, **fkw))
-    return Problem(np.zeros(eq.dims, eq.T), Clock(T, dt), eq, grid, vars_, params, ts)
+    return owned_problem(owner, np.zeros(eq.dims, eq.T), Clock(T, dt), eq, grid, vars_, params, ts)
 
 
 def ty_problem(tw, *, nx=128, ny=None, Lx=2 * np.pi, Ly=None, nu=3.5e-25, nnu=8, Ro=0.2, stepper="ETDRK4",
@@ -303,14 +338,15 @@ def ty_problem(tw, *, nx=128, ny=None, Lx=2 * np.pi, Ly=None, nu=3.5e-25, nnu=8,
     Ly = Lx if Ly is None else Ly
     grid = O.TwoDGrid(nx, Lx, ny=ny, Ly=Ly, aliased_fraction=aliased_fraction)
     params = types.SimpleNamespace(ν=T(nu), nν=nnu, Ro=T(Ro))
+    owner = Owner(tw)
     vars_ = _host_vars(grid, T, ("uch", "vch", "uth", "vth", "ζth", "ψth", "pch", "qch"),
-                       ("uc", "vc", "ut", "vt", "ζt", "ψt", "pc", "qc"))
+                       ("uc", "vc", "ut", "vt", "ζt", "ψt", "pc", "qc"), owner=owner)
     eq = Equation(T, (4, grid.nl, grid.nkr))
     cfg = tw.config(_lib.SW_MODEL_TY, stepper, nx=nx, ny=ny, Lx=Lx, Ly=Ly, aliased_fraction=aliased_fraction,
                     dt=dt, T=T)
     cfg.nu, cfg.nnu, cfg.Ro = float(params.ν), nnu, float(params.Ro)
     ts = tw.SWStepper(cfg, eq, _filter(grid, 4, False, T))
-    return Problem(np.zeros(eq.dims, eq.T), Clock(T, dt), eq, grid, vars_, params, ts)
+    return owned_problem(owner, np.zeros(eq.dims, eq.T), Clock(T, dt), eq, grid, vars_, params, ts)
 
 
 def mlqg_problem(tw, nlayers, *, nx, Lx, f0, H, b, U, mu, beta, dt, stepper="FilteredRK4", aliased_fraction=1 / 3,
@@ -339,6 +375,7 @@ def rsw_updatevars(tw, prob):
     v, g, sol, ts = prob.vars, prob.grid, prob.sol, prob.timestepper
     tw.sync(prob)
     g.dealias(sol)  # :104
+    ts.rec_step = -1
     v.uh[...], v.vh[...], v.ηh[...] = sol[0], sol[1], sol[2]
     v.ζh[...] = 1j * g.kr[None, :] * v.vh - 1j * g.l[:, None] * v.uh - prob.params.f * v.ηh
     tw.physical(v.u, ts, 0)
@@ -350,6 +387,8 @@ def rsw_updatevars(tw, prob):
 def ty_updatevars(tw, prob, all_=True):
     v, g, sol, ts = prob.vars, prob.grid, prob.sol, prob.timestepper
     tw.sync(prob)
+    g.dealias(sol)  # thomasyamada/ThomasYamada.jl:79 / :106
+    ts.rec_step = -1
     v.ζth[...], v.uch[...], v.vch[...], v.pch[...] = sol[0], sol[1], sol[2], sol[3]
     tw.physical(v.ζt, ts, 3)
     tw.physical(v.uc, ts, 0)
@@ -370,6 +409,7 @@ def ty_updatevars(tw, prob, all_=True):
 def mlqg_updatevars(tw, prob):
     v, g, sol, p, ts = prob.vars, prob.grid, prob.sol, prob.params, prob.timestepper
     tw.sync(prob)
+    ts.rec_step = -1
     v.qh[...] = sol
     v.ψh[...] = O.mlqg_streamfunction(v.qh.astype(np.complex128), g, p)
     v.uh[...] = -1j * g.l[:, None] * v.ψh
@@ -400,12 +440,23 @@ def mlqg_set_q(tw, prob, q):
 
 
 # ------------------------------------------------------ the drivers' start!
+class BlewUp(RuntimeError):
+    """rsw/RSWDriver.jl:213-218: println("Blew up at step ", clock.step);
+    throw("Solution is NaN") — with what the driver had written by then"""
+
+    def __init__(self, step, outputs, diags, prob, ic):
+        super().__init__(f"Solution is NaN (blew up at step {step})")
+        self.step, self.outputs, self.diags, self.prob, self.ic = step, outputs, diags, prob, ic
+
+
 def rsw_driver_start(tw, nx=128, nsteps=240, output_freq=20, diags_freq=10, spinup_step=120, seed=20261015,
-                     T=np.float32):
+                     T=np.float32, parameters=None):
     """rsw/RSWDriver.jl:134-226 with RSWParameters.jl values, dev = GPU(),
-    T = Float32; nsteps / output_freq / diags_freq at test size."""
+    T = Float32; nsteps / output_freq / diags_freq at test size;
+    `parameters` overrides RSWParameters.jl entries (a user's edit of it)."""
     P = dict(L=2 * np.pi, f=3.0, Cg=1.0, nnu=4, nutune=20.0, cfltune=0.01, filter_order=8, af=1 / 3,
              Kg=(10, 13), ag=0.2, Kw=(0, 5), aw=0.1)
+    P.update(parameters or {})
     # initialize_problem (:134-176)
     Lx, dx = P["L"], P["L"] / nx
     kmax = (nx / 2 - 1) * Lx / (2 * np.pi) * (1 - P["af"])
@@ -455,7 +506,7 @@ def rsw_driver_start(tw, nx=128, nsteps=240, output_freq=20, diags_freq=10, spin
             cfls.append(float(prob.clock.dt) * max(np.max(np.abs(v.u)) / grid.dx, np.max(np.abs(v.v)) / grid.dy))
         ff_stepforward(tw, prob, diags, output_freq)
         if np.any(np.isnan(prob.vars.η)):
-            raise RuntimeError("Solution is NaN")
+            raise BlewUp(prob.clock.step, outputs, diags, prob, ic)
         rsw_updatevars(tw, prob)
         if prob.clock.step >= spinup_step:
             outputs.append((prob.clock.step, prob.sol.copy()))

@@ -22,10 +22,12 @@ def _plan(*args):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("n", [2, 4])
+@pytest.mark.parametrize("n", [2, 4, 8])
 def test_gpus_n_launches_n_ranks_slab(n):
+    # config 5 runs over every rank, config 4 over min(N, 4) (BASELINE: "RSW
+    # 4096² slab-decomposed across 4 MI355X")
     assert _plan("--gpus", str(n)) == {"n_gpus": n, "parallelism": f"slab{n}", "scaling": "strong",
-                                        "rank0_of": n}
+                                        "rank0_of": n, "config5_ranks": n, "config4_ranks": min(n, 4)}
 
 
 def test_ensemble_mode_and_single_gpu():

@@ -100,6 +100,59 @@ def test_rsw_driver_float32_replay():
     prob.timestepper.finalizer()
 
 
+def test_rsw_driver_blowup_throws_on_its_frame():
+    """RSWDriver's real cadence: diags_freq ≫ output_freq (RSWParameters.jl:
+    diag_dt = 0.5 against output_dt = 0.025/f, ≈ 60×), so most frames run no
+    energy Diagnostic, and the counted steps of a frame are still pending
+    when the driver scans vars.η (rsw/RSWDriver.jl:212-213).  With the
+    reference's CFL raised to 0.5 (a user's edit of RSWParameters.jl) the
+    advection goes unstable on its own; the scan's read of vars.η (an SWField)
+    runs the frame's steps, so the throw comes on the frame where the state
+    went non-finite, no NaN snapshot is written, and prob.sol is still
+    downloaded only once per frame."""
+    tw = R.Twin()
+    ofreq, dfreq = 20, 1000
+    with pytest.raises(R.BlewUp) as ei:
+        R.rsw_driver_start(tw, nx=128, nsteps=2000, output_freq=ofreq, diags_freq=dfreq, spinup_step=0,
+                           parameters=dict(cfltune=0.5))
+    bu = ei.value
+    prob = bu.prob
+    # the first non-finite step, from the same Float32 state on a second
+    # context stepped one step per sw_step
+    tw2 = R.Twin()
+    p2 = R.rsw_problem(tw2, Lx=2 * np.pi, nx=128, dt=float(prob.clock.dt), f=3.0, Cg=1.0, T=np.float32, nnu=4,
+                       nu=float(prob.params.ν), aliased_fraction=1 / 3, order=8, use_filter=False)
+    p2.sol[...] = bu.ic
+    tw2.load_solution(p2)
+    first = None
+    for k in range(1, 2001):
+        rc = tw2.c("sw_step", p2.timestepper.ctx, 1)
+        if rc == R.SW_E_NAN:
+            first = k
+            break
+        assert rc == 0
+    assert first is not None and first > 3 * ofreq, first  # mid-run, past the first frames
+    # thrown on the frame that holds the first non-finite step
+    assert bu.step == -(-first // ofreq) * ofreq, (bu.step, first)
+    assert prob.clock.step == bu.step
+    # every snapshot written is finite and precedes the blow-up
+    snaps = [o for o in bu.outputs[1:]]
+    assert len(snaps) == bu.step // ofreq  # frame 0's enforce_reality_condition! output + one per frame before
+    assert all(np.all(np.isfinite(o[1])) for o in snaps)
+    assert max(o[0] for o in snaps) < first
+    # no per-step state traffic: load_solution! + one download per completed frame
+    c = tw.calls
+    assert c.count("sw_get_state") == 1 + (bu.step // ofreq - 1)
+    assert c.count("sw_step") == bu.step // ofreq  # one per frame (updatevars!'s, then the scan's)
+    assert c.count("sw_step_record") == 0  # no Diagnostic step before the blow-up (dfreq ≫ first)
+    # the throw's frame ran its steps in one sw_step (the scan's vars.η read) and
+    # downloaded nothing
+    assert c[-1] == "sw_step"
+    assert np.all(np.isnan(prob.vars.η))
+    prob.timestepper.finalizer()
+    p2.timestepper.finalizer()
+
+
 def test_ty_driver_replay():
     tw = R.Twin()
     sp, sdiags, diags, _, outputs, ic, startup_steps = R.ty_driver_start(

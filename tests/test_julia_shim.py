@@ -183,6 +183,7 @@ HELPERS_PY = r"self\.(upload|download|push_clock|flush|sync|blowup|diag_record)\
     ("config", "config"), ("SWStepper", "SWStepper"), ("upload!", "upload"), ("download!", "download"),
     ("push_clock!", "push_clock"), ("load_solution!", "load_solution"), ("stepforward!", "stepforward_seam"),
     ("flush!", "flush"), ("sync!", "sync"), ("device_energy", "device_energy"), ("diag_record", "diag_record"),
+    ("settle!", "settle"),
 ])
 def test_julia_function_matches_its_python_twin(jname, pyname):
     import sys
@@ -242,9 +243,46 @@ def test_per_step_seam_is_lazy():
     for f in ("rsw_updatevars!", "qg2_updatevars!", "ty_updatevars!", "mlqg_updatevars!"):
         fb = re.search(rf"^function {re.escape(f)}\((.*?)\nend", s, re.S | re.M).group(1)
         assert "sync!(prob)" in fb, f
-    for f in ("rsw_updatevars!", "qg2_updatevars!"):
+    for f in ("rsw_updatevars!", "qg2_updatevars!", "ty_updatevars!"):
         fb = re.search(rf"^function {re.escape(f)}\((.*?)\nend", s, re.S | re.M).group(1)
         assert fb.index("sync!(prob)") < fb.index("FourierFlows.dealias!(sol, grid)") < fb.index("@. vars.")
+    # after updatevars! the energy functions read the updated state (sw_diag),
+    # not the last step's record
+    for f in ("rsw_updatevars!", "qg2_updatevars!", "ty_updatevars!", "mlqg_updatevars!"):
+        fb = re.search(rf"^function {re.escape(f)}\((.*?)\nend", s, re.S | re.M).group(1)
+        assert "ts.rec_step = -1" in fb, f
+
+
+def test_physical_vars_run_the_counted_steps_when_read():
+    """the drivers scan vars.η / vars.q for NaN right after
+    stepforward!(prob, diags, n) (rsw/RSWDriver.jl:213, swqg/TwoLayerDriver.jl:106).
+    The physical fields of a libsw problem's vars are SWFields whose reads run
+    the pending steps first (settle! -> flush!), for RSW, 2LQG and TY; the
+    twin's DeviceVars does the same on attribute access."""
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import driver_replay
+
+    s = _strip_comments(_src())
+    assert re.search(r"^struct SWField\{T,N\} <: AbstractArray\{T,N\}", s, re.M)
+    settle = re.search(r"^function settle!\(a::SWField\)(.*?)\nend", s, re.S | re.M).group(1)
+    assert "pending == 0 || flush!(prob)" in settle
+    # every read path settles: indexing, broadcasting (isnan.(vars.η)), deepcopy
+    assert re.search(r"Base\.getindex\(a::SWField, i::Int\) = \(settle!\(a\);", s)
+    assert re.search(r"Base\.Broadcast\.broadcastable\(a::SWField\) = parent\(settle!\(a\)\)", s)
+    assert re.search(r"Base\.deepcopy_internal\(a::SWField, d::IdDict\) = .*settle!\(a\)", s)
+    # writes do not
+    assert re.search(r"Base\.setindex!\(a::SWField, x, i::Int\) = \(a\.data\[i\] = x; a\)", s)
+    for builder in ("rsw_problem", "qg2_problem", "ty_problem"):
+        body = re.search(rf"^function {builder}\((.*?)\nend", s, re.S | re.M).group(1)
+        assert "vars = device_vars(M.Vars(grid), owner)" in body, builder
+        assert "owned_problem(owner, sol, clock, equation, grid, vars, params, ts)" in body, builder
+    # blowup! fills the SWFields in place (fill! writes the host array)
+    assert re.search(r"Base\.fill!\(a::SWField, x\) = \(fill!\(a\.data, x\); a\)", s)
+    py = inspect.getsource(driver_replay.DeviceVars)
+    assert "owner.tw.settle(owner.prob)" in py
 
 
 @pytest.mark.parametrize("module,names", [
