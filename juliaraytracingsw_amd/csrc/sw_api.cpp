@@ -610,6 +610,7 @@ static void last_col_pass(sw_ctx* c, double2* Slab::*X, double2* Slab::*N, int o
 }
 
 int allgather(sw_ctx* c, const void* mine, void* dst, size_t bytes);
+int gather0(sw_ctx* c, const void* mine, void* dst, size_t bytes);
 // equation.calcN!(N, X, …): col_inv -> transpose -> row -> transpose -> col_fwd;
 // op >= 0: the stepper update of `op` fused into the col_fwd pass (use_fwd_step)
 int calcN(sw_ctx* c, double2* Slab::*X, double2* Slab::*N, int op = -1, int stage = 0) {
@@ -657,7 +658,7 @@ int calcN(sw_ctx* c, double2* Slab::*X, double2* Slab::*N, int op = -1, int stag
   if (c->alias && c->dist) {  // every rank's block of the aliased x-spectra, for slab 0's region 0 (ma_off)
     const Slab& s = c->sl[0];
     const size_t B = (size_t)c->nfwd * sw::ma_field(s.g);
-    if (int rc = allgather(c, s.a_mrow + (size_t)s.g.slab * B, s.a_mrow, B * sizeof(double2))) return rc;
+    if (int rc = gather0(c, s.a_mrow + (size_t)s.g.slab * B, s.a_mrow, B * sizeof(double2))) return rc;
   }
   if (int rc = transpose(c, false, c->nfwd)) return rc;
   {
@@ -1045,6 +1046,25 @@ int allgather(sw_ctx* c, const void* mine, void* dst, size_t bytes) {
   if (c->cfg.exchange(c->cfg.exchange_user, c->hsend, c->hrecv, bytes, c->P) != 0)
     return fail(c, SW_E_COMM, "exchange hook failed");
   HIPCHK(c, hipMemcpyAsync(dst, c->hrecv, bytes * c->P, hipMemcpyHostToDevice, c->stream));
+  return 0;
+}
+
+// dist: every rank's `bytes` at `mine` -> dst[rank * bytes] on rank 0 only
+// (mine == dst + rank * bytes).  The aliased-state x-spectra of the row pass
+// feed slab 0's region-0 column pass alone (the aliased columns kr >= kc live
+// there): RCCL grouped send/recv moves (P - 1) blocks into rank 0 instead of
+// the all-gather's P (P - 1).  The host-staged
+// transport is an all-to-all of equal blocks: it keeps the all-gather.
+int gather0(sw_ctx* c, const void* mine, void* dst, size_t bytes) {
+  if (c->hostx) return allgather(c, mine, dst, bytes);
+  NCCLCHK(c, ncclGroupStart());
+  if (c->sl[0].g.slab == 0) {  // one slab per process: the slab index is the rank
+    for (int q = 1; q < c->P; ++q)
+      NCCLCHK(c, ncclRecv(static_cast<char*>(dst) + q * bytes, bytes, ncclUint8, q, c->nccl, c->stream));
+  } else {
+    NCCLCHK(c, ncclSend(mine, bytes, ncclUint8, 0, c->nccl, c->stream));
+  }
+  NCCLCHK(c, ncclGroupEnd());
   return 0;
 }
 
@@ -2140,6 +2160,24 @@ int sw_get_checkpoint(const sw_ctx* cc, void* buf, size_t bytes) {
   return SW_OK;
 }
 
+// any nonzero (nkr, nl, nf) mode of the blob's state or history outside the
+// 2/3-rule live set (kr >= kc, or l in [lc, lr2)): only an aliased_state
+// context writes those
+static bool ckpt_has_aliased_modes(const sw_ctx* c, const CkptHeader& h, const void* buf) {
+  const sw::Geom& g = c->sl[0].g;
+  const double* d = reinterpret_cast<const double*>(static_cast<const char*>(buf) + sizeof(CkptHeader));
+  const size_t nkr = g.nkr, nl = g.nl;
+  for (int k = 0; k <= h.nslots; ++k)
+    for (int f = 0; f < c->nf; ++f)
+      for (size_t l = 0; l < nl; ++l) {
+        const bool dead_row = (int)l >= g.lc && (int)l < g.lr2;
+        const double* row = d + 2 * (((size_t)(k * c->nf + f) * nl + l) * nkr);
+        for (size_t kr = dead_row ? 0 : (size_t)g.kc; kr < nkr; ++kr)
+          if (row[2 * kr] != 0.0 || row[2 * kr + 1] != 0.0) return true;
+      }
+  return false;
+}
+
 int sw_set_checkpoint(sw_ctx* c, const void* buf, size_t bytes) {
   if (!ready(c)) return SW_E_STATE;
   if (!buf || bytes != ckpt_bytes(c)) return fail(c, SW_E_INVALID, "sw_set_checkpoint: size mismatch");
@@ -2149,9 +2187,18 @@ int sw_set_checkpoint(sw_ctx* c, const void* buf, size_t bytes) {
   // the blob layout is that of ABI 7 (its introduction) up to this one
   if (h.abi < 7 || h.abi > SW_ABI_VERSION) return fail(c, SW_E_INVALID, "sw_set_checkpoint: unknown checkpoint ABI");
   // an aliased-state blob carries modes a default context drops, and the
-  // reverse lacks them: neither continues bitwise
-  if (h.aliased_state != (c->alias ? 1 : 0))
-    return fail(c, SW_E_INVALID, "sw_set_checkpoint: aliased_state differs from the checkpoint's");
+  // reverse lacks them: neither continues bitwise.  Before ABI 9
+  // the header's field was reserved (0) whatever the writer tracked (ADVICE
+  // r04): the blob's own aliased modes tell — a context that tracked them
+  // leaves them nonzero, a default one writes zeros there.
+  const int64_t blob_alias = h.abi >= 9 ? h.aliased_state : (ckpt_has_aliased_modes(c, h, buf) ? 1 : 0);
+  if (blob_alias != (c->alias ? 1 : 0))
+    return fail(c, SW_E_INVALID,
+                h.abi >= 9 ? "sw_set_checkpoint: aliased_state differs from the checkpoint's"
+                           : (blob_alias ? "sw_set_checkpoint: an ABI < 9 checkpoint holding aliased modes (written "
+                                           "with aliased_state) into a context without aliased_state"
+                                         : "sw_set_checkpoint: an ABI < 9 checkpoint with zero aliased modes (written "
+                                           "without aliased_state) into an aliased_state context"));
   if (h.model != c->cfg.model || h.stepper != c->cfg.stepper || h.nx != c->cfg.nx || h.ny != c->cfg.ny ||
       h.nf != c->nf || h.nslots != ckpt_slots(c) || h.step < 0 || h.euler_left < 0 || h.euler_left > 3)
     return fail(c, SW_E_INVALID, "sw_set_checkpoint: checkpoint of a different problem or stepper");

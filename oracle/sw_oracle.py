@@ -181,8 +181,26 @@ def expm_batched(A):
         raise RuntimeError("scipy is required for the oracle's expm")
     sh = A.shape
     flat = A.reshape(-1, sh[-2], sh[-1])
-    out = _sla.expm(flat)
+    if _EXPM_WORKERS > 1 and flat.shape[0] > 400_000:
+        # scipy's per-slice loop holds the GIL: large batches (the 8192²
+        # fixture's 30 M matrices) go to forked worker processes
+        import multiprocessing as mp
+
+        with mp.get_context("fork").Pool(_EXPM_WORKERS) as pool:
+            parts = pool.map(_sla.expm, np.array_split(flat, 4 * _EXPM_WORKERS))
+        out = np.concatenate(parts)
+    else:
+        out = _sla.expm(flat)
     return out.reshape(sh)
+
+
+_EXPM_WORKERS = 1
+
+
+def set_expm_workers(n):
+    """processes for scipy's expm over large batches (None/1: in process)"""
+    global _EXPM_WORKERS
+    _EXPM_WORKERS = max(1, int(n or 1))
 
 
 def expm_2x2(A):
@@ -211,9 +229,29 @@ def expm_2x2(A):
     return out
 
 
-def expm_modes(A):
-    """Per-mode exp: the closed form for 2×2 operators, scipy's expm otherwise."""
-    return expm_2x2(A) if A.shape[-2:] == (2, 2) else expm_batched(A)
+def expm_modes(A, method="scipy", live=None):
+    """Per-mode exp (utils/IFMAB3.jl:26-30: Julia's Padé ``exp`` per mode).
+
+    method "scipy" (default): scipy's expm (Al-Mohy & Higham scaling and
+    squaring; scipy >= 1.11 has no 2×2 special case), independent of the
+    device's closed-form ``ExpOf`` — with `live` (a
+    mask of the modes the 2/3 rule keeps), scipy on those modes and the
+    closed form on the aliased ones, whose values never reach a live mode
+    (calcN! dealiases its input).  method "closed": ``expm_2x2`` for 2×2
+    operators — the 8192² fixture (tests/golden/make_qg2_8192.py), where
+    scipy over 33.5 M matrices is not affordable; it is pinned to scipy on
+    that fixture's own operator rows (tests/test_oracle.py)."""
+    if A.shape[-2:] != (2, 2):
+        return expm_batched(A)
+    if method == "closed":
+        return expm_2x2(A)
+    if method != "scipy":
+        raise ValueError(method)
+    if live is None:
+        return expm_batched(A)
+    out = expm_2x2(A)
+    out[live] = expm_batched(A[live])
+    return out
 
 
 def mvmul(A, x):
@@ -729,12 +767,18 @@ class FilteredRK4:
         clock.step += 1
 
 
+def live_mask(grid):
+    """the (nl, nkr) modes FF's dealias! keeps"""
+    return grid.dealias(np.ones((1, grid.nl, grid.nkr), np.complex128))[0] != 0
+
+
 class IFMAB3:
     """utils/IFMAB3.jl:68-88, 128-169 (CPU method)."""
 
-    def __init__(self, L, dt, grid, nf, use_filter=False, diagonal=False, **filter_kw):
-        self.expLdt = expm_modes(L * dt)
-        self.exp2Ldt = expm_modes(L * 2 * dt)
+    def __init__(self, L, dt, grid, nf, use_filter=False, diagonal=False, expm="scipy", **filter_kw):
+        self.expm = expm
+        self.expLdt = expm_modes(L * dt, expm, live_mask(grid))
+        self.exp2Ldt = expm_modes(L * 2 * dt, expm, live_mask(grid))
         shape = (nf, grid.nl, grid.nkr)
         self.N = np.zeros(shape, np.complex128)
         self.Nm1 = np.zeros(shape, np.complex128)
@@ -769,9 +813,10 @@ class IFMRK4:
       k4 = N(E u + dt H k3); u <- E u + dt/6 (E k1 + 2H(k2 + k3) + k4); filter.
     """
 
-    def __init__(self, L, dt, grid, nf, use_filter=False, **filter_kw):
-        self.expLdt = expm_modes(L * dt)
-        self.expLhdt = expm_modes(L * 0.5 * dt)
+    def __init__(self, L, dt, grid, nf, use_filter=False, expm="scipy", **filter_kw):
+        self.expm = expm
+        self.expLdt = expm_modes(L * dt, expm, live_mask(grid))
+        self.expLhdt = expm_modes(L * 0.5 * dt, expm, live_mask(grid))
         if use_filter:
             self.filter = makefilter(grid, **filter_kw)[None]
         else:
@@ -849,7 +894,8 @@ class Problem:
     "IFMRK4"}, or "NOP" calcN for the linear-only check)."""
 
     def __init__(self, model, stepper, nx, dt, Lx=2 * np.pi, aliased_fraction=1 / 3,
-                 params=None, use_filter=False, calcN=None, ny=None, Ly=None, **filter_kw):
+                 params=None, use_filter=False, calcN=None, ny=None, Ly=None, expm="scipy", **filter_kw):
+        # expm: the integrating factors' matrix exponential (expm_modes)
         # model "ty" (thomasyamada/ThomasYamada.jl:55-74) takes stepper "ETDRK4"
         self.grid = TwoDGrid(nx, Lx, ny=ny, Ly=Ly, aliased_fraction=aliased_fraction)
         self.params = params
@@ -884,9 +930,9 @@ class Problem:
         elif stepper == "FilteredRK4":
             self.ts = FilteredRK4(self.L, self.grid, self.nf, **filter_kw)
         elif stepper == "IFMAB3":
-            self.ts = IFMAB3(self.L, dt, self.grid, self.nf, use_filter=use_filter, **filter_kw)
+            self.ts = IFMAB3(self.L, dt, self.grid, self.nf, use_filter=use_filter, expm=expm, **filter_kw)
         elif stepper == "IFMRK4":
-            self.ts = IFMRK4(self.L, dt, self.grid, self.nf, use_filter=use_filter, **filter_kw)
+            self.ts = IFMRK4(self.L, dt, self.grid, self.nf, use_filter=use_filter, expm=expm, **filter_kw)
         else:
             raise ValueError(stepper)
         self.sol = np.zeros((self.nf, self.grid.nl, self.grid.nkr), np.complex128)

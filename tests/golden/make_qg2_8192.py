@@ -2,10 +2,13 @@
 TwoLayerQG 8192² IFMRK4 from the seeded driver IC (sw_cases "qg2_ifmrk4",
 swqg/TwoLayerDriver.jl:10-15 amplitude 1e-2), two full IFMRK4 steps of the
 oracle (utils/IFMRK4.jl:157-163 as SURVEY A9 defines it, swqg/TwoLayerQG.jl
-:152-198 calcN and L), with the 2×2 integrating factors in closed form
-(sw_oracle.expm_2x2, pinned to scipy's expm in tests/test_oracle.py).
+:152-198 calcN and L), with the 2×2 integrating factors from scipy's expm on
+every live mode (round 5, VERDICT r04 weak #1: independent of the device's
+closed-form ExpOf; forked worker processes, sw_oracle.set_expm_workers; the
+round-4 fixture used the closed form sw_oracle.expm_2x2, which
+tests/test_oracle.py pins to scipy on these rows).
 
-    python tests/golden/make_qg2_8192.py        (≈ 5 min, ≈ 25 GB, 8 cores)
+    python tests/golden/make_qg2_8192.py        (≈ 8 min, ≈ 30 GB, 8 cores)
 
 The state is 1.07 GB, so the fixture keeps a sample: every live kr of 24 l
 rows (low, middle, high, negative), both layers, after 2 steps; the full
@@ -38,8 +41,9 @@ ROWS = [0, 1, 2, 3, 5, 8, 13, 34, 89, 233, 610, 1597, 2000, 2500, 2729,
 def main():
     t0 = time.time()
     O.set_fft_workers(os.cpu_count())
+    O.set_expm_workers(os.cpu_count())
     p = sw_cases.case_params("qg2_ifmrk4", N)
-    pr = sw_cases.oracle_problem(p)
+    pr = sw_cases.oracle_problem(p, expm="scipy")
     g = pr.grid
     ic = sw_cases.initial_condition(p, g)
     pr.set_solution(ic)
@@ -54,6 +58,7 @@ def main():
     sol = g.dealias(pr.sol.copy())
     srows = sol[:, rows, :kc]
     out = {"params": np.array(json.dumps(p)), "rows": rows, "kc": np.array(kc), "steps": np.array(STEPS),
+           "expm": np.array(pr.ts.expm),
            "sol_rows": srows, "sumsq": np.array([float(np.sum(np.abs(sol[f]) ** 2)) for f in range(2)]),
            "ic_check": ic_check(s0),
            "nonlinear_part": np.array(np.max(np.abs(srows - lin)) / np.max(np.abs(srows)))}

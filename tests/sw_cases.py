@@ -62,7 +62,9 @@ def case_params(name, n):
                 order=8, seed=1234)
 
 
-def oracle_problem(p):
+def oracle_problem(p, expm="scipy"):
+    """the oracle Problem of a case; expm: its integrating factors' matrix
+    exponential (sw_oracle.expm_modes: scipy's expm, or "closed")"""
     if p["model"] == "mlqg":
         params = O.MLQGParams(p["f0"], p["H"], p["b"], p["U"], p["mu"], p["beta"], p["nu"], p["nnu"])
         return O.Problem("mlqg", p["stepper"], p["n"], p["dt"], aliased_fraction=p["af"], params=params)
@@ -74,7 +76,7 @@ def oracle_problem(p):
     else:
         params = O.QG2Params(p["U"], p["mu"], p["nu"], p["nnu"], F=p["F"])
     fk = dict(order=p["order"]) if p["stepper"] == "FilteredAB3" else {}
-    return O.Problem(p["model"], p["stepper"], p["n"], p["dt"], params=params, **fk)
+    return O.Problem(p["model"], p["stepper"], p["n"], p["dt"], params=params, expm=expm, **fk)
 
 
 def initial_condition(p, grid):

@@ -178,6 +178,47 @@ def test_checkpoint_carries_the_aliased_history():
     prob.close()
 
 
+def test_abi8_checkpoint_aliased_state_inferred():
+    """before ABI 9 the checkpoint header's aliased_state field
+    was reserved (0) whatever the writer tracked.  An ABI-8 blob is matched
+    by its own aliased modes: one written with aliased_state (nonzero there)
+    restores into an aliased context — bitwise, as an ABI-9 one — and is
+    refused by a default one (which would drop those modes); a default
+    context's ABI-8 blob (zeros there) restores into a default context and is
+    refused by an aliased one."""
+
+    def abi8(blob):
+        b = blob.copy()
+        b[8:12] = np.frombuffer(np.int32(8).tobytes(), np.uint8)     # CkptHeader.abi
+        b[56:64] = np.frombuffer(np.int64(0).tobytes(), np.uint8)    # aliased_state: reserved then
+        return b
+
+    p, pr, prob = _setup("qg2_ifmab3")
+    prob.stepforward(7)
+    blob = abi8(prob.ctx.get_checkpoint())
+    prob.stepforward(5)
+    want = prob.sol
+    b = sw_cases.libsw_problem(p, aliased_state=True)
+    b.ctx.set_checkpoint(blob)
+    b.stepforward(5)
+    assert np.array_equal(b.sol, want)
+    d = sw_cases.libsw_problem(p)
+    with pytest.raises(LibSWError, match="holding aliased modes"):
+        d.ctx.set_checkpoint(blob)
+    d.sol = pr.sol
+    d.stepforward(4)
+    dblob = abi8(d.ctx.get_checkpoint())
+    d2 = sw_cases.libsw_problem(p)
+    d2.ctx.set_checkpoint(dblob)
+    d.stepforward(3)
+    d2.stepforward(3)
+    assert np.array_equal(d.sol, d2.sol)
+    with pytest.raises(LibSWError, match="zero aliased modes"):
+        b.ctx.set_checkpoint(dblob)
+    for x in (b, d, d2, prob):
+        x.close()
+
+
 def test_updatevars_dealiases_the_state():
     """updatevars! begins with dealias!(sol, grid) (swqg/TwoLayerQG.jl:115):
     after it prob.sol has zeros at the aliased modes, as the reference's."""

@@ -9,10 +9,12 @@
   closed-form pins at this size, one slab and four);
 * config 5 — TwoLayerQG 8192² IFMRK4 at the TwoLayerDriver parameters
   (swqg/TwoLayerDriver.jl:29-68, stepper utils/IFMRK4.jl as the build defines
-  it): the 8-slab decomposition is bitwise equal to one slab for 2 steps, and
-  calcN at 8192² matches the oracle to 1e-10 (the oracle's per-mode scipy
-  expm of 33.5 M 2×2 operators is too slow for a stepped 8192² oracle run; the
-  IFMRK4 update is checked against the oracle on 8192-point lines by
+  it): the 8-slab decomposition is bitwise equal to one slab for 2 steps,
+  calcN at 8192² matches the oracle to 1e-10, and the state after 2 steps
+  matches tests/golden/qg2_ifmrk4_8192_rows.npz (24 l rows of an oracle run
+  whose integrating factors are scipy's expm on every live mode, forked over
+  8 processes: round 5, independent of the device's closed form; the IFMRK4
+  update is also checked on 8192-point lines by
   test_gpu_parity.py::test_rectangular_long_lines).
 
 What the RCCL transport itself adds (the same blocks moved by grouped

@@ -431,6 +431,40 @@ def test_expm_2x2_matches_scipy(model, tau):
     assert np.median(r) < 1e-14
 
 
+@pytest.mark.parametrize("case,n,taus", [
+    ("qg2_ifmab3", 2048, (1, 2)),    # BASELINE config 3: E = exp(dt L), E2 = exp(2 dt L) (utils/IFMAB3.jl:26-30)
+    ("qg2_ifmrk4", 8192, (1, 0.5)),  # config 5: E, H = exp(dt L / 2), on the fixture's 24 rows
+])
+def test_expm_2x2_pinned_at_the_config_operators(case, n, taus):
+    """the closed-form 2×2 exponential (the device's ExpOf<2>
+    formula, sw_oracle.expm_2x2) against scipy's expm (Padé scaling and
+    squaring, no 2×2 special case) on the actual BASELINE operators — config
+    3 on every live mode of 2048², config 5 on every live kr of the config-5
+    fixture's 24 l rows of 8192² — ≤ 1e-13 of each mode's norm.  (The
+    oracle's stepped parity runs on scipy's expm by default; this pins the
+    closed form the device evaluates, at the parameters it runs.)"""
+    p = sw_cases.case_params(case, n)
+    g = O.TwoDGrid(n)
+    L = O.qg2_L(g, O.QG2Params(p["U"], p["mu"], p["nu"], p["nnu"], F=p["F"]))
+    if n == 8192:
+        fx = np.load(os.path.join(GOLDEN, "qg2_ifmrk4_8192_rows.npz"))
+        L = L[fx["rows"]][:, :int(fx["kc"])].reshape(-1, 2, 2)
+    else:
+        L = L[O.live_mask(g)]
+    worst = []
+    for tau in taus:
+        A = L * (tau * p["dt"])
+        a = np.concatenate([O.expm_batched(A[i:i + 250_000]) for i in range(0, len(A), 250_000)])
+        b = O.expm_2x2(A)
+        na = np.linalg.norm(a, axis=(-2, -1))
+        r = np.linalg.norm(a - b, axis=(-2, -1)) / na
+        worst.append(float(r.max()))
+        assert np.all(na > 0)
+        assert r.max() <= 1e-13, (tau, r.max(), A[np.argmax(r)].ravel())
+        assert np.median(r) < 1e-15
+    print(f"{case} {n}²: {len(L)} modes, worst relative mode error {worst}")
+
+
 def test_config5_fixture_ic_is_the_seeded_driver_ic():
     """tests/golden/qg2_ifmrk4_8192_rows.npz was generated from the seeded
     driver IC that the GPU test regenerates (numpy PCG64 + pocketfft)."""
