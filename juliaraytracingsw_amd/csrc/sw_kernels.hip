@@ -1162,197 +1162,6 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
 }
 
 // ===========================================================================
-// The RSW row at 2048 points, persistent, its next row's inputs staged by
-// LDS-DMA (round 5).  k_row loads a row's U, V, H, Uy into registers at the
-// row's start and waits for them there: at two blocks (two waves per SIMD)
-// per CU, set by its two 32 KB line buffers and 222 VGPRs, that wait is
-// exposed (round 2: 16 µs of 87 with the loads made L1 hits).  Here a block
-// walks rows v = b, b + G, … (G = two blocks per CU) and fetches row v + G's
-// inputs with global_load_lds_dwordx4 (no VGPR destination) while it
-// transforms row v:
-//   * Uy (kc entries) into its own 11 KB region, right after this row has
-//     read its staged inputs;
-//   * U, V, H (3 kc <= 2048 entries) into line buffer 2, which the row's last
-//     transform (the real K line, C = 1) leaves free, after the forward
-//     pairs' split.
-// A row's wait is then `s_waitcnt vmcnt(4)`: the LDS-DMA is older than the
-// last four vector-memory operations of every wave (the K and P stores of
-// slots 0 and 1, live on every thread when kc >= 2 NT; in-order counting,
-// MI355X_MICROARCH.md), so the stores stay in flight.  The DMA is inline asm
-// (M0 set and restored in the same statement): hipcc neither counts it nor
-// drains it at the barriers (lds_barrier waits lgkmcnt only).  The
-// arithmetic is k_row's (MODEL_RSW, decimated W = 4 transforms, PRUNE), so
-// the outputs are bitwise the same (tests/test_gpu_parity.py's fused ==
-// unfused / slab checks, SW_ROW_DMA=0 for the A/B).
-// ===========================================================================
-#ifndef SW_ROW_DMA
-#define SW_ROW_DMA 1
-#endif
-// one wave-instruction of LDS-DMA: lane i's 16 B at gsrc land at LDS byte
-// lds_byte + 16 i (lds_byte wave-uniform)
-__device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_byte) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(gsrc), "s"(lds_byte)
-      : "memory");
-}
-__device__ __forceinline__ unsigned lds_byte_addr(const void* p) { return (unsigned)(uintptr_t)p; }
-
-template <int LOG2N>
-struct RowDma {
-  static constexpr int N = 1 << LOG2N, NT = N / 8, LS = FftPlan<LOG2N>::LDS;
-  static constexpr int US = ((N / 3 + 1 + 63) / 64) * 64;  // the Uy region (entries >= kc)
-  static constexpr size_t SMEM = (2 * LS + US) * sizeof(double2);
-};
-template <int LOG2N>
-__host__ __device__ constexpr bool row_dma_len() {
-  return SW_ROW_DMA && LOG2N == 11 && roww<LOG2N>() == 4 && row_lds_lines<MODEL_RSW, LOG2N>() == 2;
-}
-
-template <int LOG2N>
-static __global__ void __launch_bounds__(FftPlan<LOG2N>::NT, SW_MINW_ROW)
-    k_row_rsw_dma(Geom g, Phys p, const double2* __restrict__ Mi, double2* __restrict__ Mo,
-                  const double2* __restrict__ tw, int yoff, int nrows) {
-  using R = RowIdx<LOG2N>;
-  using D = RowDma<LOG2N>;
-  constexpr int NT = D::NT, LS = D::LS, W = roww<LOG2N>();
-  extern __shared__ double2 smem[];
-  double2* line = smem;           // two line buffers (k_row's)
-  double2* st3 = smem + LS;       // U, V, H of the next row: line buffer 2 between rows
-  double2* stu = smem + 2 * LS;   // Uy of the next row
-  const int t0 = threadIdx.x;
-  const long long MF = g.mfield;
-  const int kc = g.kc;
-  Twiddles<9> tq;
-  tq.load(t0 & 63, tw, LOG2N - 9);
-  const double2 wt = tw[t0];
-  // U, V, H of local row y into st3: entry e = f kc + kr (f = 0, 1, 2), 2048
-  // entries = 32 wave-instructions, 8 per wave (entries >= 3 kc: junk, unread)
-  auto dma_uvh = [&](int y) {
-    int tl = threadIdx.x;
-    asm volatile("" : "+v"(tl));
-    const int wv = tl >> 6, lane = tl & 63;
-    const unsigned base = lds_byte_addr(st3);
-#pragma unroll
-    for (int q = 0; q < LS / 256; ++q) {
-      const int j = wv + 4 * q;
-      const int e = 64 * j + lane;
-      const int f = (e >= kc) + (e >= 2 * kc);
-      const bool ok = f < 3;
-      const int kr = ok ? e - f * kc : 0;
-      glds16(Mi + (ok ? f : 0) * MF + midx_i(g, kr, y), __builtin_amdgcn_readfirstlane(base + 1024u * j));
-    }
-  };
-  // Uy of local row y into stu (entry kr)
-  auto dma_uy = [&](int y) {
-    int tl = threadIdx.x;
-    asm volatile("" : "+v"(tl));
-    const int wv = tl >> 6, lane = tl & 63;
-    const unsigned base = lds_byte_addr(stu);
-#pragma unroll
-    for (int q = 0; q < (D::US / 64 + 3) / 4; ++q) {
-      const int j = wv + 4 * q;
-      if (j < D::US / 64) {  // wave-uniform
-        const int kr = 64 * j + lane;
-        glds16(Mi + 3 * MF + midx_i(g, kr < kc ? kr : 0, y), __builtin_amdgcn_readfirstlane(base + 1024u * j));
-      }
-    }
-  };
-  const int G = gridDim.x;
-  int v = blockIdx.x;
-  int y = yoff + col_of_block(v, nrows);
-  dma_uy(y);
-  dma_uvh(y);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  for (;;) {
-    // the thread index made opaque per row: its derived offsets and
-    // wavenumbers are formed per row, not hoisted out of the loop and held
-    // across it (77 spilled VGPRs without)
-    int t = threadIdx.x;
-    asm volatile("" : "+v"(t));
-    const int vn = v + G;
-    const bool more = vn < nrows;  // uniform
-    const int yn = more ? yoff + col_of_block(vn, nrows) : y;
-    lds_barrier();  // every wave's LDS-DMA of this row has landed (each waited before the barrier)
-    RowIdx<LOG2N> ri;
-    ri.init(g, t, y);
-    // u + i v and η + i ζ from the staged U, V, H, Uy (load_uv_eta_zeta's pairs)
-    double2 w[2][8];
-    {
-      double2 u[8], vv[8], h[8], uy[8];
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        u[s] = vv[s] = h[s] = uy[s] = zero2();
-        if (R::inv_any(g, s)) {
-          const int kk = R::kk(t, s);
-          const int i = kk < kc ? kk : 0;
-          u[s] = st3[i];
-          vv[s] = st3[kc + i];
-          h[s] = st3[2 * kc + i];
-          uy[s] = stu[i];
-        }
-      }
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        const int kk = R::kk(t, s);
-        const bool mir = s >= 4 && kk != (D::N >> 1), live = kk < kc;
-        w[0][s] = pair_z(u[s], vv[s], kk, mir, live);
-        w[1][s] = pair_z(h[s], csub(cmul_i(vv[s], kk * g.mk), uy[s]), kk, mir, live);
-      }
-    }
-    lds_barrier();  // every thread has read st3 and stu
-    if (more) dma_uy(yn);
-    fftw_dif<W, +1, 2, false, false, SW_ROW_TW_SHARE, true>(w, t, wt, tq, line, LS);
-    double kk2[8];
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const double u = w[0][s].x, vv = w[0][s].y, eta = w[1][s].x, zeta = w[1][s].y;
-      kk2[s] = 0.5 * (u * u + vv * vv);
-      w[0][s] = make_double2(zeta * u, zeta * vv);  // ζu + i ζv
-      w[1][s] = make_double2(u * eta, vv * eta);    // uη + i vη
-    }
-    fftw_dit<W, -1, 2, false, false, SW_ROW_TW_SHARE, true>(w, t, wt, tq, line, LS);
-    double2 zv[8];
-#pragma unroll
-    for (int s = 0; s < 8; ++s) zv[s] = zero2();
-    split_pairs<LOG2N, 2, true>(w, t, g, line, LS, [&](int cc, int k, int s, double2 a, double2 b) {
-      const int o = ri.ofwd(g, s);
-      if (cc == 0) {
-        Mo[2 * MF + o] = a;
-        zv[s] = b;
-      } else {
-        Mo[3 * MF + o] = cmul_i(a, -(k * g.mk));
-        Mo[4 * MF + o] = b;
-      }
-    });
-    double2 kv[8];
-#pragma unroll
-    for (int s = 0; s < 8; ++s) kv[s] = make_double2(kk2[s], 0.0);
-    lds_barrier();  // split_pairs' mirror reads are done: line buffer 2 is free
-    if (more) dma_uvh(yn);
-    fftw_dit<W, -1, 1, false, false, SW_ROW_TW_SHARE, true>(reinterpret_cast<double2(&)[1][8]>(kv), t, wt, tq,
-                                                            line, LS);
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const int k = t + s * NT;
-      if (R::fwd_any(g, s) && k < kc) {
-        const int o = ri.ofwd(g, s);
-        Mo[o] = cadd(cmul_i(kv[s], -(k * g.mk)), zv[s]);
-        Mo[MF + o] = kv[s];
-      }
-    }
-    if (!more) break;
-    // the next row's LDS-DMA (older than the K and P stores just issued) has landed
-    if (kc >= 2 * NT) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    v = vn;
-    y = yn;
-  }
-}
-
-// ===========================================================================
 // 2LQG / MultiLayerQG row with half-length real transforms.  Each real line
 // of N = nx points travels alone as one complex line of M = N/2 points,
 // z[m] = x[2m] + i x[2m+1] (W = exp(-2πi/N), all transforms unnormalised):
@@ -3116,34 +2925,6 @@ static bool row_prunable(const Geom& g) {
   return SW_ROW_PRUNE && roww<L>() > 0 && 8 * g.kc <= 3 * g.nx;
 }
 
-// the persistent LDS-DMA RSW row (k_row_rsw_dma): its length, the staging
-// fitting line buffer 2 (3 kc entries) and the Uy region, and slots 0, 1 live
-// on every thread (the vmcnt(4) count); SW_ROW_DMA=0 in the environment: k_row
-static bool row_dma_env() {
-  const char* e = getenv("SW_ROW_DMA");  // read per launch: the A/B test toggles it in one process
-  return e ? atoi(e) != 0 : true;
-}
-template <int L>
-static bool row_dma_ok(const Geom& g) {
-  if constexpr (!row_dma_len<L>()) {
-    return false;
-  } else {
-    using D = RowDma<L>;
-    return row_dma_env() && 3 * g.kc <= D::LS && g.kc <= D::US && g.kc >= 2 * D::NT;
-  }
-}
-// two persistent blocks per CU (the LDS of two: 2 × 75 KB), a multiple of 8
-// so that each block keeps its XCD's rows (col_of_block over the rows)
-static int row_dma_grid(int nrows) {
-  static const int cus = [] {
-    int dev = 0, n = 256;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-    return n;
-  }();
-  const int gsz = (2 * cus) & ~7;
-  return nrows < gsz ? nrows : gsz;
-}
-
 template <int L>
 void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, double2* Mo, const double2* tw,
                     hipStream_t s, int y0, int nrows, double2* Ma) {
@@ -3160,11 +2941,7 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
       hipLaunchKernelGGL((k_row_rsw_h<L>), dim3(nrows / nbr), dim3(RowH<L>::NTH * nbr),
                          nbr * rsw_rowh_lines<L>() * FftPlan<L - 1>::LDS * sizeof(double2), s, g, p, Mi, Mo,
                          tw, y0);
-    else if (row_dma_ok<L>(g) && row_prunable<L>(g)) {
-      if constexpr (row_dma_len<L>())
-        hipLaunchKernelGGL((k_row_rsw_dma<L>), dim3(row_dma_grid(nrows)), dim3(FftPlan<L>::NT), RowDma<L>::SMEM, s,
-                           g, p, Mi, Mo, tw, y0, nrows);
-    } else if (row_prunable<L>(g))
+    else if (row_prunable<L>(g))
       hipLaunchKernelGGL((k_row<MODEL_RSW, L, false, true>), dim3(nrows / BR::NB), dim3(BR::THREADS), sh_rsw, s, g,
                          p, Mi, Mo, tw, y0, nullptr);
     else

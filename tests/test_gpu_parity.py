@@ -174,30 +174,6 @@ def test_determinism_2048():
     b.close()
 
 
-@pytest.mark.parametrize("slabs", [1, 2])
-def test_row_dma_equals_k_row_2048(slabs, monkeypatch):
-    """The persistent LDS-DMA RSW row (k_row_rsw_dma, the default at 2048
-    points) and k_row (SW_ROW_DMA=0) give bitwise-identical states: the same
-    arithmetic, only the inputs' path into registers differs.  At 2048², the
-    metric configuration, over the Euler start-up and AB3 steps, on one slab
-    and on two (in-process; the row pass then runs per slab with 1024 rows)."""
-    from juliaraytracingsw_amd import drivers
-
-    dec = None if slabs == 1 else dict(nranks=slabs, local_slabs=slabs)
-    a, _ = drivers.rsw_problem(2048, "FilteredAB3", decomposition=dec)
-    monkeypatch.setenv("SW_ROW_DMA", "0")
-    b, _ = drivers.rsw_problem(2048, "FilteredAB3", decomposition=dec)
-    for n in (2, 5):
-        monkeypatch.delenv("SW_ROW_DMA", raising=False)
-        a.stepforward(n)
-        monkeypatch.setenv("SW_ROW_DMA", "0")
-        b.stepforward(n)
-        assert np.array_equal(a.sol, b.sol), n
-    monkeypatch.delenv("SW_ROW_DMA", raising=False)
-    a.close()
-    b.close()
-
-
 def test_physical_and_energy():
     """updatevars! (rsw/RotatingShallowWater.jl:101-116) and KE/PE (:323-336)."""
     from juliaraytracingsw_amd import rotating_shallow_water as RSW

@@ -3,7 +3,7 @@
 # (k_row_rsw_dma) against SW_ROW_DMA=0 (k_row)
 set -o pipefail
 O=gpurun_out/r05/dma; mkdir -p $O
-strings juliaraytracingsw_amd/libsw.so | grep -q k_row_rsw_dma || { echo "stale libsw.so"; exit 3; }
+python -c "import sys; sys.exit(0 if b'k_row_rsw_dma' in open('juliaraytracingsw_amd/libsw.so','rb').read() else 1)" || { echo "stale libsw.so"; exit 3; }
 timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_parity.py \
   tests/test_gpu_aliased.py tests/test_gpu_large.py \
   -k "row_dma or large or determinism or checkpoint or config5" > $O/tests.txt 2>&1 || { tail -30 $O/tests.txt; exit 1; }
