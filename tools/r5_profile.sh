@@ -1,0 +1,15 @@
+# round 5 profiles: every BASELINE configuration warm (tools/profile_round.sh),
+# the default bench command under rocprofv3 --kernel-trace --stats, then the
+# N = 8 bench line rehearsed on this one GPU over gloo (config 4 on ranks 0-3)
+set -o pipefail
+export TMPDIR=/tmp
+bash tools/profile_round.sh r05 || exit 1
+O=gpurun_out/r05
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_bench -o run -- \
+  python bench.py --no-cpu-baseline > $O/bench_traced.json 2> $O/bench_traced.err || exit 2
+cp $(find $O/trace_bench -name '*kernel_stats.csv') $O/kernel_stats_bench.csv || exit 3
+rm -rf $O/trace_bench
+SW_BENCH_BACKEND=gloo timeout -k 10 600 python bench.py --gpus 8 --steps 10 --warmup 2 --no-config5 \
+  --config4-steps 3 --no-cpu-baseline --no-cold-profile > $O/bench_gloo8_rehearsal.json 2> $O/bench_gloo8.err \
+  || { tail -20 $O/bench_gloo8.err; exit 4; }
+python -c "import json; b=json.load(open('$O/bench_gloo8_rehearsal.json')); print(b['n_gpus'], b['config']['parallelism'], b['slab_error'], b['config4']['n_gpus'], b['config4']['ranks_idle'], b['config4']['value'])"
