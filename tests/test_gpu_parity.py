@@ -174,6 +174,32 @@ def test_determinism_2048():
     b.close()
 
 
+def test_rsw_eta_floor_at_the_driver_state():
+    """the RSW row transforms η + iζ as one complex line,
+    so η carries an absolute error ~ eps·max|ζ̂| from the pair split — a floor
+    relative to η of ~ eps·|ζ|/|η|, state-dependent.  At the metric
+    configuration's own state (RSWDriver IC at 2048², 20 FilteredAB3 steps,
+    |ζ|/|η| ≈ 60), each field's error against the oracle relative to that
+    field's own magnitude: η within 1e-12 (the SURVEY metric divides by the
+    largest field, which hides η's share), u and v within 1e-12 too."""
+    p = sw_cases.case_params("rsw_fab3", 2048)
+    pr = sw_cases.oracle_problem(p)
+    pr.set_solution(sw_cases.initial_condition(p, pr.grid))
+    prob = sw_cases.libsw_problem(p)
+    prob.sol = pr.sol
+    pr.stepforward(20)
+    prob.stepforward(20)
+    got, ref, m = prob.sol, pr.sol, pr.grid.live
+    rel = [float(np.max(np.abs(np.where(m, got[f] - ref[f], 0))) / np.max(np.abs(np.where(m, ref[f], 0))))
+           for f in range(3)]
+    v = O.rsw_updatevars(ref.copy(), pr.grid, pr.params)
+    ratio = float(np.max(np.abs(v["zeta"])) / np.max(np.abs(v["eta"])))
+    print(f"[eta floor] per-field relative errors u {rel[0]:.2e} v {rel[1]:.2e} eta {rel[2]:.2e}; "
+          f"max|zeta| / max|eta| = {ratio:.1f}")
+    assert max(rel) < 1e-12, rel
+    prob.close()
+
+
 def test_physical_and_energy():
     """updatevars! (rsw/RotatingShallowWater.jl:101-116) and KE/PE (:323-336)."""
     from juliaraytracingsw_amd import rotating_shallow_water as RSW
