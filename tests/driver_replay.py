@@ -10,6 +10,7 @@ text), plus host stand-ins for the FourierFlows objects the drivers touch
 ``start!`` bodies statement by statement, at test sizes:
 
 * ``rsw_driver_start``   rsw/RSWDriver.jl:134-226 (T = Float32, dev = GPU())
+* ``two_layer_driver_start`` swqg/TwoLayerDriver.jl:10-117 (T = Float32, dev = GPU())
 * ``ty_driver_start``    thomasyamada/TYdriver.jl:111-231 (ARGS = ["GPU"];
                          the second Problem(CPU()) with LIBSW_CPU=1)
 * ``mlqg_simulation_start`` simulation/TwoLayerSimulation.jl:13-143
@@ -331,6 +332,27 @@ def rsw_problem(tw, *, nx=128, ny=None, Lx=2 * np.pi, Ly=None, nu=1.0e-16, nnu=4
     return owned_problem(owner, np.zeros(eq.dims, eq.T), Clock(T, dt), eq, grid, vars_, params, ts)
 
 
+def qg2_problem(tw, *, nx=128, ny=None, Lx=2 * np.pi, Ly=None, U=0.5, mu=1e-2, nu=1e-6, nnu=4, f0=3.0, Cg=1.0,
+                drhorho0=0.2, stepper="IFMAB3", dt=5e-2, aliased_fraction=1 / 3, T=np.float32, use_filter=False,
+                **skw):
+    """SWLib.qg2_problem (swqg/TwoLayerQG.jl:55-90 keywords; Params(T(U),
+    T(μ), T(ν), nν, T(2 f0²/Cg²/δρρ0)) as the reference rounds them)."""
+    ny = nx if ny is None else ny
+    Ly = Lx if Ly is None else Ly
+    grid = O.TwoDGrid(nx, Lx, ny=ny, Ly=Ly, aliased_fraction=aliased_fraction)
+    params = types.SimpleNamespace(U=T(U), μ=T(mu), ν=T(nu), nν=nnu, F=T(2 * f0 ** 2 / Cg ** 2 / drhorho0))
+    owner = Owner(tw)
+    vars_ = _host_vars(grid, T, ("ψh", "qh", "ζh", "uh", "vh"), ("ψ", "q", "ζ", "u", "v"), nlayers=2, owner=owner)
+    eq = Equation(T, (2, grid.nl, grid.nkr))
+    cfg = tw.config(_lib.SW_MODEL_QG2, stepper, nx=nx, ny=ny, Lx=Lx, Ly=Ly, aliased_fraction=aliased_fraction,
+                    dt=dt, T=T)
+    cfg.U, cfg.mu, cfg.nu, cfg.nnu, cfg.F = float(params.U), float(params.μ), float(params.ν), nnu, float(params.F)
+    filters = stepper in ("FilteredAB3", "FilteredRK4") or use_filter
+    fkw = tw.set_filter(cfg, use_filter, **skw)
+    ts = tw.SWStepper(cfg, eq, _filter(grid, 2, filters, T, **fkw))
+    return owned_problem(owner, np.zeros(eq.dims, eq.T), Clock(T, dt), eq, grid, vars_, params, ts)
+
+
 def ty_problem(tw, *, nx=128, ny=None, Lx=2 * np.pi, Ly=None, nu=3.5e-25, nnu=8, Ro=0.2, stepper="ETDRK4",
                dt=5e-2, aliased_fraction=1 / 3, T=np.float64):
     """SWLib.ty_problem (thomasyamada/ThomasYamada.jl:55-74)."""
@@ -384,6 +406,22 @@ def rsw_updatevars(tw, prob):
     tw.physical(v.ζ, ts, 3)
 
 
+def qg2_updatevars(tw, prob):
+    """SWLib.qg2_updatevars! (swqg/TwoLayerQG.jl:113-129)"""
+    v, g, sol, p, ts = prob.vars, prob.grid, prob.sol, prob.params, prob.timestepper
+    tw.sync(prob)
+    g.dealias(sol)  # :115
+    ts.rec_step = -1
+    v.qh[...] = sol
+    v.ψh[...] = O.qg2_streamfunction(v.qh.astype(np.complex128), g, O.QG2Params(p.U, p.μ, p.ν, p.nν, F=p.F))
+    v.ζh[...] = -g.Krsq * v.ψh
+    v.uh[...] = -1j * g.l[:, None] * v.ψh
+    v.vh[...] = 1j * g.kr[None, :] * v.ψh
+    for layer in range(2):
+        for field, fid in ((v.q, 4), (v.ψ, 5), (v.ζ, 3), (v.u, 0), (v.v, 1)):
+            tw.physical(field[layer], ts, 8 * layer + fid)
+
+
 def ty_updatevars(tw, prob, all_=True):
     v, g, sol, ts = prob.vars, prob.grid, prob.sol, prob.timestepper
     tw.sync(prob)
@@ -424,6 +462,12 @@ def rsw_set_solution(tw, prob, u0h, v0h, eta0h):
     prob.sol[0], prob.sol[1], prob.sol[2] = u0h, v0h, eta0h
     tw.load_solution(prob)
     rsw_updatevars(tw, prob)
+
+
+def qg2_set_solution(tw, prob, q0h):
+    prob.sol[...] = q0h
+    tw.load_solution(prob)
+    qg2_updatevars(tw, prob)
 
 
 def ty_set_solution(tw, prob, z0h, u0h, v0h, p0h):
@@ -508,6 +552,58 @@ def rsw_driver_start(tw, nx=128, nsteps=240, output_freq=20, diags_freq=10, spin
         if np.any(np.isnan(prob.vars.η)):
             raise BlewUp(prob.clock.step, outputs, diags, prob, ic)
         rsw_updatevars(tw, prob)
+        if prob.clock.step >= spinup_step:
+            outputs.append((prob.clock.step, prob.sol.copy()))
+    return prob, diags, outputs, ic, cfls
+
+
+def two_layer_driver_start(tw, nx=128, nsteps=240, output_freq=20, diags_freq=10, spinup_step=120, seed=1234,
+                           T=np.float32, parameters=None):
+    """swqg/TwoLayerDriver.jl:10-117 with swqg/TwoLayerParameters.jl values,
+    dev = GPU(), T = Float32, stepper IFMAB3; nsteps / output_freq /
+    diags_freq at test size; `parameters` overrides TwoLayerParameters.jl
+    entries (L, nnu, nutune, cfltune, ug, f, Cg, rd, lv, af)."""
+    P = dict(L=2 * np.pi, nnu=4, nutune=40.0, cfltune=0.025, ug=0.025, f=3.0, Cg=1.0, rd=1 / 6, lv=1.0, af=1 / 3)
+    P.update(parameters or {})
+    # initialize_problem (:29-68)
+    d = O.qg2_driver_params(nx, Lx=P["L"], aliased_fraction=P["af"], nnu=P["nnu"], nutune=P["nutune"],
+                            cfltune=P["cfltune"], ug=P["ug"], f=P["f"], Cg=P["Cg"], rd=P["rd"], lv=P["lv"])
+    prob = qg2_problem(tw, Lx=P["L"], nx=nx, dt=d["dt"], f0=P["f"], Cg=P["Cg"], U=d["U"], drhorho0=d["drhorho0"],
+                       T=T, nnu=P["nnu"], nu=d["nu"], mu=d["mu"], aliased_fraction=P["af"], stepper="IFMAB3",
+                       use_filter=False)
+    grid, params = prob.grid, prob.params
+    # set_seed_initial_condition! (:10-15): the host FFTW r2c of the seeded PV
+    qg2_set_solution(tw, prob, O.qg2_seed_ic(grid, np.random.default_rng(seed)))
+    ic = prob.sol.copy()
+    op = O.QG2Params(params.U, params.μ, params.ν, params.nν, F=params.F)
+
+    def host_kinetic_energy(pr):  # swqg/TwoLayerQG.jl:230-246 (the reference's method)
+        return O.qg2_energies(pr.sol.copy(), grid, op)[0]
+
+    def host_potential_energy(pr):  # :248-252
+        return O.qg2_energies(pr.sol.copy(), grid, op)[1]
+
+    kinetic_energy = tw.energy_method(host_kinetic_energy, lambda r: (r.ke, r.ke2))
+    potential_energy = tw.energy_method(host_potential_energy, lambda r: r.pe)
+    diags = [Diagnostic(kinetic_energy, prob, nsteps=nsteps, freq=diags_freq),
+             Diagnostic(potential_energy, prob, nsteps=nsteps, freq=diags_freq)]
+    # enforce_reality_condition! (swqg/TwoLayerQG.jl:139-150): the reference's
+    # method; its updatevars! is the libsw one, fwdtransform! FFTW on the host
+    grid.dealias(prob.sol)
+    prob.vars.qh[...] = prob.sol
+    qg2_updatevars(tw, prob)
+    prob.vars.qh[...] = grid.rfft(prob.vars.q)
+    prob.vars.ψh[...] = grid.rfft(prob.vars.ψ)
+    outputs = [("problem",), (prob.clock.step, prob.sol.copy())]
+    cfls = []
+    for step in range(0, round(nsteps / output_freq) + 1):
+        if step % 100 == 0:
+            v = prob.vars
+            cfls.append(float(prob.clock.dt) * max(np.max(np.abs(v.u)) / grid.dx, np.max(np.abs(v.v)) / grid.dy))
+        ff_stepforward(tw, prob, diags, output_freq)
+        if np.any(np.isnan(prob.vars.q)):  # :106
+            raise BlewUp(prob.clock.step, outputs, diags, prob, ic)
+        qg2_updatevars(tw, prob)
         if prob.clock.step >= spinup_step:
             outputs.append((prob.clock.step, prob.sol.copy()))
     return prob, diags, outputs, ic, cfls

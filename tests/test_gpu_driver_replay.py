@@ -153,6 +153,97 @@ def test_rsw_driver_blowup_throws_on_its_frame():
     p2.timestepper.finalizer()
 
 
+def test_two_layer_driver_float32_replay():
+    """TwoLayerDriver.start! (swqg/TwoLayerDriver.jl:10-117): dev = GPU(),
+    T = Float32, IFMAB3, KE/PE Diagnostics, frames of output_freq steps, the
+    NaN scan of vars.q (a 3-D SWField of the two layers) after each frame."""
+    tw = R.Twin()
+    nsteps, ofreq, dfreq = 240, 20, 10
+    prob, diags, outputs, ic, cfls = R.two_layer_driver_start(tw, nx=128, nsteps=nsteps, output_freq=ofreq,
+                                                              diags_freq=dfreq, spinup_step=120)
+    nframes = round(nsteps / ofreq) + 1
+    total = nframes * ofreq
+    c = tw.calls
+    i = _sub(c, ["sw_set_state", "sw_get_state", "sw_set_clock"] + ["sw_get_physical"] * 10)
+    assert i >= 0, "set_solution! (load_solution! + updatevars!: 5 fields x 2 layers)"
+    frame = ["sw_step_record"] * (ofreq // dfreq) + ["sw_get_state"] + ["sw_get_physical"] * 10
+    first = _sub(c, frame)
+    assert first > i
+    full = nsteps // ofreq
+    late = ["sw_step", "sw_get_state"] + ["sw_get_physical"] * 10
+    assert c[first:] == frame * full + late * (nframes - full)
+    assert c.count("sw_get_state") == 1 + nframes  # none per step
+    assert prob.sol.dtype == np.complex64 and prob.vars.q.dtype == np.float32
+    assert prob.clock.step == total
+    # the oracle from the same Float32 state, the Problem's Float32 parameters
+    p = prob.params
+    op = O.QG2Params(float(p.U), float(p.μ), float(p.ν), p.nν, F=float(p.F))
+    pr = O.Problem("qg2", "IFMAB3", 128, float(prob.clock.dt), params=op)
+    pr.set_solution(ic.astype(np.complex128))
+    ke, pe = [], []
+    for s in range(total):
+        pr.stepforward(1)
+        if (s + 1) % dfreq == 0:  # 2LQG energies read prob.sol after the step
+            (k1, k2), e = O.qg2_energies(pr.grid.dealias(pr.sol.copy()), pr.grid, op)
+            ke.append((k1, k2))
+            pe.append(e)
+    assert O.parity_error(prob.sol.astype(np.complex128), pr.sol, pr.grid) < 2e-7
+    n = diags[0].i - 1
+    assert n == len(diags[0].t) - 1
+    got_ke = np.array([np.array(x, float) for x in diags[0].data[1:1 + n]])
+    assert np.allclose(got_ke, np.array(ke[:n]), rtol=2e-7, atol=0)
+    assert np.allclose(np.array(diags[1].data[1:1 + n], float), pe[:n], rtol=2e-7, atol=0)
+    # the physical PV the driver scans (updatevars! after the last frame)
+    q1 = pr.grid.irfft(pr.grid.dealias(pr.sol.copy())[0])
+    assert np.max(np.abs(prob.vars.q[0] - q1)) < 1e-6 * np.max(np.abs(q1))
+    assert len(cfls) == 1 and 0 < cfls[0] < 1
+    prob.timestepper.finalizer()
+
+
+def test_two_layer_driver_blowup_throws_on_its_frame():
+    """TwoLayerDriver's cadence (swqg/TwoLayerParameters.jl: diag_dt = 0.5/f
+    against output_dt = 0.025/f, 20×) with the CFL raised to 1: the IFMAB3
+    advection goes unstable mid-run; the NaN scan of vars.q
+    (swqg/TwoLayerDriver.jl:106) runs the frame's steps and throws on the frame
+    where the state went non-finite, with every snapshot finite."""
+    tw = R.Twin()
+    ofreq, dfreq = 20, 400
+    with pytest.raises(R.BlewUp) as ei:
+        R.two_layer_driver_start(tw, nx=128, nsteps=3000, output_freq=ofreq, diags_freq=dfreq, spinup_step=0,
+                                 parameters=dict(cfltune=1.0))
+    bu = ei.value
+    prob = bu.prob
+    # the first non-finite step, from the same Float32 state and parameters on
+    # a second context stepped one sw_step at a time
+    tw2 = R.Twin()
+    d = O.qg2_driver_params(128, cfltune=1.0)
+    p2 = R.qg2_problem(tw2, nx=128, dt=d["dt"], f0=3.0, Cg=1.0, U=d["U"], drhorho0=d["drhorho0"], mu=d["mu"],
+                       nu=d["nu"], nnu=4, T=np.float32, stepper="IFMAB3")
+    for a, b in ((p2.params.U, prob.params.U), (p2.params.μ, prob.params.μ), (p2.params.ν, prob.params.ν),
+                 (p2.params.F, prob.params.F), (p2.clock.dt, prob.clock.dt)):
+        assert a == b
+    p2.sol[...] = bu.ic
+    tw2.load_solution(p2)
+    first = None
+    for k in range(1, 3001):
+        rc = tw2.c("sw_step", p2.timestepper.ctx, 1)
+        if rc == R.SW_E_NAN:
+            first = k
+            break
+        assert rc == 0
+    assert first is not None and first > 3 * ofreq, first
+    assert bu.step == -(-first // ofreq) * ofreq, (bu.step, first)
+    snaps = bu.outputs[1:]
+    assert len(snaps) == bu.step // ofreq
+    assert all(np.all(np.isfinite(o[1])) for o in snaps)
+    c = tw.calls
+    assert c.count("sw_get_state") == 1 + (bu.step // ofreq - 1)
+    assert c[-1] == "sw_step"
+    assert np.all(np.isnan(prob.vars.q))
+    prob.timestepper.finalizer()
+    p2.timestepper.finalizer()
+
+
 def test_ty_driver_replay():
     tw = R.Twin()
     sp, sdiags, diags, _, outputs, ic, startup_steps = R.ty_driver_start(
