@@ -195,10 +195,10 @@ function config(model, stepper::AbstractString; nx, ny, Lx, Ly, aliased_fraction
     cfg.aliased_fraction, cfg.dt = aliased_fraction, T(dt)
     cfg.precision = T == Float32 ? SW_PREC_F32 : SW_PREC_F64
     cfg.device = parse(Int32, get(ENV, "LIBSW_DEVICE", "0"))
-    # LIBSW_ALIASED_STATE=1: RotatingShallowWater's / TwoLayerQG's / ThomasYamada's prob.sol,
-    # calcN! and energies on the full array, the modes the 2/3 rule removes
-    # included (include/sw.h)
-    model in (SW_MODEL_RSW, SW_MODEL_QG2, SW_MODEL_TY) &&
+    # LIBSW_ALIASED_STATE=1: RotatingShallowWater's / TwoLayerQG's / ThomasYamada's /
+    # MultiLayerQG's prob.sol, calcN! and energies on the full array, the modes
+    # dealias! removes included (include/sw.h)
+    model in (SW_MODEL_RSW, SW_MODEL_QG2, SW_MODEL_TY, SW_MODEL_MLQG) &&
         (cfg.aliased_state = get(ENV, "LIBSW_ALIASED_STATE", "0") == "1" ? 1 : 0)
     return cfg
 end
@@ -513,11 +513,12 @@ function ty_updatevars!(prob; all=true)
     return nothing
 end
 
-# GeophysicalFlows MultiLayerQG.updatevars!: qh = sol, ψh = S⁻¹ qh, uh, vh,
-# then q, ψ, u, v per layer
+# GeophysicalFlows MultiLayerQG.updatevars!: dealias!(sol), qh = sol, ψh = S⁻¹ qh,
+# uh, vh, then q, ψ, u, v per layer
 function mlqg_updatevars!(M, prob)
     vars, grid, sol, params, ts = prob.vars, prob.grid, prob.sol, prob.params, prob.timestepper
     sync!(prob)
+    FourierFlows.dealias!(sol, grid)   # (the device's copy is dealiased by sw_get_physical)
     ts.rec_step = -1
     @. vars.qh = sol
     M.streamfunctionfrompv!(vars.ψh, vars.qh, params, grid)

@@ -725,7 +725,7 @@ bool fwd_step_lds(const sw_ctx* c) {
 void set_alias_nbuf(sw_ctx* c) {
   if (!c->alias) return;
   const int st = c->cfg.stepper;
-  const bool sep = st == SW_STEP_IFMRK4 || st == SW_STEP_ETDRK4;  // N into its own buffer
+  const bool sep = st == SW_STEP_IFMRK4 || st == SW_STEP_ETDRK4 || st == SW_STEP_FILTERED_RK4;  // N into its own buffer
   for (Slab& s : c->sl)
     for (int r = 0; r < 2; ++r) s.a_nbuf[r] = sep ? s.a_n[r] : s.a_hist[c->head][r];
 }
@@ -737,7 +737,7 @@ sw::StepPtrs alias_step_ptrs(const sw_ctx* c, const Slab& s, int r) {
   a.xs = s.a_xs[r];
   a.euler = (c->step < 3 || c->euler_left > 0) ? 1 : 0;
   a.stream = 0;
-  if (c->cfg.stepper == SW_STEP_IFMRK4) {
+  if (c->cfg.stepper == SW_STEP_IFMRK4 || c->cfg.stepper == SW_STEP_FILTERED_RK4) {
     a.h0 = s.a_acc[r];
   } else if (c->cfg.stepper == SW_STEP_ETDRK4) {
     a.h0 = s.a_acc[r];
@@ -855,11 +855,21 @@ int run_stage(sw_ctx* c, int op, int stage, double2* Slab::*X) {
         b.stage = stage;
         sw::launch_step_elem(c->nf, op, s.ga[r], c->p, b, s.a_nbuf[r], s.a_xs[r], c->stream);
         if (c->cfg.nop_calcN) HIPCHK(c, hipMemsetAsync(s.a_zero[r], 0, cb, c->stream));
+        // FilteredRK4 adds L·x of the stage input x, which the reference's
+        // next calcN! has dealiased in place (zero here) before
+        // addlinearterm! reads it: the stage input there is discarded
+        if (op == sw::OP_FRK4 && stage < 4) HIPCHK(c, hipMemsetAsync(s.a_xs[r], 0, cb, c->stream));
       }
     }
     c->mixed_valid = false;
   }
   return 0;
+}
+
+// aliased-state energies: 2LQG's, Thomas–Yamada's and MultiLayerQG's energy
+// functions read the full post-step array (RSW's the dealiased vars.uh)
+bool alias_energy(const sw_ctx* c) {
+  return c->alias && (c->cfg.model == SW_MODEL_QG2 || c->cfg.model == SW_MODEL_TY || c->cfg.model == SW_MODEL_MLQG);
 }
 
 // The state FF's energy diagnostics read after a step: RSW's
@@ -875,7 +885,8 @@ int alias_energy_cols(sw_ctx* c, bool post_step_state, int ncols) {
   // 2LQG energies read prob.sol (the post-step state); RSW's read vars.uh,
   // the dealiased calcN input (rsw/RotatingShallowWater.jl:323-333)
   // (Thomas–Yamada's read prob.sol too: thomasyamada/ThomasYamada.jl:333-360)
-  if (!c->alias || !post_step_state || (c->cfg.model != SW_MODEL_QG2 && c->cfg.model != SW_MODEL_TY)) return ncols;
+  // (GF MultiLayerQG.energies: qh = sol, the full array)
+  if (!c->alias || !post_step_state || !alias_energy(c)) return ncols;
   // region 0 (slab 0), then every slab's region 1 in slab order: the global
   // column order, whatever the decomposition (bitwise the same sums)
   for (int r = 0; r < 2; ++r)
@@ -887,11 +898,6 @@ int alias_energy_cols(sw_ctx* c, bool post_step_state, int ncols) {
   return ncols;
 }
 
-// aliased-state energies: 2LQG's and Thomas–Yamada's energy functions read
-// the full post-step array (RSW's the dealiased vars.uh)
-bool alias_energy(const sw_ctx* c) {
-  return c->alias && (c->cfg.model == SW_MODEL_QG2 || c->cfg.model == SW_MODEL_TY);
-}
 // energy columns of one rank's record (one slab per process): the kcl live
 // columns, then (alias_energy) region 0's nkr - kc columns (slab 0; zeros on
 // the others) and the slab's region 1 padded to kcl columns
@@ -1251,12 +1257,14 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
     const bool ab_or_if = k.stepper == SW_STEP_IFMAB3 || k.stepper == SW_STEP_IFMRK4 ||
                           k.stepper == SW_STEP_FILTERED_AB3;
     if (!(((k.model == SW_MODEL_QG2 || k.model == SW_MODEL_RSW) && ab_or_if) ||
-          (k.model == SW_MODEL_TY && k.stepper == SW_STEP_ETDRK4)))
+          (k.model == SW_MODEL_TY && k.stepper == SW_STEP_ETDRK4) || k.model == SW_MODEL_MLQG))
       return fail(c, SW_E_INVALID,
-                  "aliased_state: RSW or 2LQG with IFMAB3, IFMRK4 or FilteredAB3, or Thomas-Yamada with ETDRK4");
+                  "aliased_state: RSW or 2LQG with IFMAB3, IFMRK4 or FilteredAB3, Thomas-Yamada with ETDRK4, "
+                  "or MultiLayerQG");
     // (one slab per process: region 0's y-transforms need every row of the
     // row pass's aliased x-spectra, all-gathered per calcN)
-    if (!sw::row_alias_built(k.model == SW_MODEL_RSW ? sw::MODEL_RSWA : k.model, ilog2(k.nx)))
+    const int amodel = k.model == SW_MODEL_RSW ? sw::MODEL_RSWA : k.model == SW_MODEL_MLQG ? sw::MODEL_QG2 : k.model;
+    if (!sw::row_alias_built(amodel, ilog2(k.nx)))
       return fail(c, SW_E_INVALID, "aliased_state: the row pass's aliased output is not built at this nx");
   }
   const int P = k.nranks;
@@ -1406,7 +1414,8 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
       const size_t cb = (size_t)c->nf * s.ga[r].cfield * sizeof(double2);
       for (double2** q : {&s.a_sol[r], &s.a_zero[r], &s.a_xs[r]})
         if ((rc = alloc(c, (void**)q, cb))) return rc;
-      if (k.stepper == SW_STEP_IFMRK4 || k.stepper == SW_STEP_ETDRK4) {
+      const bool rk = k.stepper == SW_STEP_IFMRK4 || k.stepper == SW_STEP_FILTERED_RK4;
+      if (rk || k.stepper == SW_STEP_ETDRK4) {
         if ((rc = alloc(c, (void**)&s.a_acc[r], cb))) return rc;
         if ((rc = alloc(c, (void**)&s.a_n[r], cb))) return rc;
       }
@@ -1416,7 +1425,7 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
         if ((rc = alloc(c, (void**)&s.a_etd[r], (size_t)sw::ETD_N * s.ga[r].cfield * sizeof(double)))) return rc;
         sw::launch_etd_coeffs(s.ga[r], c->p, s.a_etd[r], c->stream);
         HIPCHK(c, hipGetLastError());
-      } else if (k.stepper != SW_STEP_IFMRK4) {
+      } else if (!rk) {
         for (int i = 0; i < 3; ++i)
           if ((rc = alloc(c, (void**)&s.a_hist[i][r], cb))) return rc;
       }

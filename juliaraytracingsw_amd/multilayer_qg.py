@@ -25,9 +25,13 @@ from .problem import Diagnostic, Problem as _Problem, increment, stepforward  # 
 def Problem(nlayers=2, dev="gpu", *, nx=128, ny=None, Lx=2 * np.pi, Ly=None, f0=1.0, beta=0.0,
             H=(0.5, 0.5), b=(1.0, 0.0), U=(0.0, 0.0), mu=0.0, nu=0.0, nnu=1, dt=0.01,
             stepper="FilteredRK4", aliased_fraction=1 / 3, T=np.float64, device=0, check_nan=True,
-            unfused=False, decomposition=None, **stepper_kwargs):
+            unfused=False, decomposition=None, aliased_state=False, **stepper_kwargs):
     """``MultiLayerQG.Problem(nlayers, dev; nx, Lx, f₀, H, b, U, μ, β, ν, nν, dt,
-    stepper, aliased_fraction)``; nlayers must be 2 (TwoLayerSimulation's)."""
+    stepper, aliased_fraction)``; nlayers must be 2 (TwoLayerSimulation's).
+    ``aliased_state=True`` also carries the modes dealias! removes (with
+    aliased_fraction = 0 the Nyquist column and row), as GF's prob.sol holds
+    them between steps: calcN! returns N there and the FilteredRK4 update
+    writes filter·dt·(N₁/6 + N₂/3 + N₃/3 + N₄/6) into them."""
     if nlayers != 2:
         raise _lib.LibSWError("libsw's MultiLayerQG has nlayers = 2")
     if dev not in ("gpu", "GPU", "GPU()"):
@@ -38,7 +42,8 @@ def Problem(nlayers=2, dev="gpu", *, nx=128, ny=None, Lx=2 * np.pi, Ly=None, f0=
                   nu=float(nu), nnu=int(nnu))
     prob = _Problem(_lib.SW_MODEL_MLQG, nx=nx, ny=ny, Lx=Lx, Ly=Ly, dt=dt, aliased_fraction=aliased_fraction,
                     stepper=stepper, params=params, filter_kw=stepper_kwargs, device=device,
-                    check_nan=check_nan, T=T, unfused=unfused, **(decomposition or {}))
+                    check_nan=check_nan, T=T, unfused=unfused, aliased_state=aliased_state,
+                    **(decomposition or {}))
     gp = b[0] - b[1]
     prob.params.update(F1=f0 ** 2 / (gp * H[0]), F2=f0 ** 2 / (gp * H[1]))
     return prob

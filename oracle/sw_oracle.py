@@ -726,7 +726,8 @@ class FilteredAB3:
 
     def stepforward(self, sol, clock, calcN, grid, params):
         self.RHS = calcN(sol, grid, params)
-        self.RHS += mvmul(self.L, sol)                  # addlinearterm! (matvec)
+        # addlinearterm! (matvec; a diagonal L — MultiLayerQG's — per field)
+        self.RHS += mvmul(self.L, sol) if self.L.ndim == 4 else self.L * sol
         if clock.step < 3:
             sol += clock.dt * self.RHS
         else:

@@ -30,11 +30,18 @@ def main():
     rank, world = dist.get_rank(), dist.get_world_size()
     import sw_cases
     import sw_oracle as O
-    from juliaraytracingsw_amd import rotating_shallow_water as RSW, slab_comm, two_layer_qg as QG2
+    from juliaraytracingsw_amd import multilayer_qg as MLQG, rotating_shallow_water as RSW, slab_comm
+    from juliaraytracingsw_amd import two_layer_qg as QG2
 
-    M = RSW if a.case.startswith("rsw") else QG2
+    M = RSW if a.case.startswith("rsw") else MLQG if a.case.startswith("mlqg") else QG2
     p = sw_cases.case_params(a.case, a.n)
-    grid = O.TwoDGrid(a.n)
+    grid = O.TwoDGrid(a.n, aliased_fraction=p.get("af", 1 / 3))
+
+    def energies(pb):  # (ΣKE, PE) of the model's energy functions
+        if M is MLQG:
+            (k1, k2), (pe,) = MLQG.energies(pb)
+            return k1 + k2, pe
+        return np.sum(M.kinetic_energy(pb)), M.potential_energy(pb)
     ic = sw_cases.initial_condition(p, grid)
     kw = dict(aliased_state=True) if a.aliased else {}
     prob = sw_cases.libsw_problem(p, decomposition=slab_comm.host_decomposition(rank, world), **kw)
@@ -49,7 +56,7 @@ def main():
     sol = prob.sol
     # (energies of prob.sol before updatevars!, which dealiases it: with
     # aliased_state they include the aliased modes)
-    ke, pe = np.sum(M.kinetic_energy(prob)), M.potential_energy(prob)
+    ke, pe = energies(prob)
     phys = M.updatevars(prob)
     recs, cfl = prob.ctx.energy_diagnostics(), M.cfl(prob)
     res = {}
@@ -60,7 +67,7 @@ def main():
         ref.ctx.set_energy_diagnostics(a.freq, cap)
         ref.stepforward(a.steps)
         rsol = ref.sol
-        rke, rpe = np.sum(M.kinetic_energy(ref)), M.potential_energy(ref)
+        rke, rpe = energies(ref)
         pr = M.updatevars(ref)
         res = dict(
             state_equal=bool(np.array_equal(sol, rsol)),
@@ -74,7 +81,7 @@ def main():
             cfl_equal=bool(cfl == M.cfl(ref)),
             world=world,
             # the largest aliased mode of the state (aliased_state: nonzero)
-            aliased_max=float(np.max(np.abs(np.where(O.TwoDGrid(a.n).dealias(np.ones_like(sol)) == 0, sol, 0)))),
+            aliased_max=float(np.max(np.abs(np.where(grid.dealias(np.ones_like(sol)) == 0, sol, 0)))),
         )
         ref.close()
     prob.close()

@@ -8,7 +8,7 @@ N), and the IF/AB3 update writes E·dt·(…N…) into prob.sol there
 which its energies (:230-252) count and the next calcN!/updatevars!
 discards.  Thomas–Yamada's calcN! and ETDRK4 update do the same
 (thomasyamada/ThomasYamada.jl:130; its energies read prob.sol).  With
-aliased_state = 1 libsw carries them too (RSW, 2LQG and TY, any
+aliased_state = 1 libsw carries them too (RSW, 2LQG, TY and MultiLayerQG, any
 nx up to 8192, one slab or several in one process); the oracle keeps the
 full arrays, so every comparison here is
 over ALL modes of the full (nkr, nl) array, at the strongly nonlinear 64²
@@ -245,10 +245,68 @@ def test_default_mode_unchanged():
     prob.close()
 
 
+@pytest.mark.parametrize("stepper,slabs", [("FilteredRK4", (1, 2)), ("FilteredAB3", (1, 2))])
+def test_mlqg_full_state(stepper, slabs):
+    """GeophysicalFlows MultiLayerQG with aliased_fraction = 0, stepped by
+    FilteredRK4 (simulation/TwoLayerSimulation.jl:37-38, Parameters.jl:25) or
+    FilteredAB3 (FreelyEvolvingSimulation.jl:38-39, FreelyEvolvingParameters
+    .jl:7).  GF's calcN! dealiases its input (the Nyquist column and row) and
+    returns N there; the update writes filter·dt·(RK4 or AB3 sum of N) into
+    prob.sol there (the stage inputs' L·x reads the dealiased zeros), with
+    the filter ≤ tol = 1e-15 at K ≥ 1: values ~1e-18 of the state, compared
+    here on their own scale.  Also: calcN on every mode, the full-array
+    energies, updatevars! clearing them, and in-process slabs bitwise."""
+    from juliaraytracingsw_amd import multilayer_qg as MLQG
+
+    p = dict(sw_cases.case_params("mlqg_frk4", 64), stepper=stepper)
+    pr = sw_cases.oracle_problem(p)
+    pr.set_solution(sw_cases.initial_condition(p, pr.grid))
+    ic = pr.sol.copy()
+    mask = _aliased_mask(pr.grid)
+    steps = 12
+    pr.stepforward(steps)
+    got = {}
+    for P in slabs:
+        prob = sw_cases.libsw_problem(p, aliased_state=True,
+                                      decomposition=None if P == 1 else dict(nranks=P, local_slabs=P))
+        prob.sol = ic
+        prob.stepforward(steps)
+        got[P] = prob.sol
+        if P != slabs[0]:
+            prob.close()
+            continue
+        keep = prob
+    for P in slabs[1:]:
+        assert np.array_equal(got[P], got[slabs[0]]), P
+    prob, sol = keep, got[slabs[0]]
+    assert _full_err(sol, pr.sol) < RTOL
+    amax = np.max(np.abs(pr.sol[:, mask]))
+    assert amax > 0  # the aliased modes are there, however small
+    aerr = np.max(np.abs(sol[:, mask] - pr.sol[:, mask])) / amax
+    print(f"[aliased] mlqg {stepper}: aliased modes {amax / np.max(np.abs(pr.sol)):.1e} of the state, "
+          f"their error {aerr:.1e} of themselves")
+    assert aerr < 1e-8
+    (k1, k2), (pe,) = MLQG.energies(prob)
+    (o1, o2), po = O.mlqg_energies(pr.sol, pr.grid, pr.params)
+    assert np.allclose([k1, k2, pe], [o1, o2, po], rtol=RTOL, atol=0)
+    x = pr.sol.copy()
+    ref = pr.calcN(x.copy(), pr.grid, pr.params)
+    gotN = prob.calcN(x)
+    nmax = np.max(np.abs(ref[:, mask]))
+    assert nmax > 1e-3 * np.max(np.abs(ref))
+    assert _full_err(gotN, ref) < RTOL
+    # (the oracle's mean-flow and background-gradient terms go through the
+    # transforms as GF's do: round-off at the Nyquist modes, ~1e-15 of N there)
+    assert np.max(np.abs(gotN[:, mask] - ref[:, mask])) < 1e-8 * nmax
+    MLQG.updatevars(prob)  # GF's updatevars! dealiases sol first
+    assert np.max(np.abs(prob.sol[:, mask])) == 0
+    prob.close()
+
+
 def test_rejected_where_not_built():
-    """Only where it is built: RSW / 2LQG with IFMAB3/IFMRK4/FilteredAB3 or
-    Thomas–Yamada with ETDRK4 (not GeophysicalFlows' FilteredRK4).  (One slab
-    per process is built: tests/test_gpu_multiprocess.py.)"""
+    """Only where it is built: RSW / 2LQG with IFMAB3/IFMRK4/FilteredAB3,
+    Thomas–Yamada with ETDRK4, MultiLayerQG (not 2LQG with FilteredRK4).
+    (One slab per process is built: tests/test_gpu_multiprocess.py.)"""
     from juliaraytracingsw_amd import _lib
 
     cfg = _lib.default_config()

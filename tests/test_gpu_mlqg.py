@@ -64,6 +64,20 @@ def test_mlqg_unequal_layers_beta_drag_viscosity():
     prob.close()
 
 
+def test_mlqg_filtered_ab3():
+    """simulation/FreelyEvolvingSimulation.jl:38-39 steps MultiLayerQG with
+    FreelyEvolvingParameters.jl:7's FilteredAB3 (aliased_fraction = 0):
+    forward Euler for clock.step < 3, AB3 after, filter after each update;
+    L = −νK^(2nν) per layer added to N (addlinearterm!)."""
+    p, pr, prob = _pair("mlqg_frk4", 128, stepper="FilteredAB3", nu=1e-16, nnu=4)
+    for nsteps in (1, 2, 4):
+        pr.stepforward(nsteps)
+        prob.stepforward(nsteps)
+        e = O.parity_error(prob.sol, pr.sol, pr.grid)
+        assert e < RTOL, (nsteps, e)
+    prob.close()
+
+
 @pytest.mark.parametrize("name", ["rsw_fab3", "qg2_ifmab3"])
 def test_filtered_rk4_other_models(name):
     """FF FilteredRK4 is generic: RSW (3×3 L matvec) and 2LQG (2×2, with the

@@ -32,7 +32,10 @@ def _free_port():
                                                            # columns' x-spectra all-gathered per calcN, the
                                                            # full-array state/calcN/energies gathered
                                                            ("qg2_ifmrk4", 2, 6, 2, True), ("qg2_ifmab3", 4, 6, 2, True),
-                                                           ("rsw_fab3", 2, 6, 2, True)])
+                                                           ("rsw_fab3", 2, 6, 2, True),
+                                                           # MultiLayerQG (aliased_fraction = 0: the Nyquist
+                                                           # column on slab 0, the Nyquist row of each slab)
+                                                           ("mlqg_frk4", 2, 6, 2, True), ("mlqg_frk4", 2, 6, 2, False)])
 def test_one_process_per_slab(case, world, steps, freq, aliased, tmp_path):
     out = tmp_path / "res.json"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",

@@ -238,12 +238,12 @@ def test_per_step_seam_is_lazy():
     assert "ts.pending += 1" in body and "clock.step += 1" in body
     py = inspect.getsource(driver_replay.Twin.stepforward_seam)
     assert "self.c(" not in py and "ts.pending += 1" in py
-    # every libsw updatevars! shim syncs first (and RSW / 2LQG dealias the host
-    # sol as the reference's :104 / :115 do — ADVICE r03)
+    # every libsw updatevars! shim syncs first (and dealiases the host sol as
+    # the reference's :104 / :115 and GF's updatevars! do — ADVICE r03)
     for f in ("rsw_updatevars!", "qg2_updatevars!", "ty_updatevars!", "mlqg_updatevars!"):
         fb = re.search(rf"^function {re.escape(f)}\((.*?)\nend", s, re.S | re.M).group(1)
         assert "sync!(prob)" in fb, f
-    for f in ("rsw_updatevars!", "qg2_updatevars!", "ty_updatevars!"):
+    for f in ("rsw_updatevars!", "qg2_updatevars!", "ty_updatevars!", "mlqg_updatevars!"):
         fb = re.search(rf"^function {re.escape(f)}\((.*?)\nend", s, re.S | re.M).group(1)
         assert fb.index("sync!(prob)") < fb.index("FourierFlows.dealias!(sol, grid)") < fb.index("@. vars.")
     # after updatevars! the energy functions read the updated state (sw_diag),
