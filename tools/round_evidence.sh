@@ -1,10 +1,12 @@
-# round 5 profiles: every BASELINE configuration warm (tools/profile_round.sh),
-# the default bench command under rocprofv3 --kernel-trace --stats, then the
-# N = 8 bench line rehearsed on this one GPU over gloo (config 4 on ranks 0-3)
+# A round's profile evidence on one GPU box: every BASELINE configuration warm
+# (tools/profile_round.sh), the default bench command under rocprofv3
+# --kernel-trace --stats, then the N = 8 bench line rehearsed on this one GPU
+# over gloo (config 4 on ranks 0-3).  usage: bash tools/round_evidence.sh rNN
 set -o pipefail
 export TMPDIR=/tmp
-bash tools/profile_round.sh r05 || exit 1
-O=gpurun_out/r05
+TAG=${1:?usage: round_evidence.sh rNN}
+bash tools/profile_round.sh $TAG || exit 1
+O=gpurun_out/$TAG
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_bench -o run -- \
   python bench.py --no-cpu-baseline > $O/bench_traced.json 2> $O/bench_traced.err || exit 2
 cp $(find $O/trace_bench -name '*kernel_stats.csv') $O/kernel_stats_bench.csv || exit 3
