@@ -696,8 +696,9 @@ bool use_fused(const sw_ctx* c) {
 // k_col_fwd + k_step_elem as one column pass (k_col_step<…, INV = false>: one
 // block per column, every field's N in registers, the update at each live
 // mode, no N in HBM); the next calcN's col_inv runs separately.  Built for
-// RSW IFMAB3/IFMRK4 and 2LQG FilteredAB3/IFMAB3/IFMRK4 (not MultiLayerQG,
-// whose N adds terms from the calcN input in k_col_fwd), bitwise equal to the
+// RSW IFMAB3/IFMRK4, 2LQG FilteredAB3/IFMAB3/IFMRK4 and (round 5) MultiLayerQG
+// FilteredRK4, whose N adds k_col_fwd's terms from the calcN input
+// (mlqg_linear_terms, read per mode beside the update), bitwise equal to the
 // two kernels; used where it wins (tools/ab/fwdstep_ab.sh): 2LQG
 // FilteredAB3 on lines up to 2048 points (0 spills; 5409 -> 5601 steps/s at
 // 2048²).  The coupled IF/RK4 updates hold every field's N next to the
@@ -709,14 +710,19 @@ bool use_fwd_step(const sw_ctx* c) {
   const int m = c->cfg.model, st = c->cfg.stepper;
   const bool built = (c->kmodel == SW_MODEL_RSW && (st == SW_STEP_IFMAB3 || st == SW_STEP_IFMRK4)) ||
                      (m == SW_MODEL_QG2 && (st == SW_STEP_FILTERED_AB3 || st == SW_STEP_IFMAB3 ||
-                                            st == SW_STEP_IFMRK4));
+                                            st == SW_STEP_IFMRK4)) ||
+                     (m == SW_MODEL_MLQG && st == SW_STEP_FILTERED_RK4);
   if (!built) return false;
   if (c->fwd_step == 1) return true;
   if (c->fwd_step == 2) return fwd_step_lds(c);
   return m == SW_MODEL_QG2 && st == SW_STEP_FILTERED_AB3 && c->sl[0].g.log2ny <= 11;
 }
 // the LDS-parked variant (k_col_fwd_step_lds, SW_FWD_STEP=2) where its
-// line buffer and parked N fit one CU's 160 KB
+// line buffer and parked N fit one CU's 160 KB.  (MultiLayerQG FilteredRK4,
+// round 5: its register variant spills 16-34 VGPRs at 512-2048, the LDS one
+// none; against the separate kernels the LDS one measured 5845-6348 vs
+// 6473-6726 steps/s at 512², 3530-3563 vs 3404-3418 at 1024², 752-755 vs
+// 758-761 at 2048²: off by default)
 bool fwd_step_lds(const sw_ctx* c) {
   return c->fwd_step == 2 && sw::fwd_step_lds_bytes(c->kmodel, c->sl[0].g) <= 160 * 1024;
 }

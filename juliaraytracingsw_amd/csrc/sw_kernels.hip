@@ -63,6 +63,23 @@ __device__ __forceinline__ double2 mix_ld_col(const double2* p) {
 #endif
 }
 
+// MultiLayerQG calcN!'s terms linear in the calcN input q (layer grp): the
+// mean flow and background gradient -ik U_j q_j - ik Qy_j ψ_j, and the
+// bottom drag μ K² ψ_2 on the lower layer, added to the Jacobian part r.
+// One definition for k_col_fwd and the fused forward + update passes, so
+// both round alike.
+__device__ __forceinline__ double2 mlqg_linear_terms(const Phys& p, double k, double l, double2 q1, double2 q2,
+                                                     int grp, double2 r) {
+#pragma clang fp contract(off)
+  const double K2 = k * k + l * l;
+  double2 ps;
+  qg_psi(p, K2, q1.x, q1.y, q2.x, q2.y, grp, ps.x, ps.y);
+  const double2 qg = grp ? q2 : q1;
+  r = csub(csub(r, cmul_i(qg, k * (grp ? p.U2 : p.U1))), cmul_i(ps, k * (grp ? p.Qy2 : p.Qy1)));
+  if (grp == 1) r = cadd(r, cscale(ps, p.mu * K2));
+  return r;
+}
+
 // block -> line mapping.  When one line per block and the grid is a multiple
 // of 64, the 8 lines (columns, or rows in the row pass) that share each 128-B
 // chunk of a mixed layout are placed on blocks b, b+8, …, b+56, which the
@@ -1640,18 +1657,8 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
         double2 r = acc[s];
         if constexpr (MODEL == MODEL_QG2) {
           if (p.model == MODEL_MLQG) {
-            // MultiLayerQG calcN!: the mean flow and background-gradient
-            // terms -ik U_j q_j - ik Qy_j ψ_j, and the bottom drag μ K² ψ_2
-            // on the lower layer, from the calcN input
             const long long i = (long long)krl * g.LrP + j;
-            const double l = lwav(g, c.t + s * NT);
-            const double K2 = k * k + l * l;
-            const double2 q1 = X[i], q2 = X[g.cfield + i];
-            double2 ps;
-            qg_psi(p, K2, q1.x, q1.y, q2.x, q2.y, grp, ps.x, ps.y);
-            const double2 qg = grp ? q2 : q1;
-            r = csub(csub(r, cmul_i(qg, k * (grp ? p.U2 : p.U1))), cmul_i(ps, k * (grp ? p.Qy2 : p.Qy1)));
-            if (grp == 1) r = cadd(r, cscale(ps, p.mu * K2));
+            r = mlqg_linear_terms(p, k, lwav(g, c.t + s * NT), X[i], X[g.cfield + i], grp, r);
           }
         }
         if constexpr (MODEL == MODEL_TY) {
@@ -2241,9 +2248,17 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
       const int j = compact_of(g, m);
       if (live && j >= 0) {
         cplx n[NF], x[NF];
+        const long long i = (long long)krl * g.LrP + j;
+        if constexpr (MODEL == MODEL_QG2 && OP == OP_FRK4) {
+          if (p.model == MODEL_MLQG) {  // (k_col_fwd's terms, from this stage's calcN input)
+            const double2* Xin = a.stage == 1 ? a.sol : a.xs;
+            const double2 q1 = Xin[i], q2 = Xin[g.cfield + i];
+#pragma unroll
+            for (int f = 0; f < NF; ++f) X[f][s] = mlqg_linear_terms(p, k, lwav(g, m), q1, q2, f, X[f][s]);
+          }
+        }
 #pragma unroll
         for (int f = 0; f < NF; ++f) n[f] = cx(X[f][s].x, X[f][s].y);
-        const long long i = (long long)krl * g.LrP + j;
         step_op<NF, OP, STREAM>(g, p, a, i, k, lwav(g, m), n, x);
         if (OP == OP_RK4 && a.stage < 4) store_vec<NF>(a.xs, g.cfield, i, x);
       }
@@ -2381,12 +2396,22 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     const int j = compact_of(g, m);
     if (j >= 0) {
       cplx nn[NF], x[NF];
+      const long long i = (long long)krl * g.LrP + j;
+      double2 q1 = zero2(), q2 = zero2();
+      if constexpr (MODEL == MODEL_QG2 && OP == OP_FRK4) {
+        if (p.model == MODEL_MLQG) {
+          const double2* Xin = a.stage == 1 ? a.sol : a.xs;
+          q1 = Xin[i];
+          q2 = Xin[g.cfield + i];
+        }
+      }
 #pragma unroll
       for (int f = 0; f < NF; ++f) {
-        const double2 t = park[f * g.Lr + j];
+        double2 t = park[f * g.Lr + j];
+        if constexpr (MODEL == MODEL_QG2 && OP == OP_FRK4)
+          if (p.model == MODEL_MLQG) t = mlqg_linear_terms(p, k, lwav(g, m), q1, q2, f, t);
         nn[f] = cx(t.x, t.y);
       }
-      const long long i = (long long)krl * g.LrP + j;
       step_op<NF, OP, STREAM>(g, p, a, i, k, lwav(g, m), nn, x);
       if (OP == OP_RK4 && a.stage < 4) store_vec<NF>(a.xs, g.cfield, i, x);
     }
@@ -3072,6 +3097,7 @@ void LenOps<L>::col_fwd_step(int model, int op, const Geom& g, const Phys& p, co
   } else {
     if (op == OP_FAB3) SW_FS(MODEL_QG2, OP_FAB3);
     else if (op == OP_IFMAB3) SW_FS(MODEL_QG2, OP_IFMAB3);
+    else if (op == OP_FRK4) SW_FS(MODEL_QG2, OP_FRK4);
     else SW_FS(MODEL_QG2, OP_RK4);
   }
 #undef SW_FS

@@ -129,7 +129,7 @@ def test_nop_calcN_linear_exactness():
 
 
 @pytest.mark.parametrize("mode", ["default", "fuse_all", "fwd_step", "fwd_step_lds"])
-@pytest.mark.parametrize("name", sw_cases.CASES)
+@pytest.mark.parametrize("name", sw_cases.CASES + sw_cases.MLQG_CASES)
 def test_fused_equals_unfused(name, mode, monkeypatch):
     """The fused column passes (RSW FilteredAB3: col_fwd + update + next col_inv
     in one kernel; the coupled-update pairs: col_fwd + update in one kernel)
