@@ -74,6 +74,7 @@ struct Geom {
   // chunk by chunk).  fa = 1 (2×4 tiles) but for the 2LQG half-length rows
   // at 8192 points (fa = 2: 4×2, sw_api.cpp make_geom)
   int fsy, fsk, fa;
+  int isplit;         // 2LQG/MLQG/TY column inverse: one output per block (k_col_inv SPLIT)
 };
 
 struct Phys {

@@ -267,7 +267,12 @@ __device__ __forceinline__ void store_col_p(const Geom& g, int krl, int t, F put
 //   QG2  outputs (swqg/TwoLayerQG.jl:155-176):          0 Q1, 1 Q2, 2 Ψ1, 3 Ψ2, 4 Ψy1, 5 Ψy2
 // grid: (columns, groups); RSW group f reads field f; QG2 group = layer.
 // ===========================================================================
-template <int MODEL, int LOG2N>
+// SPLIT: one output per block — grid (columns, 3 × groups) for 2LQG /
+// MultiLayerQG (a layer's q, ψ or ∂yψ), (columns, 2 × groups) for
+// Thomas–Yamada (a group's one or two outputs) — so that small grids, whose
+// one-line blocks are a single wave, put 2-3 times the waves on the chip (the
+// same arithmetic per output; Geom::isplit, sw_api.cpp make_geom)
+template <int MODEL, int LOG2N, bool SPLIT = false>
 static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, LOG2N))
     k_col_inv(Geom g, Phys p, const double2* __restrict__ X, double2* __restrict__ M,
               const double2* __restrict__ tw, int gbase) {
@@ -287,8 +292,11 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
     krl = (q << 6) + (x << 3) + (jj >> 1);
   } else {
     krl = (B::NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * B::NB + c.ln;
-    grp = gbase + blockIdx.y;
+    constexpr int PER = MODEL == MODEL_TY ? 2 : 3;  // SPLIT: blocks per group
+    grp = gbase + (SPLIT ? (int)blockIdx.y / PER : (int)blockIdx.y);
   }
+  const int out = SPLIT ? (int)blockIdx.y % (MODEL == MODEL_TY ? 2 : 3) : -1;  // -1: every output
+  if (MODEL == MODEL_TY && out == 1 && grp == 3) return;  // (vc: one output)
   const bool live = krl < g.kcn;
   if (B::NB == 1 && !live) return;  // padding column: nobody reads it
   double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
@@ -359,31 +367,41 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
         psi[s] = v[s];
         v[s] = cscale(x[s], scale);
       }
-      col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
-      store(0);
-#pragma unroll
-      for (int s = 0; s < 8; ++s) v[s] = cscale(psi[s], scale);
-      col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
-      store(1);
-    } else if (grp == 1) {  // x = ψ
-#pragma unroll
-      for (int s = 0; s < 8; ++s) v[s] = cmul_i(x[s], -lwav(g, c.t + s * NT) * scale);
-      col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
-      store(2);
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        const double l = lwav(g, c.t + s * NT);
-        v[s] = cscale(x[s], (l * l) * scale);
+      if (out <= 0) {
+        col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
+        store(0);
       }
-      col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
-      store(3);
+      if (out != 0) {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) v[s] = cscale(psi[s], scale);
+        col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
+        store(1);
+      }
+    } else if (grp == 1) {  // x = ψ
+      if (out <= 0) {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) v[s] = cmul_i(x[s], -lwav(g, c.t + s * NT) * scale);
+        col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
+        store(2);
+      }
+      if (out != 0) {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          const double l = lwav(g, c.t + s * NT);
+          v[s] = cscale(x[s], (l * l) * scale);
+        }
+        col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
+        store(3);
+      }
     } else {
       const int o = grp == 2 ? 4 : (grp == 3 ? 6 : 7);
+      if (out <= 0) {
 #pragma unroll
-      for (int s = 0; s < 8; ++s) v[s] = cscale(x[s], scale);
-      col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
-      store(o);
-      if (grp != 3) {  // ∂y uc, ∂y pc
+        for (int s = 0; s < 8; ++s) v[s] = cscale(x[s], scale);
+        col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
+        store(o);
+      }
+      if (grp != 3 && out != 0) {  // ∂y uc, ∂y pc
 #pragma unroll
         for (int s = 0; s < 8; ++s) v[s] = cmul_i(x[s], lwav(g, c.t + s * NT) * scale);
         col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
@@ -411,16 +429,22 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
       qg_psi(p, K2, q1.x, q1.y, q2.x, q2.y, grp, psi[s].x, psi[s].y);
       v[s] = cscale(qg, scale);
     }
-    col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
-    store(grp);
+    if (out <= 0) {
+      col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
+      store(grp);
+    }
+    if (out < 0 || out == 1) {
 #pragma unroll
-    for (int s = 0; s < 8; ++s) v[s] = cscale(psi[s], scale);
-    col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
-    store(2 + grp);
+      for (int s = 0; s < 8; ++s) v[s] = cscale(psi[s], scale);
+      col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
+      store(2 + grp);
+    }
+    if (out < 0 || out == 2) {
 #pragma unroll
-    for (int s = 0; s < 8; ++s) v[s] = cmul_i(psi[s], lwav(g, c.t + s * NT) * scale);
-    col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
-    store(4 + grp);
+      for (int s = 0; s < 8; ++s) v[s] = cmul_i(psi[s], lwav(g, c.t + s * NT) * scale);
+      col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
+      store(4 + grp);
+    }
   }
 }
 
@@ -2928,12 +2952,18 @@ void LenOps<L>::col_inv(int model, const Geom& g, const Phys& p, const double2* 
     hipLaunchKernelGGL((k_col_inv<MODEL_RSW, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
   else if (model == MODEL_RSWA)
     hipLaunchKernelGGL((k_col_inv<MODEL_RSWA, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
+  else if (model == MODEL_TY && g.isplit)
+    hipLaunchKernelGGL((k_col_inv<MODEL_TY, L, true>), dim3(col_blocks<L>(g), 2 * ng), dim3(Blk<L>::THREADS),
+                       lds_bytes<L>(), s, g, p, X, M, tw, g0);
   else if (model == MODEL_TY)
     hipLaunchKernelGGL((k_col_inv<MODEL_TY, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
   else if (g0 == 0 && ng == 2 && Blk<L>::NB == 1 && g.kcl % 64 == 0 &&
            (SW_QG_INV_PAIR == 2 || (SW_QG_INV_PAIR == 1 && L >= 13)))
     hipLaunchKernelGGL((k_col_inv<MODEL_QG2, L>), dim3(2 * g.kcl), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X,
                        M, tw, -1);
+  else if (g.isplit)
+    hipLaunchKernelGGL((k_col_inv<MODEL_QG2, L, true>), dim3(col_blocks<L>(g), 3 * ng), dim3(Blk<L>::THREADS),
+                       lds_bytes<L>(), s, g, p, X, M, tw, g0);
   else
     hipLaunchKernelGGL((k_col_inv<MODEL_QG2, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
 }

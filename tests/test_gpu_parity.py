@@ -161,6 +161,31 @@ def test_fused_equals_unfused(name, mode, monkeypatch):
     b.close()
 
 
+@pytest.mark.parametrize("name,n", [("qg2_ifmab3", 128), ("mlqg_frk4", 512), ("qg2_fab3", 1024),
+                                    ("ty_etdrk4", 128), ("ty_etdrk4", 512)])
+def test_split_column_inverse_bitwise(name, n, monkeypatch):
+    """The 2LQG / MultiLayerQG / Thomas–Yamada column inverse with one output
+    per block (Geom::isplit, the default on lines of up to 512 points) and
+    with a group's outputs in one block give bitwise-identical states."""
+    p = sw_cases.case_params(name, n)
+    pr = sw_cases.oracle_problem(p)
+    pr.set_solution(sw_cases.initial_condition(p, pr.grid))
+    monkeypatch.setenv("SW_INV_SPLIT", "1")
+    a = sw_cases.libsw_problem(p)
+    monkeypatch.setenv("SW_INV_SPLIT", "0")
+    b = sw_cases.libsw_problem(p)
+    monkeypatch.delenv("SW_INV_SPLIT", raising=False)
+    a.sol = pr.sol
+    b.sol = pr.sol
+    for k in (2, 3):
+        a.stepforward(k)
+        b.stepforward(k)
+        assert np.array_equal(a.sol, b.sol), k
+    assert np.array_equal(a.calcN(pr.sol), b.calcN(pr.sol))
+    a.close()
+    b.close()
+
+
 def test_determinism_2048():
     """Same inputs -> bitwise-identical state (no atomics on the data path)."""
     from juliaraytracingsw_amd import drivers
