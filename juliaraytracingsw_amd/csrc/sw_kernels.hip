@@ -866,7 +866,10 @@ __host__ __device__ constexpr bool row_fly() {
 }
 // PRUNE: a live band kc <= 3N/8 (row_prunable): the decimated transforms
 // skip the zero inputs and unused outputs of slots 3 and 4 (sw_fft.hpp)
-template <int MODEL, int LOG2N, bool ALIAS = false, bool PRUNE = false>
+// SPLIT (2LQG / MultiLayerQG): grid (rows, 2), block y = 0 forms ψx q, 1
+// forms ψy q, each with its own q transform — three transforms per block
+// instead of five, twice the waves on short rows (Geom::rsplit)
+template <int MODEL, int LOG2N, bool ALIAS = false, bool PRUNE = false, bool SPLIT = false>
 static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
                                          (BlkRow<MODEL, LOG2N>::THREADS >= 1024 ? 4
                                           : (MODEL == MODEL_QG2 ? (row_fly<MODEL, LOG2N>() ? 4 : SW_MINW_ROW_QG)
@@ -1184,21 +1187,27 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
         store_pair<LOG2N, row_fly<MODEL, LOG2N>(), PR>(v, ri, g, line, A, B);
       }
     };
-    // ψx1 + i ψx2;  ψx q per layer (swqg/TwoLayerQG.jl:169)
-    load_pair<LOG2N>(v, ri, g, P1, P2, true);
-    inv(v);
-#pragma unroll
-    for (int s = 0; s < 8; ++s) v[s] = make_double2(v[s].x * q[s].x, v[s].y * q[s].y);
-    fwd_store(Mo, Mo + MF);
+    const int part = SPLIT ? (int)blockIdx.y : -1;
     const long long MA = ma_field(g);  // aliased columns × rows per field
-    if constexpr (ALIAS) store_alias_pair<LOG2N, ma_nfa(MODEL)>(v, c.t, g, line, Ma, Ma + MA, y + g.y0);
-    // ψy q per layer (:177)
-    load_pair<LOG2N>(v, ri, g, Py1, Py2, false);
-    inv(v);
+    if (part != 1) {
+      // ψx1 + i ψx2;  ψx q per layer (swqg/TwoLayerQG.jl:169)
+      load_pair<LOG2N>(v, ri, g, P1, P2, true);
+      inv(v);
 #pragma unroll
-    for (int s = 0; s < 8; ++s) v[s] = make_double2(v[s].x * q[s].x, v[s].y * q[s].y);
-    fwd_store(Mo + 2 * MF, Mo + 3 * MF);
-    if constexpr (ALIAS) store_alias_pair<LOG2N, ma_nfa(MODEL)>(v, c.t, g, line, Ma + 2 * MA, Ma + 3 * MA, y + g.y0);
+      for (int s = 0; s < 8; ++s) v[s] = make_double2(v[s].x * q[s].x, v[s].y * q[s].y);
+      fwd_store(Mo, Mo + MF);
+      if constexpr (ALIAS) store_alias_pair<LOG2N, ma_nfa(MODEL)>(v, c.t, g, line, Ma, Ma + MA, y + g.y0);
+    }
+    if (part != 0) {
+      // ψy q per layer (:177)
+      load_pair<LOG2N>(v, ri, g, Py1, Py2, false);
+      inv(v);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) v[s] = make_double2(v[s].x * q[s].x, v[s].y * q[s].y);
+      fwd_store(Mo + 2 * MF, Mo + 3 * MF);
+      if constexpr (ALIAS)
+        store_alias_pair<LOG2N, ma_nfa(MODEL)>(v, c.t, g, line, Ma + 2 * MA, Ma + 3 * MA, y + g.y0);
+    }
   }
 }
 
@@ -3027,6 +3036,9 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
   } else if (row_prunable<L>(g)) {
     hipLaunchKernelGGL((k_row<MODEL_QG2, L, false, true>), dim3(nrows / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p,
                        Mi, Mo, tw, y0, nullptr);
+  } else if (g.rsplit) {
+    hipLaunchKernelGGL((k_row<MODEL_QG2, L, false, false, true>), dim3(nrows / BQ::NB, 2), dim3(BQ::THREADS), sh_qg2,
+                       s, g, p, Mi, Mo, tw, y0, nullptr);
   } else {
     hipLaunchKernelGGL((k_row<MODEL_QG2, L>), dim3(nrows / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p, Mi, Mo, tw,
                        y0, nullptr);

@@ -161,20 +161,23 @@ def test_fused_equals_unfused(name, mode, monkeypatch):
     b.close()
 
 
+@pytest.mark.parametrize("knob", ["SW_INV_SPLIT", "SW_ROW_SPLIT"])
 @pytest.mark.parametrize("name,n", [("qg2_ifmab3", 128), ("mlqg_frk4", 512), ("qg2_fab3", 1024),
                                     ("ty_etdrk4", 128), ("ty_etdrk4", 512)])
-def test_split_column_inverse_bitwise(name, n, monkeypatch):
-    """The 2LQG / MultiLayerQG / Thomas–Yamada column inverse with one output
-    per block (Geom::isplit, the default on lines of up to 512 points) and
-    with a group's outputs in one block give bitwise-identical states."""
+def test_split_passes_bitwise(name, n, knob, monkeypatch):
+    """Short lines split over more blocks — the column inverse with one
+    output per block (SW_INV_SPLIT, Geom::isplit: 2LQG / MultiLayerQG /
+    Thomas–Yamada) and the 2LQG / MultiLayerQG row in two blocks
+    (SW_ROW_SPLIT, Geom::rsplit) — give bitwise the states and calcN of the
+    one-block passes."""
     p = sw_cases.case_params(name, n)
     pr = sw_cases.oracle_problem(p)
     pr.set_solution(sw_cases.initial_condition(p, pr.grid))
-    monkeypatch.setenv("SW_INV_SPLIT", "1")
+    monkeypatch.setenv(knob, "1")
     a = sw_cases.libsw_problem(p)
-    monkeypatch.setenv("SW_INV_SPLIT", "0")
+    monkeypatch.setenv(knob, "0")
     b = sw_cases.libsw_problem(p)
-    monkeypatch.delenv("SW_INV_SPLIT", raising=False)
+    monkeypatch.delenv(knob, raising=False)
     a.sol = pr.sol
     b.sol = pr.sol
     for k in (2, 3):
