@@ -866,9 +866,11 @@ __host__ __device__ constexpr bool row_fly() {
 }
 // PRUNE: a live band kc <= 3N/8 (row_prunable): the decimated transforms
 // skip the zero inputs and unused outputs of slots 3 and 4 (sw_fft.hpp)
-// SPLIT (2LQG / MultiLayerQG): grid (rows, 2), block y = 0 forms ψx q, 1
-// forms ψy q, each with its own q transform — three transforms per block
-// instead of five, twice the waves on short rows (Geom::rsplit)
+// SPLIT: more blocks per row on short rows (Geom::rsplit), each running a
+// subset of the row's transforms on the same pairs (bitwise the same
+// outputs): 2LQG / MultiLayerQG grid (rows, 2), block y = 0 forms ψx q, 1
+// forms ψy q, each with its own q transform (three transforms per block
+// instead of five); Thomas–Yamada grid (rows, 4), the parts of its branch
 template <int MODEL, int LOG2N, bool ALIAS = false, bool PRUNE = false, bool SPLIT = false>
 static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
                                          (BlkRow<MODEL, LOG2N>::THREADS >= 1024 ? 4
@@ -1035,8 +1037,17 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
 #pragma unroll
     for (int i = 0; i < 9; ++i) F[i] = Mi + i * MF;
     const double nRo = -p.Ro;
+    // SPLIT: grid (rows, 4), block y = part: 0 outputs 0-2 (transforms I1-I3),
+    // 1 output 3 (I1-I4), 2 outputs 4-5 (I1-I5), 3 output 6 (I1, I2, I5, I6);
+    // each part runs the same transforms of the same pairs as the whole row
+    const int part = SPLIT ? (int)blockIdx.y : -1;
+    auto want = [&](int q) { return part < 0 || part == q; };
     double zt[8], ut[8], vt[8], uc[8], vc[8], p6[8], p7[8], p8[8], p9[8], p10[8];
-    // ζ + i ut, vt + i uc
+    if constexpr (SPLIT) {  // (a part skipping a transform leaves its products unused; defined anyway)
+#pragma unroll
+      for (int s = 0; s < 8; ++s) vc[s] = p7[s] = p8[s] = p9[s] = 0.0;
+    }
+    // I1: ζ + i ut, I2: vt + i uc
     load_pair_m<LOG2N>(v, ri, g, F[0], 0, F[2], 0);
     fft_line<LOG2N, +1>(v, c.t, tws, line);
 #pragma unroll
@@ -1052,93 +1063,107 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
       uc[s] = v[s].y;
       p6[s] = ut[s] * uc[s];
     }
-    // vc + i ∂y uc
-    load_pair_m<LOG2N>(v, ri, g, F[6], 0, F[5], 0);
-    fft_line<LOG2N, +1>(v, c.t, tws, line);
-    double2 w[8];
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      vc[s] = v[s].x;
-      p7[s] = vt[s] * vc[s];
-      p8[s] = vt[s] * v[s].y;
-      w[s] = make_double2(ut[s] * zt[s], uc[s] * vc[s]);          // p2 + i p3
-      v[s] = make_double2(vt[s] * zt[s], uc[s] * uc[s] - vc[s] * vc[s]);  // p1 + i p4
-    }
     // aliased-state tracking: the x-spectra kc <= k <= nx/2 of every output
     // into Ma (ma_off: field, k - kc, stored row; k_col_fwd_alias), as the live ones
     const long long MA = ma_field(g);
     const int yg = y + g.y0;
-    fft_line<LOG2N, -1>(w, c.t, tws, line);
-    split_pair<LOG2N>(w, c.t, g, line, [&](int k, int s, double2 a, double2 b) {
-      const double kw = k * g.mk;
-      const int o = ri.ofwd(g, s);
-      Mo[o] = cscale(csub(cmul_i(a, kw), cscale(b, kw * kw)), nRo);
-      Mo[2 * MF + o] = cscale(b, nRo);
-    });
-    if constexpr (ALIAS)
-      store_alias_with<LOG2N, ma_nfa(MODEL)>(w, c.t, g, line, yg, [&](long long o, int k, double2 a, double2 b) {
-        const double kw = k * g.mk;
-        Ma[o] = cscale(csub(cmul_i(a, kw), cscale(b, kw * kw)), nRo);
-        Ma[2 * MA + o] = cscale(b, nRo);
-      });
-    fft_line<LOG2N, -1>(v, c.t, tws, line);
-    split_pair<LOG2N>(v, c.t, g, line, [&](int k, int s, double2 a, double2 b) {
-      const double kw = k * g.mk;
-      Mo[MF + ri.ofwd(g, s)] = cscale(cadd(cmul_i(a, 1.0), cscale(b, kw)), nRo);
-    });
-    if constexpr (ALIAS)
-      store_alias_with<LOG2N, ma_nfa(MODEL)>(v, c.t, g, line, yg, [&](long long o, int k, double2 a, double2 b) {
-        Ma[MA + o] = cscale(cadd(cmul_i(a, 1.0), cscale(b, k * g.mk)), nRo);
-      });
-    // ∂y ut + i ∂x vc
-    load_pair_m<LOG2N>(v, ri, g, F[3], 0, F[6], 1);
-    fft_line<LOG2N, +1>(v, c.t, tws, line);
+    if (part != 3) {
+      // I3: vc + i ∂y uc
+      load_pair_m<LOG2N>(v, ri, g, F[6], 0, F[5], 0);
+      fft_line<LOG2N, +1>(v, c.t, tws, line);
+      double2 w[8];
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      p8[s] = p8[s] + vc[s] * v[s].x;
-      p9[s] = ut[s] * v[s].y;
-      v[s] = make_double2(p6[s], p8[s]);
+      for (int s = 0; s < 8; ++s) {
+        vc[s] = v[s].x;
+        p7[s] = vt[s] * vc[s];
+        p8[s] = vt[s] * v[s].y;
+        w[s] = make_double2(ut[s] * zt[s], uc[s] * vc[s]);          // p2 + i p3
+        v[s] = make_double2(vt[s] * zt[s], uc[s] * uc[s] - vc[s] * vc[s]);  // p1 + i p4
+      }
+      if (want(0)) {
+        fft_line<LOG2N, -1>(w, c.t, tws, line);
+        split_pair<LOG2N>(w, c.t, g, line, [&](int k, int s, double2 a, double2 b) {
+          const double kw = k * g.mk;
+          const int o = ri.ofwd(g, s);
+          Mo[o] = cscale(csub(cmul_i(a, kw), cscale(b, kw * kw)), nRo);
+          Mo[2 * MF + o] = cscale(b, nRo);
+        });
+        if constexpr (ALIAS)
+          store_alias_with<LOG2N, ma_nfa(MODEL)>(w, c.t, g, line, yg, [&](long long o, int k, double2 a, double2 b) {
+            const double kw = k * g.mk;
+            Ma[o] = cscale(csub(cmul_i(a, kw), cscale(b, kw * kw)), nRo);
+            Ma[2 * MA + o] = cscale(b, nRo);
+          });
+        fft_line<LOG2N, -1>(v, c.t, tws, line);
+        split_pair<LOG2N>(v, c.t, g, line, [&](int k, int s, double2 a, double2 b) {
+          const double kw = k * g.mk;
+          Mo[MF + ri.ofwd(g, s)] = cscale(cadd(cmul_i(a, 1.0), cscale(b, kw)), nRo);
+        });
+        if constexpr (ALIAS)
+          store_alias_with<LOG2N, ma_nfa(MODEL)>(v, c.t, g, line, yg, [&](long long o, int k, double2 a, double2 b) {
+            Ma[MA + o] = cscale(cadd(cmul_i(a, 1.0), cscale(b, k * g.mk)), nRo);
+          });
+      }
     }
-    fft_line<LOG2N, -1>(v, c.t, tws, line);
-    split_pair<LOG2N>(v, c.t, g, line, [&](int k, int s, double2 a, double2 b) {
-      Mo[3 * MF + ri.ofwd(g, s)] = cscale(cadd(cmul_i(a, k * g.mk), b), nRo);
-    });
-    if constexpr (ALIAS)
-      store_alias_with<LOG2N, ma_nfa(MODEL)>(v, c.t, g, line, yg, [&](long long o, int k, double2 a, double2 b) {
-        Ma[3 * MA + o] = cscale(cadd(cmul_i(a, k * g.mk), b), nRo);
-      });
-    // ∂x vt + i ∂x pc
-    load_pair_m<LOG2N>(v, ri, g, F[1], 2, F[7], 1);
-    fft_line<LOG2N, +1>(v, c.t, tws, line);
+    if (part < 0 || part == 1 || part == 2) {
+      // I4: ∂y ut + i ∂x vc
+      load_pair_m<LOG2N>(v, ri, g, F[3], 0, F[6], 1);
+      fft_line<LOG2N, +1>(v, c.t, tws, line);
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      p9[s] = p9[s] + uc[s] * v[s].x;
-      p10[s] = ut[s] * v[s].y;
-      v[s] = make_double2(p7[s], p9[s]);
+      for (int s = 0; s < 8; ++s) {
+        p8[s] = p8[s] + vc[s] * v[s].x;
+        p9[s] = ut[s] * v[s].y;
+        v[s] = make_double2(p6[s], p8[s]);
+      }
+      if (want(1)) {
+        fft_line<LOG2N, -1>(v, c.t, tws, line);
+        split_pair<LOG2N>(v, c.t, g, line, [&](int k, int s, double2 a, double2 b) {
+          Mo[3 * MF + ri.ofwd(g, s)] = cscale(cadd(cmul_i(a, k * g.mk), b), nRo);
+        });
+        if constexpr (ALIAS)
+          store_alias_with<LOG2N, ma_nfa(MODEL)>(v, c.t, g, line, yg, [&](long long o, int k, double2 a, double2 b) {
+            Ma[3 * MA + o] = cscale(cadd(cmul_i(a, k * g.mk), b), nRo);
+          });
+      }
     }
-    fft_line<LOG2N, -1>(v, c.t, tws, line);
-    split_pair<LOG2N>(v, c.t, g, line, [&](int k, int s, double2 a, double2 b) {
-      const int o = ri.ofwd(g, s);
-      Mo[4 * MF + o] = cscale(a, nRo);
-      Mo[5 * MF + o] = cscale(b, nRo);
-    });
-    if constexpr (ALIAS)
-      store_alias_with<LOG2N, ma_nfa(MODEL)>(v, c.t, g, line, yg, [&](long long o, int, double2 a, double2 b) {
-        Ma[4 * MA + o] = cscale(a, nRo);
-        Ma[5 * MA + o] = cscale(b, nRo);
-      });
-    // ∂y pc
-    load_pair_m<LOG2N>(v, ri, g, F[8], 0, nullptr, 0);
-    fft_line<LOG2N, +1>(v, c.t, tws, line);
+    if (part < 0 || part == 2 || part == 3) {
+      // I5: ∂x vt + i ∂x pc
+      load_pair_m<LOG2N>(v, ri, g, F[1], 2, F[7], 1);
+      fft_line<LOG2N, +1>(v, c.t, tws, line);
 #pragma unroll
-    for (int s = 0; s < 8; ++s) v[s] = make_double2(p10[s] + vt[s] * v[s].x, 0.0);
-    fft_line<LOG2N, -1>(v, c.t, tws, line);
+      for (int s = 0; s < 8; ++s) {
+        p9[s] = p9[s] + uc[s] * v[s].x;
+        p10[s] = ut[s] * v[s].y;
+        v[s] = make_double2(p7[s], p9[s]);
+      }
+      if (want(2)) {
+        fft_line<LOG2N, -1>(v, c.t, tws, line);
+        split_pair<LOG2N>(v, c.t, g, line, [&](int k, int s, double2 a, double2 b) {
+          const int o = ri.ofwd(g, s);
+          Mo[4 * MF + o] = cscale(a, nRo);
+          Mo[5 * MF + o] = cscale(b, nRo);
+        });
+        if constexpr (ALIAS)
+          store_alias_with<LOG2N, ma_nfa(MODEL)>(v, c.t, g, line, yg, [&](long long o, int, double2 a, double2 b) {
+            Ma[4 * MA + o] = cscale(a, nRo);
+            Ma[5 * MA + o] = cscale(b, nRo);
+          });
+      }
+    }
+    if (want(3)) {
+      // I6: ∂y pc
+      load_pair_m<LOG2N>(v, ri, g, F[8], 0, nullptr, 0);
+      fft_line<LOG2N, +1>(v, c.t, tws, line);
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const int k = c.t + s * Bk::NT;
-      if (RowIdx<LOG2N>::fwd_any(g, s) && k < g.kc) Mo[6 * MF + ri.ofwd(g, s)] = cscale(v[s], nRo);
-      if constexpr (ALIAS)  // (a real line: its transform is the spectrum itself)
-        if (k >= g.kc && k <= Bk::NT * 4) Ma[6 * MA + ma_off(g, ma_nfa(MODEL), k - g.kc, yg)] = cscale(v[s], nRo);
+      for (int s = 0; s < 8; ++s) v[s] = make_double2(p10[s] + vt[s] * v[s].x, 0.0);
+      fft_line<LOG2N, -1>(v, c.t, tws, line);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const int k = c.t + s * Bk::NT;
+        if (RowIdx<LOG2N>::fwd_any(g, s) && k < g.kc) Mo[6 * MF + ri.ofwd(g, s)] = cscale(v[s], nRo);
+        if constexpr (ALIAS)  // (a real line: its transform is the spectrum itself)
+          if (k >= g.kc && k <= Bk::NT * 4) Ma[6 * MA + ma_off(g, ma_nfa(MODEL), k - g.kc, yg)] = cscale(v[s], nRo);
+      }
     }
   } else {
     const double2 *Q1 = Mi, *Q2 = Mi + MF, *P1 = Mi + 2 * MF, *P2 = Mi + 3 * MF,
@@ -3015,6 +3040,9 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
     if (Ma)
       hipLaunchKernelGGL((k_row<MODEL_TY, L, true>), dim3(nrows / BT::NB), dim3(BT::THREADS), sh_ty, s, g, p, Mi,
                          Mo, tw, y0, Ma);
+    else if (g.rsplit)
+      hipLaunchKernelGGL((k_row<MODEL_TY, L, false, false, true>), dim3(nrows / BT::NB, 4), dim3(BT::THREADS), sh_ty,
+                         s, g, p, Mi, Mo, tw, y0, nullptr);
     else
       hipLaunchKernelGGL((k_row<MODEL_TY, L>), dim3(nrows / BT::NB), dim3(BT::THREADS), sh_ty, s, g, p, Mi, Mo, tw,
                          y0, nullptr);
