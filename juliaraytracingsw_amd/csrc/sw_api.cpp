@@ -251,9 +251,9 @@ Geom make_geom(const sw_config& k, int P, int s) {
   // SW_INV_SPLIT=0/1 forces it off/on
   g.isplit = g.log2ny <= (k.model == SW_MODEL_TY ? 10 : 9);
   if (const char* e = std::getenv("SW_INV_SPLIT")) g.isplit = e[0] == '1';
-  // the 2LQG / MultiLayerQG row in two blocks, Thomas–Yamada's in four
-  // (k_row SPLIT), on short rows (round 5); SW_ROW_SPLIT=0/1
-  // forces it off/on
+  // the RSW and 2LQG / MultiLayerQG rows in two blocks, Thomas–Yamada's in
+  // four (k_row SPLIT), on short rows (round 5);
+  // SW_ROW_SPLIT=0/1 forces it off/on
   g.rsplit = g.log2nx <= 9;
   if (const char* e = std::getenv("SW_ROW_SPLIT")) g.rsplit = e[0] == '1';
   g.fsy = ford ? 1 : g.kcl >> g.fa;

@@ -75,7 +75,7 @@ struct Geom {
   // at 8192 points (fa = 2: 4×2, sw_api.cpp make_geom)
   int fsy, fsk, fa;
   int isplit;         // 2LQG/MLQG/TY column inverse: one output per block (k_col_inv SPLIT)
-  int rsplit;         // 2LQG/MLQG/TY row over 2 / 4 blocks (k_row SPLIT)
+  int rsplit;         // RSW/2LQG/MLQG/TY row over 2 / 4 blocks (k_row SPLIT)
 };
 
 struct Phys {

@@ -870,7 +870,9 @@ __host__ __device__ constexpr bool row_fly() {
 // subset of the row's transforms on the same pairs (bitwise the same
 // outputs): 2LQG / MultiLayerQG grid (rows, 2), block y = 0 forms ψx q, 1
 // forms ψy q, each with its own q transform (three transforms per block
-// instead of five); Thomas–Yamada grid (rows, 4), the parts of its branch
+// instead of five); Thomas–Yamada grid (rows, 4), the parts of its branch;
+// RSW (two line buffers, undecimated lines) grid (rows, 2), the two forward
+// lines apart
 template <int MODEL, int LOG2N, bool ALIAS = false, bool PRUNE = false, bool SPLIT = false>
 static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
                                          (BlkRow<MODEL, LOG2N>::THREADS >= 1024 ? 4
@@ -915,6 +917,56 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
       wt = tw[c.t];
     }
     // u + i v and η + i ζ, transformed together (fft_lines leaves z[x = t + s*NT])
+    if constexpr (SPLIT && CB == 2 && W == 0) {
+      // short rows in two blocks (Geom::rsplit): both inverse pairs, then
+      // block y = 0 the ζu + i ζv line and K (outputs 0-2), y = 1 the
+      // uη + i vη line (outputs 3-4)
+      load_pair<LOG2N>(w[0], ri, g, U, V, false);
+      load_eta_zeta<LOG2N>(w[1], ri, g, H, V, Uy);
+      fft_pair<LOG2N, +1, CB>(w, c.t, tws, line, LS);
+      const int part = blockIdx.y;
+      double kk[8];
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const double u = w[0][s].x, vv = w[0][s].y, eta = w[1][s].x, zeta = w[1][s].y;
+        kk[s] = 0.5 * (u * u + vv * vv);
+        w[0][s] = make_double2(zeta * u, zeta * vv);  // ζu + i ζv
+        w[1][s] = make_double2(u * eta, vv * eta);    // uη + i vη
+      }
+      if (part == 1) {
+        fft_line<LOG2N, -1>(w[1], c.t, tws, line);
+        split_pairs<LOG2N, 1>(reinterpret_cast<const double2(&)[1][8]>(w[1]), c.t, g, line, LS,
+                              [&](int, int k, int s, double2 a, double2 b) {
+                                const int o = ri.ofwd(g, s);
+                                Mo[3 * MF + o] = cmul_i(a, -(k * g.mk));
+                                Mo[4 * MF + o] = b;
+                              });
+        return;
+      }
+      fft_line<LOG2N, -1>(w[0], c.t, tws, line);
+      double2 zv[8];
+#pragma unroll
+      for (int s = 0; s < 8; ++s) zv[s] = zero2();
+      split_pairs<LOG2N, 1>(reinterpret_cast<const double2(&)[1][8]>(w[0]), c.t, g, line, LS,
+                            [&](int, int, int s, double2 a, double2 b) {
+                              Mo[2 * MF + ri.ofwd(g, s)] = a;
+                              zv[s] = b;
+                            });
+#pragma unroll
+      for (int s = 0; s < 8; ++s) v[s] = make_double2(kk[s], 0.0);
+      lds_barrier();  // split_pairs' mirror reads are done
+      fft_line<LOG2N, -1>(v, c.t, tws, line);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const int k = c.t + s * Bk::NT;
+        if (RowIdx<LOG2N>::fwd_any(g, s) && k < g.kc) {
+          const int o = ri.ofwd(g, s);
+          Mo[o] = cadd(cmul_i(v[s], -(k * g.mk)), zv[s]);
+          Mo[MF + o] = v[s];
+        }
+      }
+      return;
+    }
     if constexpr (W > 0) {
       load_uv_eta_zeta<LOG2N>(w, ri, g, U, V, H, Uy);  // V read once (row 74.9 -> 73.5 µs)
       fftw_dif<W, +1, 2, false, false, SW_ROW_TW_SHARE, PRUNE>(w, c.t, wt, tq, line, LS);
@@ -3033,6 +3085,9 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
     else if (row_prunable<L>(g))
       hipLaunchKernelGGL((k_row<MODEL_RSW, L, false, true>), dim3(nrows / BR::NB), dim3(BR::THREADS), sh_rsw, s, g,
                          p, Mi, Mo, tw, y0, nullptr);
+    else if (g.rsplit && row_lds_lines<MODEL_RSW, L>() == 2 && roww<L>() == 0)
+      hipLaunchKernelGGL((k_row<MODEL_RSW, L, false, false, true>), dim3(nrows / BR::NB, 2), dim3(BR::THREADS),
+                         sh_rsw, s, g, p, Mi, Mo, tw, y0, nullptr);
     else
       hipLaunchKernelGGL((k_row<MODEL_RSW, L>), dim3(nrows / BR::NB), dim3(BR::THREADS), sh_rsw, s, g, p, Mi, Mo,
                          tw, y0, nullptr);

@@ -162,7 +162,7 @@ def test_fused_equals_unfused(name, mode, monkeypatch):
 
 
 @pytest.mark.parametrize("knob", ["SW_INV_SPLIT", "SW_ROW_SPLIT"])
-@pytest.mark.parametrize("name,n", [("qg2_ifmab3", 128), ("mlqg_frk4", 512), ("qg2_fab3", 1024),
+@pytest.mark.parametrize("name,n", [("qg2_ifmab3", 128), ("mlqg_frk4", 512), ("qg2_fab3", 1024), ("rsw_ifmab3", 512), ("rsw_fab3", 256),
                                     ("ty_etdrk4", 128), ("ty_etdrk4", 512), ("ty_etdrk4", 1024)])
 def test_split_passes_bitwise(name, n, knob, monkeypatch):
     """Short lines split over more blocks — the column inverse with one
