@@ -245,8 +245,8 @@ Geom make_geom(const sw_config& k, int P, int s) {
   g.fa = 1;
   if ((k.model == SW_MODEL_QG2 || k.model == SW_MODEL_MLQG) && g.log2nx >= SW_TILE_F4_QG) g.fa = 2;
   if (const char* e = std::getenv("SW_TILE_FA")) g.fa = (e[0] == '2') ? 2 : 1;
-  // 2LQG / MultiLayerQG / Thomas–Yamada column inverse with one output per
-  // block on short lines, where a one-line block is one or two waves (round 5,
+  // RSW / 2LQG / MultiLayerQG / Thomas–Yamada column inverse with one output
+  // per block on short lines, where a one-line block is one or two waves (round 5,
   // DESIGN.md §3d, measured: 512-point lines, and 1024 for Thomas–Yamada);
   // SW_INV_SPLIT=0/1 forces it off/on
   g.isplit = g.log2ny <= (k.model == SW_MODEL_TY ? 10 : 9);

@@ -267,9 +267,11 @@ __device__ __forceinline__ void store_col_p(const Geom& g, int krl, int t, F put
 //   QG2  outputs (swqg/TwoLayerQG.jl:155-176):          0 Q1, 1 Q2, 2 Ψ1, 3 Ψ2, 4 Ψy1, 5 Ψy2
 // grid: (columns, groups); RSW group f reads field f; QG2 group = layer.
 // ===========================================================================
+template <int MODEL>
+__host__ __device__ constexpr int inv_split_per() { return MODEL == MODEL_QG2 ? 3 : 2; }
 // SPLIT: one output per block — grid (columns, 3 × groups) for 2LQG /
 // MultiLayerQG (a layer's q, ψ or ∂yψ), (columns, 2 × groups) for
-// Thomas–Yamada (a group's one or two outputs) — so that small grids, whose
+// Thomas–Yamada and RSW (a group's one or two outputs) — so that small grids, whose
 // one-line blocks are a single wave, put 2-3 times the waves on the chip (the
 // same arithmetic per output; Geom::isplit, sw_api.cpp make_geom)
 template <int MODEL, int LOG2N, bool SPLIT = false>
@@ -292,11 +294,12 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
     krl = (q << 6) + (x << 3) + (jj >> 1);
   } else {
     krl = (B::NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * B::NB + c.ln;
-    constexpr int PER = MODEL == MODEL_TY ? 2 : 3;  // SPLIT: blocks per group
-    grp = gbase + (SPLIT ? (int)blockIdx.y / PER : (int)blockIdx.y);
+    grp = gbase + (SPLIT ? (int)blockIdx.y / inv_split_per<MODEL>() : (int)blockIdx.y);
   }
-  const int out = SPLIT ? (int)blockIdx.y % (MODEL == MODEL_TY ? 2 : 3) : -1;  // -1: every output
+  const int out = SPLIT ? (int)blockIdx.y % inv_split_per<MODEL>() : -1;  // -1: every output
   if (MODEL == MODEL_TY && out == 1 && grp == 3) return;  // (vc: one output)
+  if ((MODEL == MODEL_RSW || MODEL == MODEL_RSWA) && out == 1 && !(grp == 0 || (MODEL == MODEL_RSWA && grp == 1)))
+    return;  // (V, H: one output; the advective form's V: two)
   const bool live = krl < g.kcn;
   if (B::NB == 1 && !live) return;  // padding column: nobody reads it
   double2* line = smem + c.ln * FftPlan<LOG2N>::LDS;
@@ -328,9 +331,11 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
       x[s] = (live && j >= 0) ? t : zero2();
       v[s] = cscale(x[s], scale);
     }
-    col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
-    store(grp);
-    if (grp == 0 || (MODEL == MODEL_RSWA && grp == 1)) {  // ∂y u: Uy (advective form: and ∂y v: Vy)
+    if (out <= 0) {
+      col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
+      store(grp);
+    }
+    if (out != 0 && (grp == 0 || (MODEL == MODEL_RSWA && grp == 1))) {  // ∂y u: Uy (advective form: and ∂y v: Vy)
 #pragma unroll
       for (int s = 0; s < 8; ++s) v[s] = cmul_i(x[s], lwav(g, c.t + s * NT) * scale);
       col_fft<LOG2N, +1, CD>(v, c.t, tws, line);
@@ -3034,8 +3039,15 @@ template <int L>
 void LenOps<L>::col_inv(int model, const Geom& g, const Phys& p, const double2* X, double2* M, const double2* tw,
                         hipStream_t s, int g0, int ng) {
   const dim3 grid(col_blocks<L>(g), ng);
-  if (model == MODEL_RSW)
+  const dim3 grid2(col_blocks<L>(g), 2 * ng);
+  if (model == MODEL_RSW && g.isplit)
+    hipLaunchKernelGGL((k_col_inv<MODEL_RSW, L, true>), grid2, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M,
+                       tw, g0);
+  else if (model == MODEL_RSW)
     hipLaunchKernelGGL((k_col_inv<MODEL_RSW, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
+  else if (model == MODEL_RSWA && g.isplit)
+    hipLaunchKernelGGL((k_col_inv<MODEL_RSWA, L, true>), grid2, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M,
+                       tw, g0);
   else if (model == MODEL_RSWA)
     hipLaunchKernelGGL((k_col_inv<MODEL_RSWA, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
   else if (model == MODEL_TY && g.isplit)
