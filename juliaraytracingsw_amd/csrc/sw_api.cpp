@@ -32,6 +32,8 @@ struct Slab {
   Geom g{};
   double2* sol = nullptr;                    // compact state, nf fields
   double2* sol2 = nullptr;                   // FilteredAB3: the other state buffer (ping-pong)
+  double2* nt1 = nullptr;                    // fsplit: terms 1 and 2 of a split N (k_col_fwd SPLIT)
+  double2* nt2 = nullptr;
   double2* hist[3] = {nullptr, nullptr, nullptr};  // FAB3 RHS ring / IFMAB3 N ring
   double2* acc = nullptr;                    // IFMRK4 running stage combination
   double2* nbuf = nullptr;                   // unfused IFMRK4 / sw_calcN: calcN output
@@ -86,6 +88,7 @@ struct sw_ctx {
   int head = 0;
   bool mixed_valid = false;                  // mir == transposed col_inv(sol) (fused pipeline primed)
   bool fuse_all = false;                     // SW_FUSE_ALL=1: fused pass for every pair (experiments)
+  bool fsplit = false;                       // k_col_fwd one term per block, completed by the update
   int fwd_step = -1;                         // use_fwd_step: -1 where measured faster, SW_FWD_STEP=0/1 off/on
   bool stream_state = false;                 // state/history accesses non-temporal (StepPtrs::stream)
   double2* stage = nullptr;                  // full (nkr,nl,nf) staging
@@ -612,7 +615,7 @@ sw::StepPtrs step_ptrs(const sw_ctx* c, const Slab& s);
 // and the stepper update in one kernel (N never in HBM)
 static void last_col_pass(sw_ctx* c, double2* Slab::*X, double2* Slab::*N, int op, int stage, const Slab& s) {
   if (op < 0) {
-    sw::launch_col_fwd(c->kmodel, s.g, c->p, s.mfc, s.*N, s.*X, c->tw_y, c->stream);
+    sw::launch_col_fwd(c->kmodel, s.g, c->p, s.mfc, s.*N, s.*X, c->tw_y, c->stream, 0, -1, s.nt1, s.nt2);
     return;
   }
   sw::StepPtrs a = step_ptrs(c, s);
@@ -652,7 +655,8 @@ int calcN(sw_ctx* c, double2* Slab::*X, double2* Slab::*N, int op = -1, int stag
     }
     for (int f = 0; f < ps.nfc; ++f) {
       if (int rc = wait_comm(c, c->ev_fwd[f])) return rc;
-      for (Slab& s : c->sl) sw::launch_col_fwd(model, s.g, c->p, s.mfc, s.*N, s.*X, c->tw_y, c->stream, f, 1);
+      for (Slab& s : c->sl)
+        sw::launch_col_fwd(model, s.g, c->p, s.mfc, s.*N, s.*X, c->tw_y, c->stream, f, 1, s.nt1, s.nt2);
     }
     return 0;
   }
@@ -857,6 +861,9 @@ int run_stage(sw_ctx* c, int op, int stage, double2* Slab::*X) {
     for (Slab& s : c->sl) {
       sw::StepPtrs a = step_ptrs(c, s);
       a.stage = stage;
+      a.nt1 = s.nt1;  // (fsplit: N's terms 1-2, summed with the linear terms per mode)
+      a.nt2 = s.nt2;
+      a.xin = s.*X;
       sw::launch_step_elem(c->nf, op, s.g, c->p, a, s.nbuf, s.xs, c->stream);
       // the same update at the aliased modes, from the zero (dealiased) state:
       // the post-step values the reference's update writes there
@@ -1138,7 +1145,7 @@ int nan_flag(sw_ctx* c, int& h) {
 }
 
 void free_slab(Slab& s, bool own_mrow) {
-  void* ptrs[] = {s.sol, s.sol2, s.hist[0], s.hist[1], s.hist[2], s.acc, s.xs, s.mic, s.mfr, s.etd};
+  void* ptrs[] = {s.sol, s.sol2, s.hist[0], s.hist[1], s.hist[2], s.acc, s.xs, s.mic, s.mfr, s.etd, s.nt1, s.nt2};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   if (s.nbuf && s.nbuf != s.hist[0] && s.nbuf != s.hist[1] && s.nbuf != s.hist[2]) (void)hipFree(s.nbuf);
@@ -1387,12 +1394,26 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   c->ninv = c->kmodel == sw::MODEL_RSWA ? 5 : k.model == SW_MODEL_RSW ? 4 : (k.model == SW_MODEL_TY ? 9 : 6);
   c->nfwd = c->kmodel == sw::MODEL_RSWA ? 4 : k.model == SW_MODEL_RSW ? 5 : (k.model == SW_MODEL_TY ? 7 : 4);
 
+  // the forward column pass with one term of N per block on short columns
+  // (k_col_fwd SPLIT; round 5): built for RSW (vorticity
+  // form), 2LQG / MultiLayerQG and Thomas–Yamada, on by default on 512-point
+  // columns for RSW, MultiLayerQG and Thomas–Yamada (2LQG IFMAB3 measured
+  // neutral to -1 %); SW_FWD_SPLIT=0/1 forces it off/on where it is built
+  {
+    const bool built = (c->kmodel == SW_MODEL_RSW || c->kmodel == SW_MODEL_QG2 || c->kmodel == SW_MODEL_TY) &&
+                       !k.aliased_state && !k.nop_calcN;
+    c->fsplit = built && k.model != SW_MODEL_QG2 && ilog2(k.ny) <= 9;
+    if (const char* e = std::getenv("SW_FWD_SPLIT")) c->fsplit = built && e[0] == '1';
+  }
   int rc;
   for (Slab& s : c->sl) {
     const Geom& g = s.g;
     const size_t cb = (size_t)g.cfield * sizeof(double2);
     const size_t mb = (size_t)g.mfield * sizeof(double2);
     if ((rc = alloc(c, (void**)&s.sol, c->nf * cb))) return rc;
+    if (c->fsplit)
+      for (double2** q : {&s.nt1, &s.nt2})
+        if ((rc = alloc(c, (void**)q, c->nf * cb))) return rc;
     if ((rc = alloc(c, (void**)&s.xs, c->nf * cb))) return rc;
     if (k.stepper == SW_STEP_FILTERED_AB3)
       if ((rc = alloc(c, (void**)&s.sol2, c->nf * cb))) return rc;
@@ -1649,6 +1670,14 @@ int sw_calcN(sw_ctx* c, const void* sol, void* N, size_t bytes) {
   }
   set_alias_nbuf(c);
   if (int rc = calcN(c, &Slab::xs, &Slab::nbuf)) return rc;
+  for (Slab& s : c->sl) {  // a split N completed (the updates complete it per mode)
+    if (!s.nt1) continue;
+    sw::StepPtrs a{};
+    a.nt1 = s.nt1;
+    a.nt2 = s.nt2;
+    a.xin = s.xs;
+    sw::launch_assemble_terms(c->nf, s.g, c->p, a, s.nbuf, c->stream);
+  }
   if (int rc = collect_full(c, &Slab::nbuf)) return rc;
   if (int rc = alias_scatter(c, A_NBUF)) return rc;
   if (int rc = download(c, c->stage, N, full_bytes(c))) return rc;

@@ -488,8 +488,11 @@ void launch_scatter_modes(int nf, const Geom& ga, const double2* compact, double
 void launch_gather_modes(int nf, const Geom& ga, const double2* full, double2* compact, hipStream_t s);
 int row_lines_per_block(int model, int log2nx);
 // X: the compact calcN input (TY adds its linear terms from it; unused otherwise)
+// T1, T2 (short columns, sw_api.cpp fsplit): one term of N per block, terms
+// 1-2 into T1 / T2, completed by the consuming update (StepPtrs nt1, nt2)
 void launch_col_fwd(int model, const Geom& g, const Phys& p, const double2* Mfwd, double2* N,
-                    const double2* X, const double2* tw_y, hipStream_t s, int f0 = 0, int nfl = -1);
+                    const double2* X, const double2* tw_y, hipStream_t s, int f0 = 0, int nfl = -1,
+                    double2* T1 = nullptr, double2* T2 = nullptr);
 // Pointers of one stepper stage (see sw_kernels.hip).
 struct StepPtrs {
   const double2* sol;  // state in
@@ -507,6 +510,11 @@ struct StepPtrs {
   double2* n2;
   double2* xs2;
   const double* etd;
+  // a split N (launch_col_fwd T1/T2): its terms 1-2 and the calcN input for
+  // the linear terms, completed per mode before the op (assemble_terms)
+  const double2* nt1;
+  const double2* nt2;
+  const double2* xin;
 };
 enum { OP_FAB3 = 0, OP_IFMAB3 = 1, OP_RK4 = 2, OP_ETDRK4 = 3, OP_FRK4 = 4 };
 enum { ETD_E = 0, ETD_E2, ETD_ZETA, ETD_ALPHA, ETD_BETA, ETD_GAMMA, ETD_N };
@@ -524,7 +532,7 @@ struct LenOps {
   static void col_fwd_alias(int model, const Geom& g, const Geom& ga, int region, const Phys& p,
                             const double2* Mf, const double2* Ma, double2* N, const double2* tw, hipStream_t s);
   static void col_fwd(int model, const Geom& g, const Phys& p, const double2* Mf, double2* N, const double2* X,
-                      const double2* tw, hipStream_t s, int f0, int nfl);
+                      const double2* tw, hipStream_t s, int f0, int nfl, double2* T1, double2* T2);
   static void col_step(int model, int op, const Geom& g, const Phys& p, const StepPtrs& a, const double2* Mf,
                        double2* Minv, const double2* tw, hipStream_t s, int f0, int nfl);
   static void col_fwd_step(int model, int op, const Geom& g, const Phys& p, const StepPtrs& a, const double2* Mf,
@@ -542,6 +550,8 @@ void launch_col_fwd_step(int model, int op, const Geom& g, const Phys& p, const 
 size_t fwd_step_lds_bytes(int model, const Geom& g);
 void launch_step_elem(int nf, int op, const Geom& g, const Phys& p, const StepPtrs& a,
                       const double2* N, double2* xs, hipStream_t s);
+// a split N completed in place (a.nt1, a.nt2, a.xin)
+void launch_assemble_terms(int nf, const Geom& g, const Phys& p, const StepPtrs& a, double2* N, hipStream_t s);
 void launch_gather(int nf, const Geom& g, const double2* full, double2* compact, hipStream_t s);
 void launch_scatter(int nf, const Geom& g, int lo, int hi, const double2* compact, double2* full,
                     hipStream_t s);

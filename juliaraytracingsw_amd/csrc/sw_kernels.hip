@@ -1716,16 +1716,42 @@ constexpr int model_nf() {
   return (MODEL == MODEL_RSW || MODEL == MODEL_RSWA) ? 3 : (MODEL == MODEL_TY ? 4 : 2);
 }
 
-template <int MODEL, int LOG2N>
+// Thomas–Yamada calcN!'s linear terms (thomasyamada/ThomasYamada.jl:142-145)
+// of field grp added to its nonlinear part r, from the dealiased calcN input
+// X (ζ, uc, vc, pc) at mode i; one definition for k_col_fwd and the updates
+// that assemble a split N (assemble_terms)
+__device__ __forceinline__ double2 ty_linear_terms(const double2* __restrict__ X, long long cf, long long i, int grp,
+                                                   double k, double l, double2 r) {
+#pragma clang fp contract(off)
+  if (grp == 1) return cadd(csub(X[2 * cf + i], cmul_i(X[3 * cf + i], k)), r);  // vc - ik pc
+  if (grp == 2) {                                                                 // -uc - il pc
+    const double2 u = X[cf + i];
+    return cadd(csub(make_double2(-u.x, -u.y), cmul_i(X[3 * cf + i], l)), r);
+  }
+  if (grp == 3) return cadd(csub(cmul_i(X[cf + i], -k), cmul_i(X[2 * cf + i], l)), r);  // -ik uc - il vc
+  return r;
+}
+
+// SPLIT (short columns, sw_api.cpp fsplit): grid (columns, 3 × fields), one
+// term of N_f (nterms) per block — its transform and multiplier, no sum and
+// no linear terms — into N (term 0), T1 or T2; the update that consumes N
+// adds them in k_col_fwd's order (assemble_terms): bitwise the same N
+template <int MODEL, int LOG2N, bool SPLIT = false>
 static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, LOG2N))
     k_col_fwd(Geom g, Phys p, const double2* __restrict__ Mf, double2* __restrict__ N,
-              const double2* __restrict__ X, const double2* __restrict__ tw, int gbase) {
+              const double2* __restrict__ X, const double2* __restrict__ tw, int gbase,
+              double2* __restrict__ T1, double2* __restrict__ T2) {
   using B = Blk<LOG2N>;
   constexpr int NT = B::NT;
   extern __shared__ double2 smem[];
   const LineCtx c = line_ctx<LOG2N>();
   const int krl = (B::NB == 1) ? col_of_block(blockIdx.x, gridDim.x) : blockIdx.x * B::NB + c.ln;
-  const int grp = gbase + blockIdx.y;
+  const int grp = gbase + (SPLIT ? (int)blockIdx.y / 3 : (int)blockIdx.y);
+  const int term = SPLIT ? (int)blockIdx.y % 3 : -1;
+  if constexpr (SPLIT) {
+    const NTerms nt0 = nterms<MODEL>(grp);
+    if ((term == 1 && nt0.fb < 0) || (term == 2 && nt0.fc < 0)) return;
+  }
   const bool live = krl < g.kcn;
   if (B::NB == 1 && !live) return;
   const int krA = krl < g.kcl ? krl : g.kcl - 1;  // in-bounds address
@@ -1746,6 +1772,21 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
   };
 
   const NTerms nt = nterms<MODEL>(grp);
+  if constexpr (SPLIT) {  // one term: its transform and multiplier
+    const int src = term == 0 ? nt.fa : (term == 1 ? nt.fb : nt.fc);
+    const int mul = term == 0 ? nt.ma : (term == 1 ? nt.mb : nt.mc);
+    load_col(Mf + src * MF);
+    col_fft<LOG2N, -1, CD>(v, c.t, tws, line);
+    if (live) {
+      double2* D = (term == 0 ? N : (term == 1 ? T1 : T2)) + (long long)grp * g.cfield + (long long)krl * g.LrP;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const int j = compact_of(g, c.t + s * NT);
+        if (j >= 0) D[j] = apply_mul(v[s], mul, k, lwav(g, c.t + s * NT));
+      }
+    }
+    return;
+  }
   // fft_line leaves F[m = t + s*NT] in v[s]; only live rows are written
   load_col(Mf + nt.fa * MF);
   col_fft<LOG2N, -1, CD>(v, c.t, tws, line);
@@ -1776,20 +1817,8 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, L
             r = mlqg_linear_terms(p, k, lwav(g, c.t + s * NT), X[i], X[g.cfield + i], grp, r);
           }
         }
-        if constexpr (MODEL == MODEL_TY) {
-          // linear terms (thomasyamada/ThomasYamada.jl:142-145), from the
-          // dealiased calcN input (ζ, uc, vc, pc)
-          const long long i = (long long)krl * g.LrP + j;
-          const double l = lwav(g, c.t + s * NT);
-          if (grp == 1) {  // vc - ik pc
-            r = cadd(csub(X[2 * g.cfield + i], cmul_i(X[3 * g.cfield + i], k)), r);
-          } else if (grp == 2) {  // -uc - il pc
-            const double2 u = X[g.cfield + i];
-            r = cadd(csub(make_double2(-u.x, -u.y), cmul_i(X[3 * g.cfield + i], l)), r);
-          } else if (grp == 3) {  // -ik uc - il vc
-            r = cadd(csub(cmul_i(X[g.cfield + i], -k), cmul_i(X[2 * g.cfield + i], l)), r);
-          }
-        }
+        if constexpr (MODEL == MODEL_TY)  // linear terms, from the dealiased calcN input
+          r = ty_linear_terms(X, g.cfield, (long long)krl * g.LrP + j, grp, k, lwav(g, c.t + s * NT), r);
         Nf[j] = r;
       }
     }
@@ -2203,6 +2232,28 @@ __device__ __forceinline__ void op_frk4(const Geom& g, const Phys& p, const Step
   }
 }
 
+// a split N (k_col_fwd SPLIT: term 0 in N, terms 1-2 in a.nt1 / a.nt2, no
+// linear terms) completed at mode i in k_col_fwd's order: the terms summed
+// left to right, then MultiLayerQG's / Thomas–Yamada's linear terms from the
+// calcN input a.xin
+template <int NF>
+__device__ __forceinline__ void assemble_terms(const Geom& g, const Phys& p, const StepPtrs& a, long long i,
+                                               double k, double l, cplx (&n)[NF]) {
+  constexpr int MODEL = NF == 3 ? MODEL_RSW : (NF == 4 ? MODEL_TY : MODEL_QG2);
+  const long long cf = g.cfield;
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    const NTerms nt = nterms<MODEL>(f);
+    double2 r = make_double2(n[f].re, n[f].im);
+    if (nt.fb >= 0) r = cadd(r, a.nt1[f * cf + i]);
+    if (nt.fc >= 0) r = cadd(r, a.nt2[f * cf + i]);
+    if constexpr (MODEL == MODEL_QG2)
+      if (p.model == MODEL_MLQG) r = mlqg_linear_terms(p, k, l, a.xin[i], a.xin[cf + i], f, r);
+    if constexpr (MODEL == MODEL_TY) r = ty_linear_terms(a.xin, cf, i, f, k, l, r);
+    n[f] = cx(r.x, r.y);
+  }
+}
+
 template <int NF, int OP, bool NT = false>
 __device__ __forceinline__ void step_op(const Geom& g, const Phys& p, const StepPtrs& a, long long i,
                                         double k, double l, const cplx n[NF], cplx x[NF]) {
@@ -2265,6 +2316,7 @@ static __global__ void __launch_bounds__(256) k_step_elem(Geom g, Phys p, StepPt
   const double k = kr * g.mk, l = lwav(g, lrow_of(g, j));
   cplx n[NF], x[NF];
   load_vec_once<NF, NT>(N, g.cfield, i, n);  // last use of this calcN output
+  if (a.nt1) assemble_terms<NF>(g, p, a, i, k, l, n);
   step_op<NF, OP, NT>(g, p, a, i, k, l, n, x);
   if (OP == OP_RK4 && a.stage < 4) store_vec<NF>(a.xs, g.cfield, i, x);
 }
@@ -3157,20 +3209,24 @@ void LenOps<L>::col_fwd_alias(int model, const Geom& g, const Geom& ga, int regi
 
 template <int L>
 void LenOps<L>::col_fwd(int model, const Geom& g, const Phys& p, const double2* Mf, double2* N, const double2* X,
-                        const double2* tw, hipStream_t s, int f0, int nfl) {
-  const dim3 grid(col_blocks<L>(g), nfl);
-  if (model == MODEL_RSW)
-    hipLaunchKernelGGL((k_col_fwd<MODEL_RSW, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, Mf, N, X,
-                       tw, f0);
+                        const double2* tw, hipStream_t s, int f0, int nfl, double2* T1, double2* T2) {
+  const dim3 grid(col_blocks<L>(g), nfl), grid3(col_blocks<L>(g), 3 * nfl), blk(Blk<L>::THREADS);
+  const size_t sh = lds_bytes<L>();
+  const bool split = T1 != nullptr;  // (RSW, 2LQG / MultiLayerQG, Thomas–Yamada)
+  if (model == MODEL_RSW && split)
+    hipLaunchKernelGGL((k_col_fwd<MODEL_RSW, L, true>), grid3, blk, sh, s, g, p, Mf, N, X, tw, f0, T1, T2);
+  else if (model == MODEL_RSW)
+    hipLaunchKernelGGL((k_col_fwd<MODEL_RSW, L>), grid, blk, sh, s, g, p, Mf, N, X, tw, f0, nullptr, nullptr);
   else if (model == MODEL_RSWA)
-    hipLaunchKernelGGL((k_col_fwd<MODEL_RSWA, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, Mf, N, X,
-                       tw, f0);
+    hipLaunchKernelGGL((k_col_fwd<MODEL_RSWA, L>), grid, blk, sh, s, g, p, Mf, N, X, tw, f0, nullptr, nullptr);
+  else if (model == MODEL_TY && split)
+    hipLaunchKernelGGL((k_col_fwd<MODEL_TY, L, true>), grid3, blk, sh, s, g, p, Mf, N, X, tw, f0, T1, T2);
   else if (model == MODEL_TY)
-    hipLaunchKernelGGL((k_col_fwd<MODEL_TY, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, Mf, N, X,
-                       tw, f0);
+    hipLaunchKernelGGL((k_col_fwd<MODEL_TY, L>), grid, blk, sh, s, g, p, Mf, N, X, tw, f0, nullptr, nullptr);
+  else if (split)
+    hipLaunchKernelGGL((k_col_fwd<MODEL_QG2, L, true>), grid3, blk, sh, s, g, p, Mf, N, X, tw, f0, T1, T2);
   else
-    hipLaunchKernelGGL((k_col_fwd<MODEL_QG2, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, Mf, N, X,
-                       tw, f0);
+    hipLaunchKernelGGL((k_col_fwd<MODEL_QG2, L>), grid, blk, sh, s, g, p, Mf, N, X, tw, f0, nullptr, nullptr);
 }
 
 template <int L>
@@ -3314,9 +3370,11 @@ int row_lines_per_block(int model, int log2nx) {
   return nb;
 }
 void launch_col_fwd(int model, const Geom& g, const Phys& p, const double2* Mfwd, double2* N,
-                    const double2* X, const double2* tw_y, hipStream_t s, int f0, int nfl) {
+                    const double2* X, const double2* tw_y, hipStream_t s, int f0, int nfl, double2* T1,
+                    double2* T2) {
   if (nfl < 0) nfl = col_fields(model) - f0;
-  by_len(g.log2ny, [&](auto L) { LenOps<decltype(L)::value>::col_fwd(model, g, p, Mfwd, N, X, tw_y, s, f0, nfl); });
+  by_len(g.log2ny,
+         [&](auto L) { LenOps<decltype(L)::value>::col_fwd(model, g, p, Mfwd, N, X, tw_y, s, f0, nfl, T1, T2); });
 }
 
 static inline dim3 mode_grid(const Geom& g) { return dim3((unsigned)((g.cfield + 255) / 256)); }
@@ -3358,6 +3416,23 @@ void launch_step_elem(int nf, int op, const Geom& g, const Phys& p, const StepPt
     else SW_SE(2, OP_RK4);
   }
 #undef SW_SE
+}
+
+// a split N completed in place (sw_calcN: the caller reads N itself)
+template <int NF>
+static __global__ void __launch_bounds__(256) k_assemble(Geom g, Phys p, StepPtrs a, double2* __restrict__ N) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  int kr, j;
+  if (i >= g.cfield || !mode_of(g, i, kr, j)) return;
+  cplx n[NF];
+  load_vec<NF>(N, g.cfield, i, n);
+  assemble_terms<NF>(g, p, a, i, kr * g.mk, lwav(g, lrow_of(g, j)), n);
+  store_vec<NF>(N, g.cfield, i, n);
+}
+void launch_assemble_terms(int nf, const Geom& g, const Phys& p, const StepPtrs& a, double2* N, hipStream_t s) {
+  if (nf == 4) hipLaunchKernelGGL((k_assemble<4>), mode_grid(g), dim3(256), 0, s, g, p, a, N);
+  else if (nf == 3) hipLaunchKernelGGL((k_assemble<3>), mode_grid(g), dim3(256), 0, s, g, p, a, N);
+  else hipLaunchKernelGGL((k_assemble<2>), mode_grid(g), dim3(256), 0, s, g, p, a, N);
 }
 
 void launch_gather(int nf, const Geom& g, const double2* full, double2* cmp, hipStream_t s) {

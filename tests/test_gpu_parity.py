@@ -161,15 +161,17 @@ def test_fused_equals_unfused(name, mode, monkeypatch):
     b.close()
 
 
-@pytest.mark.parametrize("knob", ["SW_INV_SPLIT", "SW_ROW_SPLIT"])
-@pytest.mark.parametrize("name,n", [("qg2_ifmab3", 128), ("mlqg_frk4", 512), ("qg2_fab3", 1024), ("rsw_ifmab3", 512), ("rsw_fab3", 256),
+@pytest.mark.parametrize("knob", ["SW_INV_SPLIT", "SW_ROW_SPLIT", "SW_FWD_SPLIT"])
+@pytest.mark.parametrize("name,n", [("qg2_ifmab3", 128), ("mlqg_frk4", 512), ("qg2_fab3", 1024), ("rsw_ifmab3", 512),
+                                    ("rsw_ifmrk4", 256), ("qg2_ifmrk4", 256), ("rsw_fab3", 256),
                                     ("ty_etdrk4", 128), ("ty_etdrk4", 512), ("ty_etdrk4", 1024)])
 def test_split_passes_bitwise(name, n, knob, monkeypatch):
     """Short lines split over more blocks — the column inverse with one
     output per block (SW_INV_SPLIT, Geom::isplit: 2LQG / MultiLayerQG /
     Thomas–Yamada) and the 2LQG / MultiLayerQG row in two blocks
-    (SW_ROW_SPLIT, Geom::rsplit) — give bitwise the states and calcN of the
-    one-block passes."""
+    (SW_ROW_SPLIT, Geom::rsplit) and the forward column pass with one term
+    of N per block, completed by the update (SW_FWD_SPLIT) — give bitwise
+    the states and calcN of the one-block passes."""
     p = sw_cases.case_params(name, n)
     pr = sw_cases.oracle_problem(p)
     pr.set_solution(sw_cases.initial_condition(p, pr.grid))
