@@ -348,7 +348,11 @@ double kernel_bytes(const sw_ctx* c, int kid) {
       case K_COLINV: b += nf * F + c->ninv * Mc; break;
       case K_ROW: b += (c->ninv + c->nfwd) * Mr; break;
       case K_COLFWD: b += c->nfwd * Mc + nf * F; break;
-      case K_UPD: b += (op_fields(c) + nf) * F; break;  // + N read
+      case K_UPD: {  // + N read; IFMAB3's N already in its history slot is not written again
+        const bool n_in_slot = c->cfg.stepper == SW_STEP_IFMAB3 && !c->fsplit;
+        b += (op_fields(c) + nf - (n_in_slot ? nf : 0)) * F;
+        break;
+      }
       case K_COLSTEP: b += c->nfwd * Mc + op_fields(c) * F + c->ninv * Mc; break;
       case K_FWDSTEP: b += c->nfwd * Mc + op_fields(c) * F; break;  // N never in HBM
       case K_XCHG:  // bytes leaving this slab in one inverse + one forward transpose

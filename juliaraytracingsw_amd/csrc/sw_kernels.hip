@@ -2041,9 +2041,11 @@ __device__ __forceinline__ void op_fab3(const Geom& g, const Phys& p, const Step
 // utils/IFMAB3.jl:129-160: Euler for step < 3, else AB3 with E N₋₁, E2 N₋₂;
 // then sol = E·(…); filter.  N becomes history.  E = exp(dt L), E2 =
 // exp(2 dt L) evaluated per mode in closed form (sw_internal.hpp ExpOf).
+// the new state x at mode i without stores (op_ifmab3; k_step_elem when N
+// already sits in the history slot the op would store it to)
 template <int NF, bool NT>
-__device__ __forceinline__ void op_ifmab3(const Geom& g, const Phys& p, const StepPtrs& a, long long i,
-                                          double k, double l, const cplx n[NF], cplx x[NF]) {
+__device__ __forceinline__ void ifmab3_x(const Geom& g, const Phys& p, const StepPtrs& a, long long i, double k,
+                                         double l, const cplx n[NF], cplx x[NF]) {
 #pragma clang fp contract(off)
   const long long cf = g.cfield;
   cplx s[NF], y[NF];
@@ -2070,8 +2072,13 @@ __device__ __forceinline__ void op_ifmab3(const Geom& g, const Phys& p, const St
 #pragma unroll
     for (int f = 0; f < NF; ++f) x[f] = cx(x[f].re * filt, x[f].im * filt);
   }
-  store_vec_once<NF, NT>(a.h0, cf, i, n);
-  store_vec<NF>(a.sol_out, cf, i, x);  // the next col_inv reads it
+}
+template <int NF, bool NT>
+__device__ __forceinline__ void op_ifmab3(const Geom& g, const Phys& p, const StepPtrs& a, long long i,
+                                          double k, double l, const cplx n[NF], cplx x[NF]) {
+  ifmab3_x<NF, NT>(g, p, a, i, k, l, n, x);
+  store_vec_once<NF, NT>(a.h0, g.cfield, i, n);
+  store_vec<NF>(a.sol_out, g.cfield, i, x);  // the next col_inv reads it
 }
 
 // Lawson IF-RK4, one calcN result per stage, H = exp(dt L / 2)
@@ -2317,6 +2324,16 @@ static __global__ void __launch_bounds__(256) k_step_elem(Geom g, Phys p, StepPt
   cplx n[NF], x[NF];
   load_vec_once<NF, NT>(N, g.cfield, i, n);  // last use of this calcN output
   if (a.nt1) assemble_terms<NF>(g, p, a, i, k, l, n);
+  if constexpr (OP == OP_IFMAB3) {
+    // N already sits in the history slot op_ifmab3 stores it to (calcN wrote
+    // it there: sw_api.cpp run_stage): only the new state is written — unless
+    // it was completed here from split terms
+    if (N == a.h0 && !a.nt1) {
+      ifmab3_x<NF, NT>(g, p, a, i, k, l, n, x);
+      store_vec<NF>(a.sol_out, g.cfield, i, x);
+      return;
+    }
+  }
   step_op<NF, OP, NT>(g, p, a, i, k, l, n, x);
   if (OP == OP_RK4 && a.stage < 4) store_vec<NF>(a.xs, g.cfield, i, x);
 }
