@@ -351,6 +351,11 @@ def main():
         barrier_sync()
         dt = max_over_ranks(time.perf_counter() - t0)
         extra = 0
+        # the box monitor covers the extra warm-up and the timed steps (a
+        # 20-step region alone is ~3 ms, one amdsmi sample): regions[tag] is
+        # the whole window, tag_warmup and tag_timed its two parts
+        if monitor is not None:
+            monitor.start()
         if args.min_warmup_s > 0 and dt < args.min_warmup_s:
             per = dt / warmup if warmup > 0 else 1e-3
             extra = int(min(100000, math.ceil((args.min_warmup_s - dt) / max(per, 1e-6))))
@@ -359,14 +364,18 @@ def main():
         extra_warmup[tag] = extra
         barrier_sync()
         if monitor is not None:
-            monitor.start()
+            box_regions[tag + "_warmup"] = dict(monitor.lap(), steps=extra)
         t0 = time.perf_counter()
         if prob is not None:
             prob.stepforward(steps)  # sw_step returns when its stream is drained
         barrier_sync()
         el = time.perf_counter() - t0
         if monitor is not None:
-            box_regions[tag] = monitor.stop()
+            box_regions[tag + "_timed"] = dict(monitor.lap(), steps=steps)
+            whole = monitor.stop(whole=True)
+            n = extra + steps
+            whole.update(steps=n, energy_J_per_step=(whole["energy_J"] / n if whole.get("energy_J") and n else None))
+            box_regions[tag] = whole
         return max_over_ranks(el)
 
     over = {k: v for k, v in (("nutune", args.nutune), ("cfltune", args.cfltune)) if v is not None}

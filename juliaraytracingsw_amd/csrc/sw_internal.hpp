@@ -76,6 +76,7 @@ struct Geom {
   int fsy, fsk, fa;
   int isplit;         // 2LQG/MLQG/TY column inverse: one output per block (k_col_inv SPLIT)
   int rsplit;         // RSW/2LQG/MLQG/TY row over 2 / 4 blocks (k_row SPLIT)
+  int rsp;            // RSW decimated row over 2 one-line blocks (k_row_rsw_sp, SW_ROW_SP)
 };
 
 struct Phys {
@@ -515,6 +516,10 @@ struct StepPtrs {
   const double2* nt1;
   const double2* nt2;
   const double2* xin;
+  // sw_step's NaN/Inf scan folded into the update: the ops
+  // that store the new state set *nan when one of its live values is not
+  // finite (nullptr: no scan — the aliased-mode updates, profiling)
+  int* nan;
 };
 enum { OP_FAB3 = 0, OP_IFMAB3 = 1, OP_RK4 = 2, OP_ETDRK4 = 3, OP_FRK4 = 4 };
 enum { ETD_E = 0, ETD_E2, ETD_ZETA, ETD_ALPHA, ETD_BETA, ETD_GAMMA, ETD_N };

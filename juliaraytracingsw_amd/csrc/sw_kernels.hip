@@ -46,6 +46,28 @@ __device__ __forceinline__ void state_st(double2* p, double2 v) {
 #endif
   *p = v;
 }
+// sw_step's blow-up check (rsw/RSWDriver.jl:213-218) at the store of the new
+// state, whose values are in registers there: one flag per call instead of a
+// separate pass over the state after the steps (k_nan_check, 44.8 MB at
+// 2048²).  `bad` = some value this lane stored is not finite; the first such
+// active lane of the wave stores 1 (a plain vector store: every writer writes
+// the same value, and the flag may be pinned host memory, sw_api.cpp hflag).
+__device__ __forceinline__ bool nonfinite(double2 v) { return !isfinite(v.x) || !isfinite(v.y); }
+__device__ __forceinline__ bool nonfinite(cplx v) { return !isfinite(v.re) || !isfinite(v.im); }
+__device__ __forceinline__ void note_nonfinite(int* flag, bool bad) {
+  if (flag == nullptr) return;
+  const unsigned long long m = __ballot(bad);
+  if (m != 0ull && (int)__lane_id() == __ffsll((long long)m) - 1)
+    __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <int NF>
+__device__ __forceinline__ void note_state(const StepPtrs& a, const cplx* x) {
+  bool bad = false;
+#pragma unroll
+  for (int f = 0; f < NF; ++f) bad |= nonfinite(x[f]);
+  note_nonfinite(a.nan, bad);
+}
+
 // mixed-field reads: the row pass's inverse inputs, the column pass's
 // forward inputs (read once; their writer's stores stay temporal)
 __device__ __forceinline__ double2 mix_ld_row(const double2* p) {
@@ -2027,6 +2049,7 @@ __device__ __forceinline__ cplx op_fab3_field(const Geom& g, const Phys& p, cons
   fab3_compute<NF, F>(g, p, a.euler, k, l, n, s, r1, r2, x, rhs);
   state_st<NT>(a.h0 + F * cf + i, make_double2(rhs.re, rhs.im));
   a.sol_out[F * cf + i] = make_double2(x.re, x.im);  // the next col_inv reads it
+  note_nonfinite(a.nan, nonfinite(x));
   return x;
 }
 
@@ -2079,6 +2102,7 @@ __device__ __forceinline__ void op_ifmab3(const Geom& g, const Phys& p, const St
   ifmab3_x<NF, NT>(g, p, a, i, k, l, n, x);
   store_vec_once<NF, NT>(a.h0, g.cfield, i, n);
   store_vec<NF>(a.sol_out, g.cfield, i, x);  // the next col_inv reads it
+  note_state<NF>(a, x);
 }
 
 // Lawson IF-RK4, one calcN result per stage, H = exp(dt L / 2)
@@ -2129,6 +2153,7 @@ __device__ __forceinline__ void op_rk4(const Geom& g, const Phys& p, const StepP
       x[f] = cx(r.re * filt, r.im * filt);
     }
     store_vec<NF>(a.sol_out, cf, i, x);
+    note_state<NF>(a, x);
   }
 }
 
@@ -2188,6 +2213,7 @@ __device__ __forceinline__ void op_etdrk4(const Geom& g, const Phys& p, const St
 #pragma unroll
     for (int f = 0; f < NF; ++f) x[f] = acc[f] + G * n[f];
     store_vec<NF>(a.sol_out, cf, i, x);
+    note_state<NF>(a, x);
   }
 }
 
@@ -2236,6 +2262,7 @@ __device__ __forceinline__ void op_frk4(const Geom& g, const Phys& p, const Step
       x[f] = cx(r.re * filt, r.im * filt);
     }
     store_vec<NF>(a.sol_out, cf, i, x);
+    note_state<NF>(a, x);
   }
 }
 
@@ -2331,6 +2358,7 @@ static __global__ void __launch_bounds__(256) k_step_elem(Geom g, Phys p, StepPt
     if (N == a.h0 && !a.nt1) {
       ifmab3_x<NF, NT>(g, p, a, i, k, l, n, x);
       store_vec<NF>(a.sol_out, g.cfield, i, x);
+      note_state<NF>(a, x);
       return;
     }
   }
@@ -2682,6 +2710,7 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, (Blk<LOG2N>::THREA
   // dead modes are computed and dropped), one memory round trip per group
   // instead of two per slot.
   double2 x[8];
+  bool bad = false;  // (note_nonfinite)
   {
     const long long cf = g.cfield;
     // compact fields hold the kcn live columns only: padding lines of a
@@ -2746,9 +2775,11 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, (Blk<LOG2N>::THREA
           state_st<STREAM>(a.h0 + f * cf + i, make_double2(rhs.re, rhs.im));
           state_st<STREAM>(a.sol_out + f * cf + i, make_double2(r.re, r.im));
         }
+        bad |= ok & nonfinite(r);
       }
     }
   }
+  note_nonfinite(a.nan, bad);
   // ---- inverse transforms of field f for the next calcN (as k_col_inv)
   const double scale = 1.0 / ((double)g.nx * (double)g.ny);
   auto store = [&](int o) {
@@ -3135,6 +3166,128 @@ void LenOps<L>::col_inv(int model, const Geom& g, const Phys& p, const double2* 
     hipLaunchKernelGGL((k_col_inv<MODEL_QG2, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
 }
 
+// ===========================================================================
+// row_rsw_sp: the decimated RSW row (1024-4096-point lines)
+// over two blocks per row with ONE line buffer each and the transforms one
+// after the other.  Part 0 forms ζu + iζv and K (outputs 0-2), part 1 uη + ivη
+// (outputs 3-4); each transforms u + iv and the half of η + iζ it needs (part
+// 0 reads no H, part 1 no Uy).  7 line transforms per row instead of 5, for a
+// quarter of the LDS per block (32 KB at 2048) and half the live lines: up to
+// SW_MINW_ROW_SP waves per SIMD instead of 2.  The same arithmetic on the
+// same pairs as k_row: bitwise the same outputs.  1-D grid of 2 × rows: the
+// two parts of 8 consecutive rows on one XCD label (the rows of a 2×4 tile
+// meet in one L2).  SW_ROW_SP=1 selects it (sw_api.cpp, Geom::rsp).
+// ===========================================================================
+#ifndef SW_MINW_ROW_SP
+#define SW_MINW_ROW_SP 4
+#endif
+#ifndef SW_ROW_SP_LEAN
+#define SW_ROW_SP_LEAN false  // true: offsets per use (RowIdx LEAN)
+#endif
+#ifndef SW_ROW_SP_FLY
+#define SW_ROW_SP_FLY false  // true: the wave-local stage twiddles read per stage
+#endif
+__device__ __forceinline__ void row_part_of_block(int b, int nb, int& y, int& part) {
+  if ((nb & 127) == 0) {
+    const int q = b >> 7, j = (b >> 3) & 15, x = b & 7;
+    y = (q << 6) + (x << 3) + (j >> 1);
+    part = j & 1;
+  } else {
+    y = b >> 1;
+    part = b & 1;
+  }
+}
+template <int LOG2N, bool PRUNE>
+static __global__ void __launch_bounds__((BlkRow<MODEL_RSW, LOG2N>::THREADS), SW_MINW_ROW_SP)
+    k_row_rsw_sp(Geom g, Phys p, const double2* __restrict__ Mi, double2* __restrict__ Mo,
+                 const double2* __restrict__ tw, int yoff) {
+  using Bk = BlkRow<MODEL_RSW, LOG2N>;
+  static_assert(Bk::NB == 1 && roww<LOG2N>() > 0, "one decimated row per block");
+  constexpr int W = roww<LOG2N>();
+  extern __shared__ double2 smem[];
+  double2* line = smem;
+  const LineCtx c = line_ctx<LOG2N>();
+  int yl, part;
+  row_part_of_block(blockIdx.x, gridDim.x, yl, part);
+  const int y = yoff + yl;
+  RowIdx<LOG2N, SW_ROW_SP_LEAN> ri;
+  ri.init(g, c.t, y);
+  Twiddles<9, SW_ROW_SP_FLY> tq;
+  tq.load(c.t & 63, tw, LOG2N - 9);
+  const double2 wt = tw[c.t];
+  const long long MF = g.mfield;
+  const double2 *U = Mi, *V = Mi + MF, *H = Mi + 2 * MF, *Uy = Mi + 3 * MF;
+  using R = RowIdx<LOG2N, SW_ROW_SP_LEAN>;
+  double2 w[2][8];
+  {  // u + i v, and η (part 1) or i ζ (part 0): one read of each field a part needs
+    double2 u[8], vv[8], x[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      u[s] = vv[s] = x[s] = zero2();
+      if (R::inv_any(g, s)) {
+        const int o = ri.oinv(g, s);
+        u[s] = mix_ld_row(U + o);
+        vv[s] = mix_ld_row(V + o);
+        x[s] = mix_ld_row((part ? H : Uy) + o);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int kk = R::kk(ri.t, s);
+      const bool mir = s >= 4 && kk != (R::N >> 1), live = kk < g.kc;
+      w[0][s] = pair_z(u[s], vv[s], kk, mir, live);
+      w[1][s] = part ? pair_z(x[s], zero2(), kk, mir, live)
+                     : pair_z(zero2(), csub(cmul_i(vv[s], kk * g.mk), x[s]), kk, mir, live);
+    }
+  }
+  fftw_dif<W, +1, 1, false, SW_ROW_SP_FLY, false, PRUNE>(reinterpret_cast<double2(&)[1][8]>(w[0]), c.t, wt, tq, line, 0);
+  fftw_dif<W, +1, 1, true, SW_ROW_SP_FLY, false, PRUNE>(reinterpret_cast<double2(&)[1][8]>(w[1]), c.t, wt, tq, line, 0);
+  if (part) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const double u = w[0][s].x, vv = w[0][s].y, eta = w[1][s].x;
+      w[0][s] = make_double2(u * eta, vv * eta);  // uη + i vη
+    }
+    fftw_dit<W, -1, 1, SW_ROW_SP_FLY, true, false, PRUNE>(reinterpret_cast<double2(&)[1][8]>(w[0]), c.t, wt, tq, line, 0);
+    split_pairs<LOG2N, 1, PRUNE>(reinterpret_cast<const double2(&)[1][8]>(w[0]), c.t, g, line, 0,
+                                 [&](int, int k, int s, double2 a, double2 b) {
+                                   const int o = ri.ofwd(g, s);
+                                   Mo[3 * MF + o] = cmul_i(a, -(k * g.mk));
+                                   Mo[4 * MF + o] = b;
+                                 });
+    return;
+  }
+  double kk[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const double u = w[0][s].x, vv = w[0][s].y, zeta = w[1][s].y;
+    kk[s] = 0.5 * (u * u + vv * vv);
+    w[0][s] = make_double2(zeta * u, zeta * vv);  // ζu + i ζv
+  }
+  fftw_dit<W, -1, 1, SW_ROW_SP_FLY, true, false, PRUNE>(reinterpret_cast<double2(&)[1][8]>(w[0]), c.t, wt, tq, line, 0);
+  double2 zv[8];  // (ζv)^ of the live slots
+#pragma unroll
+  for (int s = 0; s < 8; ++s) zv[s] = zero2();
+  split_pairs<LOG2N, 1, PRUNE>(reinterpret_cast<const double2(&)[1][8]>(w[0]), c.t, g, line, 0,
+                               [&](int, int, int s, double2 a, double2 b) {
+                                 Mo[2 * MF + ri.ofwd(g, s)] = a;
+                                 zv[s] = b;
+                               });
+#pragma unroll
+  for (int s = 0; s < 8; ++s) w[1][s] = make_double2(kk[s], 0.0);
+  lds_barrier();  // split_pairs' mirror reads are done
+  fftw_dit<W, -1, 1, SW_ROW_SP_FLY, false, false, PRUNE>(reinterpret_cast<double2(&)[1][8]>(w[1]), c.t, wt, tq, line, 0);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const int k = c.t + s * Bk::NT;
+    if (R::fwd_any(g, s) && k < g.kc) {
+      const int o = ri.ofwd(g, s);
+      Mo[o] = cadd(cmul_i(w[1][s], -(k * g.mk)), zv[s]);
+      Mo[MF + o] = w[1][s];
+    }
+  }
+}
+
 // the pruned row transforms (k_row PRUNE) where they apply: the decimated
 // transforms (roww) and a live band kc <= 3N/8 (every 2/3-rule grid;
 // MultiLayerQG's aliased_fraction = 0 keeps the full ones).  SW_ROW_PRUNE=0:
@@ -3159,11 +3312,24 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
   constexpr size_t sh_ty = FftPlan<L>::LDS * BT::NB * sizeof(double2);
   if (model == MODEL_RSW) {
     constexpr int nbr = rowh_nb<L, true>();
-    if constexpr (rsw_row_half<L>())
+    if constexpr (rsw_row_half<L>()) {
       hipLaunchKernelGGL((k_row_rsw_h<L>), dim3(nrows / nbr), dim3(RowH<L>::NTH * nbr),
                          nbr * rsw_rowh_lines<L>() * FftPlan<L - 1>::LDS * sizeof(double2), s, g, p, Mi, Mo,
                          tw, y0);
-    else if (row_prunable<L>(g))
+      return;
+    }
+    if constexpr (roww<L>() > 0 && BR::NB == 1) {
+      if (g.rsp) {  // (Geom::rsp: the row over two blocks, k_row_rsw_sp)
+        if (row_prunable<L>(g))
+          hipLaunchKernelGGL((k_row_rsw_sp<L, true>), dim3(2 * nrows), dim3(BR::THREADS),
+                             FftPlan<L>::LDS * sizeof(double2), s, g, p, Mi, Mo, tw, y0);
+        else
+          hipLaunchKernelGGL((k_row_rsw_sp<L, false>), dim3(2 * nrows), dim3(BR::THREADS),
+                             FftPlan<L>::LDS * sizeof(double2), s, g, p, Mi, Mo, tw, y0);
+        return;
+      }
+    }
+    if (row_prunable<L>(g))
       hipLaunchKernelGGL((k_row<MODEL_RSW, L, false, true>), dim3(nrows / BR::NB), dim3(BR::THREADS), sh_rsw, s, g,
                          p, Mi, Mo, tw, y0, nullptr);
     else if (g.rsplit && row_lds_lines<MODEL_RSW, L>() == 2 && roww<L>() == 0)

@@ -25,6 +25,7 @@ from __future__ import annotations
 import ctypes as C
 import math
 import os
+import time
 import types
 import weakref
 
@@ -140,10 +141,26 @@ class Twin:
     def __init__(self):
         self.lib = _lib.load()
         self.calls = []
+        # tools/driver_cadence.py: per-entry-point wall time of the C calls
+        # ({name: [count, seconds]}) and the frame loops' marks, when set
+        self.times = None
+        self.marks = None
 
     def c(self, name, *args):
         self.calls.append(name)
-        return getattr(self.lib, name)(*args)
+        if self.times is None:
+            return getattr(self.lib, name)(*args)
+        t0 = time.perf_counter()
+        rc = getattr(self.lib, name)(*args)
+        e = self.times.setdefault(name, [0, 0.0])
+        e[0] += 1
+        e[1] += time.perf_counter() - t0
+        return rc
+
+    def mark(self, label):
+        """a frame loop's boundary (timing runs only; no C call)"""
+        if self.marks is not None:
+            self.marks.append((label, time.perf_counter(), len(self.calls)))
 
     def check(self, ts, rc, what):
         if rc != 0:
@@ -544,6 +561,7 @@ def rsw_driver_start(tw, nx=128, nsteps=240, output_freq=20, diags_freq=10, spin
                                                                grid.rfft(prob.vars.η))
     outputs.append((prob.clock.step, prob.sol.copy()))
     cfls = []
+    tw.mark("frames")
     for step in range(0, round(nsteps / output_freq) + 1):
         if step % 100 == 0:
             v = prob.vars
@@ -554,6 +572,7 @@ def rsw_driver_start(tw, nx=128, nsteps=240, output_freq=20, diags_freq=10, spin
         rsw_updatevars(tw, prob)
         if prob.clock.step >= spinup_step:
             outputs.append((prob.clock.step, prob.sol.copy()))
+    tw.mark("end")
     return prob, diags, outputs, ic, cfls
 
 
@@ -596,6 +615,7 @@ def two_layer_driver_start(tw, nx=128, nsteps=240, output_freq=20, diags_freq=10
     prob.vars.ψh[...] = grid.rfft(prob.vars.ψ)
     outputs = [("problem",), (prob.clock.step, prob.sol.copy())]
     cfls = []
+    tw.mark("frames")
     for step in range(0, round(nsteps / output_freq) + 1):
         if step % 100 == 0:
             v = prob.vars
@@ -606,6 +626,7 @@ def two_layer_driver_start(tw, nx=128, nsteps=240, output_freq=20, diags_freq=10
         qg2_updatevars(tw, prob)
         if prob.clock.step >= spinup_step:
             outputs.append((prob.clock.step, prob.sol.copy()))
+    tw.mark("end")
     return prob, diags, outputs, ic, cfls
 
 
@@ -641,6 +662,7 @@ def ty_driver_start(tw, nx=64, startup_dt=3e-2, dt=5e-3, startup_nsteps=200, sta
     ty_updatevars(tw, sp)
     outputs.append((sp.clock.step, sp.sol.copy()))
     startup_steps = 0
+    tw.mark("startup")
     for j in range(0, round(startup_nsteps / startup_nsubs) + 1):
         if j % (4000 / startup_nsubs) == 0:
             v = sp.vars
@@ -650,6 +672,7 @@ def ty_driver_start(tw, nx=64, startup_dt=3e-2, dt=5e-3, startup_nsteps=200, sta
         startup_steps += startup_nsubs
         ty_updatevars(tw, sp, all_=False)  # enforce_reality_condition!
         ty_updatevars(tw, sp)
+    tw.mark("startup_end")
     startup_diags = diags
     outputs.append((sp.clock.step, sp.sol.copy()))
     if not libsw_cpu:
@@ -662,11 +685,13 @@ def ty_driver_start(tw, nx=64, startup_dt=3e-2, dt=5e-3, startup_nsteps=200, sta
              Diagnostic(barotropic_energy, prob, nsteps=startup_nsteps, freq=25)]
     ty_updatevars(tw, prob)
     outputs.append((prob.clock.step, prob.sol.copy()))
+    tw.mark("frames")
     for j in range(0, round(nsteps / nsubs) + 1):
         ff_stepforward(tw, prob, diags, nsubs)
         ty_updatevars(tw, prob, all_=False)
         ty_updatevars(tw, prob)
         outputs.append((prob.clock.step, prob.sol.copy()))
+    tw.mark("end")
     return prob, startup_diags, diags, None, outputs, ic, startup_steps
 
 
@@ -704,6 +729,7 @@ def mlqg_simulation_start(tw, nx=64, nsteps=100, nsubs=25, seed=1234, amplitude_
     energies = tw.energy_method(host_energies, lambda r: ([r.ke, r.ke2], [r.pe]))
     diags = [Diagnostic(energies, prob, nsteps=nsteps)]
     outputs = [("problem",)]
+    tw.mark("frames")
     for j in range(0, round(nsteps / nsubs) + 1):
         if j % (1000 / nsubs) == 0:
             v = prob.vars
@@ -711,4 +737,5 @@ def mlqg_simulation_start(tw, nx=64, nsteps=100, nsubs=25, seed=1234, amplitude_
         ff_stepforward(tw, prob, diags, nsubs)
         mlqg_updatevars(tw, prob)
         outputs.append((prob.clock.step, prob.vars.ψh.copy()))
+    tw.mark("end")
     return prob, diags, outputs, ic

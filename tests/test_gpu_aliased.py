@@ -184,8 +184,7 @@ def test_abi8_checkpoint_aliased_state_inferred():
     by its own aliased modes: one written with aliased_state (nonzero there)
     restores into an aliased context — bitwise, as an ABI-9 one — and is
     refused by a default one (which would drop those modes); a default
-    context's ABI-8 blob (zeros there) restores into a default context and is
-    refused by an aliased one."""
+    context's ABI-8 blob (zeros there) restores into either."""
 
     def abi8(blob):
         b = blob.copy()
@@ -213,10 +212,58 @@ def test_abi8_checkpoint_aliased_state_inferred():
     d.stepforward(3)
     d2.stepforward(3)
     assert np.array_equal(d.sol, d2.sol)
-    with pytest.raises(LibSWError, match="zero aliased modes"):
-        b.ctx.set_checkpoint(dblob)
+    #  a blob with all-zero aliased modes is valid for an
+    # aliased_state context too: the same state as the default run's, its
+    # aliased modes then evolve from zero
+    b.ctx.set_checkpoint(dblob)
+    b.stepforward(3)
+    got = pr.grid.dealias(b.sol.copy())
+    assert np.max(np.abs(got - d2.sol)) <= 1e-13 * np.max(np.abs(d2.sol))
     for x in (b, d, d2, prob):
         x.close()
+
+
+def test_abi8_step0_aliased_blob_loads_both_ways():
+    """an aliased_state context's ABI-8 checkpoint taken right
+    after set_state with a dealiased IC (all aliased modes zero) restores into
+    a default context and into an aliased_state one, and both continue as the
+    context it was taken from does on the live modes."""
+    p, pr, prob = _setup("qg2_ifmab3")
+    prob.sol = pr.grid.dealias(pr.sol.copy())
+    blob = prob.ctx.get_checkpoint().copy()
+    blob[8:12] = np.frombuffer(np.int32(8).tobytes(), np.uint8)
+    blob[56:64] = 0
+    prob.stepforward(4)
+    want = prob.sol
+    for alias in (False, True):
+        q = sw_cases.libsw_problem(p, aliased_state=alias)
+        q.ctx.set_checkpoint(blob)
+        q.stepforward(4)
+        got = q.sol if alias else pr.grid.dealias(q.sol.copy())
+        ref = want if alias else pr.grid.dealias(want.copy())
+        assert np.max(np.abs(got - ref)) <= 1e-13 * np.max(np.abs(ref))
+        q.close()
+    prob.close()
+
+
+def test_abi8_blob_of_another_problem_same_size_refused():
+    """an ABI-8 blob of the same byte count but another
+    problem — 2LQG IFMAB3 64x64 (state + 2 history slots of 2 fields) against
+    RSW IFMRK4 64x128 (the state alone, 3 fields: 3*2*33*64 = 3*33*128
+    modes) — is refused as another problem before its aliased modes are
+    scanned (the scan would read 3 arrays of the RSW shape past the blob)."""
+    from juliaraytracingsw_amd import rotating_shallow_water as RSW
+
+    p, pr, prob = _setup("qg2_ifmab3")
+    blob = prob.ctx.get_checkpoint().copy()
+    blob[8:12] = np.frombuffer(np.int32(8).tobytes(), np.uint8)
+    blob[56:64] = 0
+    r = RSW.Problem("gpu", nx=64, ny=128, dt=1e-3, stepper="IFMRK4")
+    assert r.ctx.get_checkpoint().nbytes == blob.nbytes
+    with pytest.raises(LibSWError, match="different problem"):
+        r.ctx.set_checkpoint(blob)
+    r.close()
+    prob.close()
 
 
 def test_updatevars_dealiases_the_state():

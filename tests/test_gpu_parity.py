@@ -270,17 +270,45 @@ def test_qg2_physical_and_energy():
     prob.close()
 
 
-def test_nan_detection():
+@pytest.mark.parametrize("case", sw_cases.ALL_CASES)
+def test_nan_detection(case):
+    """sw_step's blow-up check is folded into every update kernel that stores
+    the new state (StepPtrs::nan; no separate pass over the state): one
+    non-finite mode in the state is reported as SW_E_NAN by the model/stepper
+    pair's own update path (fused column step, forward + update, elementwise)."""
     from juliaraytracingsw_amd import LibSWError
 
-    p = sw_cases.case_params("rsw_fab3", 64)
+    p = sw_cases.case_params(case, 64)
     prob = sw_cases.libsw_problem(p)
-    ic = np.zeros((3, 64, 33), complex)
+    ic = np.zeros_like(prob.sol)
     ic[0, 1, 1] = np.nan
     prob.sol = ic
     with pytest.raises(LibSWError) as ei:
         prob.stepforward(1)
     assert ei.value.code == -5
+    # a finite state steps cleanly afterwards (the flag is re-armed per call)
+    prob.sol = np.zeros_like(ic)
+    prob.stepforward(3)
+    prob.close()
+
+
+def test_nan_detection_inf_and_record():
+    """±Inf is reported as NaN is (the pass's isfinite), and sw_step_record
+    reports it after filling the record."""
+    from juliaraytracingsw_amd import LibSWError
+
+    p = sw_cases.case_params("qg2_ifmab3", 64)
+    prob = sw_cases.libsw_problem(p)
+    ic = np.zeros_like(prob.sol)
+    ic[1, 2, 3] = np.inf
+    prob.sol = ic
+    with pytest.raises(LibSWError) as ei:
+        prob.stepforward(2)
+    assert ei.value.code == -5
+    prob.sol = ic
+    with pytest.raises(LibSWError) as ei:
+        prob.ctx.step_record(2)
+    assert ei.value.code == -5 and ei.value.record[0] == prob.ctx.get_clock()[1]
     prob.close()
 
 

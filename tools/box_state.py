@@ -163,31 +163,56 @@ class BoxMonitor:
             self._m0 = None
         self._e0 = self._energy()
         self._t0 = time.perf_counter()
+        self._n0 = 0
+        self._start_mark = (self._t0, self._m0, self._e0, 0)
         self._thread = threading.Thread(target=self._sample_loop, args=(period,), daemon=True)
         self._thread.start()
 
-    def stop(self):
+    def _mark(self):
+        """(time, metrics, energy, sample count) now, for region boundaries"""
+        try:
+            m = self._metrics()
+        except Exception:  # noqa: BLE001
+            m = None
+        return time.perf_counter(), m, self._energy(), len(self._samples)
+
+    def lap(self):
+        """the region since start() or the previous lap(), sampling continues
+        (bench.py: the untimed warm-up as its own region inside the headline's)"""
+        if self.h is None:
+            return {"error": self.err}
+        t1, m1, e1, n1 = self._mark()
+        out = self._summary(self._t0, self._m0, self._e0, self._n0, t1, m1, e1, n1)
+        self._t0, self._m0, self._e0, self._n0 = t1, m1, e1, n1
+        return out
+
+    def stop(self, whole=False):
+        """the region since the last lap() (whole: since start())"""
         if self.h is None:
             return {"error": self.err}
         self._stop.set()
         if self._thread is not None:
             self._thread.join(timeout=2)
-        dt = time.perf_counter() - self._t0
-        e1 = self._energy()
-        if self._e0 and e1 and e1[0] >= self._e0[0]:
+        t1, m1, e1, n1 = self._mark()
+        if whole:
+            return self._summary(*self._start_mark, t1, m1, e1, n1)
+        return self._summary(self._t0, self._m0, self._e0, self._n0, t1, m1, e1, n1)
+
+    def _summary(self, t0, m0, e0, n0, t1, m1, e1, n1):
+        dt = t1 - t0
+        if e0 and e1 and e1[0] >= e0[0] and dt > 0:
             # energy counter x its resolution (µJ) over the region's wall time
-            out_energy = (e1[0] - self._e0[0]) * e1[1] * 1e-6 / dt
+            out_energy = (e1[0] - e0[0]) * e1[1] * 1e-6 / dt
+            joules = (e1[0] - e0[0]) * e1[1] * 1e-6
         else:
-            out_energy = None
-        try:
-            m1 = self._metrics()
-        except Exception:  # noqa: BLE001
-            m1 = None
-        out = {"seconds": dt, "samples": len(self._samples), "avg_power_W_from_energy": out_energy}
+            out_energy = joules = None
+        smp = self._samples[n0:n1]
+        out = {"seconds": dt, "samples": len(smp), "avg_power_W_from_energy": out_energy, "energy_J": joules}
         for i, name in enumerate(("gfx_MHz", "mem_MHz", "socket_W", "hotspot_C", "hbm_C")):
-            xs = [smp[i] for smp in self._samples if smp[i] is not None]
+            xs = [q[i] for q in smp if q[i] is not None]
             out[name] = ({"mean": statistics.fmean(xs), "min": min(xs), "max": max(xs)} if xs else None)
-        m0 = self._m0
+        out["throttle_fraction"] = None
+        out["throttle_status_after"] = None
         if m0 and m1:
             acc0, acc1 = _num(m0.get("accumulation_counter")), _num(m1.get("accumulation_counter"))
             res = {}
