@@ -314,18 +314,23 @@ def main():
         if world == 1:
             return None
         st = prob.ctx.comm_profile(nsteps) if prob is not None else None
+        # the link probe libsw ran at sw_create (per-peer GB/s, α, β, n½) and
+        # the schedule it chose (VERDICT r05 #4b-c)
+        lm = prob.ctx.link_model() if prob is not None else None
         per = [None] * world
         dist.all_gather_object(per, None if st is None else dict(
             rank=rank, exposed_transpose_us_per_step=st["exposed_transpose_us"], step_us=st["step_us"],
-            sent_MB_per_step=st["sent_bytes_per_step"] / 1e6))
+            sent_MB_per_step=st["sent_bytes_per_step"] / 1e6, peer_GBps=lm["peer_GBps"]))
         per = [r for r in per if r is not None]
         if st is None:
             return None
         ex = max(r["exposed_transpose_us_per_step"] for r in per)
+        link = {k: lm[k] for k in ("probed", "transport", "latency_us", "GBps_per_peer_direction", "nhalf_bytes",
+                                    "msg_bytes", "pipelined", "row_chunks")}
         return {"transport": st["transport"], "rccl_ranks": st["rccl_ranks"], "nranks": st["nranks"],
                 "schedule": st["schedule"], "row_chunks": st["row_chunks"], "profiled_steps": nsteps,
                 "exposed_transpose_us_per_step_max": ex,
-                "exposed_fraction_of_step": ex / max(r["step_us"] for r in per), "per_rank": per}
+                "exposed_fraction_of_step": ex / max(r["step_us"] for r in per), "link": link, "per_rank": per}
 
     def decomposition():
         if world == 1:

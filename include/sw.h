@@ -314,6 +314,32 @@ typedef struct sw_comm_stats {
 } sw_comm_stats;
 int sw_comm_profile(sw_ctx* ctx, int64_t nsteps, sw_comm_stats* out);
 
+/* ABI 9, round 6.  The link model a one-slab-per-process context measured at
+ * sw_create (collective there): a grouped exchange of m bytes with every peer
+ * at two sizes, t(m) = α + m/β (the slowest rank's times, so every rank
+ * decides alike), and one peer at a time (a shift: send to rank + d, receive
+ * from rank - d) at 4 MiB.  The slab schedule follows from it: the transposes
+ * are pipelined on the side stream when this decomposition's per-(peer,
+ * field) message is at least n½ = α·β (the size at which a message moves at
+ * half the link rate), and the last inverse group goes in row chunks while a
+ * chunk's messages stay at least n½ (before round 6: a fixed 1 MiB).
+ * SW_LINK_PROBE=0 skips the probe (the 1 MiB rule); SW_OVERLAP and
+ * SW_ROW_CHUNKS still force the schedule.  The reference has no multi-GPU
+ * path (north-star scope). */
+typedef struct sw_link_model {
+  int32_t probed;           /* 1: measured (one slab per process, P > 1)           */
+  int32_t transport;        /* SW_XPORT_* the probe ran on                         */
+  int32_t pipelined;        /* the schedule chosen: 1 pipelined, 0 sequential      */
+  int32_t row_chunks;       /* row chunks of the pipelined schedule                */
+  double  latency_us;       /* α                                                   */
+  double  GBps;             /* β: per peer and direction, every peer at once      */
+  double  nhalf_bytes;      /* α·β                                                 */
+  double  msg_bytes;        /* this decomposition's per-(peer, field) message      */
+  double  peer_GBps[8];     /* peer_GBps[d-1]: one peer at a time, to rank + d, d < P
+                               (RCCL only; 0 otherwise and beyond P - 1)           */
+} sw_link_model;
+int sw_get_link_model(const sw_ctx* ctx, sw_link_model* out);
+
 /* Per-kernel HIP-event timing of `nsteps` steps (the state advances).
  * Fills up to max_stats entries; *n_stats receives the count.  With
  * SW_PROF_COLD=1 in the environment a read of a 512 MiB buffer precedes each

@@ -30,7 +30,7 @@ EXPORTS = [
     "sw_profile_steps", "sw_step_alg_bytes", "sw_comm_unique_id",
     "sw_history_slots", "sw_get_history", "sw_set_history", "sw_reset_history", "sw_slab_geometry",
     "sw_checkpoint_bytes", "sw_get_checkpoint", "sw_set_checkpoint", "sw_step_record",
-    "sw_comm_profile",
+    "sw_comm_profile", "sw_get_link_model",
 ]
 
 
@@ -79,6 +79,12 @@ class SwCommStats(C.Structure):
 
 
 XPORT_NAMES = {0: "none", 1: "rccl", 2: "host-staged", 3: "in-process"}
+
+
+class SwLinkModel(C.Structure):
+    _fields_ = [("probed", C.c_int32), ("transport", C.c_int32), ("pipelined", C.c_int32),
+                ("row_chunks", C.c_int32), ("latency_us", C.c_double), ("GBps", C.c_double),
+                ("nhalf_bytes", C.c_double), ("msg_bytes", C.c_double), ("peer_GBps", C.c_double * 8)]
 
 
 class SwKernelStat(C.Structure):
@@ -132,8 +138,11 @@ def load(path: str | None = None):
         "sw_set_checkpoint": (C.c_int, [vp, vp, sz]),
         "sw_step_record": (C.c_int, [vp, i64, C.POINTER(SwEnergyRecord)]),
         "sw_comm_profile": (C.c_int, [vp, i64, C.POINTER(SwCommStats)]),
+        "sw_get_link_model": (C.c_int, [vp, C.POINTER(SwLinkModel)]),
     }
     for name, (res, args) in sig.items():
+        if name == "sw_get_link_model" and not hasattr(lib, name):
+            continue  # (a library from before round 6: diagnostics only; tests/test_abi.py requires it)
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -331,6 +340,16 @@ class Context:
                     rccl_ranks=st.rccl_ranks, schedule="pipelined" if st.pipelined else "sequential",
                     row_chunks=st.row_chunks, step_us=st.step_us, exposed_transpose_us=st.exposed_us,
                     sent_bytes_per_step=st.bytes_sent)
+
+    def link_model(self):
+        """sw_get_link_model: the link probe of sw_create (one slab per
+        process) and the slab schedule chosen from it."""
+        m = SwLinkModel()
+        self._check(self.lib.sw_get_link_model(self._h, C.byref(m)), "sw_get_link_model")
+        return dict(probed=bool(m.probed), transport=XPORT_NAMES.get(m.transport, str(m.transport)),
+                    pipelined=bool(m.pipelined), row_chunks=m.row_chunks, latency_us=m.latency_us,
+                    GBps_per_peer_direction=m.GBps, nhalf_bytes=m.nhalf_bytes, msg_bytes=m.msg_bytes,
+                    peer_GBps=[x for x in m.peer_GBps])
 
     def profile(self, nsteps):
         st = (SwKernelStat * 16)()

@@ -84,6 +84,7 @@ def main():
             aliased_max=float(np.max(np.abs(np.where(grid.dealias(np.ones_like(sol)) == 0, sol, 0)))),
         )
         ref.close()
+        res["link"] = prob.ctx.link_model()  # the probe of sw_create (host-staged here)
     prob.close()
     dist.barrier()
     if rank == 0:

@@ -50,6 +50,13 @@ def test_one_process_per_slab(case, world, steps, freq, aliased, tmp_path):
     assert res["ke_rel"] == 0 and res["pe_rel"] == 0, res
     assert res["records_equal"] and res["cfl_equal"], res
     assert (res["aliased_max"] > 0) == aliased, res
+    # the link probe of sw_create ran on the host-staged transport (round 6,
+    # VERDICT r05 #4b): α ≥ 0, β > 0, the message size of this decomposition;
+    # the host-staged transport keeps the sequential schedule
+    lk = res["link"]
+    assert lk["probed"] and lk["transport"] == "host-staged", lk
+    assert lk["GBps_per_peer_direction"] > 0 and lk["latency_us"] >= 0 and lk["msg_bytes"] > 0, lk
+    assert not lk["pipelined"] and lk["row_chunks"] == 1 and lk["peer_GBps"] == [0.0] * 8, lk
 
 
 def test_bench_line_explains_the_exchange():
@@ -70,6 +77,8 @@ def test_bench_line_explains_the_exchange():
     assert c["transport"] == "host-staged" and c["rccl_ranks"] == 0 and c["nranks"] == 2
     assert c["schedule"] == "sequential" and c["row_chunks"] == 1
     assert [p["rank"] for p in c["per_rank"]] == [0, 1]
+    assert c["link"]["probed"] and c["link"]["transport"] == "host-staged" and c["link"]["GBps_per_peer_direction"] > 0
+    assert c["link"]["msg_bytes"] == 48 * 128 * 16  # kcl · nyl · 16 B per (peer, field)
     for p in c["per_rank"]:
         # RSW 256²: 9 mixed fields of kcl·nyl·16 B per step, half of each
         # slab's blocks go to the other rank
