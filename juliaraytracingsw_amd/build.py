@@ -4,7 +4,8 @@ travels to the GPU box with the repository snapshot).
 The kernel file is compiled as one translation unit per transform length
 (``-DSW_PART=L``, L = log2 N = 5 … 13) plus the length-independent part
 (``SW_PART=0``: element-wise kernels and the dispatch), in parallel, then
-linked with the host-side API (``sw_api.cpp``)."""
+linked with the host-side API (``sw_api.cpp``) and the generic engine for
+grids that are not powers of two (``sw_generic.hip``)."""
 from __future__ import annotations
 
 import os
@@ -16,8 +17,8 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
-SOURCES = ["sw_kernels.hip", "sw_api.cpp"]
-HEADERS = ["sw_fft.hpp", "sw_internal.hpp"]
+SOURCES = ["sw_kernels.hip", "sw_api.cpp", "sw_generic.hip"]
+HEADERS = ["sw_fft.hpp", "sw_internal.hpp", "sw_generic.hpp"]
 OUT = os.path.join(HERE, "libsw.so")
 PARTS = [0, 13, 12, 11, 10, 9, 8, 7, 6, 5]  # longest first (compile time)
 
@@ -60,12 +61,14 @@ def build_lib(verbose=False, force=False, out=OUT, extra_flags=(), jobs=None, pa
             cmds.append(common + only + ["-c", f"-DSW_PART={part}", os.path.join(CSRC, "sw_kernels.hip"),
                                          "-o", os.path.join(tmp, f"k{part}.o")])
         cmds.append(common + ["-c", os.path.join(CSRC, "sw_api.cpp"), "-o", os.path.join(tmp, "api.o")])
+        # the generic engine (grids that are not powers of two, sw_generic.hpp)
+        cmds.append(common + ["-c", os.path.join(CSRC, "sw_generic.hip"), "-o", os.path.join(tmp, "gen.o")])
         if verbose:
             for c in cmds:
                 print(" ".join(c))
         with ThreadPoolExecutor(jobs) as ex:
             list(ex.map(_run, cmds))
-        objs = [os.path.join(tmp, f"k{p}.o") for p in plist] + [os.path.join(tmp, "api.o")]
+        objs = [os.path.join(tmp, f"k{p}.o") for p in plist] + [os.path.join(tmp, "api.o"), os.path.join(tmp, "gen.o")]
         link = [hipcc, "--offload-arch=gfx950", "-fPIC", "-shared", "-o", out + ".tmp", *objs,
                 "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
         if verbose:

@@ -4,6 +4,7 @@
 // replaced are cited per function.
 #include "sw.h"
 #include "sw_internal.hpp"
+#include "sw_generic.hpp"
 
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -86,6 +87,10 @@ struct sw_ctx {
   hipEvent_t ev_rowc[8] = {};                // row chunk k has been transformed (its forward rows written)
   bool overlap = false;                      // pipelined exchange (default: RCCL; SW_OVERLAP=0/1)
   sw_link_model link{};                      // the link probe of sw_create (sw_get_link_model)
+  // grids that are not powers of two (MultiLayerQG + FilteredRK4 on
+  // 2^a 3^b 5^c points, simulation/MattParameters.jl:8): the generic engine
+  // (sw_generic.hpp) on the full-array state in sl[0].sol
+  sw::gen::Engine* gen = nullptr;
   int row_chunks = 1;                        // pipelined: row pass in chunks behind the last inverse transposes
   double2 *tw_x = nullptr, *tw_y = nullptr;
   std::vector<Slab> sl;                      // slabs held by this process
@@ -339,8 +344,9 @@ double live_field_bytes(const Geom& g) { return 16.0 * g.kcn * g.Lr; }
 double mixed_col_bytes(const Geom& g) { return 16.0 * g.kcn * g.ny; }
 double mixed_row_bytes(const Geom& g) { return 16.0 * g.kc * g.nyl; }
 
-enum KId { K_COLINV = 0, K_ROW, K_COLFWD, K_UPD, K_COLSTEP, K_FWDSTEP, K_XCHG, K_NKERN };
-const char* kname[K_NKERN] = {"col_inv", "row", "col_fwd", "update", "col_step", "col_fwd_step", "transpose"};
+enum KId { K_COLINV = 0, K_ROW, K_COLFWD, K_UPD, K_COLSTEP, K_FWDSTEP, K_XCHG, K_GEN, K_NKERN };
+const char* kname[K_NKERN] = {"col_inv", "row", "col_fwd", "update", "col_step", "col_fwd_step", "transpose",
+                              "generic_step"};
 
 // state/history bytes of one stepper op per live mode, in live-field units
 // (reads + writes; AB3 steady state; IFMRK4 averaged over its four stages)
@@ -991,6 +997,10 @@ void sum_rank_cols(const sw_ctx* c, const double* all, size_t per, size_t off, d
 // process) this rank's column sums [rank_cols][SW_NSUM], added over ranks at
 // retrieval
 void record_energy_to(sw_ctx* c, double2* Slab::*X, double* dst) {
+  if (c->gen) {
+    sw::gen::energy_sums(c->gen, c->sl[0].*X, dst);
+    return;
+  }
   if (c->dist) {
     const Slab& s = c->sl[0];
     sw::launch_energy_cols(c->cfg.model, s.g, c->p, s.*X, dst, c->stream);
@@ -1018,7 +1028,29 @@ void record_energy(sw_ctx* c, double2* Slab::*X, bool rec, bool frec) {
   if (frec) record_energy_to(c, X, c->erec1);
 }
 
+// the generic engine's step (FilteredRK4, MultiLayerQG): its four stages, then
+// the records of a MultiLayerQG step (prob.sol after the step)
+int gen_step_once(sw_ctx* c) {
+  const bool rec = c->diag_freq > 0 && (c->step + 1) % c->diag_freq == 0 && c->diag_n < c->diag_cap;
+  const bool frec = c->force_rec;
+  {
+    Timer tm(c, K_GEN);
+    sw::gen::step(c->gen, c->scan ? (c->hflag ? c->hflag_dev : c->sflag) : nullptr);
+  }
+  HIPCHK(c, hipGetLastError());
+  c->t += c->cfg.dt;
+  c->step += 1;
+  record_energy(c, &Slab::sol, rec, frec);
+  if (rec) {
+    c->diag_steps.push_back(c->step);
+    c->diag_t.push_back(c->t);
+    c->diag_n += 1;
+  }
+  return 0;
+}
+
 int step_once(sw_ctx* c) {
+  if (c->gen) return gen_step_once(c);
   const int st = c->cfg.stepper;
   const bool rec = c->diag_freq > 0 && (c->step + 1) % c->diag_freq == 0 && c->diag_n < c->diag_cap;
   const bool frec = c->force_rec;
@@ -1153,6 +1185,10 @@ int gather0(sw_ctx* c, const void* mine, void* dst, size_t bytes) {
 
 // c->stage <- the full (nkr, nl, nf) array of the per-slab compact field set
 int collect_full(sw_ctx* c, double2* Slab::*X) {
+  if (c->gen) {  // the generic engine's state is the full array already
+    HIPCHK(c, hipMemcpyAsync(c->stage, c->sl[0].*X, full_bytes(c), hipMemcpyDeviceToDevice, c->stream));
+    return 0;
+  }
   if (!c->dist) {
     for (Slab& s : c->sl) {
       int lo, hi;
@@ -1198,7 +1234,9 @@ int read_flag(sw_ctx* c, int* f, int& h) {
 // NaN/Inf anywhere in the live modes of the state: a pass over it (sw_diag)
 int nan_flag(sw_ctx* c, int& h) {
   HIPCHK(c, hipMemsetAsync(c->flag, 0, sizeof(int), c->stream));
-  for (Slab& s : c->sl) sw::launch_nan_check(c->nf, s.g, s.sol, c->flag, c->stream);
+  if (c->gen) sw::gen::nan_scan(c->gen, c->sl[0].sol, c->flag);
+  else
+    for (Slab& s : c->sl) sw::launch_nan_check(c->nf, s.g, s.sol, c->flag, c->stream);
   HIPCHK(c, hipGetLastError());
   return read_flag(c, c->flag, h);
 }
@@ -1431,6 +1469,106 @@ void sw_config_default(sw_config* cfg) {
 
 const char* sw_last_error(const sw_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
+static void setup_phys(sw_ctx* c) {
+  const sw_config& k = c->cfg;
+  Phys& p = c->p;
+  p.f = k.f;
+  p.Cg2 = k.Cg * k.Cg;
+  p.nu = k.nu;
+  p.nnu = k.nnu;
+  p.U = k.U;
+  p.mu = k.mu;
+  p.F = k.F;
+  p.Ro = k.Ro;
+  p.model = k.model;
+  if (k.model == SW_MODEL_MLQG) {  // MultiLayerQG.Params, 2 layers, no topography
+    const double gp = k.b[0] - k.b[1];
+    p.F = k.f0 * k.f0 / (gp * k.H[0]);
+    p.F2 = k.f0 * k.f0 / (gp * k.H[1]);
+    p.U1 = k.Ulayer[0];
+    p.U2 = k.Ulayer[1];
+    p.Qy1 = k.beta - p.F * (k.Ulayer[1] - k.Ulayer[0]);
+    p.Qy2 = k.beta - p.F2 * (k.Ulayer[0] - k.Ulayer[1]);
+  }
+  p.dt = k.dt;
+  p.use_filter = (k.stepper == SW_STEP_FILTERED_AB3 || k.stepper == SW_STEP_FILTERED_RK4) ? 1 : (k.use_filter ? 1 : 0);
+  p.forder = k.filter_order;
+  p.innerK = k.filter_innerK;
+  p.decay = -std::log(k.filter_tol) / std::pow(k.filter_outerK - k.filter_innerK, (double)k.filter_order);
+
+}
+
+// A grid that is not a power of two per side: the generic engine
+// (sw_generic.hpp) for MultiLayerQG + FilteredRK4 — TwoLayerSimulation with
+// simulation/MattParameters.jl (nx = 384) — on one device.  Slabs in one
+// process (local_slabs == nranks) hold the whole grid (the results are the
+// undecomposed run's: bitwise equal for any P); one slab per process, the
+// aliased-state mode and other model/stepper pairs are refused.
+int create_generic(sw_ctx* c) {
+  const sw_config& k = c->cfg;
+  int rx[24], ry[24];
+  if (!sw::gen::radices(k.nx, rx) || !sw::gen::radices(k.ny, ry))
+    return fail(c, SW_E_INVALID,
+                "nx, ny must be powers of two in [32, 8192], or (MultiLayerQG with FilteredRK4) even sizes of the "
+                "form 2^a 3^b 5^c in [16, 4096]");
+  if (k.model != SW_MODEL_MLQG || k.stepper != SW_STEP_FILTERED_RK4)
+    return fail(c, SW_E_INVALID,
+                "grids that are not powers of two: MultiLayerQG with FilteredRK4 only (simulation/MattParameters.jl)");
+  if (!(k.aliased_fraction >= 0 && k.aliased_fraction < 1))
+    return fail(c, SW_E_INVALID, "aliased_fraction must be in [0,1)");
+  if (k.precision != SW_PREC_F64 && k.precision != SW_PREC_F32)
+    return fail(c, SW_E_INVALID, "precision must be SW_PREC_F64 or SW_PREC_F32");
+  if (k.aliased_state) return fail(c, SW_E_INVALID, "aliased_state: power-of-two grids only");
+  if (k.nnu < 0 || k.nnu > 255 || k.filter_order < 0 || k.filter_order > 255)
+    return fail(c, SW_E_INVALID, "nnu and filter_order must be in [0, 255]");
+  const int P = k.nranks < 1 ? 1 : k.nranks;
+  const int nlocal = k.local_slabs <= 1 ? 1 : k.local_slabs;
+  if (P > 1 && nlocal != P)
+    return fail(c, SW_E_INVALID, "grids that are not powers of two: one process holds every slab (local_slabs = nranks)");
+  int ndev = 0;
+  HIPCHK(c, hipGetDeviceCount(&ndev));
+  if (k.device < 0 || k.device >= ndev) return fail(c, SW_E_INVALID, "bad device ordinal");
+  HIPCHK(c, hipSetDevice(k.device));
+  HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  HIPCHK(c, hipEventCreate(&c->ev0));
+  HIPCHK(c, hipEventCreate(&c->ev1));
+  c->P = 1;  // (every slab on this device: the undecomposed grid)
+  c->dist = false;
+  setup_phys(c);
+  c->nf = 2;
+  c->kmodel = SW_MODEL_QG2;
+  c->sl.resize(1);
+  Slab& s = c->sl[0];
+  s.g = make_geom(k, 1, 0);
+  const Geom& g = s.g;
+  if (g.kc <= 0 || g.lc > g.lr2) return fail(c, SW_E_INVALID, "degenerate dealiasing geometry");
+  int rc;
+  if ((rc = alloc(c, (void**)&s.sol, full_bytes(c)))) return rc;
+  HIPCHK(c, hipMemsetAsync(s.sol, 0, full_bytes(c), c->stream));
+  if ((rc = alloc(c, (void**)&c->stage, full_bytes(c)))) return rc;
+  if (k.precision == SW_PREC_F32)
+    if ((rc = alloc(c, (void**)&c->stage32, full_bytes(c) / 2))) return rc;
+  if ((rc = alloc(c, (void**)&c->dflt, (size_t)g.nx * g.ny * sizeof(double)))) return rc;
+  if ((rc = alloc(c, (void**)&c->flag, 1024 * sizeof(int)))) return rc;
+  if ((rc = alloc(c, (void**)&c->sflag, 2 * sizeof(int)))) return rc;
+  if ((rc = alloc(c, (void**)&c->esum, (SW_NSUM + 2) * sizeof(double)))) return rc;
+  HIPCHK(c, hipHostMalloc((void**)&c->hflag, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+  HIPCHK(c, hipHostGetDevicePointer((void**)&c->hflag_dev, c->hflag, 0));
+  *c->hflag = 0;
+  std::string err;
+  if ((rc = sw::gen::create(c->gen, k, c->p, g, s.sol, c->stream, err))) return fail(c, rc, err);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (const char* e = std::getenv("SW_CHECK_NAN")) {
+    if (e[0] == '1') c->cfg.check_nan = 1;
+#ifdef SW_EXPERIMENTS
+    else c->cfg.check_nan = 0;
+#endif
+  }
+  c->stats.resize(K_NKERN);
+  for (int i = 0; i < K_NKERN; ++i) c->stats[i].name = kname[i];
+  return SW_OK;
+}
+
 int sw_create(sw_ctx** out, const sw_config* cfg) {
   if (!out || !cfg) return SW_E_INVALID;
   *out = nullptr;
@@ -1447,7 +1585,8 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
     return fail(c, SW_E_INVALID, "MultiLayerQG needs H > 0 and b[0] != b[1]");
   if ((k.model == SW_MODEL_TY) != (k.stepper == SW_STEP_ETDRK4))
     return fail(c, SW_E_INVALID, "ETDRK4 (diagonal L) is the Thomas-Yamada stepper and TY steps with ETDRK4 only");
-  if (!pow2(k.nx) || !pow2(k.ny) || k.nx < 32 || k.ny < 32 || k.nx > 8192 || k.ny > 8192)
+  if (!pow2(k.nx) || !pow2(k.ny)) return create_generic(c);
+  if (k.nx < 32 || k.ny < 32 || k.nx > 8192 || k.ny > 8192)
     return fail(c, SW_E_INVALID, "nx, ny must be powers of two in [32, 8192]");
   if (!sw::length_built(ilog2(k.nx)) || !sw::length_built(ilog2(k.ny)))
     return fail(c, SW_E_INVALID, "nx or ny: transform length not built into this library (one-length build)");
@@ -1531,30 +1670,7 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
   if (k.nnu < 0 || k.nnu > 255 || k.filter_order < 0 || k.filter_order > 255)
     return fail(c, SW_E_INVALID, "nnu and filter_order must be in [0, 255]");
 
-  Phys& p = c->p;
-  p.f = k.f;
-  p.Cg2 = k.Cg * k.Cg;
-  p.nu = k.nu;
-  p.nnu = k.nnu;
-  p.U = k.U;
-  p.mu = k.mu;
-  p.F = k.F;
-  p.Ro = k.Ro;
-  p.model = k.model;
-  if (k.model == SW_MODEL_MLQG) {  // MultiLayerQG.Params, 2 layers, no topography
-    const double gp = k.b[0] - k.b[1];
-    p.F = k.f0 * k.f0 / (gp * k.H[0]);
-    p.F2 = k.f0 * k.f0 / (gp * k.H[1]);
-    p.U1 = k.Ulayer[0];
-    p.U2 = k.Ulayer[1];
-    p.Qy1 = k.beta - p.F * (k.Ulayer[1] - k.Ulayer[0]);
-    p.Qy2 = k.beta - p.F2 * (k.Ulayer[0] - k.Ulayer[1]);
-  }
-  p.dt = k.dt;
-  p.use_filter = (k.stepper == SW_STEP_FILTERED_AB3 || k.stepper == SW_STEP_FILTERED_RK4) ? 1 : (k.use_filter ? 1 : 0);
-  p.forder = k.filter_order;
-  p.innerK = k.filter_innerK;
-  p.decay = -std::log(k.filter_tol) / std::pow(k.filter_outerK - k.filter_innerK, (double)k.filter_order);
+  setup_phys(c);
 
   c->nf = k.model == SW_MODEL_RSW ? 3 : (k.model == SW_MODEL_TY ? 4 : 2);
   c->kmodel = k.model == SW_MODEL_MLQG ? SW_MODEL_QG2 : k.model;  // MLQG runs the 2LQG kernels
@@ -1768,6 +1884,7 @@ int sw_create(sw_ctx** out, const sw_config* cfg) {
 void sw_destroy(sw_ctx* c) {
   if (!c) return;
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  sw::gen::destroy(c->gen);
   for (Slab& s : c->sl) free_slab(s);
   void* ptrs[] = {c->tw_x, c->tw_y, c->stage, c->stage32, c->gbuf, c->abuf, c->dflt, c->flag, c->sflag, c->ecols, c->esum, c->erec,
                   c->erec1, c->cold, c->cold_out};
@@ -1808,7 +1925,12 @@ int sw_set_state(sw_ctx* c, const void* sol, size_t bytes) {
   if (!sol || bytes != caller_bytes(c, full_bytes(c))) return fail(c, SW_E_INVALID, "sw_set_state: size mismatch");
   HIPCHK(c, hipSetDevice(c->cfg.device));
   if (int rc = upload(c, sol, c->stage, full_bytes(c))) return rc;
-  for (Slab& s : c->sl) sw::launch_gather(c->nf, s.g, c->stage, s.sol, c->stream);
+  if (c->gen) {  // full-array state: a copy, then dealias!
+    HIPCHK(c, hipMemcpyAsync(c->sl[0].sol, c->stage, full_bytes(c), hipMemcpyDeviceToDevice, c->stream));
+    sw::gen::dealias(c->gen, c->sl[0].sol);
+  } else {
+    for (Slab& s : c->sl) sw::launch_gather(c->nf, s.g, c->stage, s.sol, c->stream);
+  }
   alias_gather(c, A_SOL);  // sol .= q0h keeps them until updatevars!/calcN! dealias
   c->mixed_valid = false;
   HIPCHK(c, hipGetLastError());
@@ -1869,6 +1991,14 @@ int sw_calcN(sw_ctx* c, const void* sol, void* N, size_t bytes) {
   HIPCHK(c, hipSetDevice(c->cfg.device));
   c->mixed_valid = false;  // mixed arrays are used as scratch
   if (int rc = upload(c, sol, c->stage, full_bytes(c))) return rc;
+  if (c->gen) {  // N = calcN(dealias(sol)) on the full array
+    sw::gen::calcN(c->gen, c->stage, c->gen->N);
+    HIPCHK(c, hipMemcpyAsync(c->stage, c->gen->N, full_bytes(c), hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipGetLastError());
+    if (int rc = download(c, c->stage, N, full_bytes(c))) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return SW_OK;
+  }
   for (Slab& s : c->sl) {
     sw::launch_gather(c->nf, s.g, c->stage, s.xs, c->stream);
     // scratch output: the ring slot that the next step overwrites anyway
@@ -1896,6 +2026,11 @@ int sw_calcN(sw_ctx* c, const void* sol, void* N, size_t bytes) {
 // one physical field (updatevars!) of the current state into c->dflt: this
 // rank's rows (one slab per process) or every row (all slabs here)
 static int physical_to_dflt(sw_ctx* c, int32_t fid) {
+  if (c->gen) {
+    sw::gen::physical(c->gen, c->sl[0].sol, fid, c->dflt);
+    HIPCHK(c, hipGetLastError());
+    return 0;
+  }
   c->mixed_valid = false;  // mixed arrays are used as scratch
   for (Slab& s : c->sl) {
     sw::launch_make_spec(c->cfg.model, fid, s.g, c->p, s.sol, s.xs, c->stream);
@@ -2074,8 +2209,11 @@ int sw_diag(sw_ctx* c, int32_t id, double* out) {
   if (((id == SW_DIAG_BT || wgid) && c->cfg.model != SW_MODEL_TY) ||
       ((id == SW_DIAG_KE1 || id == SW_DIAG_KE2) && c->cfg.model == SW_MODEL_TY))
     return fail(c, SW_E_INVALID, "diagnostic not defined for this model");
-  for (Slab& s : c->sl) sw::launch_energy_cols(c->cfg.model, s.g, c->p, s.sol, c->ecols + SW_NSUM * s.g.kr0, c->stream);
   int ncols = c->P * c->sl[0].g.kcl;
+  if (c->gen) {
+    sw::gen::energy_sums(c->gen, c->sl[0].sol, c->esum);
+  } else {
+  for (Slab& s : c->sl) sw::launch_energy_cols(c->cfg.model, s.g, c->p, s.sol, c->ecols + SW_NSUM * s.g.kr0, c->stream);
   if (c->dist) {
     const Slab& s = c->sl[0];
     const Geom& g0 = s.g;
@@ -2102,6 +2240,7 @@ int sw_diag(sw_ctx* c, int32_t id, double* out) {
     ncols = alias_energy_cols(c, true, ncols);
   }
   sw::launch_energy_final(c->ecols, ncols, c->esum, c->stream);
+  }
   HIPCHK(c, hipGetLastError());
   std::vector<double> sums(SW_NSUM);
   HIPCHK(c, hipMemcpyAsync(sums.data(), c->esum, SW_NSUM * sizeof(double), hipMemcpyDeviceToHost, c->stream));
@@ -2312,6 +2451,11 @@ int sw_profile_steps(sw_ctx* c, int64_t nsteps, sw_kernel_stat* out, int32_t max
 
 double sw_step_alg_bytes(const sw_ctx* c) {
   if (!ready(c)) return 0.0;
+  if (c->gen) {  // per stage: the state in, N out and back, 6 + 4 spectral and 10 physical fields once each
+    const Geom& g = c->sl[0].g;
+    const double F = 16.0 * g.nkr * g.nl, R = 8.0 * g.nx * g.ny;
+    return 4 * (2 * F * 5 + 10 * 2 * F + 10 * 2 * R);
+  }
   return step_bytes(c);
 }
 
@@ -2483,7 +2627,13 @@ int sw_set_checkpoint(sw_ctx* c, const void* buf, size_t bytes) {
   const size_t fb = full_bytes(c);
   for (int k = 0; k <= h.nslots; ++k) {
     HIPCHK(c, hipMemcpyAsync(c->stage, in + sizeof(h) + k * fb, fb, hipMemcpyHostToDevice, c->stream));
-    for (Slab& s : c->sl) sw::launch_gather(c->nf, s.g, c->stage, k == 0 ? s.sol : s.hist[hist_index(c, k)], c->stream);
+    if (c->gen) {  // (FilteredRK4: the state alone)
+      HIPCHK(c, hipMemcpyAsync(c->sl[0].sol, c->stage, fb, hipMemcpyDeviceToDevice, c->stream));
+      sw::gen::dealias(c->gen, c->sl[0].sol);
+    } else {
+      for (Slab& s : c->sl)
+        sw::launch_gather(c->nf, s.g, c->stage, k == 0 ? s.sol : s.hist[hist_index(c, k)], c->stream);
+    }
     if (k == 0) alias_gather(c, A_SOL);
     else alias_gather(c, a_hist(hist_index(c, k)));
     HIPCHK(c, hipGetLastError());

@@ -1,0 +1,430 @@
+// libsw generic engine (sw_generic.hpp): MultiLayerQG + FilteredRK4 on grids
+// of 2^a·3^b·5^c points per side (simulation/MattParameters.jl:8, nx = 384).
+#include "sw.h"
+#include "sw_generic.hpp"
+#include "sw_fft.hpp"
+
+#include <cmath>
+#include <string>
+
+namespace sw {
+namespace gen {
+
+__device__ __forceinline__ double2 zero2() { return make_double2(0.0, 0.0); }
+
+int radices(int n, int rad[24]) {
+  if (n < 16 || n > 4096 || (n & 1)) return 0;
+  int k = 0;
+  while (n % 4 == 0 && k < 24) rad[k++] = 4, n /= 4;
+  while (n % 2 == 0 && k < 24) rad[k++] = 2, n /= 2;
+  while (n % 3 == 0 && k < 24) rad[k++] = 3, n /= 3;
+  while (n % 5 == 0 && k < 24) rad[k++] = 5, n /= 5;
+  return n == 1 ? k : 0;
+}
+
+// the radix sequence of a line, passed by value to the kernels
+struct Rad {
+  int n, nr;
+  int r[24];
+};
+
+// exp(DIR 2πi num/den), num taken mod den (exact argument reduction)
+template <int DIR>
+__device__ __forceinline__ double2 w_of(long long num, int den) {
+  double sn, cs;
+  sincospi(2.0 * (double)(num % den) / (double)den, &sn, &cs);
+  return make_double2(cs, DIR * sn);
+}
+
+// One line of n points in LDS (x, ping-pong partner y), transformed in place
+// by the block: mixed-radix Stockham, DIF form (the butterfly of radix r over
+// the points p + t m, then the twiddle ω_len^(p u)):
+//   y[q + s (r p + u)] = ω_len^(p u) Σ_t x[q + s (p + t m)] ω_r^(t u)
+// with len the current sub-transform length (n, n/r₀, …), m = len/r, s the
+// stride (1, r₀, …).  Natural order in and out; returns the buffer holding
+// the result.  DIR = -1 forward (unnormalised), +1 inverse.
+template <int DIR>
+__device__ double2* fft_lds(double2* x, double2* y, const Rad& R) {
+  int len = R.n, s = 1;
+  for (int pi = 0; pi < R.nr; ++pi) {
+    const int r = R.r[pi], m = len / r;
+    for (int i = threadIdx.x; i < m * s; i += blockDim.x) {
+      const int p = i / s, q = i - p * s;
+      double2 v[5];
+      for (int t = 0; t < r; ++t) v[t] = x[q + s * (p + t * m)];
+      for (int u = 0; u < r; ++u) {
+        double2 a = v[0];
+        for (int t = 1; t < r; ++t) {
+          const int e = (t * u) % r;
+          double2 w;  // ω_r^e: exact for r = 2, 4
+          if (r == 2) w = make_double2(e == 0 ? 1.0 : -1.0, 0.0);
+          else if (r == 4) w = e == 0 ? make_double2(1.0, 0.0) : e == 1 ? make_double2(0.0, (double)DIR)
+                           : e == 2 ? make_double2(-1.0, 0.0) : make_double2(0.0, -(double)DIR);
+          else w = w_of<DIR>(e, r);
+          a = make_double2(a.x + (v[t].x * w.x - v[t].y * w.y), a.y + (v[t].x * w.y + v[t].y * w.x));
+        }
+        const double2 tw = w_of<DIR>((long long)p * u, len);
+        y[q + s * (r * p + u)] = make_double2(a.x * tw.x - a.y * tw.y, a.x * tw.y + a.y * tw.x);
+      }
+    }
+    __syncthreads();
+    double2* t = x;
+    x = y;
+    y = t;
+    len = m;
+    s *= r;
+  }
+  return x;
+}
+
+// complex lines of R.n points: element e of line L at data[L·ls + e·es]
+// (the spectral arrays' l columns: es = nkr, ls = 1 within a field, fields
+// nl·nkr apart — line L = f·nkr + kr)
+template <int DIR>
+__global__ void __launch_bounds__(256) k_lines(double2* __restrict__ data, Rad R, int nkr, long long fstride,
+                                               long long es) {
+  extern __shared__ double2 lds[];
+  double2 *x = lds, *y = lds + R.n;
+  const int L = blockIdx.x, f = L / nkr, kr = L - f * nkr;
+  double2* d = data + f * fstride + kr;
+  for (int i = threadIdx.x; i < R.n; i += blockDim.x) x[i] = d[i * es];
+  __syncthreads();
+  const double2* z = fft_lds<DIR>(x, y, R);
+  for (int i = threadIdx.x; i < R.n; i += blockDim.x) d[i * es] = z[i];
+}
+
+// c2r along x of one stored row (FF's irfft rule: c2c along l done, then
+// c2r along x with the DC and Nyquist bins' imaginary parts dropped, numpy's
+// convention): spec row [nkr] -> phys row [nx] × scale
+__global__ void __launch_bounds__(256) k_c2r_rows(const double2* __restrict__ spec, double* __restrict__ phys, Rad R,
+                                                  int nkr, double scale) {
+  extern __shared__ double2 lds[];
+  double2 *x = lds, *y = lds + R.n;
+  const int row = blockIdx.x, n = R.n;
+  const double2* a = spec + (long long)row * nkr;
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    double2 z;
+    if (k <= n / 2) {
+      z = a[k];
+      if (k == 0 || k == n / 2) z.y = 0.0;
+    } else {
+      const double2 b = a[n - k];
+      z = make_double2(b.x, -b.y);
+    }
+    x[k] = z;
+  }
+  __syncthreads();
+  const double2* z = fft_lds<+1>(x, y, R);
+  double* o = phys + (long long)row * n;
+  for (int k = threadIdx.x; k < n; k += blockDim.x) o[k] = z[k].x * scale;
+}
+
+// r2c along x: phys row [nx] -> spec row [nkr] (unnormalised)
+__global__ void __launch_bounds__(256) k_r2c_rows(const double* __restrict__ phys, double2* __restrict__ spec, Rad R,
+                                                  int nkr) {
+  extern __shared__ double2 lds[];
+  double2 *x = lds, *y = lds + R.n;
+  const int row = blockIdx.x, n = R.n;
+  const double* a = phys + (long long)row * n;
+  for (int k = threadIdx.x; k < n; k += blockDim.x) x[k] = make_double2(a[k], 0.0);
+  __syncthreads();
+  const double2* z = fft_lds<-1>(x, y, R);
+  double2* o = spec + (long long)row * nkr;
+  for (int k = threadIdx.x; k < nkr; k += blockDim.x) o[k] = z[k];
+}
+
+// mode (l, kr) of a full [nl][nkr] field: live under FF's dealias!
+__device__ __forceinline__ bool live_mode(const Geom& g, int l, int kr) { return kr < g.kc && (l < g.lc || l >= g.lr2); }
+
+// per mode of X (dealiased on the fly): the 6 spectral fields the products
+// need — per layer j: q̂_j, û_j = -il ψ̂_j, v̂_j = ik ψ̂_j (ψ̂ = S⁻¹ q̂,
+// streamfunctionfrompv!) — at spec[3 j + {0, 1, 2}]
+__global__ void k_prep(Geom g, Phys p, const double2* __restrict__ X, double2* __restrict__ spec) {
+  const long long F = (long long)g.nl * g.nkr;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= F) return;
+  const int l = (int)(i / g.nkr), kr = (int)(i - (long long)l * g.nkr);
+  const bool live = live_mode(g, l, kr);
+  const double2 q1 = live ? X[i] : zero2(), q2 = live ? X[F + i] : zero2();
+  const double k = kr * g.mk, ll = lwav(g, l), K2 = k * k + ll * ll;
+  for (int j = 0; j < 2; ++j) {
+    double2 ps;
+    qg_psi(p, K2, q1.x, q1.y, q2.x, q2.y, j, ps.x, ps.y);
+    spec[(3 * j) * F + i] = j ? q2 : q1;
+    spec[(3 * j + 1) * F + i] = cmul_i(ps, -ll);
+    spec[(3 * j + 2) * F + i] = cmul_i(ps, k);
+  }
+}
+
+// physical products per point: per layer j, (U_j + u_j) q_j and v_j q_j into
+// phys[2 j], phys[2 j + 1] (the inputs q_j, u_j, v_j at phys[3 j + {0,1,2}]
+// are read first: the outputs overwrite fields 0-3)
+__global__ void k_products(Phys p, double* __restrict__ phys, long long np) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= np) return;
+  double q[2], u[2], v[2];
+  for (int j = 0; j < 2; ++j) {
+    q[j] = phys[(3 * j) * np + i];
+    u[j] = phys[(3 * j + 1) * np + i];
+    v[j] = phys[(3 * j + 2) * np + i];
+  }
+  for (int j = 0; j < 2; ++j) {
+    const double U = j ? p.U2 : p.U1;
+    phys[(2 * j) * np + i] = (u[j] + U) * q[j];
+    phys[(2 * j + 1) * np + i] = v[j] * q[j];
+  }
+}
+
+// N_j = -ik Â_j - il B̂_j - Qy_j ik ψ̂_j (+ μ K² ψ̂₂ on the lower layer) on the
+// live modes, 0 on the aliased ones: GF's calcN_advection! + bottom drag
+// (oracle mlqg_calcN: -rfft(v Qy) is Qy·ik ψ̂ up to the transforms' roundoff)
+__global__ void k_assemble(Geom g, Phys p, const double2* __restrict__ X, const double2* __restrict__ spec,
+                           double2* __restrict__ N) {
+  const long long F = (long long)g.nl * g.nkr;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= F) return;
+  const int l = (int)(i / g.nkr), kr = (int)(i - (long long)l * g.nkr);
+  if (!live_mode(g, l, kr)) {
+    N[i] = N[F + i] = zero2();
+    return;
+  }
+  const double k = kr * g.mk, ll = lwav(g, l), K2 = k * k + ll * ll;
+  const double2 q1 = X[i], q2 = X[F + i];
+  for (int j = 0; j < 2; ++j) {
+    double2 ps;
+    qg_psi(p, K2, q1.x, q1.y, q2.x, q2.y, j, ps.x, ps.y);
+    const double Qy = j ? p.Qy2 : p.Qy1;
+    double2 r = cscale(cmul_i(ps, k), -Qy);
+    r = csub(r, cadd(cmul_i(spec[(2 * j) * F + i], k), cmul_i(spec[(2 * j + 1) * F + i], ll)));
+    if (j == 1) r = cadd(r, cscale(ps, p.mu * K2));
+    N[j * F + i] = r;
+  }
+}
+
+// FF FilteredRK4 stage `stage` per mode (op_frk4's arithmetic, L = -ν K^(2nν)):
+//   RHS = N + L x;  1: acc = RHS/6, x' = sol + dt/2 RHS;  2: acc += RHS/3,
+//   x' = sol + dt/2 RHS;  3: acc += RHS/3, x' = sol + dt RHS;
+//   4: sol = (sol + dt (acc + RHS/6)) · filter
+__global__ void k_frk4(Geom g, Phys p, int stage, double2* __restrict__ sol, double2* __restrict__ xs,
+                       double2* __restrict__ acc, const double2* __restrict__ N, int* nanflag) {
+#pragma clang fp contract(off)
+  const long long F = (long long)g.nl * g.nkr;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  bool bad = false;
+  if (i < F) {
+    const int l = (int)(i / g.nkr), kr = (int)(i - (long long)l * g.nkr);
+    if (live_mode(g, l, kr)) {
+      const double k = kr * g.mk, ll = lwav(g, l);
+      const double D = -(p.nu * ipow(k * k + ll * ll, p.nnu));
+      const double dt = p.dt;
+      for (int f = 0; f < 2; ++f) {
+        const long long o = f * F + i;
+        const cplx X = stage == 1 ? cx(sol[o].x, sol[o].y) : cx(xs[o].x, xs[o].y);
+        const cplx u = cx(sol[o].x, sol[o].y);
+        const cplx rhs = cx(N[o].x + D * X.re, N[o].y + D * X.im);
+        if (stage < 4) {
+          const double h = stage == 3 ? dt : dt / 2;
+          const cplx r = stage == 1 ? cx(rhs.re / 6, rhs.im / 6) : cx(rhs.re / 3, rhs.im / 3);
+          const cplx a = stage == 1 ? r : cx(acc[o].x + r.re, acc[o].y + r.im);
+          acc[o] = make_double2(a.re, a.im);
+          xs[o] = make_double2(u.re + h * rhs.re, u.im + h * rhs.im);
+        } else {
+          const double filt = filter_value(g, p, k, ll);
+          const cplx s6 = cx(acc[o].x + rhs.re / 6, acc[o].y + rhs.im / 6);
+          const cplx r = cx(u.re + dt * s6.re, u.im + dt * s6.im);
+          sol[o] = make_double2(r.re * filt, r.im * filt);
+          bad = bad || !isfinite(r.re * filt) || !isfinite(r.im * filt);
+        }
+      }
+    }
+  }
+  if (nanflag) {
+    const unsigned long long m = __ballot(bad);
+    if (m != 0ull && (int)__lane_id() == __ffsll((long long)m) - 1)
+      __hip_atomic_store(nanflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+__global__ void k_dealias(Geom g, double2* __restrict__ X) {
+  const long long F = (long long)g.nl * g.nkr;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= F) return;
+  const int l = (int)(i / g.nkr), kr = (int)(i - (long long)l * g.nkr);
+  if (!live_mode(g, l, kr)) X[i] = X[F + i] = zero2();
+}
+
+// updatevars! spectral field (k_make_spec's MultiLayerQG branch on the full array)
+__global__ void k_spec_field(Geom g, Phys p, int fid, const double2* __restrict__ X, double2* __restrict__ out) {
+  const long long F = (long long)g.nl * g.nkr;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= F) return;
+  const int l = (int)(i / g.nkr), kr = (int)(i - (long long)l * g.nkr);
+  double2 r = zero2();
+  if (live_mode(g, l, kr)) {
+    const int layer = fid >> 3, id = fid & 7;
+    const double2 q1 = X[i], q2 = X[F + i];
+    if (id == 4) {
+      r = layer ? q2 : q1;
+    } else {
+      const double k = kr * g.mk, ll = lwav(g, l), K2 = k * k + ll * ll;
+      double2 ps;
+      qg_psi(p, K2, q1.x, q1.y, q2.x, q2.y, layer, ps.x, ps.y);
+      if (id == 5) r = ps;
+      else if (id == 3) r = make_double2(-K2 * ps.x, -K2 * ps.y);
+      else if (id == 0) r = cmul_i(ps, -ll);
+      else if (id == 1) r = cmul_i(ps, k);
+    }
+  }
+  out[i] = r;
+}
+
+// MultiLayerQG.energies' Parseval sums per kr column (fixed order, one block
+// per column): K²|ψ̂₁|², K²|ψ̂₂|², |ψ̂₂ - ψ̂₁|² over the live modes
+__global__ void __launch_bounds__(256) k_energy_cols(Geom g, Phys p, const double2* __restrict__ X,
+                                                     double* __restrict__ cols) {
+  __shared__ double red[3][256];
+  const long long F = (long long)g.nl * g.nkr;
+  const int kr = blockIdx.x;
+  double a[3] = {0.0, 0.0, 0.0};
+  for (int l = threadIdx.x; l < g.nl; l += blockDim.x) {
+    if (!live_mode(g, l, kr)) continue;
+    const long long i = (long long)l * g.nkr + kr;
+    const double k = kr * g.mk, ll = lwav(g, l), K2 = k * k + ll * ll;
+    const double2 q1 = X[i], q2 = X[F + i];
+    double2 p1, p2;
+    qg_psi(p, K2, q1.x, q1.y, q2.x, q2.y, 0, p1.x, p1.y);
+    qg_psi(p, K2, q1.x, q1.y, q2.x, q2.y, 1, p2.x, p2.y);
+    a[0] += K2 * (p1.x * p1.x + p1.y * p1.y);
+    a[1] += K2 * (p2.x * p2.x + p2.y * p2.y);
+    const double dr = p2.x - p1.x, di = p2.y - p1.y;
+    a[2] += dr * dr + di * di;
+  }
+  for (int c = 0; c < 3; ++c) red[c][threadIdx.x] = a[c];
+  __syncthreads();
+  for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w)
+      for (int c = 0; c < 3; ++c) red[c][threadIdx.x] += red[c][threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x < 3) cols[kr * 3 + threadIdx.x] = red[threadIdx.x][0];
+}
+
+// FF parsevalsum weights (kr = 0 and the Nyquist column once, the others
+// twice), columns added in order -> out[0..2]; out[3..SW_NSUM) = 0
+__global__ void k_energy_final(Geom g, const double* __restrict__ cols, double* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double s[3] = {0.0, 0.0, 0.0};
+  for (int kr = 0; kr < g.nkr; ++kr) {
+    const double w = (kr == 0 || kr == g.nx / 2) ? 1.0 : 2.0;
+    for (int c = 0; c < 3; ++c) s[c] += w * cols[kr * 3 + c];
+  }
+  for (int c = 0; c < SW_NSUM; ++c) out[c] = c < 3 ? s[c] : 0.0;
+}
+
+__global__ void k_nan(long long n, const double* __restrict__ x, int* flag) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool bad = i < n && !isfinite(x[i]);
+  const unsigned long long m = __ballot(bad);
+  if (m != 0ull && (int)__lane_id() == __ffsll((long long)m) - 1) atomicOr(flag, 1);
+}
+
+// ----------------------------------------------------------------- host side
+static Rad rad_of(const int* r, int nr, int n) {
+  Rad R{};
+  R.n = n;
+  R.nr = nr;
+  for (int i = 0; i < nr; ++i) R.r[i] = r[i];
+  return R;
+}
+static dim3 modes_grid(const Geom& g) { return dim3((unsigned)(((long long)g.nl * g.nkr + 255) / 256)); }
+
+int create(Engine*& e, const sw_config& k, const Phys& p, const Geom& g, double2* sol, hipStream_t s,
+           std::string& err) {
+  e = new Engine();
+  e->g = g;
+  e->p = p;
+  e->s = s;
+  e->sol = sol;
+  e->nradx = radices(k.nx, e->radx);
+  e->nrady = radices(k.ny, e->rady);
+  if (!e->nradx || !e->nrady) {
+    err = "generic grids: nx, ny even, 16 ... 4096, of the form 2^a 3^b 5^c";
+    return SW_E_INVALID;
+  }
+  const size_t F = (size_t)g.nl * g.nkr, NP = (size_t)g.nx * g.ny;
+  void** bufs[] = {(void**)&e->xs, (void**)&e->acc, (void**)&e->N};
+  for (void** b : bufs)
+    if (hipMalloc(b, 2 * F * sizeof(double2)) != hipSuccess) return SW_E_NOMEM;
+  if (hipMalloc((void**)&e->spec, 6 * F * sizeof(double2)) != hipSuccess) return SW_E_NOMEM;
+  if (hipMalloc((void**)&e->phys, 6 * NP * sizeof(double)) != hipSuccess) return SW_E_NOMEM;
+  if (hipMalloc((void**)&e->cols, 3 * (size_t)g.nkr * sizeof(double)) != hipSuccess) return SW_E_NOMEM;
+  for (double2* b : {e->xs, e->acc, e->N}) (void)hipMemsetAsync(b, 0, 2 * F * sizeof(double2), s);
+  return SW_OK;
+}
+
+void destroy(Engine* e) {
+  if (!e) return;
+  for (void* b : {(void*)e->xs, (void*)e->acc, (void*)e->N, (void*)e->spec, (void*)e->phys, (void*)e->cols})
+    if (b) (void)hipFree(b);
+  delete e;
+}
+
+// nf spectral fields [nf][nl][nkr] -> physical [nf][ny][nx] (normalised c2r;
+// the spectral fields are transformed in place along l first)
+static void inverse2d(Engine* e, double2* spec, int nf, double* phys) {
+  const Geom& g = e->g;
+  const Rad Ry = rad_of(e->rady, e->nrady, g.ny), Rx = rad_of(e->radx, e->nradx, g.nx);
+  hipLaunchKernelGGL(k_lines<+1>, dim3(nf * g.nkr), dim3(256), 2 * g.ny * sizeof(double2), e->s, spec, Ry, g.nkr,
+                     (long long)g.nl * g.nkr, (long long)g.nkr);
+  hipLaunchKernelGGL(k_c2r_rows, dim3(nf * g.ny), dim3(256), 2 * g.nx * sizeof(double2), e->s, spec, phys, Rx, g.nkr,
+                     1.0 / ((double)g.nx * (double)g.ny));
+}
+
+// physical [nf][ny][nx] -> spectral [nf][nl][nkr] (unnormalised r2c)
+static void forward2d(Engine* e, const double* phys, int nf, double2* spec) {
+  const Geom& g = e->g;
+  const Rad Ry = rad_of(e->rady, e->nrady, g.ny), Rx = rad_of(e->radx, e->nradx, g.nx);
+  hipLaunchKernelGGL(k_r2c_rows, dim3(nf * g.ny), dim3(256), 2 * g.nx * sizeof(double2), e->s, phys, spec, Rx, g.nkr);
+  hipLaunchKernelGGL(k_lines<-1>, dim3(nf * g.nkr), dim3(256), 2 * g.ny * sizeof(double2), e->s, spec, Ry, g.nkr,
+                     (long long)g.nl * g.nkr, (long long)g.nkr);
+}
+
+void calcN(Engine* e, const double2* X, double2* N) {
+  const Geom& g = e->g;
+  const long long np = (long long)g.nx * g.ny;
+  hipLaunchKernelGGL(k_prep, modes_grid(g), dim3(256), 0, e->s, g, e->p, X, e->spec);
+  inverse2d(e, e->spec, 6, e->phys);
+  hipLaunchKernelGGL(k_products, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, e->s, e->p, e->phys, np);
+  forward2d(e, e->phys, 4, e->spec);
+  hipLaunchKernelGGL(k_assemble, modes_grid(g), dim3(256), 0, e->s, g, e->p, X, e->spec, N);
+}
+
+void step(Engine* e, int* nanflag) {
+  const Geom& g = e->g;
+  for (int stage = 1; stage <= 4; ++stage) {
+    calcN(e, stage == 1 ? e->sol : e->xs, e->N);
+    hipLaunchKernelGGL(k_frk4, modes_grid(g), dim3(256), 0, e->s, g, e->p, stage, e->sol, e->xs, e->acc, e->N,
+                       stage == 4 ? nanflag : nullptr);
+  }
+}
+
+void dealias(Engine* e, double2* X) { hipLaunchKernelGGL(k_dealias, modes_grid(e->g), dim3(256), 0, e->s, e->g, X); }
+
+void physical(Engine* e, const double2* X, int fid, double* out) {
+  hipLaunchKernelGGL(k_spec_field, modes_grid(e->g), dim3(256), 0, e->s, e->g, e->p, fid, X, e->spec);
+  inverse2d(e, e->spec, 1, out);
+}
+
+void energy_sums(Engine* e, const double2* X, double* out) {
+  hipLaunchKernelGGL(k_energy_cols, dim3(e->g.nkr), dim3(256), 0, e->s, e->g, e->p, X, e->cols);
+  hipLaunchKernelGGL(k_energy_final, dim3(1), dim3(64), 0, e->s, e->g, e->cols, out);
+}
+
+void nan_scan(Engine* e, const double2* X, int* flag) {
+  const long long n = 4LL * e->g.nl * e->g.nkr;  // 2 fields of complex doubles
+  hipLaunchKernelGGL(k_nan, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->s, n,
+                     reinterpret_cast<const double*>(X), flag);
+}
+
+}  // namespace gen
+}  // namespace sw
