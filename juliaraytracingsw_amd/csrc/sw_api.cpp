@@ -131,6 +131,7 @@ struct sw_ctx {
   // sums, or this rank's [kcl][SW_NSUM] column sums)
   bool force_rec = false;
   double* erec1 = nullptr;
+  double* erec1_host = nullptr;              // one slab: erec1 is pinned, device-mapped host memory
   // sw_comm_profile: event pairs on the compute stream around every wait for
   // the side stream's transposes (pipelined) or around each transpose run on
   // it (sequential), and the bytes a slab sends to the other slabs
@@ -1886,6 +1887,10 @@ void sw_destroy(sw_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   sw::gen::destroy(c->gen);
   for (Slab& s : c->sl) free_slab(s);
+  if (c->erec1_host) {  // (erec1 is its device view)
+    (void)hipHostFree(c->erec1_host);
+    c->erec1 = nullptr;
+  }
   void* ptrs[] = {c->tw_x, c->tw_y, c->stage, c->stage32, c->gbuf, c->abuf, c->dflt, c->flag, c->sflag, c->ecols, c->esum, c->erec,
                   c->erec1, c->cold, c->cold_out};
   for (void* q : ptrs)
@@ -2270,8 +2275,14 @@ int sw_step_record(sw_ctx* c, int64_t nsteps, sw_energy_record* out) {
   if (nsteps < 1) return fail(c, SW_E_INVALID, "sw_step_record: nsteps must be >= 1");
   HIPCHK(c, hipSetDevice(c->cfg.device));
   const size_t per = c->dist ? rank_cols(c) * SW_NSUM : SW_NSUM;
-  if (!c->erec1)
-    if (int rc = alloc(c, (void**)&c->erec1, per * sizeof(double))) return rc;
+  if (!c->erec1) {
+    if (c->dist) {
+      if (int rc = alloc(c, (void**)&c->erec1, per * sizeof(double))) return rc;
+    } else {  // the record's sums land in pinned host memory: no copy after the steps (round 6)
+      HIPCHK(c, hipHostMalloc((void**)&c->erec1_host, per * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent));
+      HIPCHK(c, hipHostGetDevicePointer((void**)&c->erec1, c->erec1_host, 0));
+    }
+  }
   if (int rc = scan_arm(c)) return rc;
   for (int64_t i = 0; i + 1 < nsteps; ++i)
     if (int rc = step_once(c)) return rc;
@@ -2295,8 +2306,9 @@ int sw_step_record(sw_ctx* c, int64_t nsteps, sw_energy_record* out) {
     if (rc) return rc;
     sum_rank_cols(c, all.data(), per, 0, sums.data());
   } else {
-    HIPCHK(c, hipMemcpyAsync(sums.data(), c->erec1, SW_NSUM * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    const volatile double* hs = c->erec1_host;
+    for (int k = 0; k < SW_NSUM; ++k) sums[k] = hs[k];
   }
   out->step = c->step;
   out->t = c->t;

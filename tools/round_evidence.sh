@@ -1,7 +1,9 @@
 # A round's profile evidence on one GPU box: every BASELINE configuration warm
 # (tools/profile_round.sh), the default bench command under rocprofv3
 # --kernel-trace --stats, then the N = 8 bench line rehearsed on this one GPU
-# over gloo (config 4 on ranks 0-3).  usage: bash tools/round_evidence.sh rNN
+# over gloo (config 4 on ranks 0-3; the link probe's fields in comm.link), the
+# driver-like headline line (--steps 20 --warmup 5) and the drivers' cadence
+# table (tools/driver_cadence.py).  usage: bash tools/round_evidence.sh rNN
 set -o pipefail
 export TMPDIR=/tmp
 TAG=${1:?usage: round_evidence.sh rNN}
@@ -15,3 +17,8 @@ SW_BENCH_BACKEND=gloo timeout -k 10 600 python bench.py --gpus 8 --steps 10 --wa
   --config4-steps 3 --no-cpu-baseline --no-cold-profile > $O/bench_gloo8_rehearsal.json 2> $O/bench_gloo8.err \
   || { tail -20 $O/bench_gloo8.err; exit 4; }
 python -c "import json; b=json.load(open('$O/bench_gloo8_rehearsal.json')); print(b['n_gpus'], b['config']['parallelism'], b['slab_error'], b['config4']['n_gpus'], b['config4']['ranks_idle'], b['config4']['value'])"
+python -c "import json; b=json.load(open('$O/bench_gloo8_rehearsal.json')); print('link', b['comm']['link'])"
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench_driverlike.json 2> $O/bench_driverlike.err || exit 5
+python -c "import json; b=json.load(open('$O/bench_driverlike.json')); print('driverlike', round(b['value'],1), round(b['ms_per_step']*1e3,2), [(k['name'], round(k['avg_us'],1)) for k in b['kernels']])"
+timeout -k 10 600 python tools/driver_cadence.py --out $O/driver_cadence.json > /dev/null 2> $O/driver_cadence.err || exit 6
+grep cadence $O/driver_cadence.err
