@@ -28,44 +28,94 @@ struct Rad {
   int r[24];
 };
 
-// exp(DIR 2πi num/den), num taken mod den (exact argument reduction)
-template <int DIR>
-__device__ __forceinline__ double2 w_of(long long num, int den) {
+// exp(-2πi j/n), j < n: the forward twiddle table of one line length
+// (exact argument reduction: sincospi of 2j/n); the inverse uses conj
+__global__ void k_twiddles(double2* __restrict__ tw, int n) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
   double sn, cs;
-  sincospi(2.0 * (double)(num % den) / (double)den, &sn, &cs);
-  return make_double2(cs, DIR * sn);
+  sincospi(2.0 * (double)j / (double)n, &sn, &cs);
+  tw[j] = make_double2(cs, -sn);
 }
 
-// One line of n points in LDS (x, ping-pong partner y), transformed in place
-// by the block: mixed-radix Stockham, DIF form (the butterfly of radix r over
-// the points p + t m, then the twiddle ω_len^(p u)):
+__device__ __forceinline__ double2 cadd2(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 csub2(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ double2 cmul2(double2 a, double2 b) {
+  return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+// i·DIR·a
+template <int DIR>
+__device__ __forceinline__ double2 rot(double2 a) { return DIR > 0 ? make_double2(-a.y, a.x) : make_double2(a.y, -a.x); }
+
+// the r-point DFT of v in place, sign DIR: exact ±1/±i for r = 2, 4; the
+// radix-3/5 constants cos/sin(2π/3), cos/sin(2π/5), cos/sin(4π/5)
+template <int DIR>
+__device__ __forceinline__ void dft_small(int r, double2 (&v)[5]) {
+  if (r == 4) {
+    const double2 a = cadd2(v[0], v[2]), b = csub2(v[0], v[2]), c = cadd2(v[1], v[3]), d = rot<DIR>(csub2(v[1], v[3]));
+    v[0] = cadd2(a, c);
+    v[2] = csub2(a, c);
+    v[1] = cadd2(b, d);
+    v[3] = csub2(b, d);
+  } else if (r == 2) {
+    const double2 a = v[0];
+    v[0] = cadd2(a, v[1]);
+    v[1] = csub2(a, v[1]);
+  } else if (r == 3) {
+    constexpr double S3 = 0.86602540378443864676;  // sin(2π/3)
+    const double2 s = cadd2(v[1], v[2]), d = csub2(v[1], v[2]);
+    const double2 t = make_double2(v[0].x - 0.5 * s.x, v[0].y - 0.5 * s.y);
+    const double2 e = rot<DIR>(make_double2(S3 * d.x, S3 * d.y));
+    v[0] = cadd2(v[0], s);
+    v[1] = cadd2(t, e);
+    v[2] = csub2(t, e);
+  } else {  // r == 5
+    constexpr double C1 = 0.30901699437494742410, C2 = -0.80901699437494742410;  // cos(2π/5), cos(4π/5)
+    constexpr double S1 = 0.95105651629515357212, S2 = 0.58778525229247312917;   // sin(2π/5), sin(4π/5)
+    const double2 s1 = cadd2(v[1], v[4]), d1 = csub2(v[1], v[4]), s2 = cadd2(v[2], v[3]), d2 = csub2(v[2], v[3]);
+    const double2 a1 = make_double2(v[0].x + C1 * s1.x + C2 * s2.x, v[0].y + C1 * s1.y + C2 * s2.y);
+    const double2 a2 = make_double2(v[0].x + C2 * s1.x + C1 * s2.x, v[0].y + C2 * s1.y + C1 * s2.y);
+    const double2 b1 = rot<DIR>(make_double2(S1 * d1.x + S2 * d2.x, S1 * d1.y + S2 * d2.y));
+    const double2 b2 = rot<DIR>(make_double2(S2 * d1.x - S1 * d2.x, S2 * d1.y - S1 * d2.y));
+    v[0] = cadd2(v[0], cadd2(s1, s2));
+    v[1] = cadd2(a1, b1);
+    v[4] = csub2(a1, b1);
+    v[2] = cadd2(a2, b2);
+    v[3] = csub2(a2, b2);
+  }
+}
+
+// B lines of n points in LDS (line b at x + b n, ping-pong partner y),
+// transformed in place by the block: mixed-radix Stockham, DIF form (the
+// r-point DFT over the points p + t m, then the twiddle ω_len^(p u)):
 //   y[q + s (r p + u)] = ω_len^(p u) Σ_t x[q + s (p + t m)] ω_r^(t u)
 // with len the current sub-transform length (n, n/r₀, …), m = len/r, s the
-// stride (1, r₀, …).  Natural order in and out; returns the buffer holding
-// the result.  DIR = -1 forward (unnormalised), +1 inverse.
+// stride (1, r₀, …); ω_len^(p u) = tw[p u n/len] (p u < len).  Natural order
+// in and out; returns the buffer holding the result.  DIR = -1 forward
+// (unnormalised), +1 inverse.
 template <int DIR>
-__device__ double2* fft_lds(double2* x, double2* y, const Rad& R) {
-  int len = R.n, s = 1;
+__device__ double2* fft_lds(double2* x, double2* y, const Rad& R, int B, const double2* __restrict__ tw) {
+  const int n = R.n;
+  int len = n, s = 1;
   for (int pi = 0; pi < R.nr; ++pi) {
-    const int r = R.r[pi], m = len / r;
-    for (int i = threadIdx.x; i < m * s; i += blockDim.x) {
-      const int p = i / s, q = i - p * s;
+    const int r = R.r[pi], m = len / r, nb = m * s, step = n / len;
+    for (int idx = threadIdx.x; idx < B * nb; idx += blockDim.x) {
+      const int b = idx / nb, i = idx - b * nb, p = i / s, q = i - p * s;
+      const double2* xb = x + b * n;
+      double2* yb = y + b * n;
       double2 v[5];
-      for (int t = 0; t < r; ++t) v[t] = x[q + s * (p + t * m)];
-      for (int u = 0; u < r; ++u) {
-        double2 a = v[0];
-        for (int t = 1; t < r; ++t) {
-          const int e = (t * u) % r;
-          double2 w;  // ω_r^e: exact for r = 2, 4
-          if (r == 2) w = make_double2(e == 0 ? 1.0 : -1.0, 0.0);
-          else if (r == 4) w = e == 0 ? make_double2(1.0, 0.0) : e == 1 ? make_double2(0.0, (double)DIR)
-                           : e == 2 ? make_double2(-1.0, 0.0) : make_double2(0.0, -(double)DIR);
-          else w = w_of<DIR>(e, r);
-          a = make_double2(a.x + (v[t].x * w.x - v[t].y * w.y), a.y + (v[t].x * w.y + v[t].y * w.x));
+#pragma unroll
+      for (int t = 0; t < 5; ++t)
+        if (t < r) v[t] = xb[q + s * (p + t * m)];
+      dft_small<DIR>(r, v);
+      yb[q + s * r * p] = v[0];
+#pragma unroll
+      for (int u = 1; u < 5; ++u)
+        if (u < r) {
+          double2 w = tw[p * u * step];
+          if (DIR > 0) w.y = -w.y;
+          yb[q + s * (r * p + u)] = cmul2(v[u], w);
         }
-        const double2 tw = w_of<DIR>((long long)p * u, len);
-        y[q + s * (r * p + u)] = make_double2(a.x * tw.x - a.y * tw.y, a.x * tw.y + a.y * tw.x);
-      }
     }
     __syncthreads();
     double2* t = x;
@@ -77,60 +127,73 @@ __device__ double2* fft_lds(double2* x, double2* y, const Rad& R) {
   return x;
 }
 
-// complex lines of R.n points: element e of line L at data[L·ls + e·es]
-// (the spectral arrays' l columns: es = nkr, ls = 1 within a field, fields
-// nl·nkr apart — line L = f·nkr + kr)
+// complex lines of R.n points, B per block (adjacent kr: one row of B points
+// per load): element e of line kr of field f at data[f·fstride + kr + e·es]
 template <int DIR>
-__global__ void __launch_bounds__(256) k_lines(double2* __restrict__ data, Rad R, int nkr, long long fstride,
-                                               long long es) {
+__global__ void __launch_bounds__(256) k_lines(double2* __restrict__ data, Rad R, int B, int nkr, long long fstride,
+                                               long long es, const double2* __restrict__ tw) {
   extern __shared__ double2 lds[];
-  double2 *x = lds, *y = lds + R.n;
-  const int L = blockIdx.x, f = L / nkr, kr = L - f * nkr;
-  double2* d = data + f * fstride + kr;
-  for (int i = threadIdx.x; i < R.n; i += blockDim.x) x[i] = d[i * es];
-  __syncthreads();
-  const double2* z = fft_lds<DIR>(x, y, R);
-  for (int i = threadIdx.x; i < R.n; i += blockDim.x) d[i * es] = z[i];
-}
-
-// c2r along x of one stored row (FF's irfft rule: c2c along l done, then
-// c2r along x with the DC and Nyquist bins' imaginary parts dropped, numpy's
-// convention): spec row [nkr] -> phys row [nx] × scale
-__global__ void __launch_bounds__(256) k_c2r_rows(const double2* __restrict__ spec, double* __restrict__ phys, Rad R,
-                                                  int nkr, double scale) {
-  extern __shared__ double2 lds[];
-  double2 *x = lds, *y = lds + R.n;
-  const int row = blockIdx.x, n = R.n;
-  const double2* a = spec + (long long)row * nkr;
-  for (int k = threadIdx.x; k < n; k += blockDim.x) {
-    double2 z;
-    if (k <= n / 2) {
-      z = a[k];
-      if (k == 0 || k == n / 2) z.y = 0.0;
-    } else {
-      const double2 b = a[n - k];
-      z = make_double2(b.x, -b.y);
-    }
-    x[k] = z;
+  const int n = R.n, groups = (nkr + B - 1) / B;
+  double2 *x = lds, *y = lds + B * n;
+  const int f = blockIdx.x / groups, kr0 = (blockIdx.x - f * groups) * B;
+  const int nv = min(B, nkr - kr0);
+  double2* d = data + f * fstride + kr0;
+  for (int idx = threadIdx.x; idx < B * n; idx += blockDim.x) {
+    const int e = idx / B, b = idx - e * B;
+    x[b * n + e] = b < nv ? d[e * es + b] : zero2();
   }
   __syncthreads();
-  const double2* z = fft_lds<+1>(x, y, R);
-  double* o = phys + (long long)row * n;
-  for (int k = threadIdx.x; k < n; k += blockDim.x) o[k] = z[k].x * scale;
+  const double2* z = fft_lds<DIR>(x, y, R, B, tw);
+  for (int idx = threadIdx.x; idx < B * n; idx += blockDim.x) {
+    const int e = idx / B, b = idx - e * B;
+    if (b < nv) d[e * es + b] = z[b * n + e];
+  }
 }
 
-// r2c along x: phys row [nx] -> spec row [nkr] (unnormalised)
-__global__ void __launch_bounds__(256) k_r2c_rows(const double* __restrict__ phys, double2* __restrict__ spec, Rad R,
-                                                  int nkr) {
+// c2r along x of B stored rows (FF's irfft rule: c2c along l done, then c2r
+// along x with the DC and Nyquist bins' imaginary parts dropped, numpy's
+// convention): spec rows [nkr] -> phys rows [nx] × scale
+__global__ void __launch_bounds__(256) k_c2r_rows(const double2* __restrict__ spec, double* __restrict__ phys, Rad R,
+                                                  int B, int nkr, double scale, const double2* __restrict__ tw) {
   extern __shared__ double2 lds[];
-  double2 *x = lds, *y = lds + R.n;
-  const int row = blockIdx.x, n = R.n;
-  const double* a = phys + (long long)row * n;
-  for (int k = threadIdx.x; k < n; k += blockDim.x) x[k] = make_double2(a[k], 0.0);
+  const int n = R.n;
+  double2 *x = lds, *y = lds + B * n;
+  const long long row0 = (long long)blockIdx.x * B;
+  const double2* a = spec + row0 * nkr;
+  for (int idx = threadIdx.x; idx < B * n; idx += blockDim.x) {
+    const int b = idx / n, k = idx - b * n;
+    double2 z;
+    if (k <= n / 2) {
+      z = a[b * nkr + k];
+      if (k == 0 || k == n / 2) z.y = 0.0;
+    } else {
+      const double2 c = a[b * nkr + n - k];
+      z = make_double2(c.x, -c.y);
+    }
+    x[idx] = z;
+  }
   __syncthreads();
-  const double2* z = fft_lds<-1>(x, y, R);
-  double2* o = spec + (long long)row * nkr;
-  for (int k = threadIdx.x; k < nkr; k += blockDim.x) o[k] = z[k];
+  const double2* z = fft_lds<+1>(x, y, R, B, tw);
+  double* o = phys + row0 * n;
+  for (int idx = threadIdx.x; idx < B * n; idx += blockDim.x) o[idx] = z[idx].x * scale;
+}
+
+// r2c along x of B rows: phys rows [nx] -> spec rows [nkr] (unnormalised)
+__global__ void __launch_bounds__(256) k_r2c_rows(const double* __restrict__ phys, double2* __restrict__ spec, Rad R,
+                                                  int B, int nkr, const double2* __restrict__ tw) {
+  extern __shared__ double2 lds[];
+  const int n = R.n;
+  double2 *x = lds, *y = lds + B * n;
+  const long long row0 = (long long)blockIdx.x * B;
+  const double* a = phys + row0 * n;
+  for (int idx = threadIdx.x; idx < B * n; idx += blockDim.x) x[idx] = make_double2(a[idx], 0.0);
+  __syncthreads();
+  const double2* z = fft_lds<-1>(x, y, R, B, tw);
+  double2* o = spec + row0 * nkr;
+  for (int idx = threadIdx.x; idx < B * nkr; idx += blockDim.x) {
+    const int b = idx / nkr, k = idx - b * nkr;
+    o[idx] = z[b * n + k];
+  }
 }
 
 // mode (l, kr) of a full [nl][nkr] field: live under FF's dealias!
@@ -325,7 +388,8 @@ __global__ void k_nan(long long n, const double* __restrict__ x, int* flag) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool bad = i < n && !isfinite(x[i]);
   const unsigned long long m = __ballot(bad);
-  if (m != 0ull && (int)__lane_id() == __ffsll((long long)m) - 1) atomicOr(flag, 1);
+  if (m != 0ull && (int)__lane_id() == __ffsll((long long)m) - 1)
+    __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ----------------------------------------------------------------- host side
@@ -337,6 +401,8 @@ static Rad rad_of(const int* r, int nr, int n) {
   return R;
 }
 static dim3 modes_grid(const Geom& g) { return dim3((unsigned)(((long long)g.nl * g.nkr + 255) / 256)); }
+
+static int lines_per_block(int n);
 
 int create(Engine*& e, const sw_config& k, const Phys& p, const Geom& g, double2* sol, hipStream_t s,
            std::string& err) {
@@ -359,70 +425,88 @@ int create(Engine*& e, const sw_config& k, const Phys& p, const Geom& g, double2
   if (hipMalloc((void**)&e->phys, 6 * NP * sizeof(double)) != hipSuccess) return SW_E_NOMEM;
   if (hipMalloc((void**)&e->cols, 3 * (size_t)g.nkr * sizeof(double)) != hipSuccess) return SW_E_NOMEM;
   for (double2* b : {e->xs, e->acc, e->N}) (void)hipMemsetAsync(b, 0, 2 * F * sizeof(double2), s);
+  if (hipMalloc((void**)&e->twx, (size_t)g.nx * sizeof(double2)) != hipSuccess) return SW_E_NOMEM;
+  if (hipMalloc((void**)&e->twy, (size_t)g.ny * sizeof(double2)) != hipSuccess) return SW_E_NOMEM;
+  SW_LAUNCH(k_twiddles, dim3((g.nx + 255) / 256), dim3(256), 0, s, e->twx, g.nx);
+  SW_LAUNCH(k_twiddles, dim3((g.ny + 255) / 256), dim3(256), 0, s, e->twy, g.ny);
+  // rows per block: B·nx ≤ 2048 with B dividing ny (ny is even, B a power of two)
+  e->bx = lines_per_block(g.nx);
+  while (g.ny % e->bx) e->bx /= 2;
   return SW_OK;
 }
 
 void destroy(Engine* e) {
   if (!e) return;
-  for (void* b : {(void*)e->xs, (void*)e->acc, (void*)e->N, (void*)e->spec, (void*)e->phys, (void*)e->cols})
+  for (void* b : {(void*)e->xs, (void*)e->acc, (void*)e->N, (void*)e->spec, (void*)e->phys, (void*)e->cols,
+                  (void*)e->twx, (void*)e->twy})
     if (b) (void)hipFree(b);
   delete e;
 }
 
 // nf spectral fields [nf][nl][nkr] -> physical [nf][ny][nx] (normalised c2r;
 // the spectral fields are transformed in place along l first)
+// lines per block: B·n ≤ 2048 points (≤ 64 KB of LDS with the ping-pong buffer), at most 8
+static int lines_per_block(int n) {
+  int B = 1;
+  while (B < 8 && 2 * B * n <= 2048) B *= 2;
+  return B;
+}
+
 static void inverse2d(Engine* e, double2* spec, int nf, double* phys) {
   const Geom& g = e->g;
   const Rad Ry = rad_of(e->rady, e->nrady, g.ny), Rx = rad_of(e->radx, e->nradx, g.nx);
-  hipLaunchKernelGGL(k_lines<+1>, dim3(nf * g.nkr), dim3(256), 2 * g.ny * sizeof(double2), e->s, spec, Ry, g.nkr,
-                     (long long)g.nl * g.nkr, (long long)g.nkr);
-  hipLaunchKernelGGL(k_c2r_rows, dim3(nf * g.ny), dim3(256), 2 * g.nx * sizeof(double2), e->s, spec, phys, Rx, g.nkr,
-                     1.0 / ((double)g.nx * (double)g.ny));
+  const int By = lines_per_block(g.ny), Bx = e->bx;
+  SW_LAUNCH(k_lines<+1>, dim3(nf * ((g.nkr + By - 1) / By)), dim3(256), 2 * By * g.ny * sizeof(double2), e->s, spec,
+            Ry, By, g.nkr, (long long)g.nl * g.nkr, (long long)g.nkr, e->twy);
+  SW_LAUNCH(k_c2r_rows, dim3(nf * g.ny / Bx), dim3(256), 2 * Bx * g.nx * sizeof(double2), e->s, spec, phys, Rx, Bx,
+            g.nkr, 1.0 / ((double)g.nx * (double)g.ny), e->twx);
 }
 
 // physical [nf][ny][nx] -> spectral [nf][nl][nkr] (unnormalised r2c)
 static void forward2d(Engine* e, const double* phys, int nf, double2* spec) {
   const Geom& g = e->g;
   const Rad Ry = rad_of(e->rady, e->nrady, g.ny), Rx = rad_of(e->radx, e->nradx, g.nx);
-  hipLaunchKernelGGL(k_r2c_rows, dim3(nf * g.ny), dim3(256), 2 * g.nx * sizeof(double2), e->s, phys, spec, Rx, g.nkr);
-  hipLaunchKernelGGL(k_lines<-1>, dim3(nf * g.nkr), dim3(256), 2 * g.ny * sizeof(double2), e->s, spec, Ry, g.nkr,
-                     (long long)g.nl * g.nkr, (long long)g.nkr);
+  const int By = lines_per_block(g.ny), Bx = e->bx;
+  SW_LAUNCH(k_r2c_rows, dim3(nf * g.ny / Bx), dim3(256), 2 * Bx * g.nx * sizeof(double2), e->s, phys, spec, Rx, Bx,
+            g.nkr, e->twx);
+  SW_LAUNCH(k_lines<-1>, dim3(nf * ((g.nkr + By - 1) / By)), dim3(256), 2 * By * g.ny * sizeof(double2), e->s, spec,
+            Ry, By, g.nkr, (long long)g.nl * g.nkr, (long long)g.nkr, e->twy);
 }
 
 void calcN(Engine* e, const double2* X, double2* N) {
   const Geom& g = e->g;
   const long long np = (long long)g.nx * g.ny;
-  hipLaunchKernelGGL(k_prep, modes_grid(g), dim3(256), 0, e->s, g, e->p, X, e->spec);
+  SW_LAUNCH(k_prep, modes_grid(g), dim3(256), 0, e->s, g, e->p, X, e->spec);
   inverse2d(e, e->spec, 6, e->phys);
-  hipLaunchKernelGGL(k_products, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, e->s, e->p, e->phys, np);
+  SW_LAUNCH(k_products, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, e->s, e->p, e->phys, np);
   forward2d(e, e->phys, 4, e->spec);
-  hipLaunchKernelGGL(k_assemble, modes_grid(g), dim3(256), 0, e->s, g, e->p, X, e->spec, N);
+  SW_LAUNCH(k_assemble, modes_grid(g), dim3(256), 0, e->s, g, e->p, X, e->spec, N);
 }
 
 void step(Engine* e, int* nanflag) {
   const Geom& g = e->g;
   for (int stage = 1; stage <= 4; ++stage) {
     calcN(e, stage == 1 ? e->sol : e->xs, e->N);
-    hipLaunchKernelGGL(k_frk4, modes_grid(g), dim3(256), 0, e->s, g, e->p, stage, e->sol, e->xs, e->acc, e->N,
+    SW_LAUNCH(k_frk4, modes_grid(g), dim3(256), 0, e->s, g, e->p, stage, e->sol, e->xs, e->acc, e->N,
                        stage == 4 ? nanflag : nullptr);
   }
 }
 
-void dealias(Engine* e, double2* X) { hipLaunchKernelGGL(k_dealias, modes_grid(e->g), dim3(256), 0, e->s, e->g, X); }
+void dealias(Engine* e, double2* X) { SW_LAUNCH(k_dealias, modes_grid(e->g), dim3(256), 0, e->s, e->g, X); }
 
 void physical(Engine* e, const double2* X, int fid, double* out) {
-  hipLaunchKernelGGL(k_spec_field, modes_grid(e->g), dim3(256), 0, e->s, e->g, e->p, fid, X, e->spec);
+  SW_LAUNCH(k_spec_field, modes_grid(e->g), dim3(256), 0, e->s, e->g, e->p, fid, X, e->spec);
   inverse2d(e, e->spec, 1, out);
 }
 
 void energy_sums(Engine* e, const double2* X, double* out) {
-  hipLaunchKernelGGL(k_energy_cols, dim3(e->g.nkr), dim3(256), 0, e->s, e->g, e->p, X, e->cols);
-  hipLaunchKernelGGL(k_energy_final, dim3(1), dim3(64), 0, e->s, e->g, e->cols, out);
+  SW_LAUNCH(k_energy_cols, dim3(e->g.nkr), dim3(256), 0, e->s, e->g, e->p, X, e->cols);
+  SW_LAUNCH(k_energy_final, dim3(1), dim3(64), 0, e->s, e->g, e->cols, out);
 }
 
 void nan_scan(Engine* e, const double2* X, int* flag) {
   const long long n = 4LL * e->g.nl * e->g.nkr;  // 2 fields of complex doubles
-  hipLaunchKernelGGL(k_nan, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->s, n,
+  SW_LAUNCH(k_nan, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->s, n,
                      reinterpret_cast<const double*>(X), flag);
 }
 

@@ -40,6 +40,9 @@ struct Engine {
   double2* spec = nullptr;  // 6 spectral work fields [6][nl][nkr]
   double* phys = nullptr;   // 6 physical work fields [6][ny][nx]
   double* cols = nullptr;   // energy column sums [nkr][3]
+  double2* twx = nullptr;   // forward twiddles exp(-2πi j/nx), j < nx
+  double2* twy = nullptr;   // … along y
+  int bx = 1;               // rows per block of the x transforms
 };
 
 int create(Engine*& e, const sw_config& k, const Phys& p, const Geom& g, double2* sol, hipStream_t s,

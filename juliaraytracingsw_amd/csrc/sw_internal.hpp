@@ -32,7 +32,29 @@
 // 7 for TY with its wave/balanced split)
 #define SW_NSUM 7
 
+#include <hip/hip_ext.h>
+
 namespace sw {
+
+// sw_profile_steps' kernel timing (sw_api.cpp Timer): while `stop` is set,
+// every launch is a hipExtLaunchKernel whose events take the dispatch's own
+// start/end timestamps — the first launch of a timed scope `start`, each
+// launch `stop` (the last one holds) — so a scope's interval is its kernels'
+// execution, as the kernel trace reports it, without the event markers'
+// own packets in it.
+struct ProfEv {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+extern thread_local ProfEv prof_ev;
+#define SW_LAUNCH(k, gr, bl, sh, st, ...)                                                             \
+  do {                                                                                               \
+    if (::sw::prof_ev.stop) {                                                                        \
+      hipExtLaunchKernelGGL(k, gr, bl, sh, st, ::sw::prof_ev.start, ::sw::prof_ev.stop, 0, __VA_ARGS__); \
+      ::sw::prof_ev.start = nullptr;                                                                 \
+    } else {                                                                                         \
+      hipLaunchKernelGGL(k, gr, bl, sh, st, __VA_ARGS__);                                            \
+    }                                                                                                \
+  } while (0)
 
 // MODEL_MLQG (GeophysicalFlows MultiLayerQG, 2 layers) runs the MODEL_QG2
 // kernels; Phys::model selects its streamfunction and linear terms at run time

@@ -3141,29 +3141,29 @@ void LenOps<L>::col_inv(int model, const Geom& g, const Phys& p, const double2* 
   const dim3 grid(col_blocks<L>(g), ng);
   const dim3 grid2(col_blocks<L>(g), 2 * ng);
   if (model == MODEL_RSW && g.isplit)
-    hipLaunchKernelGGL((k_col_inv<MODEL_RSW, L, true>), grid2, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M,
+    SW_LAUNCH((k_col_inv<MODEL_RSW, L, true>), grid2, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M,
                        tw, g0);
   else if (model == MODEL_RSW)
-    hipLaunchKernelGGL((k_col_inv<MODEL_RSW, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
+    SW_LAUNCH((k_col_inv<MODEL_RSW, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
   else if (model == MODEL_RSWA && g.isplit)
-    hipLaunchKernelGGL((k_col_inv<MODEL_RSWA, L, true>), grid2, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M,
+    SW_LAUNCH((k_col_inv<MODEL_RSWA, L, true>), grid2, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M,
                        tw, g0);
   else if (model == MODEL_RSWA)
-    hipLaunchKernelGGL((k_col_inv<MODEL_RSWA, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
+    SW_LAUNCH((k_col_inv<MODEL_RSWA, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
   else if (model == MODEL_TY && g.isplit)
-    hipLaunchKernelGGL((k_col_inv<MODEL_TY, L, true>), dim3(col_blocks<L>(g), 2 * ng), dim3(Blk<L>::THREADS),
+    SW_LAUNCH((k_col_inv<MODEL_TY, L, true>), dim3(col_blocks<L>(g), 2 * ng), dim3(Blk<L>::THREADS),
                        lds_bytes<L>(), s, g, p, X, M, tw, g0);
   else if (model == MODEL_TY)
-    hipLaunchKernelGGL((k_col_inv<MODEL_TY, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
+    SW_LAUNCH((k_col_inv<MODEL_TY, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
   else if (g0 == 0 && ng == 2 && Blk<L>::NB == 1 && g.kcl % 64 == 0 &&
            (SW_QG_INV_PAIR == 2 || (SW_QG_INV_PAIR == 1 && L >= 13)))
-    hipLaunchKernelGGL((k_col_inv<MODEL_QG2, L>), dim3(2 * g.kcl), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X,
+    SW_LAUNCH((k_col_inv<MODEL_QG2, L>), dim3(2 * g.kcl), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X,
                        M, tw, -1);
   else if (g.isplit)
-    hipLaunchKernelGGL((k_col_inv<MODEL_QG2, L, true>), dim3(col_blocks<L>(g), 3 * ng), dim3(Blk<L>::THREADS),
+    SW_LAUNCH((k_col_inv<MODEL_QG2, L, true>), dim3(col_blocks<L>(g), 3 * ng), dim3(Blk<L>::THREADS),
                        lds_bytes<L>(), s, g, p, X, M, tw, g0);
   else
-    hipLaunchKernelGGL((k_col_inv<MODEL_QG2, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
+    SW_LAUNCH((k_col_inv<MODEL_QG2, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
 }
 
 // ===========================================================================
@@ -3313,7 +3313,7 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
   if (model == MODEL_RSW) {
     constexpr int nbr = rowh_nb<L, true>();
     if constexpr (rsw_row_half<L>()) {
-      hipLaunchKernelGGL((k_row_rsw_h<L>), dim3(nrows / nbr), dim3(RowH<L>::NTH * nbr),
+      SW_LAUNCH((k_row_rsw_h<L>), dim3(nrows / nbr), dim3(RowH<L>::NTH * nbr),
                          nbr * rsw_rowh_lines<L>() * FftPlan<L - 1>::LDS * sizeof(double2), s, g, p, Mi, Mo,
                          tw, y0);
       return;
@@ -3321,56 +3321,56 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
     if constexpr (roww<L>() > 0 && BR::NB == 1) {
       if (g.rsp) {  // (Geom::rsp: the row over two blocks, k_row_rsw_sp)
         if (row_prunable<L>(g))
-          hipLaunchKernelGGL((k_row_rsw_sp<L, true>), dim3(2 * nrows), dim3(BR::THREADS),
+          SW_LAUNCH((k_row_rsw_sp<L, true>), dim3(2 * nrows), dim3(BR::THREADS),
                              FftPlan<L>::LDS * sizeof(double2), s, g, p, Mi, Mo, tw, y0);
         else
-          hipLaunchKernelGGL((k_row_rsw_sp<L, false>), dim3(2 * nrows), dim3(BR::THREADS),
+          SW_LAUNCH((k_row_rsw_sp<L, false>), dim3(2 * nrows), dim3(BR::THREADS),
                              FftPlan<L>::LDS * sizeof(double2), s, g, p, Mi, Mo, tw, y0);
         return;
       }
     }
     if (row_prunable<L>(g))
-      hipLaunchKernelGGL((k_row<MODEL_RSW, L, false, true>), dim3(nrows / BR::NB), dim3(BR::THREADS), sh_rsw, s, g,
+      SW_LAUNCH((k_row<MODEL_RSW, L, false, true>), dim3(nrows / BR::NB), dim3(BR::THREADS), sh_rsw, s, g,
                          p, Mi, Mo, tw, y0, nullptr);
     else if (g.rsplit && row_lds_lines<MODEL_RSW, L>() == 2 && roww<L>() == 0)
-      hipLaunchKernelGGL((k_row<MODEL_RSW, L, false, false, true>), dim3(nrows / BR::NB, 2), dim3(BR::THREADS),
+      SW_LAUNCH((k_row<MODEL_RSW, L, false, false, true>), dim3(nrows / BR::NB, 2), dim3(BR::THREADS),
                          sh_rsw, s, g, p, Mi, Mo, tw, y0, nullptr);
     else
-      hipLaunchKernelGGL((k_row<MODEL_RSW, L>), dim3(nrows / BR::NB), dim3(BR::THREADS), sh_rsw, s, g, p, Mi, Mo,
+      SW_LAUNCH((k_row<MODEL_RSW, L>), dim3(nrows / BR::NB), dim3(BR::THREADS), sh_rsw, s, g, p, Mi, Mo,
                          tw, y0, nullptr);
   } else if (model == MODEL_TY) {
     if (Ma)
-      hipLaunchKernelGGL((k_row<MODEL_TY, L, true>), dim3(nrows / BT::NB), dim3(BT::THREADS), sh_ty, s, g, p, Mi,
+      SW_LAUNCH((k_row<MODEL_TY, L, true>), dim3(nrows / BT::NB), dim3(BT::THREADS), sh_ty, s, g, p, Mi,
                          Mo, tw, y0, Ma);
     else if (g.rsplit)
-      hipLaunchKernelGGL((k_row<MODEL_TY, L, false, false, true>), dim3(nrows / BT::NB, 4), dim3(BT::THREADS), sh_ty,
+      SW_LAUNCH((k_row<MODEL_TY, L, false, false, true>), dim3(nrows / BT::NB, 4), dim3(BT::THREADS), sh_ty,
                          s, g, p, Mi, Mo, tw, y0, nullptr);
     else
-      hipLaunchKernelGGL((k_row<MODEL_TY, L>), dim3(nrows / BT::NB), dim3(BT::THREADS), sh_ty, s, g, p, Mi, Mo, tw,
+      SW_LAUNCH((k_row<MODEL_TY, L>), dim3(nrows / BT::NB), dim3(BT::THREADS), sh_ty, s, g, p, Mi, Mo, tw,
                          y0, nullptr);
   } else if (model == MODEL_RSWA) {
     using BA = BlkRow<MODEL_RSWA, L>;
     if (Ma)
-      hipLaunchKernelGGL((k_row<MODEL_RSWA, L, true>), dim3(nrows / BA::NB), dim3(BA::THREADS),
+      SW_LAUNCH((k_row<MODEL_RSWA, L, true>), dim3(nrows / BA::NB), dim3(BA::THREADS),
                          FftPlan<L>::LDS * BA::NB * sizeof(double2), s, g, p, Mi, Mo, tw, y0, Ma);
     else
-      hipLaunchKernelGGL((k_row<MODEL_RSWA, L>), dim3(nrows / BA::NB), dim3(BA::THREADS),
+      SW_LAUNCH((k_row<MODEL_RSWA, L>), dim3(nrows / BA::NB), dim3(BA::THREADS),
                          FftPlan<L>::LDS * BA::NB * sizeof(double2), s, g, p, Mi, Mo, tw, y0, nullptr);
   }
   else if (Ma) {  // aliased-state tracking: the full-length row (it writes the aliased x-spectra)
-    hipLaunchKernelGGL((k_row<MODEL_QG2, L, true>), dim3(nrows / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p, Mi,
+    SW_LAUNCH((k_row<MODEL_QG2, L, true>), dim3(nrows / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p, Mi,
                        Mo, tw, y0, Ma);
   } else if constexpr (qg_row_half<L>()) {
-    hipLaunchKernelGGL((k_row_qg_h<L>), dim3(nrows / rowh_nb<L>()), dim3(RowH<L>::NTH * rowh_nb<L>()),
+    SW_LAUNCH((k_row_qg_h<L>), dim3(nrows / rowh_nb<L>()), dim3(RowH<L>::NTH * rowh_nb<L>()),
                        rowh_nb<L>() * FftPlan<L - 1>::LDS * sizeof(double2), s, g, p, Mi, Mo, tw, y0);
   } else if (row_prunable<L>(g)) {
-    hipLaunchKernelGGL((k_row<MODEL_QG2, L, false, true>), dim3(nrows / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p,
+    SW_LAUNCH((k_row<MODEL_QG2, L, false, true>), dim3(nrows / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p,
                        Mi, Mo, tw, y0, nullptr);
   } else if (g.rsplit) {
-    hipLaunchKernelGGL((k_row<MODEL_QG2, L, false, false, true>), dim3(nrows / BQ::NB, 2), dim3(BQ::THREADS), sh_qg2,
+    SW_LAUNCH((k_row<MODEL_QG2, L, false, false, true>), dim3(nrows / BQ::NB, 2), dim3(BQ::THREADS), sh_qg2,
                        s, g, p, Mi, Mo, tw, y0, nullptr);
   } else {
-    hipLaunchKernelGGL((k_row<MODEL_QG2, L>), dim3(nrows / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p, Mi, Mo, tw,
+    SW_LAUNCH((k_row<MODEL_QG2, L>), dim3(nrows / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p, Mi, Mo, tw,
                        y0, nullptr);
   }
 }
@@ -3380,13 +3380,13 @@ void LenOps<L>::col_fwd_alias(int model, const Geom& g, const Geom& ga, int regi
                               const double2* Mf, const double2* Ma, double2* N, const double2* tw, hipStream_t s) {
   const int nb = (ga.kcn + Blk<L>::NB - 1) / Blk<L>::NB;
   if (model == MODEL_RSWA)
-    hipLaunchKernelGGL((k_col_fwd_alias<MODEL_RSWA, L>), dim3(nb, 3), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g,
+    SW_LAUNCH((k_col_fwd_alias<MODEL_RSWA, L>), dim3(nb, 3), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g,
                        ga, region, p, Mf, Ma, N, tw);
   else if (model == MODEL_TY)
-    hipLaunchKernelGGL((k_col_fwd_alias<MODEL_TY, L>), dim3(nb, 4), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g,
+    SW_LAUNCH((k_col_fwd_alias<MODEL_TY, L>), dim3(nb, 4), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g,
                        ga, region, p, Mf, Ma, N, tw);
   else
-    hipLaunchKernelGGL((k_col_fwd_alias<MODEL_QG2, L>), dim3(nb, 2), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g,
+    SW_LAUNCH((k_col_fwd_alias<MODEL_QG2, L>), dim3(nb, 2), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g,
                        ga, region, p, Mf, Ma, N, tw);
 }
 
@@ -3397,29 +3397,29 @@ void LenOps<L>::col_fwd(int model, const Geom& g, const Phys& p, const double2* 
   const size_t sh = lds_bytes<L>();
   const bool split = T1 != nullptr;  // (RSW, 2LQG / MultiLayerQG, Thomas–Yamada)
   if (model == MODEL_RSW && split)
-    hipLaunchKernelGGL((k_col_fwd<MODEL_RSW, L, true>), grid3, blk, sh, s, g, p, Mf, N, X, tw, f0, T1, T2);
+    SW_LAUNCH((k_col_fwd<MODEL_RSW, L, true>), grid3, blk, sh, s, g, p, Mf, N, X, tw, f0, T1, T2);
   else if (model == MODEL_RSW)
-    hipLaunchKernelGGL((k_col_fwd<MODEL_RSW, L>), grid, blk, sh, s, g, p, Mf, N, X, tw, f0, nullptr, nullptr);
+    SW_LAUNCH((k_col_fwd<MODEL_RSW, L>), grid, blk, sh, s, g, p, Mf, N, X, tw, f0, nullptr, nullptr);
   else if (model == MODEL_RSWA)
-    hipLaunchKernelGGL((k_col_fwd<MODEL_RSWA, L>), grid, blk, sh, s, g, p, Mf, N, X, tw, f0, nullptr, nullptr);
+    SW_LAUNCH((k_col_fwd<MODEL_RSWA, L>), grid, blk, sh, s, g, p, Mf, N, X, tw, f0, nullptr, nullptr);
   else if (model == MODEL_TY && split)
-    hipLaunchKernelGGL((k_col_fwd<MODEL_TY, L, true>), grid3, blk, sh, s, g, p, Mf, N, X, tw, f0, T1, T2);
+    SW_LAUNCH((k_col_fwd<MODEL_TY, L, true>), grid3, blk, sh, s, g, p, Mf, N, X, tw, f0, T1, T2);
   else if (model == MODEL_TY)
-    hipLaunchKernelGGL((k_col_fwd<MODEL_TY, L>), grid, blk, sh, s, g, p, Mf, N, X, tw, f0, nullptr, nullptr);
+    SW_LAUNCH((k_col_fwd<MODEL_TY, L>), grid, blk, sh, s, g, p, Mf, N, X, tw, f0, nullptr, nullptr);
   else if (split)
-    hipLaunchKernelGGL((k_col_fwd<MODEL_QG2, L, true>), grid3, blk, sh, s, g, p, Mf, N, X, tw, f0, T1, T2);
+    SW_LAUNCH((k_col_fwd<MODEL_QG2, L, true>), grid3, blk, sh, s, g, p, Mf, N, X, tw, f0, T1, T2);
   else
-    hipLaunchKernelGGL((k_col_fwd<MODEL_QG2, L>), grid, blk, sh, s, g, p, Mf, N, X, tw, f0, nullptr, nullptr);
+    SW_LAUNCH((k_col_fwd<MODEL_QG2, L>), grid, blk, sh, s, g, p, Mf, N, X, tw, f0, nullptr, nullptr);
 }
 
 template <int L>
 void LenOps<L>::col_inv1(const Geom& g, const double2* X, double2* M, const double2* tw, hipStream_t s) {
-  hipLaunchKernelGGL((k_col_inv1<L>), dim3(col_blocks<L>(g)), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, X, M, tw);
+  SW_LAUNCH((k_col_inv1<L>), dim3(col_blocks<L>(g)), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, X, M, tw);
 }
 
 template <int L>
 void LenOps<L>::row_c2r1(const Geom& g, const double2* M, double* out, const double2* tw, hipStream_t s) {
-  hipLaunchKernelGGL((k_row_c2r1<L>), dim3(row_blocks<L>(g)), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, M, out, tw);
+  SW_LAUNCH((k_row_c2r1<L>), dim3(row_blocks<L>(g)), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, M, out, tw);
 }
 
 template <int L>
@@ -3427,7 +3427,7 @@ void LenOps<L>::col_step(int model, int op, const Geom& g, const Phys& p, const 
                          double2* Minv, const double2* tw, hipStream_t s, int f0, int nfl) {
   const dim3 grid(col_blocks<L>(g)), blk(Blk<L>::THREADS);
   const size_t sh = lds_bytes<L>();
-#define SW_CS(M, O) hipLaunchKernelGGL((k_col_step<M, L, O>), grid, blk, sh, s, g, p, a, Mf, Minv, tw)
+#define SW_CS(M, O) SW_LAUNCH((k_col_step<M, L, O>), grid, blk, sh, s, g, p, a, Mf, Minv, tw)
   if (model == MODEL_RSW) {
     // all three fields: the XCD-interleaved 1-D grid where it applies; a
     // field range (pipelined slab exchange): one grid row per field
@@ -3436,9 +3436,9 @@ void LenOps<L>::col_step(int model, int op, const Geom& g, const Phys& p, const 
       const bool one = all && Blk<L>::NB == 1 && g.kcl % 64 == 0;
       const dim3 gr = one ? dim3(3 * g.kcl) : dim3(col_blocks<L>(g), nfl);
       if (a.stream)
-        hipLaunchKernelGGL((k_col_step_fab3_rsw<L, true>), gr, blk, sh, s, g, p, a, Mf, Minv, tw, one ? -1 : f0);
+        SW_LAUNCH((k_col_step_fab3_rsw<L, true>), gr, blk, sh, s, g, p, a, Mf, Minv, tw, one ? -1 : f0);
       else
-        hipLaunchKernelGGL((k_col_step_fab3_rsw<L, false>), gr, blk, sh, s, g, p, a, Mf, Minv, tw, one ? -1 : f0);
+        SW_LAUNCH((k_col_step_fab3_rsw<L, false>), gr, blk, sh, s, g, p, a, Mf, Minv, tw, one ? -1 : f0);
     } else if (op == OP_IFMAB3) SW_CS(MODEL_RSW, OP_IFMAB3);
     else SW_CS(MODEL_RSW, OP_RK4);
   } else {
@@ -3462,10 +3462,10 @@ void LenOps<L>::col_fwd_step(int model, int op, const Geom& g, const Phys& p, co
 #define SW_FS(M, O)                                                                                         \
   do {                                                                                                      \
     if (lds) {                                                                                              \
-      if (a.stream) hipLaunchKernelGGL((k_col_fwd_step_lds<M, L, O, true>), grid, blk, sh, s, g, p, a, Mf, tw); \
-      else hipLaunchKernelGGL((k_col_fwd_step_lds<M, L, O, false>), grid, blk, sh, s, g, p, a, Mf, tw);        \
-    } else if (a.stream) hipLaunchKernelGGL((k_col_step<M, L, O, false, true>), grid, blk, sh, s, g, p, a, Mf, nullptr, tw); \
-    else hipLaunchKernelGGL((k_col_step<M, L, O, false, false>), grid, blk, sh, s, g, p, a, Mf, nullptr, tw);        \
+      if (a.stream) SW_LAUNCH((k_col_fwd_step_lds<M, L, O, true>), grid, blk, sh, s, g, p, a, Mf, tw); \
+      else SW_LAUNCH((k_col_fwd_step_lds<M, L, O, false>), grid, blk, sh, s, g, p, a, Mf, tw);        \
+    } else if (a.stream) SW_LAUNCH((k_col_step<M, L, O, false, true>), grid, blk, sh, s, g, p, a, Mf, nullptr, tw); \
+    else SW_LAUNCH((k_col_step<M, L, O, false, false>), grid, blk, sh, s, g, p, a, Mf, nullptr, tw);        \
   } while (0)
   if (model == MODEL_RSW) {
     if (op == OP_IFMAB3) SW_FS(MODEL_RSW, OP_IFMAB3);
@@ -3535,11 +3535,11 @@ void launch_col_fwd_alias(int model, const Geom& g, const Geom& ga, int region, 
 }
 void launch_scatter_modes(int nf, const Geom& ga, const double2* cmp, double2* full, hipStream_t s) {
   if (ga.cfield <= 0 || ga.kcn <= 0) return;
-  hipLaunchKernelGGL(k_scatter_modes, dim3((unsigned)((ga.cfield + 255) / 256)), dim3(256), 0, s, ga, nf, cmp, full);
+  SW_LAUNCH(k_scatter_modes, dim3((unsigned)((ga.cfield + 255) / 256)), dim3(256), 0, s, ga, nf, cmp, full);
 }
 void launch_gather_modes(int nf, const Geom& ga, const double2* full, double2* cmp, hipStream_t s) {
   if (ga.cfield <= 0 || ga.kcn <= 0) return;
-  hipLaunchKernelGGL(k_gather_modes, dim3((unsigned)((ga.cfield + 255) / 256)), dim3(256), 0, s, ga, nf, full, cmp);
+  SW_LAUNCH(k_gather_modes, dim3((unsigned)((ga.cfield + 255) / 256)), dim3(256), 0, s, ga, nf, full, cmp);
 }
 int row_lines_per_block(int model, int log2nx) {
   int nb = 1;
@@ -3582,8 +3582,8 @@ void launch_step_elem(int nf, int op, const Geom& g, const Phys& p, const StepPt
                       const double2* N, double2* xs, hipStream_t s) {
 #define SW_SE(F, O)                                                                                \
   do {                                                                                             \
-    if (a.stream) hipLaunchKernelGGL((k_step_elem<F, O, true>), mode_grid(g), dim3(256), 0, s, g, p, a, N, xs); \
-    else hipLaunchKernelGGL((k_step_elem<F, O, false>), mode_grid(g), dim3(256), 0, s, g, p, a, N, xs);       \
+    if (a.stream) SW_LAUNCH((k_step_elem<F, O, true>), mode_grid(g), dim3(256), 0, s, g, p, a, N, xs); \
+    else SW_LAUNCH((k_step_elem<F, O, false>), mode_grid(g), dim3(256), 0, s, g, p, a, N, xs);       \
   } while (0)
   if (nf == 4) {
     SW_SE(4, OP_ETDRK4);
@@ -3613,30 +3613,30 @@ static __global__ void __launch_bounds__(256) k_assemble(Geom g, Phys p, StepPtr
   store_vec<NF>(N, g.cfield, i, n);
 }
 void launch_assemble_terms(int nf, const Geom& g, const Phys& p, const StepPtrs& a, double2* N, hipStream_t s) {
-  if (nf == 4) hipLaunchKernelGGL((k_assemble<4>), mode_grid(g), dim3(256), 0, s, g, p, a, N);
-  else if (nf == 3) hipLaunchKernelGGL((k_assemble<3>), mode_grid(g), dim3(256), 0, s, g, p, a, N);
-  else hipLaunchKernelGGL((k_assemble<2>), mode_grid(g), dim3(256), 0, s, g, p, a, N);
+  if (nf == 4) SW_LAUNCH((k_assemble<4>), mode_grid(g), dim3(256), 0, s, g, p, a, N);
+  else if (nf == 3) SW_LAUNCH((k_assemble<3>), mode_grid(g), dim3(256), 0, s, g, p, a, N);
+  else SW_LAUNCH((k_assemble<2>), mode_grid(g), dim3(256), 0, s, g, p, a, N);
 }
 
 void launch_gather(int nf, const Geom& g, const double2* full, double2* cmp, hipStream_t s) {
   const long long n = (long long)g.kcn * g.Lr * nf;
   if (n == 0) return;
-  hipLaunchKernelGGL(k_gather, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g, nf, full, cmp);
+  SW_LAUNCH(k_gather, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g, nf, full, cmp);
 }
 
 void launch_scatter(int nf, const Geom& g, int lo, int hi, const double2* cmp, double2* full, hipStream_t s) {
   const long long n = (long long)(hi - lo) * g.nl * nf;
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_scatter, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g, nf, lo, hi, cmp, full);
+  SW_LAUNCH(k_scatter, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g, nf, lo, hi, cmp, full);
 }
 
 void launch_nan_check(int nf, const Geom& g, const double2* cmp, int* flag, hipStream_t s) {
-  hipLaunchKernelGGL(k_nan_check, mode_grid(g), dim3(256), 0, s, g, nf, cmp, flag);
+  SW_LAUNCH(k_nan_check, mode_grid(g), dim3(256), 0, s, g, nf, cmp, flag);
 }
 
 void launch_make_spec(int model, int fid, const Geom& g, const Phys& p, const double2* sol,
                       double2* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_make_spec, mode_grid(g), dim3(256), 0, s, g, p, model, fid, sol, out);
+  SW_LAUNCH(k_make_spec, mode_grid(g), dim3(256), 0, s, g, p, model, fid, sol, out);
 }
 
 void launch_col_inv1(const Geom& g, const double2* X, double2* M, const double2* tw_y, hipStream_t s) {
@@ -3649,15 +3649,15 @@ void launch_row_c2r1(const Geom& g, const double2* M, double* out, const double2
 
 void launch_energy_cols(int model, const Geom& g, const Phys& p, const double2* sol, double* cols,
                         hipStream_t s) {
-  hipLaunchKernelGGL(k_energy_cols, dim3(g.kcl), dim3(256), 0, s, g, p, model, sol, cols);
+  SW_LAUNCH(k_energy_cols, dim3(g.kcl), dim3(256), 0, s, g, p, model, sol, cols);
 }
 
 void launch_energy_final(const double* cols, int ncols, double* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_energy_final, dim3(1), dim3(64), 0, s, cols, ncols, out);
+  SW_LAUNCH(k_energy_final, dim3(1), dim3(64), 0, s, cols, ncols, out);
 }
 
 void launch_absmax(const double* f, long long n, unsigned long long* out, int sgn, hipStream_t s) {
-  hipLaunchKernelGGL(k_absmax, dim3(1024), dim3(256), 0, s, f, n, out, sgn);
+  SW_LAUNCH(k_absmax, dim3(1024), dim3(256), 0, s, f, n, out, sgn);
 }
 
 // caller-buffer precision (sw_config.precision = SW_PREC_F32): one rounding
@@ -3671,14 +3671,14 @@ static __global__ void k_narrow(const double* __restrict__ in, float* __restrict
     out[i] = (float)in[i];
 }
 void launch_widen(const float* in, double* out, long long n, hipStream_t s) {
-  hipLaunchKernelGGL(k_widen, dim3(2048), dim3(256), 0, s, in, out, n);
+  SW_LAUNCH(k_widen, dim3(2048), dim3(256), 0, s, in, out, n);
 }
 void launch_narrow(const double* in, float* out, long long n, hipStream_t s) {
-  hipLaunchKernelGGL(k_narrow, dim3(2048), dim3(256), 0, s, in, out, n);
+  SW_LAUNCH(k_narrow, dim3(2048), dim3(256), 0, s, in, out, n);
 }
 
 void launch_etd_coeffs(const Geom& g, const Phys& p, double* etd, hipStream_t s) {
-  hipLaunchKernelGGL(k_etd_coeffs, mode_grid(g), dim3(256), 0, s, g, p, etd);
+  SW_LAUNCH(k_etd_coeffs, mode_grid(g), dim3(256), 0, s, g, p, etd);
 }
 
 #endif  // SW_PART == 0

@@ -1,6 +1,8 @@
 """CPU model of the generic engine's line transform (csrc/sw_generic.hip
 fft_lds): the radix sequence of `radices` and the mixed-radix Stockham DIF
-index algebra — y[q + s(rp + u)] = ω_len^(pu) Σ_t x[q + s(p + tm)] ω_r^(tu) —
+index algebra — y[q + s(rp + u)] = ω_len^(pu) Σ_t x[q + s(p + tm)] ω_r^(tu),
+the r-point DFTs as dft_small writes them and ω_len^(pu) from the n-point
+table (k_twiddles) —
 checked against numpy's FFT in both directions on the grids the engine
 accepts (2^a·3^b·5^c, even, 16 … 4096), and the c2r row rule (the DC and
 Nyquist bins' imaginary parts dropped, numpy's irfft convention)."""
@@ -20,19 +22,42 @@ def radices(n):
     return out if n == 1 else None
 
 
+def dft_small(v, d):
+    """sw_generic.hip dft_small: the r-point DFTs as written there (exact ±1/±i
+    for r = 2, 4; the radix-3/5 constants); v: [r, ...] complex, d = DIR"""
+    r = len(v)
+    rot = lambda a: 1j * d * a  # noqa: E731
+    if r == 4:
+        a, b, c, e = v[0] + v[2], v[0] - v[2], v[1] + v[3], rot(v[1] - v[3])
+        return np.stack([a + c, b + e, a - c, b - e])
+    if r == 2:
+        return np.stack([v[0] + v[1], v[0] - v[1]])
+    if r == 3:
+        s3 = 0.86602540378443864676
+        sm, df = v[1] + v[2], v[1] - v[2]
+        t, e = v[0] - 0.5 * sm, rot(s3 * df)
+        return np.stack([v[0] + sm, t + e, t - e])
+    c1, c2, s1, s2 = 0.30901699437494742410, -0.80901699437494742410, 0.95105651629515357212, 0.58778525229247312917
+    p1, d1, p2, d2 = v[1] + v[4], v[1] - v[4], v[2] + v[3], v[2] - v[3]
+    a1, a2 = v[0] + c1 * p1 + c2 * p2, v[0] + c2 * p1 + c1 * p2
+    b1, b2 = rot(s1 * d1 + s2 * d2), rot(s2 * d1 - s1 * d2)
+    return np.stack([v[0] + p1 + p2, a1 + b1, a2 + b2, a2 - b2, a1 - b1])
+
+
 def fft_lds(x, d):
     n = len(x)
+    tw = np.exp(-2j * np.pi * np.arange(n) / n)  # k_twiddles: the forward table, conj for d = +1
+    if d > 0:
+        tw = tw.conj()
     X, Y = x.astype(complex).copy(), np.zeros(n, complex)
     L, s = n, 1
     for r in radices(n):
         m = L // r
         i = np.arange(m * s)
         p, q = i // s, i % s
-        v = np.stack([X[q + s * (p + t * m)] for t in range(r)])
+        v = dft_small(np.stack([X[q + s * (p + t * m)] for t in range(r)]), d)
         for u in range(r):
-            wr = np.exp(d * 2j * np.pi * ((np.arange(r) * u) % r) / r)
-            a = (v * wr[:, None]).sum(0)
-            Y[q + s * (r * p + u)] = a * np.exp(d * 2j * np.pi * ((p * u) % L) / L)
+            Y[q + s * (r * p + u)] = v[u] * tw[p * u * (n // L)]
         X, Y = Y, X
         L, s = m, s * r
     return X
