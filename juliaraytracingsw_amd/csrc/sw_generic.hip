@@ -5,6 +5,7 @@
 #include "sw_fft.hpp"
 
 #include <cmath>
+#include <cstdlib>
 #include <string>
 
 namespace sw {
@@ -130,11 +131,12 @@ __device__ double2* fft_lds(double2* x, double2* y, const Rad& R, int B, const d
 // complex lines of R.n points, B per block (adjacent kr: one row of B points
 // per load): element e of line kr of field f at data[f·fstride + kr + e·es]
 template <int DIR>
-__global__ void __launch_bounds__(256) k_lines(double2* __restrict__ data, Rad R, int B, int nkr, long long fstride,
+__global__ void __launch_bounds__(1024) k_lines(double2* __restrict__ data, Rad R, int B, int nkr, long long fstride,
                                                long long es, const double2* __restrict__ tw) {
   extern __shared__ double2 lds[];
   const int n = R.n, groups = (nkr + B - 1) / B;
-  double2 *x = lds, *y = lds + B * n;
+  double2 *twl = lds, *x = lds + n, *y = x + B * n;
+  for (int j = threadIdx.x; j < n; j += blockDim.x) twl[j] = tw[j];
   const int f = blockIdx.x / groups, kr0 = (blockIdx.x - f * groups) * B;
   const int nv = min(B, nkr - kr0);
   double2* d = data + f * fstride + kr0;
@@ -143,7 +145,7 @@ __global__ void __launch_bounds__(256) k_lines(double2* __restrict__ data, Rad R
     x[b * n + e] = b < nv ? d[e * es + b] : zero2();
   }
   __syncthreads();
-  const double2* z = fft_lds<DIR>(x, y, R, B, tw);
+  const double2* z = fft_lds<DIR>(x, y, R, B, twl);
   for (int idx = threadIdx.x; idx < B * n; idx += blockDim.x) {
     const int e = idx / B, b = idx - e * B;
     if (b < nv) d[e * es + b] = z[b * n + e];
@@ -153,11 +155,12 @@ __global__ void __launch_bounds__(256) k_lines(double2* __restrict__ data, Rad R
 // c2r along x of B stored rows (FF's irfft rule: c2c along l done, then c2r
 // along x with the DC and Nyquist bins' imaginary parts dropped, numpy's
 // convention): spec rows [nkr] -> phys rows [nx] × scale
-__global__ void __launch_bounds__(256) k_c2r_rows(const double2* __restrict__ spec, double* __restrict__ phys, Rad R,
+__global__ void __launch_bounds__(1024) k_c2r_rows(const double2* __restrict__ spec, double* __restrict__ phys, Rad R,
                                                   int B, int nkr, double scale, const double2* __restrict__ tw) {
   extern __shared__ double2 lds[];
   const int n = R.n;
-  double2 *x = lds, *y = lds + B * n;
+  double2 *twl = lds, *x = lds + n, *y = x + B * n;
+  for (int j = threadIdx.x; j < n; j += blockDim.x) twl[j] = tw[j];
   const long long row0 = (long long)blockIdx.x * B;
   const double2* a = spec + row0 * nkr;
   for (int idx = threadIdx.x; idx < B * n; idx += blockDim.x) {
@@ -173,22 +176,23 @@ __global__ void __launch_bounds__(256) k_c2r_rows(const double2* __restrict__ sp
     x[idx] = z;
   }
   __syncthreads();
-  const double2* z = fft_lds<+1>(x, y, R, B, tw);
+  const double2* z = fft_lds<+1>(x, y, R, B, twl);
   double* o = phys + row0 * n;
   for (int idx = threadIdx.x; idx < B * n; idx += blockDim.x) o[idx] = z[idx].x * scale;
 }
 
 // r2c along x of B rows: phys rows [nx] -> spec rows [nkr] (unnormalised)
-__global__ void __launch_bounds__(256) k_r2c_rows(const double* __restrict__ phys, double2* __restrict__ spec, Rad R,
+__global__ void __launch_bounds__(1024) k_r2c_rows(const double* __restrict__ phys, double2* __restrict__ spec, Rad R,
                                                   int B, int nkr, const double2* __restrict__ tw) {
   extern __shared__ double2 lds[];
   const int n = R.n;
-  double2 *x = lds, *y = lds + B * n;
+  double2 *twl = lds, *x = lds + n, *y = x + B * n;
+  for (int j = threadIdx.x; j < n; j += blockDim.x) twl[j] = tw[j];
   const long long row0 = (long long)blockIdx.x * B;
   const double* a = phys + row0 * n;
   for (int idx = threadIdx.x; idx < B * n; idx += blockDim.x) x[idx] = make_double2(a[idx], 0.0);
   __syncthreads();
-  const double2* z = fft_lds<-1>(x, y, R, B, tw);
+  const double2* z = fft_lds<-1>(x, y, R, B, twl);
   double2* o = spec + row0 * nkr;
   for (int idx = threadIdx.x; idx < B * nkr; idx += blockDim.x) {
     const int b = idx / nkr, k = idx - b * nkr;
@@ -268,9 +272,46 @@ __global__ void k_assemble(Geom g, Phys p, const double2* __restrict__ X, const 
 //   RHS = N + L x;  1: acc = RHS/6, x' = sol + dt/2 RHS;  2: acc += RHS/3,
 //   x' = sol + dt/2 RHS;  3: acc += RHS/3, x' = sol + dt RHS;
 //   4: sol = (sol + dt (acc + RHS/6)) · filter
+// one field of one live mode (o = f·F + i): X the stage input, writes acc
+// and the next stage input xo (stages 1-3) or the new state (stage 4);
+// returns the stored new state at stage 4 (for the NaN check)
+__device__ __forceinline__ double2 frk4_mode(const Geom& g, const Phys& p, int stage, long long o, double k, double ll,
+                                             double D, double2 Xv, const double2 nv, double2* __restrict__ sol,
+                                             double2* __restrict__ xo, double2* __restrict__ acc) {
+#pragma clang fp contract(off)
+  const double dt = p.dt;
+  const cplx X = cx(Xv.x, Xv.y);
+  const cplx u = cx(sol[o].x, sol[o].y);
+  const cplx rhs = cx(nv.x + D * X.re, nv.y + D * X.im);
+  if (stage < 4) {
+    const double h = stage == 3 ? dt : dt / 2;
+    const cplx r = stage == 1 ? cx(rhs.re / 6, rhs.im / 6) : cx(rhs.re / 3, rhs.im / 3);
+    const cplx a = stage == 1 ? r : cx(acc[o].x + r.re, acc[o].y + r.im);
+    acc[o] = make_double2(a.re, a.im);
+    xo[o] = make_double2(u.re + h * rhs.re, u.im + h * rhs.im);
+    return zero2();
+  }
+  const double filt = filter_value(g, p, k, ll);
+  const cplx s6 = cx(acc[o].x + rhs.re / 6, acc[o].y + rhs.im / 6);
+  const cplx r = cx(u.re + dt * s6.re, u.im + dt * s6.im);
+  const double2 v = make_double2(r.re * filt, r.im * filt);
+  sol[o] = v;
+  return v;
+}
+
+__device__ __forceinline__ void note_bad(int* nanflag, bool bad) {
+  if (!nanflag) return;
+  const unsigned long long m = __ballot(bad);
+  if (m != 0ull && (int)__lane_id() == __ffsll((long long)m) - 1)
+    __hip_atomic_store(nanflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// FF FilteredRK4 stage `stage` per mode (op_frk4's arithmetic, L = -ν K^(2nν)):
+//   RHS = N + L x;  1: acc = RHS/6, x' = sol + dt/2 RHS;  2: acc += RHS/3,
+//   x' = sol + dt/2 RHS;  3: acc += RHS/3, x' = sol + dt RHS;
+//   4: sol = (sol + dt (acc + RHS/6)) · filter
 __global__ void k_frk4(Geom g, Phys p, int stage, double2* __restrict__ sol, double2* __restrict__ xs,
                        double2* __restrict__ acc, const double2* __restrict__ N, int* nanflag) {
-#pragma clang fp contract(off)
   const long long F = (long long)g.nl * g.nkr;
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   bool bad = false;
@@ -279,33 +320,152 @@ __global__ void k_frk4(Geom g, Phys p, int stage, double2* __restrict__ sol, dou
     if (live_mode(g, l, kr)) {
       const double k = kr * g.mk, ll = lwav(g, l);
       const double D = -(p.nu * ipow(k * k + ll * ll, p.nnu));
-      const double dt = p.dt;
       for (int f = 0; f < 2; ++f) {
         const long long o = f * F + i;
-        const cplx X = stage == 1 ? cx(sol[o].x, sol[o].y) : cx(xs[o].x, xs[o].y);
-        const cplx u = cx(sol[o].x, sol[o].y);
-        const cplx rhs = cx(N[o].x + D * X.re, N[o].y + D * X.im);
-        if (stage < 4) {
-          const double h = stage == 3 ? dt : dt / 2;
-          const cplx r = stage == 1 ? cx(rhs.re / 6, rhs.im / 6) : cx(rhs.re / 3, rhs.im / 3);
-          const cplx a = stage == 1 ? r : cx(acc[o].x + r.re, acc[o].y + r.im);
-          acc[o] = make_double2(a.re, a.im);
-          xs[o] = make_double2(u.re + h * rhs.re, u.im + h * rhs.im);
-        } else {
-          const double filt = filter_value(g, p, k, ll);
-          const cplx s6 = cx(acc[o].x + rhs.re / 6, acc[o].y + rhs.im / 6);
-          const cplx r = cx(u.re + dt * s6.re, u.im + dt * s6.im);
-          sol[o] = make_double2(r.re * filt, r.im * filt);
-          bad = bad || !isfinite(r.re * filt) || !isfinite(r.im * filt);
-        }
+        const double2 X = stage == 1 ? sol[o] : xs[o];
+        const double2 r = frk4_mode(g, p, stage, o, k, ll, D, X, N[o], sol, xs, acc);
+        bad = bad || !isfinite(r.x) || !isfinite(r.y);
       }
     }
   }
-  if (nanflag) {
-    const unsigned long long m = __ballot(bad);
-    if (m != 0ull && (int)__lane_id() == __ffsll((long long)m) - 1)
-      __hip_atomic_store(nanflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  note_bad(nanflag, bad);
+}
+
+// ---------------------------------------------------------------- fused step
+// Three kernels per FilteredRK4 stage (Engine::fused), the power-of-two
+// engine's col_inv / row / col_step split on the generic transforms:
+//   k_gcol_inv   one spectral field (q_j, u_j, v_j of X, dealiased) per block,
+//                formed on load, inverse transform along l;
+//   k_grow       one row: the six fields' c2r as three complex lines
+//                (q₁ + iu₁, v₁ + iq₂, u₂ + iv₂), the products, their r2c as
+//                two complex lines ((U₁+u₁)q₁ + i v₁q₁, (U₂+u₂)q₂ + i v₂q₂)
+//                split by Hermitian symmetry;
+//   k_gcol_fwd   one layer per block: forward transforms of its two product
+//                fields along l, N_j (k_assemble's arithmetic) and the stage
+//                update (frk4_mode) per live mode.
+// X is read by both layers' blocks, so stages write the next input to the
+// other xs buffer (ping-pong).
+__global__ void __launch_bounds__(1024) k_gcol_inv(Geom g, Phys p, const double2* __restrict__ X,
+                                                  double2* __restrict__ spec, Rad R, int B,
+                                                  const double2* __restrict__ tw) {
+  extern __shared__ double2 lds[];
+  const int n = R.n, groups = (g.nkr + B - 1) / B;
+  double2 *twl = lds, *x = lds + n, *y = x + B * n;
+  for (int j = threadIdx.x; j < n; j += blockDim.x) twl[j] = tw[j];
+  const int fid = blockIdx.x / groups, kr0 = (blockIdx.x - fid * groups) * B;
+  const int layer = fid / 3, comp = fid - 3 * layer;
+  const long long F = (long long)g.nl * g.nkr;
+  for (int idx = threadIdx.x; idx < B * n; idx += blockDim.x) {
+    const int l = idx / B, b = idx - l * B, kr = kr0 + b;
+    double2 v = zero2();
+    if (kr < g.nkr && live_mode(g, l, kr)) {
+      const long long i = (long long)l * g.nkr + kr;
+      const double2 q1 = X[i], q2 = X[F + i];
+      if (comp == 0) {
+        v = layer ? q2 : q1;
+      } else {
+        const double k = kr * g.mk, ll = lwav(g, l), K2 = k * k + ll * ll;
+        double2 ps;
+        qg_psi(p, K2, q1.x, q1.y, q2.x, q2.y, layer, ps.x, ps.y);
+        v = comp == 1 ? cmul_i(ps, -ll) : cmul_i(ps, k);
+      }
+    }
+    x[b * n + l] = v;
   }
+  __syncthreads();
+  const double2* z = fft_lds<+1>(x, y, R, B, twl);
+  double2* d = spec + fid * F + kr0;
+  const int nv = min(B, g.nkr - kr0);
+  for (int idx = threadIdx.x; idx < B * n; idx += blockDim.x) {
+    const int l = idx / B, b = idx - l * B;
+    if (b < nv) d[(long long)l * g.nkr + b] = z[b * n + l];
+  }
+}
+
+// c2r of two Hermitian half rows A, B (FF/numpy's rule: the DC and Nyquist
+// bins' imaginary parts dropped) as one complex line: Z_k = A_k + i B_k over
+// the full length, IFFT(Z) = a + i b
+__device__ __forceinline__ double2 pack_c2r(const double2* __restrict__ A, const double2* __restrict__ Bv, int k,
+                                            int n) {
+  if (k <= n / 2) {
+    double2 a = A[k], b = Bv[k];
+    if (k == 0 || k == n / 2) a.y = b.y = 0.0;
+    return make_double2(a.x - b.y, a.y + b.x);
+  }
+  const double2 a = A[n - k], b = Bv[n - k];
+  return make_double2(a.x + b.y, b.x - a.y);
+}
+
+__global__ void __launch_bounds__(1024) k_grow(Geom g, Phys p, double2* __restrict__ spec, Rad R, double scale,
+                                              const double2* __restrict__ tw) {
+  extern __shared__ double2 lds[];
+  const int n = R.n, row = blockIdx.x;
+  const long long F = (long long)g.nl * g.nkr;
+  double2 *twl = lds, *x = lds + n, *y = x + 3 * n;
+  for (int j = threadIdx.x; j < n; j += blockDim.x) twl[j] = tw[j];
+  const double2* S = spec + (long long)row * g.nkr;
+  for (int idx = threadIdx.x; idx < 3 * n; idx += blockDim.x) {
+    const int c = idx / n, k = idx - c * n;  // lines: (q1, u1), (v1, q2), (u2, v2) = fields (0,1), (2,3), (4,5)
+    x[idx] = pack_c2r(S + (2 * c) * F, S + (2 * c + 1) * F, k, n);
+  }
+  __syncthreads();
+  double2* z = fft_lds<+1>(x, y, R, 3, twl);
+  double2* w = z == x ? y : x;  // the free buffer
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    const double2 a = z[k], b = z[n + k], c = z[2 * n + k];
+    const double q1 = a.x * scale, u1 = a.y * scale, v1 = b.x * scale, q2 = b.y * scale;
+    const double u2 = c.x * scale, v2 = c.y * scale;
+    w[k] = make_double2((u1 + p.U1) * q1, v1 * q1);
+    w[n + k] = make_double2((u2 + p.U2) * q2, v2 * q2);
+  }
+  __syncthreads();
+  const double2* Z = fft_lds<-1>(w, z, R, 2, twl);
+  double2* O = spec + (long long)row * g.nkr;
+  for (int idx = threadIdx.x; idx < 2 * g.nkr; idx += blockDim.x) {
+    const int c = idx / g.nkr, k = idx - c * g.nkr;
+    const double2 zk = Z[c * n + k], zm = Z[c * n + (k == 0 ? 0 : n - k)];
+    // P = (Z_k + conj Z_{n-k})/2, Q = (Z_k - conj Z_{n-k})/(2i)
+    O[(2 * c) * F + k] = make_double2(0.5 * (zk.x + zm.x), 0.5 * (zk.y - zm.y));
+    O[(2 * c + 1) * F + k] = make_double2(0.5 * (zk.y + zm.y), -0.5 * (zk.x - zm.x));
+  }
+}
+
+__global__ void __launch_bounds__(1024) k_gcol_fwd(Geom g, Phys p, int stage, const double2* X,  // (= sol at stage 1)
+                                                  const double2* __restrict__ spec, double2* __restrict__ sol,
+                                                  double2* __restrict__ xo, double2* __restrict__ acc, Rad R, int B,
+                                                  const double2* __restrict__ tw, int* nanflag) {
+  extern __shared__ double2 lds[];
+  const int n = R.n, groups = (g.nkr + B - 1) / B;
+  double2 *twl = lds, *x = lds + n, *y = x + 2 * B * n;
+  for (int j = threadIdx.x; j < n; j += blockDim.x) twl[j] = tw[j];
+  const int j = blockIdx.x / groups, kr0 = (blockIdx.x - j * groups) * B;
+  const long long F = (long long)g.nl * g.nkr;
+  const int nv = min(B, g.nkr - kr0);
+  // lines 2b: (U_j + u_j) q_j, 2b + 1: v_j q_j of column kr0 + b
+  for (int idx = threadIdx.x; idx < 2 * B * n; idx += blockDim.x) {
+    const int l = idx / (2 * B), r = idx - l * (2 * B), b = r >> 1, c = r & 1;
+    x[r * n + l] = b < nv ? spec[(2 * j + c) * F + (long long)l * g.nkr + kr0 + b] : zero2();
+  }
+  __syncthreads();
+  const double2* z = fft_lds<-1>(x, y, R, 2 * B, twl);
+  bool bad = false;
+  for (int idx = threadIdx.x; idx < B * n; idx += blockDim.x) {
+    const int l = idx / B, b = idx - l * B, kr = kr0 + b;
+    if (b >= nv || !live_mode(g, l, kr)) continue;
+    const long long i = (long long)l * g.nkr + kr, o = j * F + i;
+    const double k = kr * g.mk, ll = lwav(g, l), K2 = k * k + ll * ll;
+    const double2 q1 = X[i], q2 = X[F + i];
+    double2 ps;
+    qg_psi(p, K2, q1.x, q1.y, q2.x, q2.y, j, ps.x, ps.y);
+    const double Qy = j ? p.Qy2 : p.Qy1;
+    double2 r = cscale(cmul_i(ps, k), -Qy);
+    r = csub(r, cadd(cmul_i(z[(2 * b) * n + l], k), cmul_i(z[(2 * b + 1) * n + l], ll)));
+    if (j == 1) r = cadd(r, cscale(ps, p.mu * K2));
+    const double D = -(p.nu * ipow(K2, p.nnu));
+    const double2 v = frk4_mode(g, p, stage, o, k, ll, D, j ? q2 : q1, r, sol, xo, acc);
+    bad = bad || !isfinite(v.x) || !isfinite(v.y);
+  }
+  if (stage == 4) note_bad(nanflag, bad);
 }
 
 __global__ void k_dealias(Geom g, double2* __restrict__ X) {
@@ -413,8 +573,9 @@ int create(Engine*& e, const sw_config& k, const Phys& p, const Geom& g, double2
   e->sol = sol;
   e->nradx = radices(k.nx, e->radx);
   e->nrady = radices(k.ny, e->rady);
-  if (!e->nradx || !e->nrady) {
-    err = "generic grids: nx, ny even, 16 ... 4096, of the form 2^a 3^b 5^c";
+  // one line and its ping-pong partner plus the twiddle table in 160 KB of LDS
+  if (!e->nradx || !e->nrady || k.nx > 3328 || k.ny > 3328) {
+    err = "generic grids: nx, ny even, 16 ... 3328, of the form 2^a 3^b 5^c";
     return SW_E_INVALID;
   }
   const size_t F = (size_t)g.nl * g.nkr, NP = (size_t)g.nx * g.ny;
@@ -432,13 +593,19 @@ int create(Engine*& e, const sw_config& k, const Phys& p, const Geom& g, double2
   // rows per block: B·nx ≤ 2048 with B dividing ny (ny is even, B a power of two)
   e->bx = lines_per_block(g.nx);
   while (g.ny % e->bx) e->bx /= 2;
+  // the fused stages (k_grow holds 3 complex lines of nx points twice: ≤ 96 KB
+  // of LDS; k_gcol_fwd 2 lines of ny): nx, ny ≤ 1024; SW_GEN_FUSED=0 forces
+  // the separate passes (tests run both)
+  const char* fe = std::getenv("SW_GEN_FUSED");
+  e->fused = g.nx <= 1024 && g.ny <= 1024 && !(fe && fe[0] == '0');
+  if (e->fused && hipMalloc((void**)&e->xs2, 2 * F * sizeof(double2)) != hipSuccess) return SW_E_NOMEM;
   return SW_OK;
 }
 
 void destroy(Engine* e) {
   if (!e) return;
-  for (void* b : {(void*)e->xs, (void*)e->acc, (void*)e->N, (void*)e->spec, (void*)e->phys, (void*)e->cols,
-                  (void*)e->twx, (void*)e->twy})
+  for (void* b : {(void*)e->xs, (void*)e->xs2, (void*)e->acc, (void*)e->N, (void*)e->spec, (void*)e->phys,
+                  (void*)e->cols, (void*)e->twx, (void*)e->twy})
     if (b) (void)hipFree(b);
   delete e;
 }
@@ -452,13 +619,23 @@ static int lines_per_block(int n) {
   return B;
 }
 
+// threads of a transform block: one per butterfly of its widest (radix-2)
+// stage over its lines, 64 … 1024 (small grids: the latency of each stage
+// is spread over more waves)
+static int blk_threads(int lines, int n) {
+  const int t = (lines * n / 2 + 63) / 64 * 64;
+  return t < 64 ? 64 : (t > 1024 ? 1024 : t);
+}
+
 static void inverse2d(Engine* e, double2* spec, int nf, double* phys) {
   const Geom& g = e->g;
   const Rad Ry = rad_of(e->rady, e->nrady, g.ny), Rx = rad_of(e->radx, e->nradx, g.nx);
   const int By = lines_per_block(g.ny), Bx = e->bx;
-  SW_LAUNCH(k_lines<+1>, dim3(nf * ((g.nkr + By - 1) / By)), dim3(256), 2 * By * g.ny * sizeof(double2), e->s, spec,
+  SW_LAUNCH(k_lines<+1>, dim3(nf * ((g.nkr + By - 1) / By)), dim3(blk_threads(By, g.ny)),
+            (2 * By + 1) * g.ny * sizeof(double2), e->s, spec,
             Ry, By, g.nkr, (long long)g.nl * g.nkr, (long long)g.nkr, e->twy);
-  SW_LAUNCH(k_c2r_rows, dim3(nf * g.ny / Bx), dim3(256), 2 * Bx * g.nx * sizeof(double2), e->s, spec, phys, Rx, Bx,
+  SW_LAUNCH(k_c2r_rows, dim3(nf * g.ny / Bx), dim3(blk_threads(Bx, g.nx)), (2 * Bx + 1) * g.nx * sizeof(double2), e->s,
+            spec, phys, Rx, Bx,
             g.nkr, 1.0 / ((double)g.nx * (double)g.ny), e->twx);
 }
 
@@ -467,9 +644,11 @@ static void forward2d(Engine* e, const double* phys, int nf, double2* spec) {
   const Geom& g = e->g;
   const Rad Ry = rad_of(e->rady, e->nrady, g.ny), Rx = rad_of(e->radx, e->nradx, g.nx);
   const int By = lines_per_block(g.ny), Bx = e->bx;
-  SW_LAUNCH(k_r2c_rows, dim3(nf * g.ny / Bx), dim3(256), 2 * Bx * g.nx * sizeof(double2), e->s, phys, spec, Rx, Bx,
+  SW_LAUNCH(k_r2c_rows, dim3(nf * g.ny / Bx), dim3(blk_threads(Bx, g.nx)), (2 * Bx + 1) * g.nx * sizeof(double2), e->s,
+            phys, spec, Rx, Bx,
             g.nkr, e->twx);
-  SW_LAUNCH(k_lines<-1>, dim3(nf * ((g.nkr + By - 1) / By)), dim3(256), 2 * By * g.ny * sizeof(double2), e->s, spec,
+  SW_LAUNCH(k_lines<-1>, dim3(nf * ((g.nkr + By - 1) / By)), dim3(blk_threads(By, g.ny)),
+            (2 * By + 1) * g.ny * sizeof(double2), e->s, spec,
             Ry, By, g.nkr, (long long)g.nl * g.nkr, (long long)g.nkr, e->twy);
 }
 
@@ -483,8 +662,35 @@ void calcN(Engine* e, const double2* X, double2* N) {
   SW_LAUNCH(k_assemble, modes_grid(g), dim3(256), 0, e->s, g, e->p, X, e->spec, N);
 }
 
+// the fused stage sequence (k_gcol_inv, k_grow, k_gcol_fwd; Engine::fused)
+static void step_fused(Engine* e, int* nanflag) {
+  const Geom& g = e->g;
+  const Rad Ry = rad_of(e->rady, e->nrady, g.ny), Rx = rad_of(e->radx, e->nradx, g.nx);
+  const int Bi = lines_per_block(g.ny), Bf = Bi > 1 ? Bi / 2 : 1;
+  const int gi = (g.nkr + Bi - 1) / Bi, gf = (g.nkr + Bf - 1) / Bf;
+  const double scale = 1.0 / ((double)g.nx * (double)g.ny);
+  const double2* X = e->sol;
+  for (int stage = 1; stage <= 4; ++stage) {
+    // stage inputs: sol, xs, xs2, xs; the next input goes to the other buffer
+    double2* xo = stage == 4 ? nullptr : (stage & 1 ? e->xs : e->xs2);
+    SW_LAUNCH(k_gcol_inv, dim3(6 * gi), dim3(blk_threads(Bi, g.ny)), (2 * Bi + 1) * g.ny * sizeof(double2), e->s, g,
+              e->p, X, e->spec, Ry,
+              Bi, e->twy);
+    SW_LAUNCH(k_grow, dim3(g.ny), dim3(blk_threads(3, g.nx)), 7 * g.nx * sizeof(double2), e->s, g, e->p, e->spec, Rx,
+              scale, e->twx);
+    SW_LAUNCH(k_gcol_fwd, dim3(2 * gf), dim3(blk_threads(2 * Bf, g.ny)), (4 * Bf + 1) * g.ny * sizeof(double2), e->s, g,
+              e->p, stage, X, e->spec,
+              e->sol, xo, e->acc, Ry, Bf, e->twy, stage == 4 ? nanflag : nullptr);
+    X = xo;
+  }
+}
+
 void step(Engine* e, int* nanflag) {
   const Geom& g = e->g;
+  if (e->fused) {
+    step_fused(e, nanflag);
+    return;
+  }
   for (int stage = 1; stage <= 4; ++stage) {
     calcN(e, stage == 1 ? e->sol : e->xs, e->N);
     SW_LAUNCH(k_frk4, modes_grid(g), dim3(256), 0, e->s, g, e->p, stage, e->sol, e->xs, e->acc, e->N,

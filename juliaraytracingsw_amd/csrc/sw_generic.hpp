@@ -7,7 +7,7 @@
 // TwoLayerSimulation (GeophysicalFlows MultiLayerQG, 2 layers, FilteredRK4,
 // aliased_fraction = 0; VERDICT r05 missing #4).  This engine runs that
 // model/stepper pair on any even grid of 2^a·3^b·5^c points per side (16 …
-// 4096): mixed-radix (2, 3, 4, 5) Stockham line transforms in LDS, the
+// 3328): mixed-radix (2, 3, 4, 5) Stockham line transforms in LDS, the
 // state on the full (nkr, nl) array (Julia's prob.sol layout, the aliased
 // modes held at zero as libsw's default mode does), the calcN as the
 // reference's op sequence (simulation/TwoLayerSimulation.jl:37-47; GF
@@ -43,6 +43,8 @@ struct Engine {
   double2* twx = nullptr;   // forward twiddles exp(-2πi j/nx), j < nx
   double2* twy = nullptr;   // … along y
   int bx = 1;               // rows per block of the x transforms
+  bool fused = false;       // three kernels per stage (k_gcol_inv, k_grow, k_gcol_fwd)
+  double2* xs2 = nullptr;   // the fused stages' second stage-input buffer
 };
 
 int create(Engine*& e, const sw_config& k, const Phys& p, const Geom& g, double2* sol, hipStream_t s,

@@ -414,19 +414,27 @@ __host__ __device__ inline void exp_apply(const Phys& p, const RswExp& E, const 
 struct Qg2Exp {
   cplx E[2][2];
 };
-__host__ __device__ inline cplx csinhc_(cplx z) {  // sinh(z)/z
+// cosh z and sinh(z)/z: for |z| < 0.5 their Taylor series to z^20 (no
+// transcendental; the terms past it are < 1e-24), else from sinh/cosh of z.re
+// and sin/cos of z.im
+__host__ __device__ inline void ccosh_sinhc(cplx z, cplx& ch, cplx& sc) {
 #pragma clang fp contract(off)
-  if (hypot(z.re, z.im) < 0.5) {  // Σ z^(2n)/(2n+1)!, n <= 10
+  if (z.re * z.re + z.im * z.im < 0.25) {
     const cplx z2 = z * z;
-    cplx r = cx(1.0), t = cx(1.0);
+    cplx rs = cx(1.0), ts = cx(1.0), rc = cx(1.0), tc = cx(1.0);
     for (int n = 1; n <= 10; ++n) {
-      t = (1.0 / ((2.0 * n) * (2.0 * n + 1.0))) * (t * z2);
-      r = r + t;
+      ts = (1.0 / ((2.0 * n) * (2.0 * n + 1.0))) * (ts * z2);  // z^(2n)/(2n+1)!
+      tc = (1.0 / ((2.0 * n - 1.0) * (2.0 * n))) * (tc * z2);  // z^(2n)/(2n)!
+      rs = rs + ts;
+      rc = rc + tc;
     }
-    return r;
+    sc = rs;
+    ch = rc;
+    return;
   }
-  const cplx sh = cx(sinh(z.re) * cos(z.im), cosh(z.re) * sin(z.im));
-  return cdiv(sh, z);
+  const double shr = sinh(z.re), chr = cosh(z.re), sn = sin(z.im), cs = cos(z.im);
+  ch = cx(chr * cs, shr * sn);
+  sc = cdiv(cx(shr * cs, chr * sn), z);
 }
 __host__ __device__ inline Qg2Exp qg2_exp(const Phys& p, double k, double l, double tau) {
 #pragma clang fp contract(off)
@@ -436,9 +444,11 @@ __host__ __device__ inline Qg2Exp qg2_exp(const Phys& p, double k, double l, dou
   const cplx b00 = (0.5 * tau) * (L[0][0] - L[1][1]);
   const cplx b01 = tau * L[0][1], b10 = tau * L[1][0];
   const cplx d = csqrt_(b00 * b00 + b01 * b10);
-  const cplx em = cexp_(m);
-  const cplx ch = cx(cosh(d.re) * cos(d.im), sinh(d.re) * sin(d.im));
-  const cplx sc = csinhc_(d);
+  // tr L is real for the 2LQG operator (pv₂ = -pv₁, ∓kU): e^m without the
+  // sin/cos of 0 (cos 0 = 1 and sin 0 = 0 exactly)
+  const cplx em = m.im == 0.0 ? cx(exp(m.re), 0.0) : cexp_(m);
+  cplx ch, sc;
+  ccosh_sinhc(d, ch, sc);
   Qg2Exp X;
   X.E[0][0] = em * (ch + sc * b00);
   X.E[1][1] = em * (ch - sc * b00);

@@ -47,6 +47,25 @@ def test_generic_calcN_and_steps(n):
     prob.close()
 
 
+@pytest.mark.parametrize("n", [120, 384])
+def test_generic_separate_passes(n, monkeypatch):
+    """SW_GEN_FUSED=0: the separate-pass stages (k_prep … k_frk4, the path of
+    grids above 1024) against the oracle, and the fused stages (k_gcol_inv,
+    k_grow, k_gcol_fwd) against them."""
+    p, pr, prob = _pair(n)
+    monkeypatch.setenv("SW_GEN_FUSED", "0")
+    sep = sw_cases.libsw_problem(p)
+    monkeypatch.delenv("SW_GEN_FUSED")
+    sep.sol = pr.sol
+    pr.stepforward(5)
+    prob.stepforward(5)
+    sep.stepforward(5)
+    assert O.parity_error(sep.sol, pr.sol, pr.grid) < RTOL
+    assert O.parity_error(prob.sol, sep.sol, pr.grid) < 1e-12
+    prob.close()
+    sep.close()
+
+
 def test_generic_every_term_rectangular():
     """H₁ ≠ H₂, β, drag, hyperviscosity, the 2/3 rule, and nx ≠ ny (96 × 48)."""
     from juliaraytracingsw_amd import multilayer_qg as MLQG
