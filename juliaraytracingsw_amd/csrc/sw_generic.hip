@@ -94,6 +94,25 @@ __device__ __forceinline__ void dft_small(int r, double2 (&v)[5]) {
 // stride (1, r₀, …); ω_len^(p u) = tw[p u n/len] (p u < len).  Natural order
 // in and out; returns the buffer holding the result.  DIR = -1 forward
 // (unnormalised), +1 inverse.
+// one r-point butterfly (p, q) of a stage (len = r m, stride s)
+template <int DIR>
+__device__ __forceinline__ void bfly(const double2* __restrict__ xb, double2* __restrict__ yb, int r, int m, int s,
+                                     int step, int p, int q, const double2* __restrict__ tw) {
+  double2 v[5];
+#pragma unroll
+  for (int t = 0; t < 5; ++t)
+    if (t < r) v[t] = xb[q + s * (p + t * m)];
+  dft_small<DIR>(r, v);
+  yb[q + s * r * p] = v[0];
+#pragma unroll
+  for (int u = 1; u < 5; ++u)
+    if (u < r) {
+      double2 w = tw[p * u * step];
+      if (DIR > 0) w.y = -w.y;
+      yb[q + s * (r * p + u)] = cmul2(v[u], w);
+    }
+}
+
 template <int DIR>
 __device__ double2* fft_lds(double2* x, double2* y, const Rad& R, int B, const double2* __restrict__ tw) {
   const int n = R.n;
@@ -102,21 +121,7 @@ __device__ double2* fft_lds(double2* x, double2* y, const Rad& R, int B, const d
     const int r = R.r[pi], m = len / r, nb = m * s, step = n / len;
     for (int idx = threadIdx.x; idx < B * nb; idx += blockDim.x) {
       const int b = idx / nb, i = idx - b * nb, p = i / s, q = i - p * s;
-      const double2* xb = x + b * n;
-      double2* yb = y + b * n;
-      double2 v[5];
-#pragma unroll
-      for (int t = 0; t < 5; ++t)
-        if (t < r) v[t] = xb[q + s * (p + t * m)];
-      dft_small<DIR>(r, v);
-      yb[q + s * r * p] = v[0];
-#pragma unroll
-      for (int u = 1; u < 5; ++u)
-        if (u < r) {
-          double2 w = tw[p * u * step];
-          if (DIR > 0) w.y = -w.y;
-          yb[q + s * (r * p + u)] = cmul2(v[u], w);
-        }
+      bfly<DIR>(x + b * n, y + b * n, r, m, s, step, p, q, tw);
     }
     __syncthreads();
     double2* t = x;
@@ -126,6 +131,77 @@ __device__ double2* fft_lds(double2* x, double2* y, const Rad& R, int B, const d
     s *= r;
   }
   return x;
+}
+
+// ---- compile-time lines (round 6): the same stages for a line length N, B
+// lines and NTH threads known at compile time — the radix, the index
+// divisions and the thread loops fold (the runtime form spends more VALU on
+// its index divisions than on the butterflies); the same butterflies in the
+// same order, so bitwise the runtime form's results.
+constexpr int ct_nrad(int n) {
+  int k = 0;
+  while (n % 4 == 0) ++k, n /= 4;
+  while (n % 2 == 0) ++k, n /= 2;
+  while (n % 3 == 0) ++k, n /= 3;
+  while (n % 5 == 0) ++k, n /= 5;
+  return k;
+}
+constexpr int ct_rad(int n, int pi) {  // radices()'s pi-th radix
+  int k = 0;
+  while (n % 4 == 0) { if (k++ == pi) return 4; n /= 4; }
+  while (n % 2 == 0) { if (k++ == pi) return 2; n /= 2; }
+  while (n % 3 == 0) { if (k++ == pi) return 3; n /= 3; }
+  while (n % 5 == 0) { if (k++ == pi) return 5; n /= 5; }
+  return 0;
+}
+// lines per block / threads per block (host and device: the launch and the kernel agree)
+constexpr int ct_lines_per_block(int n) {
+  int B = 1;
+  while (B < 8 && 2 * B * n <= 2048) B *= 2;
+  return B;
+}
+constexpr int ct_blk_threads(int lines, int n) {
+  const int t = (lines * n / 2 + 63) / 64 * 64;
+  return t < 64 ? 64 : (t > 1024 ? 1024 : t);
+}
+
+// f(idx) for idx < TOT over the block's NTH threads (TOT > 0: unrolled,
+// constant trip count), else for idx < tot over blockDim.x threads
+template <int TOT, int NTH, typename F>
+__device__ __forceinline__ void gfor(int tot, F f) {
+  if constexpr (TOT > 0) {
+#pragma unroll
+    for (int i0 = 0; i0 < TOT; i0 += NTH) {
+      const int idx = i0 + (int)threadIdx.x;
+      if (TOT % NTH == 0 || idx < TOT) f(idx);
+    }
+  } else {
+    for (int idx = threadIdx.x; idx < tot; idx += blockDim.x) f(idx);
+  }
+}
+
+template <int DIR, int N, int B, int NTH, int PI = 0, int LEN = N, int S = 1>
+__device__ __forceinline__ double2* fft_ct(double2* x, double2* y, const double2* __restrict__ tw) {
+  if constexpr (PI == ct_nrad(N)) {
+    return x;
+  } else {
+    constexpr int r = ct_rad(N, PI), m = LEN / r, nb = m * S, step = N / LEN;
+    gfor<B * nb, NTH>(0, [&](int idx) {
+      const unsigned u = (unsigned)idx;
+      const int b = (int)(u / nb), i = idx - b * nb, p = (int)((unsigned)i / S), q = i - p * S;
+      bfly<DIR>(x + b * N, y + b * N, r, m, S, step, p, q, tw);
+    });
+    __syncthreads();
+    return fft_ct<DIR, N, B, NTH, PI + 1, m, S * r>(y, x, tw);
+  }
+}
+
+// N > 0: the compile-time stages; else the runtime ones
+template <int DIR, int N, int B, int NTH>
+__device__ __forceinline__ double2* fft_any(double2* x, double2* y, const Rad& R, int Br,
+                                            const double2* __restrict__ tw) {
+  if constexpr (N > 0) return fft_ct<DIR, N, B, NTH>(x, y, tw);
+  else return fft_lds<DIR>(x, y, R, Br, tw);
 }
 
 // complex lines of R.n points, B per block (adjacent kr: one row of B points
@@ -345,18 +421,21 @@ __global__ void k_frk4(Geom g, Phys p, int stage, double2* __restrict__ sol, dou
 //                update (frk4_mode) per live mode.
 // X is read by both layers' blocks, so stages write the next input to the
 // other xs buffer (ping-pong).
-__global__ void __launch_bounds__(1024) k_gcol_inv(Geom g, Phys p, const double2* __restrict__ X,
-                                                  double2* __restrict__ spec, Rad R, int B,
-                                                  const double2* __restrict__ tw) {
+// (kernel templates: NC > 0 the compile-time line length, BC lines per block,
+// NTH threads — launched with exactly those; NC = 0 the runtime form)
+template <int NC, int BC, int NTH>
+__global__ void __launch_bounds__(NTH > 0 ? NTH : 1024) k_gcol_inv(Geom g, Phys p, const double2* __restrict__ X,
+                                                                  double2* __restrict__ spec, Rad R, int Bp,
+                                                                  const double2* __restrict__ tw) {
   extern __shared__ double2 lds[];
-  const int n = R.n, groups = (g.nkr + B - 1) / B;
+  const int n = NC > 0 ? NC : R.n, B = NC > 0 ? BC : Bp, groups = (g.nkr + B - 1) / B;
   double2 *twl = lds, *x = lds + n, *y = x + B * n;
-  for (int j = threadIdx.x; j < n; j += blockDim.x) twl[j] = tw[j];
+  gfor<NC, NTH>(n, [&](int j) { twl[j] = tw[j]; });
   const int fid = blockIdx.x / groups, kr0 = (blockIdx.x - fid * groups) * B;
   const int layer = fid / 3, comp = fid - 3 * layer;
   const long long F = (long long)g.nl * g.nkr;
-  for (int idx = threadIdx.x; idx < B * n; idx += blockDim.x) {
-    const int l = idx / B, b = idx - l * B, kr = kr0 + b;
+  gfor<NC * BC, NTH>(B * n, [&](int idx) {
+    const int l = (int)((unsigned)idx / B), b = idx - l * B, kr = kr0 + b;
     double2 v = zero2();
     if (kr < g.nkr && live_mode(g, l, kr)) {
       const long long i = (long long)l * g.nkr + kr;
@@ -371,15 +450,15 @@ __global__ void __launch_bounds__(1024) k_gcol_inv(Geom g, Phys p, const double2
       }
     }
     x[b * n + l] = v;
-  }
+  });
   __syncthreads();
-  const double2* z = fft_lds<+1>(x, y, R, B, twl);
+  const double2* z = fft_any<+1, NC, BC, NTH>(x, y, R, B, twl);
   double2* d = spec + fid * F + kr0;
   const int nv = min(B, g.nkr - kr0);
-  for (int idx = threadIdx.x; idx < B * n; idx += blockDim.x) {
-    const int l = idx / B, b = idx - l * B;
+  gfor<NC * BC, NTH>(B * n, [&](int idx) {
+    const int l = (int)((unsigned)idx / B), b = idx - l * B;
     if (b < nv) d[(long long)l * g.nkr + b] = z[b * n + l];
-  }
+  });
 }
 
 // c2r of two Hermitian half rows A, B (FF/numpy's rule: the DC and Nyquist
@@ -396,62 +475,65 @@ __device__ __forceinline__ double2 pack_c2r(const double2* __restrict__ A, const
   return make_double2(a.x + b.y, b.x - a.y);
 }
 
-__global__ void __launch_bounds__(1024) k_grow(Geom g, Phys p, double2* __restrict__ spec, Rad R, double scale,
-                                              const double2* __restrict__ tw) {
+template <int NC, int NTH>
+__global__ void __launch_bounds__(NTH > 0 ? NTH : 1024) k_grow(Geom g, Phys p, double2* __restrict__ spec, Rad R,
+                                                              double scale, const double2* __restrict__ tw) {
   extern __shared__ double2 lds[];
-  const int n = R.n, row = blockIdx.x;
-  const long long F = (long long)g.nl * g.nkr;
+  const int n = NC > 0 ? NC : R.n, row = blockIdx.x;
+  const int nkr = NC > 0 ? NC / 2 + 1 : g.nkr;  // (the x transforms: nkr = nx/2 + 1)
+  const long long F = (long long)g.nl * nkr;
   double2 *twl = lds, *x = lds + n, *y = x + 3 * n;
-  for (int j = threadIdx.x; j < n; j += blockDim.x) twl[j] = tw[j];
-  const double2* S = spec + (long long)row * g.nkr;
-  for (int idx = threadIdx.x; idx < 3 * n; idx += blockDim.x) {
-    const int c = idx / n, k = idx - c * n;  // lines: (q1, u1), (v1, q2), (u2, v2) = fields (0,1), (2,3), (4,5)
+  gfor<NC, NTH>(n, [&](int j) { twl[j] = tw[j]; });
+  const double2* S = spec + (long long)row * nkr;
+  gfor<3 * NC, NTH>(3 * n, [&](int idx) {
+    const int c = (int)((unsigned)idx / n), k = idx - c * n;  // lines: (q1, u1), (v1, q2), (u2, v2) = fields (0,1), (2,3), (4,5)
     x[idx] = pack_c2r(S + (2 * c) * F, S + (2 * c + 1) * F, k, n);
-  }
+  });
   __syncthreads();
-  double2* z = fft_lds<+1>(x, y, R, 3, twl);
+  double2* z = fft_any<+1, NC, 3, NTH>(x, y, R, 3, twl);
   double2* w = z == x ? y : x;  // the free buffer
-  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+  gfor<NC, NTH>(n, [&](int k) {
     const double2 a = z[k], b = z[n + k], c = z[2 * n + k];
     const double q1 = a.x * scale, u1 = a.y * scale, v1 = b.x * scale, q2 = b.y * scale;
     const double u2 = c.x * scale, v2 = c.y * scale;
     w[k] = make_double2((u1 + p.U1) * q1, v1 * q1);
     w[n + k] = make_double2((u2 + p.U2) * q2, v2 * q2);
-  }
+  });
   __syncthreads();
-  const double2* Z = fft_lds<-1>(w, z, R, 2, twl);
-  double2* O = spec + (long long)row * g.nkr;
-  for (int idx = threadIdx.x; idx < 2 * g.nkr; idx += blockDim.x) {
-    const int c = idx / g.nkr, k = idx - c * g.nkr;
+  const double2* Z = fft_any<-1, NC, 2, NTH>(w, z, R, 2, twl);
+  double2* O = spec + (long long)row * nkr;
+  gfor<2 * (NC / 2 + 1) * (NC > 0), NTH>(2 * nkr, [&](int idx) {
+    const int c = (int)((unsigned)idx / nkr), k = idx - c * nkr;
     const double2 zk = Z[c * n + k], zm = Z[c * n + (k == 0 ? 0 : n - k)];
     // P = (Z_k + conj Z_{n-k})/2, Q = (Z_k - conj Z_{n-k})/(2i)
     O[(2 * c) * F + k] = make_double2(0.5 * (zk.x + zm.x), 0.5 * (zk.y - zm.y));
     O[(2 * c + 1) * F + k] = make_double2(0.5 * (zk.y + zm.y), -0.5 * (zk.x - zm.x));
-  }
+  });
 }
 
-__global__ void __launch_bounds__(1024) k_gcol_fwd(Geom g, Phys p, int stage, const double2* X,  // (= sol at stage 1)
-                                                  const double2* __restrict__ spec, double2* __restrict__ sol,
-                                                  double2* __restrict__ xo, double2* __restrict__ acc, Rad R, int B,
-                                                  const double2* __restrict__ tw, int* nanflag) {
+template <int NC, int BC, int NTH>
+__global__ void __launch_bounds__(NTH > 0 ? NTH : 1024)
+    k_gcol_fwd(Geom g, Phys p, int stage, const double2* X,  // (= sol at stage 1)
+               const double2* __restrict__ spec, double2* __restrict__ sol, double2* __restrict__ xo,
+               double2* __restrict__ acc, Rad R, int Bp, const double2* __restrict__ tw, int* nanflag) {
   extern __shared__ double2 lds[];
-  const int n = R.n, groups = (g.nkr + B - 1) / B;
+  const int n = NC > 0 ? NC : R.n, B = NC > 0 ? BC : Bp, groups = (g.nkr + B - 1) / B;
   double2 *twl = lds, *x = lds + n, *y = x + 2 * B * n;
-  for (int j = threadIdx.x; j < n; j += blockDim.x) twl[j] = tw[j];
+  gfor<NC, NTH>(n, [&](int j) { twl[j] = tw[j]; });
   const int j = blockIdx.x / groups, kr0 = (blockIdx.x - j * groups) * B;
   const long long F = (long long)g.nl * g.nkr;
   const int nv = min(B, g.nkr - kr0);
   // lines 2b: (U_j + u_j) q_j, 2b + 1: v_j q_j of column kr0 + b
-  for (int idx = threadIdx.x; idx < 2 * B * n; idx += blockDim.x) {
-    const int l = idx / (2 * B), r = idx - l * (2 * B), b = r >> 1, c = r & 1;
+  gfor<2 * BC * NC, NTH>(2 * B * n, [&](int idx) {
+    const int l = (int)((unsigned)idx / (2 * B)), r = idx - l * (2 * B), b = r >> 1, c = r & 1;
     x[r * n + l] = b < nv ? spec[(2 * j + c) * F + (long long)l * g.nkr + kr0 + b] : zero2();
-  }
+  });
   __syncthreads();
-  const double2* z = fft_lds<-1>(x, y, R, 2 * B, twl);
+  const double2* z = fft_any<-1, NC, 2 * BC, NTH>(x, y, R, 2 * B, twl);
   bool bad = false;
-  for (int idx = threadIdx.x; idx < B * n; idx += blockDim.x) {
-    const int l = idx / B, b = idx - l * B, kr = kr0 + b;
-    if (b >= nv || !live_mode(g, l, kr)) continue;
+  gfor<BC * NC, NTH>(B * n, [&](int idx) {
+    const int l = (int)((unsigned)idx / B), b = idx - l * B, kr = kr0 + b;
+    if (b >= nv || !live_mode(g, l, kr)) return;
     const long long i = (long long)l * g.nkr + kr, o = j * F + i;
     const double k = kr * g.mk, ll = lwav(g, l), K2 = k * k + ll * ll;
     const double2 q1 = X[i], q2 = X[F + i];
@@ -464,7 +546,7 @@ __global__ void __launch_bounds__(1024) k_gcol_fwd(Geom g, Phys p, int stage, co
     const double D = -(p.nu * ipow(K2, p.nnu));
     const double2 v = frk4_mode(g, p, stage, o, k, ll, D, j ? q2 : q1, r, sol, xo, acc);
     bad = bad || !isfinite(v.x) || !isfinite(v.y);
-  }
+  });
   if (stage == 4) note_bad(nanflag, bad);
 }
 
@@ -598,6 +680,8 @@ int create(Engine*& e, const sw_config& k, const Phys& p, const Geom& g, double2
   // the separate passes (tests run both)
   const char* fe = std::getenv("SW_GEN_FUSED");
   e->fused = g.nx <= 1024 && g.ny <= 1024 && !(fe && fe[0] == '0');
+  const char* ce = std::getenv("SW_GEN_CT");
+  e->ct = !(ce && ce[0] == '0');
   if (e->fused && hipMalloc((void**)&e->xs2, 2 * F * sizeof(double2)) != hipSuccess) return SW_E_NOMEM;
   return SW_OK;
 }
@@ -613,19 +697,12 @@ void destroy(Engine* e) {
 // nf spectral fields [nf][nl][nkr] -> physical [nf][ny][nx] (normalised c2r;
 // the spectral fields are transformed in place along l first)
 // lines per block: B·n ≤ 2048 points (≤ 64 KB of LDS with the ping-pong buffer), at most 8
-static int lines_per_block(int n) {
-  int B = 1;
-  while (B < 8 && 2 * B * n <= 2048) B *= 2;
-  return B;
-}
+static int lines_per_block(int n) { return ct_lines_per_block(n); }
 
 // threads of a transform block: one per butterfly of its widest (radix-2)
 // stage over its lines, 64 … 1024 (small grids: the latency of each stage
 // is spread over more waves)
-static int blk_threads(int lines, int n) {
-  const int t = (lines * n / 2 + 63) / 64 * 64;
-  return t < 64 ? 64 : (t > 1024 ? 1024 : t);
-}
+static int blk_threads(int lines, int n) { return ct_blk_threads(lines, n); }
 
 static void inverse2d(Engine* e, double2* spec, int nf, double* phys) {
   const Geom& g = e->g;
@@ -662,6 +739,30 @@ void calcN(Engine* e, const double2* X, double2* N) {
   SW_LAUNCH(k_assemble, modes_grid(g), dim3(256), 0, e->s, g, e->p, X, e->spec, N);
 }
 
+// the line lengths with compile-time fused kernels (the 3·2^k family of
+// simulation/MattParameters.jl's nx = 384 and the test grids); other lengths
+// run the runtime forms.  SW_GEN_CT=0: the runtime forms everywhere (A/B, tests)
+#define SW_GEN_CT_LENGTHS(X) X(48) X(96) X(192) X(384) X(768)
+
+template <int NY>
+static void gcol_inv_ct(Engine* e, const double2* X, const Rad& Ry, int gi) {
+  constexpr int B = ct_lines_per_block(NY), T = ct_blk_threads(B, NY);
+  SW_LAUNCH((k_gcol_inv<NY, B, T>), dim3(6 * gi), dim3(T), (2 * B + 1) * NY * sizeof(double2), e->s, e->g, e->p, X,
+            e->spec, Ry, B, e->twy);
+}
+template <int NX>
+static void grow_ct(Engine* e, const Rad& Rx, double scale) {
+  constexpr int T = ct_blk_threads(3, NX);
+  SW_LAUNCH((k_grow<NX, T>), dim3(e->g.ny), dim3(T), 7 * NX * sizeof(double2), e->s, e->g, e->p, e->spec, Rx, scale,
+            e->twx);
+}
+template <int NY>
+static void gcol_fwd_ct(Engine* e, int stage, const double2* X, double2* xo, const Rad& Ry, int gf, int* nanflag) {
+  constexpr int Bi = ct_lines_per_block(NY), B = Bi > 1 ? Bi / 2 : 1, T = ct_blk_threads(2 * B, NY);
+  SW_LAUNCH((k_gcol_fwd<NY, B, T>), dim3(2 * gf), dim3(T), (4 * B + 1) * NY * sizeof(double2), e->s, e->g, e->p,
+            stage, X, e->spec, e->sol, xo, e->acc, Ry, B, e->twy, nanflag);
+}
+
 // the fused stage sequence (k_gcol_inv, k_grow, k_gcol_fwd; Engine::fused)
 static void step_fused(Engine* e, int* nanflag) {
   const Geom& g = e->g;
@@ -673,14 +774,41 @@ static void step_fused(Engine* e, int* nanflag) {
   for (int stage = 1; stage <= 4; ++stage) {
     // stage inputs: sol, xs, xs2, xs; the next input goes to the other buffer
     double2* xo = stage == 4 ? nullptr : (stage & 1 ? e->xs : e->xs2);
-    SW_LAUNCH(k_gcol_inv, dim3(6 * gi), dim3(blk_threads(Bi, g.ny)), (2 * Bi + 1) * g.ny * sizeof(double2), e->s, g,
-              e->p, X, e->spec, Ry,
-              Bi, e->twy);
-    SW_LAUNCH(k_grow, dim3(g.ny), dim3(blk_threads(3, g.nx)), 7 * g.nx * sizeof(double2), e->s, g, e->p, e->spec, Rx,
-              scale, e->twx);
-    SW_LAUNCH(k_gcol_fwd, dim3(2 * gf), dim3(blk_threads(2 * Bf, g.ny)), (4 * Bf + 1) * g.ny * sizeof(double2), e->s, g,
-              e->p, stage, X, e->spec,
-              e->sol, xo, e->acc, Ry, Bf, e->twy, stage == 4 ? nanflag : nullptr);
+    int* nf = stage == 4 ? nanflag : nullptr;
+    bool done = false;
+#define SW_GEN_CASE(N) \
+  case N:              \
+    gcol_inv_ct<N>(e, X, Ry, gi); \
+    done = true;       \
+    break;
+    if (e->ct) switch (g.ny) { SW_GEN_CT_LENGTHS(SW_GEN_CASE) default: break; }
+#undef SW_GEN_CASE
+    if (!done)
+      SW_LAUNCH((k_gcol_inv<0, 0, 0>), dim3(6 * gi), dim3(blk_threads(Bi, g.ny)), (2 * Bi + 1) * g.ny * sizeof(double2),
+                e->s, g, e->p, X, e->spec, Ry, Bi, e->twy);
+    done = false;
+#define SW_GEN_CASE(N)   \
+  case N:                \
+    grow_ct<N>(e, Rx, scale); \
+    done = true;         \
+    break;
+    if (e->ct) switch (g.nx) { SW_GEN_CT_LENGTHS(SW_GEN_CASE) default: break; }
+#undef SW_GEN_CASE
+    if (!done)
+      SW_LAUNCH((k_grow<0, 0>), dim3(g.ny), dim3(blk_threads(3, g.nx)), 7 * g.nx * sizeof(double2), e->s, g, e->p,
+                e->spec, Rx, scale, e->twx);
+    done = false;
+#define SW_GEN_CASE(N)                              \
+  case N:                                           \
+    gcol_fwd_ct<N>(e, stage, X, xo, Ry, gf, nf); \
+    done = true;                                    \
+    break;
+    if (e->ct) switch (g.ny) { SW_GEN_CT_LENGTHS(SW_GEN_CASE) default: break; }
+#undef SW_GEN_CASE
+    if (!done)
+      SW_LAUNCH((k_gcol_fwd<0, 0, 0>), dim3(2 * gf), dim3(blk_threads(2 * Bf, g.ny)),
+                (4 * Bf + 1) * g.ny * sizeof(double2), e->s, g, e->p, stage, X, e->spec, e->sol, xo, e->acc, Ry, Bf,
+                e->twy, nf);
     X = xo;
   }
 }

@@ -45,6 +45,7 @@ struct Engine {
   int bx = 1;               // rows per block of the x transforms
   bool fused = false;       // three kernels per stage (k_gcol_inv, k_grow, k_gcol_fwd)
   double2* xs2 = nullptr;   // the fused stages' second stage-input buffer
+  bool ct = true;           // compile-time fused kernels for the lengths that have them (SW_GEN_CT)
 };
 
 int create(Engine*& e, const sw_config& k, const Phys& p, const Geom& g, double2* sol, hipStream_t s,

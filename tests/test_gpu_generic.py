@@ -66,6 +66,23 @@ def test_generic_separate_passes(n, monkeypatch):
     sep.close()
 
 
+@pytest.mark.parametrize("n", [96, 384])
+def test_generic_compile_time_lines_bitwise(n, monkeypatch):
+    """The fused kernels compiled for the 3·2^k line lengths (k_gcol_inv /
+    k_grow / k_gcol_fwd<N, B, NTH>) against their runtime forms (SW_GEN_CT=0):
+    the same butterflies in the same order, bitwise the same state."""
+    p, pr, prob = _pair(n)
+    monkeypatch.setenv("SW_GEN_CT", "0")
+    rt = sw_cases.libsw_problem(p)
+    monkeypatch.delenv("SW_GEN_CT")
+    rt.sol = pr.sol
+    prob.stepforward(6)
+    rt.stepforward(6)
+    assert np.array_equal(prob.sol, rt.sol)
+    prob.close()
+    rt.close()
+
+
 def test_generic_every_term_rectangular():
     """H₁ ≠ H₂, β, drag, hyperviscosity, the 2/3 rule, and nx ≠ ny (96 × 48)."""
     from juliaraytracingsw_amd import multilayer_qg as MLQG
