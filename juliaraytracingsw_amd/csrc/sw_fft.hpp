@@ -220,6 +220,89 @@ __device__ __forceinline__ void stage_sync() {
   else lds_barrier();
 }
 
+// Two wave-local 512-point transforms software-pipelined (SW_WL_PIPE, round
+// 6): a wave's LDS instructions execute in order, so line c's exchange (its
+// stage writes, then the next stage's reads of the same region) is issued
+// without waiting, and the other line's butterflies run while it is in flight;
+// the compiler's own lgkmcnt waits hold each line's reads until it uses them.
+// The same butterflies, twiddles and exchanges as fft_lines<9, DIR, 2, FLY,
+// true, SHARE> in another order: bitwise the same results (state hashes at
+// 1024² and 2048²).  Measured (tools/ab/r6_wlpipe.sh, three interleaved
+// rounds): RSW 2048 row 66.6-67.6 → 65.3-66.6 µs, 222 → 176 VGPRs (still two
+// waves per SIMD: the two line buffers cap a CU at two blocks), 6604-6638 →
+// 6647-6680 steps/s; 1024² neutral.  Used where two wave-local lines are
+// transformed together (the RSW rows' pairs).
+#ifndef SW_WL_PIPE
+#define SW_WL_PIPE 1
+#endif
+template <int DIR, bool FLY, bool SHARE>
+__device__ __forceinline__ void fft512_wl2_pipe(double2 (&v)[2][8], int t, const Twiddles<9, FLY>& tws,
+                                                double2* __restrict__ line, int stride) {
+  using P = FftPlan<9>;
+  static_assert(P::NTW == 2 && P::REM == 0, "512 = 8·8·8");
+  if constexpr (FLY) asm volatile("" : "+v"(t));
+  constexpr bool kPre = Twiddles<9, FLY>::kPreload;
+  double2 tw1[2];
+  if constexpr (kPre) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      tw1[i] = tws.w[i];
+      if constexpr (!SHARE) asm volatile("" : "+v"(tw1[i].x), "+v"(tw1[i].y));
+    }
+  }
+  // stage lNs's outputs to the line's region, then the next stage's inputs
+  auto exch = [&](int c, int lNs) {
+    const int Ns = 1 << lNs, k = t & (Ns - 1);
+    const int idxD = ((t >> lNs) << (lNs + 3)) + k;
+    double2* ln = line + c * stride;
+    if (lNs >= 6) {
+      const int base = LPs<true>(idxD);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) ln[base + r * Ns] = v[c][r];
+    } else {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) ln[LPs<true>(idxD + r * Ns)] = v[c][r];
+    }
+    asm volatile("" ::: "memory");  // (compiler order only: the reads stay after the writes)
+    load_line<9, true>(v[c], t, ln);
+  };
+  // stage ti's twiddle powers (fft_lines' forms: all at once when preloaded,
+  // a chain when read per stage), applied to line c, then its DFT-8
+  double2 wq[8];
+  auto powers = [&](int ti) {
+    const double2 wt = kPre ? tw1[ti] : tws.get(ti);
+    wq[1] = DIR < 0 ? wt : cconj(wt);
+    if constexpr (kPre) {
+      wq[2] = cmul(wq[1], wq[1]);
+      wq[3] = cmul(wq[2], wq[1]);
+      wq[4] = cmul(wq[2], wq[2]);
+      wq[5] = cmul(wq[4], wq[1]);
+      wq[6] = cmul(wq[3], wq[3]);
+      wq[7] = cmul(wq[4], wq[3]);
+    } else {
+#pragma unroll
+      for (int r = 2; r < 8; ++r) wq[r] = cmul(wq[r - 1], wq[1]);
+    }
+  };
+  auto twdft = [&](int c) {
+#pragma unroll
+    for (int r = 1; r < 8; ++r) v[c][r] = cmul(v[c][r], wq[r]);
+    dft8<DIR>(v[c]);
+  };
+  dft8<DIR>(v[0]);
+  exch(0, 0);
+  dft8<DIR>(v[1]);
+  exch(1, 0);
+  powers(0);
+  twdft(0);
+  exch(0, 3);
+  twdft(1);
+  exch(1, 3);
+  powers(1);
+  twdft(0);
+  twdft(1);
+}
+
 // C independent transforms of one line each, sharing every barrier (C LDS
 // line buffers, `stride` complex apart).  v[c] holds x[t + s*NT] on entry and
 // X[t + s*NT] on exit.  All threads of the block must call this (barriers).
@@ -236,6 +319,10 @@ __device__ __forceinline__ void fft_lines(double2 (&v)[C][8], int t, const Twidd
   constexpr int NT = P::NT;
   constexpr bool SWZ = WL || lds_swz<LOG2N>();
   static_assert(!WL || NT == 64, "a wave-local transform is one wave's line");
+  if constexpr (WL && C == 2 && SW_WL_PIPE) {
+    fft512_wl2_pipe<DIR, FLY, SHARE>(v, t, tws, line, stride);
+    return;
+  }
   // opaque t on the long lines and in kernels with little register room (FLY)
   if constexpr (LOG2N >= SW_OPAQUE_LOG2 || FLY) asm volatile("" : "+v"(t));
   // Opaque copy of the stage twiddles: keeps the compiler from sharing the
