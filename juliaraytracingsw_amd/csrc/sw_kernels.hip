@@ -772,11 +772,24 @@ __host__ __device__ constexpr int row_tgt() {
 template <int MODEL, int LOG2N>
 using BlkRow = Blk<LOG2N, row_tgt<MODEL>()>;
 
+// the 2LQG / MultiLayerQG row on the decimated lines with two line buffers,
+// as the RSW row (round 6, SW_QG_ROW_PAIR): q and ψx inverse-transformed as
+// a pipelined pair, ψy alone, the two products' forward transforms as a
+// pipelined pair — two blocks per CU, twiddles held, instead of one buffer,
+// four blocks and per-stage twiddle reads
+#ifndef SW_QG_ROW_PAIR
+#define SW_QG_ROW_PAIR 0
+#endif
+template <int LOG2N>
+__host__ __device__ constexpr bool qg_row_pair() {
+  return SW_QG_ROW_PAIR && LOG2N >= 10 && LOG2N <= 12;  // (the decimated lines: roww)
+}
 template <int MODEL, int LOG2N>
 __host__ __device__ constexpr int row_lds_lines() {
 #ifdef SW_ROW_CB1  // sweep knob: one line buffer per row
   return 1;
 #else
+  if (MODEL == MODEL_QG2 && qg_row_pair<LOG2N>()) return 2;
   return (MODEL == MODEL_RSW && 2 * BlkRow<MODEL, LOG2N>::NB * FftPlan<LOG2N>::LDS * 16 <= 160 * 1024) ? 2 : 1;
 #endif
 }
@@ -889,7 +902,7 @@ __host__ __device__ constexpr int roww_h() {
 }
 template <int MODEL, int LOG2N>
 __host__ __device__ constexpr bool row_fly() {
-  return LOG2N >= SW_TWFLY_LOG2 || (MODEL == MODEL_QG2 && LOG2N >= SW_QG_ROW_FLY_MIN);
+  return LOG2N >= SW_TWFLY_LOG2 || (MODEL == MODEL_QG2 && LOG2N >= SW_QG_ROW_FLY_MIN && !qg_row_pair<LOG2N>());
 }
 // PRUNE: a live band kc <= 3N/8 (row_prunable): the decimated transforms
 // skip the zero inputs and unused outputs of slots 3 and 4 (sw_fft.hpp)
@@ -1271,6 +1284,30 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
       if constexpr (W > 0) fftw_dit<W, -1, 1, FL, false, false, PR>(reinterpret_cast<V1>(x), c.t, wnt(), tq, line, 0);
       else fft_line<LOG2N, -1>(x, c.t, tws, line);
     };
+    if constexpr (W > 0 && row_lds_lines<MODEL, LOG2N>() == 2 && !ALIAS && !SPLIT) {
+      // (qg_row_pair) the same transforms, products and splits as below, in pairs
+      constexpr int LS = FftPlan<LOG2N>::LDS;
+      double2 w2[2][8], q[8];
+      load_pair<LOG2N>(w2[0], ri, g, Q1, Q2, false);  // q1 + i q2
+      load_pair<LOG2N>(w2[1], ri, g, P1, P2, true);   // ψx1 + i ψx2
+      fftw_dif<W, +1, 2, false, false, false, PR>(w2, c.t, wt, tq, line, LS);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        q[s] = w2[0][s];
+        w2[0][s] = make_double2(w2[1][s].x * q[s].x, w2[1][s].y * q[s].y);  // ψx q (swqg/TwoLayerQG.jl:169)
+      }
+      load_pair<LOG2N>(w2[1], ri, g, Py1, Py2, false);  // ψy1 + i ψy2
+      fftw_dif<W, +1, 1, true, false, false, PR>(reinterpret_cast<V1>(w2[1]), c.t, wt, tq, line + LS, 0);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) w2[1][s] = make_double2(w2[1][s].x * q[s].x, w2[1][s].y * q[s].y);  // ψy q (:177)
+      fftw_dit<W, -1, 2, false, true, false, PR>(w2, c.t, wt, tq, line, LS);
+      split_pairs<LOG2N, 2, PR>(w2, c.t, g, line, LS, [&](int cc, int, int s, double2 a, double2 b) {
+        const int o = ri.ofwd(g, s);
+        Mo[(2 * cc) * MF + o] = a;
+        Mo[(2 * cc + 1) * MF + o] = b;
+      });
+      return;
+    }
     double2 q[8];
     // q1 + i q2
     load_pair<LOG2N>(v, ri, g, Q1, Q2, false);
@@ -3308,7 +3345,7 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
   using BQ = BlkRow<MODEL_QG2, L>;
   using BT = BlkRow<MODEL_TY, L>;
   constexpr size_t sh_rsw = row_lds_lines<MODEL_RSW, L>() * FftPlan<L>::LDS * BR::NB * sizeof(double2);
-  constexpr size_t sh_qg2 = FftPlan<L>::LDS * BQ::NB * sizeof(double2);
+  constexpr size_t sh_qg2 = row_lds_lines<MODEL_QG2, L>() * FftPlan<L>::LDS * BQ::NB * sizeof(double2);
   constexpr size_t sh_ty = FftPlan<L>::LDS * BT::NB * sizeof(double2);
   if (model == MODEL_RSW) {
     constexpr int nbr = rowh_nb<L, true>();
