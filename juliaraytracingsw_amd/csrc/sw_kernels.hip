@@ -776,7 +776,9 @@ using BlkRow = Blk<LOG2N, row_tgt<MODEL>()>;
 // as the RSW row (round 6, SW_QG_ROW_PAIR): q and ψx inverse-transformed as
 // a pipelined pair, ψy alone, the two products' forward transforms as a
 // pipelined pair — two blocks per CU, twiddles held, instead of one buffer,
-// four blocks and per-stage twiddle reads
+// four blocks and per-stage twiddle reads.  Measured (tools/ab/r6_qgpair.sh):
+// 2048 row 69.9-70.5 -> 73.3-75.1 µs, config 3 -2 %: off (parity green; not
+// bitwise the default at 2048, whose twiddle powers are formed as a chain)
 #ifndef SW_QG_ROW_PAIR
 #define SW_QG_ROW_PAIR 0
 #endif
