@@ -183,7 +183,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=40)
     ap.add_argument("--out", default=None)
-    ap.add_argument("--only", nargs="*", default=None, choices=["rsw", "qg2", "mlqg", "ty"])
+    ap.add_argument("--only", nargs="*", default=None, choices=["rsw", "qg2", "mlqg", "mlqg384", "ty"])
     args = ap.parse_args()
     todo = args.only or ["rsw", "qg2", "mlqg", "ty"]
     res = []
@@ -195,6 +195,8 @@ def main():
             r = [run_qg2(max(4, args.frames // 4))]
         elif name == "mlqg":
             r = [run_mlqg(max(4, args.frames // 2))]
+        elif name == "mlqg384":  # simulation/MattParameters.jl's grid (the generic engine)
+            r = [run_mlqg(max(4, args.frames // 2), nx=384)]
         else:
             r = run_ty(4 * args.frames)
         for x in r:
