@@ -14,13 +14,22 @@ sys.path.insert(0, __file__.rsplit("/", 1)[0])
 from traffic_from_pmc import short  # noqa: E402
 
 STEP_KERNELS = {"row", "col_step", "col_inv", "col_fwd", "update", "col_fwd_step"}
+# the generic engine's fused stage (csrc/sw_generic.hip): three kernels per
+# FilteredRK4 stage, four stages per step (libsw's profile counts one
+# "generic_step" launch per step)
+GEN_KERNELS = {"gen::k_gcol_inv", "gen::k_grow", "gen::k_gcol_fwd"}
 
 
 def main(trace_csv, run_json, out):
     run = json.loads([ln for ln in open(run_json) if ln.startswith("{")][-1])
-    rows = [r for r in csv.DictReader(open(trace_csv)) if short(r["Kernel_Name"]) in STEP_KERNELS]
+    allrows = list(csv.DictReader(open(trace_csv)))
+    rows = [r for r in allrows if short(r["Kernel_Name"]) in STEP_KERNELS]
+    per_step = run["launches_per_step"]
+    if not rows:
+        rows = [r for r in allrows if short(r["Kernel_Name"]) in GEN_KERNELS]
+        per_step = 3 * 4
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    n = int(round(run["steps"] * run["launches_per_step"]))
+    n = int(round(run["steps"] * per_step))
     sel = rows[-n:]
     dur = defaultdict(list)
     for r in sel:
