@@ -682,12 +682,15 @@ int create(Engine*& e, const sw_config& k, const Phys& p, const Geom& g, double2
   e->fused = g.nx <= 1024 && g.ny <= 1024 && !(fe && fe[0] == '0');
   const char* ce = std::getenv("SW_GEN_CT");
   e->ct = !(ce && ce[0] == '0');
+  const char* ge = std::getenv("SW_GEN_GRAPH");
+  e->graph_on = e->fused && ge && ge[0] == '1';
   if (e->fused && hipMalloc((void**)&e->xs2, 2 * F * sizeof(double2)) != hipSuccess) return SW_E_NOMEM;
   return SW_OK;
 }
 
 void destroy(Engine* e) {
   if (!e) return;
+  if (e->gexec) (void)hipGraphExecDestroy(e->gexec);
   for (void* b : {(void*)e->xs, (void*)e->xs2, (void*)e->acc, (void*)e->N, (void*)e->spec, (void*)e->phys,
                   (void*)e->cols, (void*)e->twx, (void*)e->twy})
     if (b) (void)hipFree(b);
@@ -813,10 +816,41 @@ static void step_fused(Engine* e, int* nanflag) {
   }
 }
 
+// The fused step as one hipGraph (round 6, SW_GEN_GRAPH=1): at 384² a step
+// is twelve kernels of 9-13 µs and the gaps between them were 7 % of the step
+// (trace span 135.9 against a kernel sum of 126.1 µs per step).  Every launch
+// of the step has the same arguments each step (the stage buffers, the flag),
+// so the step is captured once per flag pointer and replayed.  Measured
+// slower (tools/ab/ab_env.sh, three rounds): 7919-7936 → 7592-7613 steps/s,
+// TwoLayerSimulation's cadence at 384² 4717 → 3779: off (direct launches).
+static bool graph_step(Engine* e, int* nanflag) {
+  if (!e->graph_on || ::sw::prof_ev.stop) return false;
+  if (!e->gexec || e->gflag != nanflag) {
+    if (e->gexec) (void)hipGraphExecDestroy(e->gexec);
+    e->gexec = nullptr;
+    hipGraph_t gr = nullptr;
+    if (hipStreamBeginCapture(e->s, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+      e->graph_on = false;
+      return false;
+    }
+    step_fused(e, nanflag);
+    const bool ok = hipStreamEndCapture(e->s, &gr) == hipSuccess && gr &&
+                    hipGraphInstantiate(&e->gexec, gr, nullptr, nullptr, 0) == hipSuccess;
+    if (gr) (void)hipGraphDestroy(gr);
+    if (!ok) {  // (nothing was launched: the captured step runs directly)
+      e->gexec = nullptr;
+      e->graph_on = false;
+      return false;
+    }
+    e->gflag = nanflag;
+  }
+  return hipGraphLaunch(e->gexec, e->s) == hipSuccess;
+}
+
 void step(Engine* e, int* nanflag) {
   const Geom& g = e->g;
   if (e->fused) {
-    step_fused(e, nanflag);
+    if (!graph_step(e, nanflag)) step_fused(e, nanflag);
     return;
   }
   for (int stage = 1; stage <= 4; ++stage) {

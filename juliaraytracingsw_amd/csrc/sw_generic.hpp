@@ -46,6 +46,9 @@ struct Engine {
   bool fused = false;       // three kernels per stage (k_gcol_inv, k_grow, k_gcol_fwd)
   double2* xs2 = nullptr;   // the fused stages' second stage-input buffer
   bool ct = true;           // compile-time fused kernels for the lengths that have them (SW_GEN_CT)
+  bool graph_on = false;    // the fused step replayed as a hipGraph (SW_GEN_GRAPH)
+  hipGraphExec_t gexec = nullptr;
+  int* gflag = nullptr;     // the blow-up flag the graph was captured with
 };
 
 int create(Engine*& e, const sw_config& k, const Phys& p, const Geom& g, double2* sol, hipStream_t s,
