@@ -765,12 +765,19 @@ __device__ __forceinline__ void store_pair(const double2 (&v)[8], const RowIdx<L
 // down to 64 threads (512² TY / MultiLayerQG steps +11-14 %, 1024² RSW
 // col_step 31 -> 28 µs) — more, smaller blocks spread a small grid over the
 // 256 CUs.
-template <int MODEL>
+// On lines of at most 512 points (the drivers' 512² grids) the RSW row takes
+// one line per 64-thread block like the other kernels (SW_RSW_ROW_TGT_SHORT;
+// round 6, tools/ab/r6_rowtgt.sh: RSWDriver 512² IFMAB3 31669-32020 →
+// 32333-32573 steps/s at 64 against 256 threads, 128 between; bitwise equal)
+#ifndef SW_RSW_ROW_TGT_SHORT
+#define SW_RSW_ROW_TGT_SHORT 64
+#endif
+template <int MODEL, int LOG2N>
 __host__ __device__ constexpr int row_tgt() {
-  return MODEL == MODEL_RSW ? 256 : SW_BLK_THREADS;
+  return MODEL == MODEL_RSW ? (LOG2N <= 9 ? SW_RSW_ROW_TGT_SHORT : 256) : SW_BLK_THREADS;
 }
 template <int MODEL, int LOG2N>
-using BlkRow = Blk<LOG2N, row_tgt<MODEL>()>;
+using BlkRow = Blk<LOG2N, row_tgt<MODEL, LOG2N>()>;
 
 // the 2LQG / MultiLayerQG row on the decimated lines with two line buffers,
 // as the RSW row (round 6, SW_QG_ROW_PAIR): q and ψx inverse-transformed as
