@@ -1424,12 +1424,22 @@ struct SrcZeta {  // RSW ζ̂ = ik V̂ − Ûy (x-spectral, per element)
   }
 };
 
+// The half rows' live band kc (KC > 0: known at compile time — the 2/3 rule
+// on the full-length line, kc = N/3 — so every slot that is wholly live or
+// wholly dead resolves at compile time and only the boundary slot selects per
+// lane; round 6, SW_ROWH_KC; KC = 0: g.kc at run time)
+template <int KC>
+__device__ __forceinline__ int live_kc(const Geom& g) {
+  return KC > 0 ? KC : g.kc;
+}
+
 // c2r input of one real field: v[s] = Z[t + s NTH].  Loads in two batches of
 // four slots (eight loads per source array in flight)
-template <int LOG2N, typename Src>
+template <int LOG2N, typename Src, int KC = 0>
 __device__ __forceinline__ void load_real_h(double2 (&v)[8], const Geom& g, int t, int y, const Src& src,
                                             double2 wt) {
   using H = RowH<LOG2N>;
+  const int kc = live_kc<KC>(g);
   // offsets and W^k formed per call, not kept across the row's calls
   asm volatile("" : "+v"(t), "+v"(wt.x), "+v"(wt.y));
 #pragma unroll
@@ -1439,25 +1449,28 @@ __device__ __forceinline__ void load_real_h(double2 (&v)[8], const Geom& g, int 
     for (int j = 0; j < 4; ++j) {
       const int s = 4 * hb + j, k = t + s * H::NTH, km = H::M - k;
       a[j] = b[j] = Src::zero();
-      if (s * H::NTH < g.kc) a[j] = src.ld(H::inv(g, k < g.kc ? k : 0, y));
-      if (H::M - (s + 1) * H::NTH < g.kc) b[j] = src.ld(H::inv(g, km < g.kc ? km : 0, y));
+      // (all: every lane of the slot live — no clamp, no select)
+      const bool alla = (s + 1) * H::NTH <= kc, allb = H::M - s * H::NTH < kc;
+      if (s * H::NTH < kc) a[j] = src.ld(H::inv(g, (alla || k < kc) ? k : 0, y));
+      if (H::M - (s + 1) * H::NTH < kc) b[j] = src.ld(H::inv(g, (allb || km < kc) ? km : 0, y));
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int s = 4 * hb + j, k = t + s * H::NTH, km = H::M - k;
+      const bool alla = (s + 1) * H::NTH <= kc, allb = H::M - s * H::NTH < kc;
       double2 x, xm;
       if constexpr (std::is_same<Src, SrcField>::value) {  // (the 2LQG row's register budget: this order)
-        x = k < g.kc ? a[j] : zero2();
-        xm = km < g.kc ? b[j] : zero2();
-        if (k == 0) x.y = 0.0;
+        x = (alla || k < kc) ? a[j] : zero2();
+        xm = (allb || km < kc) ? b[j] : zero2();
+        if (s == 0 && k == 0) x.y = 0.0;
         if (src.deriv) {
           x = cmul_i(x, k * g.mk);
           xm = cmul_i(xm, km * g.mk);
         }
       } else {
-        x = k < g.kc ? src.val(a[j], k, g) : zero2();
-        xm = km < g.kc ? src.val(b[j], km, g) : zero2();
-        if (k == 0) x.y = 0.0;  // numpy's c2r rule; X[M] is never live
+        x = (alla || k < kc) ? src.val(a[j], k, g) : zero2();
+        xm = (allb || km < kc) ? src.val(b[j], km, g) : zero2();
+        if (s == 0 && k == 0) x.y = 0.0;  // numpy's c2r rule; X[M] is never live
       }
       const double2 S = cadd(x, cconj(xm)), D = csub(x, cconj(xm));
       const double2 T = cmul(D, cconj(H::wk(wt, s)));
@@ -1469,11 +1482,12 @@ __device__ __forceinline__ void load_real_h(double2 (&v)[8], const Geom& g, int 
 // RSW half row: the c2r inputs of v and of ζ = ik V̂ − Ûy from ONE read of V
 // (with Uy), the same arithmetic as load_real_h with SrcField{V} and
 // SrcZeta{V, Uy} (bitwise)
-template <int LOG2N>
+template <int LOG2N, int KC = 0>
 __device__ __forceinline__ void load_v_zeta_h(double2 (&v)[8], double2 (&z)[8], const Geom& g, int t, int y,
                                               const double2* __restrict__ V, const double2* __restrict__ Uy,
                                               double2 wt) {
   using H = RowH<LOG2N>;
+  const int kc = live_kc<KC>(g);
   asm volatile("" : "+v"(t), "+v"(wt.x), "+v"(wt.y));
   const SrcZeta sz{V, Uy};
   auto comb = [&](double2 x, double2 xm, int s) {
@@ -1488,18 +1502,20 @@ __device__ __forceinline__ void load_v_zeta_h(double2 (&v)[8], double2 (&z)[8], 
     for (int j = 0; j < 4; ++j) {
       const int s = 4 * hb + j, k = t + s * H::NTH, km = H::M - k;
       a[j] = b[j] = SrcZeta::zero();
-      if (s * H::NTH < g.kc) a[j] = sz.ld(H::inv(g, k < g.kc ? k : 0, y));
-      if (H::M - (s + 1) * H::NTH < g.kc) b[j] = sz.ld(H::inv(g, km < g.kc ? km : 0, y));
+      const bool alla = (s + 1) * H::NTH <= kc, allb = H::M - s * H::NTH < kc;
+      if (s * H::NTH < kc) a[j] = sz.ld(H::inv(g, (alla || k < kc) ? k : 0, y));
+      if (H::M - (s + 1) * H::NTH < kc) b[j] = sz.ld(H::inv(g, (allb || km < kc) ? km : 0, y));
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int s = 4 * hb + j, k = t + s * H::NTH, km = H::M - k;
-      double2 x = k < g.kc ? a[j].v : zero2(), xm = km < g.kc ? b[j].v : zero2();
-      if (k == 0) x.y = 0.0;
+      const bool la = (s + 1) * H::NTH <= kc || k < kc, lb = H::M - s * H::NTH < kc || km < kc;
+      double2 x = la ? a[j].v : zero2(), xm = lb ? b[j].v : zero2();
+      if (s == 0 && k == 0) x.y = 0.0;
       v[s] = comb(x, xm, s);
-      x = k < g.kc ? sz.val(a[j], k, g) : zero2();
-      xm = km < g.kc ? sz.val(b[j], km, g) : zero2();
-      if (k == 0) x.y = 0.0;
+      x = la ? sz.val(a[j], k, g) : zero2();
+      xm = lb ? sz.val(b[j], km, g) : zero2();
+      if (s == 0 && k == 0) x.y = 0.0;
       z[s] = comb(x, xm, s);
     }
   }
@@ -1507,10 +1523,11 @@ __device__ __forceinline__ void load_v_zeta_h(double2 (&v)[8], double2 (&z)[8], 
 
 // r2c output of one real field from v[s] = Z[t + s NTH]: emit(k, s, X[k]) for
 // live k (one LDS round trip for the mirrors Z[M - k])
-template <int LOG2N, typename Emit>
+template <int LOG2N, int KC = 0, typename Emit>
 __device__ __forceinline__ void split_real_h(const double2 (&v)[8], int t, const Geom& g, double2* line,
                                              double2 wt, Emit emit) {
   using H = RowH<LOG2N>;
+  const int kc = live_kc<KC>(g);
   asm volatile("" : "+v"(t), "+v"(wt.x), "+v"(wt.y));
   lds_barrier();  // previous LDS readers are done
 #pragma unroll
@@ -1519,7 +1536,7 @@ __device__ __forceinline__ void split_real_h(const double2 (&v)[8], int t, const
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
     const int k = t + s * H::NTH;
-    if (s * H::NTH < g.kc && k < g.kc) {
+    if (s * H::NTH < kc && ((s + 1) * H::NTH <= kc || k < kc)) {
       const double2 zk = v[s];
       const double2 zn = line[LP<H::LM>((H::M - k) & (H::M - 1))];
       const double2 E = make_double2(0.5 * (zk.x + zn.x), 0.5 * (zk.y - zn.y));
@@ -1552,7 +1569,7 @@ template <int NB>
 __device__ __forceinline__ int rowh_row(int b, int nb, int ln) {
   return NB == 1 ? col_of_block(b, nb) : row0_of_block<NB>(b, nb) + ln;
 }
-template <int LOG2N>
+template <int LOG2N, int KC = 0>
 static __global__ void __launch_bounds__(RowH<LOG2N>::NTH * rowh_nb<LOG2N>(), SW_MINW_ROW_H)
     k_row_qg_h(Geom g, Phys p, const double2* __restrict__ Mi, double2* __restrict__ Mo,
                const double2* __restrict__ tw, int yoff) {
@@ -1587,17 +1604,17 @@ static __global__ void __launch_bounds__(RowH<LOG2N>::NTH * rowh_nb<LOG2N>(), SW
   double2 q[8], v[8];
 #pragma unroll 1
   for (int l = 0; l < 2; ++l) {
-    load_real_h<LOG2N>(q, g, t, y, SrcField{Mi + l * MF, false}, wt);
+    load_real_h<LOG2N, SrcField, KC>(q, g, t, y, SrcField{Mi + l * MF, false}, wt);
     inv(q);
 #pragma unroll 1
     for (int d = 0; d < 2; ++d) {  // ψx q (:169), ψy q (:177)
-      load_real_h<LOG2N>(v, g, t, y, SrcField{Mi + (d == 0 ? 2 + l : 4 + l) * MF, d == 0}, wt);
+      load_real_h<LOG2N, SrcField, KC>(v, g, t, y, SrcField{Mi + (d == 0 ? 2 + l : 4 + l) * MF, d == 0}, wt);
       inv(v);
 #pragma unroll
       for (int s = 0; s < 8; ++s) v[s] = make_double2(v[s].x * q[s].x, v[s].y * q[s].y);
       fwd(v);
       double2* O = Mo + (2 * d + l) * MF;
-      split_real_h<LOG2N>(v, t, g, smem, wt, [&](int k, int, double2 X) { O[H::fwd(g, k, y)] = X; });
+      split_real_h<LOG2N, KC>(v, t, g, smem, wt, [&](int k, int, double2 X) { O[H::fwd(g, k, y)] = X; });
     }
   }
 }
@@ -1624,7 +1641,7 @@ __host__ __device__ constexpr int rowh_nb() {
   else
     return SW_ROWH_NB;
 }
-template <int LOG2N>
+template <int LOG2N, int KC = 0>
 static __global__ void __launch_bounds__((RowH<LOG2N>::NTH * rowh_nb<LOG2N, true>()), SW_MINW_ROW_RSW_H)
     k_row_rsw_h(Geom g, Phys p, const double2* __restrict__ Mi, double2* __restrict__ Mo,
                 const double2* __restrict__ tw, int yoff) {
@@ -1662,17 +1679,17 @@ static __global__ void __launch_bounds__((RowH<LOG2N>::NTH * rowh_nb<LOG2N, true
   const long long MF = g.mfield;
   const double2 *U = Mi, *V = Mi + MF, *Hh = Mi + 2 * MF, *Uy = Mi + 3 * MF;
   double2 u[8], v[8], e[8], w[8];
-  load_real_h<LOG2N>(u, g, t, y, SrcField{U, false}, wt);
+  load_real_h<LOG2N, SrcField, KC>(u, g, t, y, SrcField{U, false}, wt);
   inv(u);
   if constexpr (SW_RSW_ROWH_ZPARK) {
-    load_v_zeta_h<LOG2N>(v, e, g, t, y, V, Uy, wt);
+    load_v_zeta_h<LOG2N, KC>(v, e, g, t, y, V, Uy, wt);
 #pragma unroll
     for (int s = 0; s < 8; ++s) park[t + s * H::NTH] = e[s];  // read back by this thread only
   } else {
-    load_real_h<LOG2N>(v, g, t, y, SrcField{V, false}, wt);
+    load_real_h<LOG2N, SrcField, KC>(v, g, t, y, SrcField{V, false}, wt);
   }
   inv(v);
-  load_real_h<LOG2N>(e, g, t, y, SrcField{Hh, false}, wt);
+  load_real_h<LOG2N, SrcField, KC>(e, g, t, y, SrcField{Hh, false}, wt);
   inv(e);
   auto prod = [&](const double2 (&a)[8], const double2 (&b)[8]) {
 #pragma unroll
@@ -1681,37 +1698,37 @@ static __global__ void __launch_bounds__((RowH<LOG2N>::NTH * rowh_nb<LOG2N, true
   // 4: (vη)^
   prod(v, e);
   fwd(w, NoPre{});
-  split_real_h<LOG2N>(w, t, g, smem, wt, [&](int k, int, double2 X) { Mo[4 * MF + H::fwd(g, k, y)] = X; });
+  split_real_h<LOG2N, KC>(w, t, g, smem, wt, [&](int k, int, double2 X) { Mo[4 * MF + H::fwd(g, k, y)] = X; });
   // 3: Q = -ik (uη)^
   prod(u, e);
   fwd(w, Pre{});
-  split_real_h<LOG2N>(w, t, g, smem, wt,
+  split_real_h<LOG2N, KC>(w, t, g, smem, wt,
                       [&](int k, int, double2 X) { Mo[3 * MF + H::fwd(g, k, y)] = cmul_i(X, -(k * g.mk)); });
   // ζ = vx - uy in η's registers
   if constexpr (SW_RSW_ROWH_ZPARK) {
 #pragma unroll
     for (int s = 0; s < 8; ++s) e[s] = park[t + s * H::NTH];
   } else {
-    load_real_h<LOG2N>(e, g, t, y, SrcZeta{V, Uy}, wt);
+    load_real_h<LOG2N, SrcZeta, KC>(e, g, t, y, SrcZeta{V, Uy}, wt);
   }
   inv(e);
   // 2: (ζu)^
   prod(e, u);
   fwd(w, NoPre{});
-  split_real_h<LOG2N>(w, t, g, smem, wt, [&](int k, int, double2 X) { Mo[2 * MF + H::fwd(g, k, y)] = X; });
+  split_real_h<LOG2N, KC>(w, t, g, smem, wt, [&](int k, int, double2 X) { Mo[2 * MF + H::fwd(g, k, y)] = X; });
   // 1: K̂, K = (u² + v²)/2; kept in u
 #pragma unroll
   for (int s = 0; s < 8; ++s)
     w[s] = make_double2(0.5 * (u[s].x * u[s].x + v[s].x * v[s].x), 0.5 * (u[s].y * u[s].y + v[s].y * v[s].y));
   fwd(w, Pre{});
-  split_real_h<LOG2N>(w, t, g, smem, wt, [&](int k, int s, double2 X) {
+  split_real_h<LOG2N, KC>(w, t, g, smem, wt, [&](int k, int s, double2 X) {
     Mo[MF + H::fwd(g, k, y)] = X;
     u[s] = X;
   });
   // 0: P = -ik K̂ + (ζv)^
   prod(e, v);
   fwd(w, Pre{});
-  split_real_h<LOG2N>(w, t, g, smem, wt,
+  split_real_h<LOG2N, KC>(w, t, g, smem, wt,
                       [&](int k, int s, double2 X) { Mo[H::fwd(g, k, y)] = cadd(cmul_i(u[s], -(k * g.mk)), X); });
 }
 
@@ -3346,6 +3363,20 @@ static bool row_prunable(const Geom& g) {
   return SW_ROW_PRUNE && roww<L>() > 0 && 8 * g.kc <= 3 * g.nx;
 }
 
+// the half rows with the live band at compile time (live_kc): the 2/3 rule's
+// kc = nx/3 (SW_ROWH_KC=0: never, A/B).  Static VALU −20..−22 %, v_cndmask
+// 355 → 166 (2LQG 8192) / 613 → 326 (RSW 4096); measured (tools/ab/r6_rowkc.sh,
+// three interleaved rounds, bitwise equal): config 5 row 1598-1603 → 1545-1578
+// µs (70.9 → 71.4-72.1 steps/s), config 4 row 360-362 → 356-357 µs
+// (1349 → 1355)
+#ifndef SW_ROWH_KC
+#define SW_ROWH_KC 1
+#endif
+template <int L>
+static bool rowh_kc(const Geom& g) {
+  return SW_ROWH_KC && g.kc == (1 << L) / 3;
+}
+
 template <int L>
 void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, double2* Mo, const double2* tw,
                     hipStream_t s, int y0, int nrows, double2* Ma) {
@@ -3359,9 +3390,14 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
   if (model == MODEL_RSW) {
     constexpr int nbr = rowh_nb<L, true>();
     if constexpr (rsw_row_half<L>()) {
-      SW_LAUNCH((k_row_rsw_h<L>), dim3(nrows / nbr), dim3(RowH<L>::NTH * nbr),
-                         nbr * rsw_rowh_lines<L>() * FftPlan<L - 1>::LDS * sizeof(double2), s, g, p, Mi, Mo,
-                         tw, y0);
+      if (rowh_kc<L>(g))
+        SW_LAUNCH((k_row_rsw_h<L, (1 << L) / 3>), dim3(nrows / nbr), dim3(RowH<L>::NTH * nbr),
+                           nbr * rsw_rowh_lines<L>() * FftPlan<L - 1>::LDS * sizeof(double2), s, g, p, Mi, Mo,
+                           tw, y0);
+      else
+        SW_LAUNCH((k_row_rsw_h<L>), dim3(nrows / nbr), dim3(RowH<L>::NTH * nbr),
+                           nbr * rsw_rowh_lines<L>() * FftPlan<L - 1>::LDS * sizeof(double2), s, g, p, Mi, Mo,
+                           tw, y0);
       return;
     }
     if constexpr (roww<L>() > 0 && BR::NB == 1) {
@@ -3407,8 +3443,12 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
     SW_LAUNCH((k_row<MODEL_QG2, L, true>), dim3(nrows / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p, Mi,
                        Mo, tw, y0, Ma);
   } else if constexpr (qg_row_half<L>()) {
-    SW_LAUNCH((k_row_qg_h<L>), dim3(nrows / rowh_nb<L>()), dim3(RowH<L>::NTH * rowh_nb<L>()),
-                       rowh_nb<L>() * FftPlan<L - 1>::LDS * sizeof(double2), s, g, p, Mi, Mo, tw, y0);
+    if (rowh_kc<L>(g))
+      SW_LAUNCH((k_row_qg_h<L, (1 << L) / 3>), dim3(nrows / rowh_nb<L>()), dim3(RowH<L>::NTH * rowh_nb<L>()),
+                         rowh_nb<L>() * FftPlan<L - 1>::LDS * sizeof(double2), s, g, p, Mi, Mo, tw, y0);
+    else
+      SW_LAUNCH((k_row_qg_h<L>), dim3(nrows / rowh_nb<L>()), dim3(RowH<L>::NTH * rowh_nb<L>()),
+                         rowh_nb<L>() * FftPlan<L - 1>::LDS * sizeof(double2), s, g, p, Mi, Mo, tw, y0);
   } else if (row_prunable<L>(g)) {
     SW_LAUNCH((k_row<MODEL_QG2, L, false, true>), dim3(nrows / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p,
                        Mi, Mo, tw, y0, nullptr);
