@@ -922,13 +922,18 @@ __host__ __device__ constexpr bool row_fly() {
 // instead of five); Thomas–Yamada grid (rows, 4), the parts of its branch;
 // RSW (two line buffers, undecimated lines) grid (rows, 2), the two forward
 // lines apart
-template <int MODEL, int LOG2N, bool ALIAS = false, bool PRUNE = false, bool SPLIT = false>
+// KC > 0: the live band kc known at compile time (the 2/3 rule's N/3; a local
+// copy of the geometry with that kc, so every inlined helper's slot and lane
+// tests against it fold where they can — as the half rows' live_kc)
+template <int MODEL, int LOG2N, bool ALIAS = false, bool PRUNE = false, bool SPLIT = false, int KC = 0>
 static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
                                          (BlkRow<MODEL, LOG2N>::THREADS >= 1024 ? 4
                                           : (MODEL == MODEL_QG2 ? (row_fly<MODEL, LOG2N>() ? 4 : SW_MINW_ROW_QG)
                                                                 : SW_MINW_ROW)))
-    k_row(Geom g, Phys p, const double2* __restrict__ Mi, double2* __restrict__ Mo,
+    k_row(Geom g_in, Phys p, const double2* __restrict__ Mi, double2* __restrict__ Mo,
           const double2* __restrict__ tw, int yoff, double2* __restrict__ Ma) {
+  Geom g = g_in;
+  if constexpr (KC > 0) g.kc = KC;
   using Bk = BlkRow<MODEL, LOG2N>;
   extern __shared__ double2 smem[];
   const LineCtx c = line_ctx<LOG2N>();
@@ -3376,6 +3381,22 @@ template <int L>
 static bool rowh_kc(const Geom& g) {
   return SW_ROWH_KC && g.kc == (1 << L) / 3;
 }
+// the same for the full-length decimated rows (k_row<…, KC>; SW_ROW_KC=0:
+// never).  Measured (tools/ab/r6_rowkc2.sh, three interleaved rounds, bitwise
+// equal): RSW 2048 row static VALU 3362 → 2536, row 66.6-67.8 → 66.1-66.7 µs
+// (6650-6684 → 6679-6691 steps/s), 1024² neutral — kept for RSW; the 2LQG
+// row (4315 → 3574) ran slower, 69.9-72.1 → 71.5-73.5 µs: off there
+// (SW_ROW_KC_QG)
+#ifndef SW_ROW_KC
+#define SW_ROW_KC 1
+#endif
+#ifndef SW_ROW_KC_QG
+#define SW_ROW_KC_QG 0
+#endif
+template <int L>
+static bool row_kc(const Geom& g, bool qg = false) {
+  return SW_ROW_KC && (!qg || SW_ROW_KC_QG) && g.kc == (1 << L) / 3;
+}
 
 template <int L>
 void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, double2* Mo, const double2* tw,
@@ -3411,7 +3432,10 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
         return;
       }
     }
-    if (row_prunable<L>(g))
+    if (row_prunable<L>(g) && row_kc<L>(g))
+      SW_LAUNCH((k_row<MODEL_RSW, L, false, true, false, (1 << L) / 3>), dim3(nrows / BR::NB), dim3(BR::THREADS),
+                         sh_rsw, s, g, p, Mi, Mo, tw, y0, nullptr);
+    else if (row_prunable<L>(g))
       SW_LAUNCH((k_row<MODEL_RSW, L, false, true>), dim3(nrows / BR::NB), dim3(BR::THREADS), sh_rsw, s, g,
                          p, Mi, Mo, tw, y0, nullptr);
     else if (g.rsplit && row_lds_lines<MODEL_RSW, L>() == 2 && roww<L>() == 0)
@@ -3449,6 +3473,9 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
     else
       SW_LAUNCH((k_row_qg_h<L>), dim3(nrows / rowh_nb<L>()), dim3(RowH<L>::NTH * rowh_nb<L>()),
                          rowh_nb<L>() * FftPlan<L - 1>::LDS * sizeof(double2), s, g, p, Mi, Mo, tw, y0);
+  } else if (row_prunable<L>(g) && row_kc<L>(g, true)) {
+    SW_LAUNCH((k_row<MODEL_QG2, L, false, true, false, (1 << L) / 3>), dim3(nrows / BQ::NB), dim3(BQ::THREADS),
+                       sh_qg2, s, g, p, Mi, Mo, tw, y0, nullptr);
   } else if (row_prunable<L>(g)) {
     SW_LAUNCH((k_row<MODEL_QG2, L, false, true>), dim3(nrows / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p,
                        Mi, Mo, tw, y0, nullptr);
