@@ -3393,9 +3393,22 @@ static bool rowh_kc(const Geom& g) {
 #ifndef SW_ROW_KC_QG
 #define SW_ROW_KC_QG 0
 #endif
+// short (split) rows of the drivers' 512² grids, RSW and Thomas–Yamada
+// (SW_ROW_KC_SHORT).  Measured (tools/ab/r6_rowkc9.sh, three rounds, bitwise
+// equal): TYdriver 512² ETDRK4 6289-6336 → 6656-6725 steps/s (row 18.0 →
+// 16.0-16.7 µs), RSWDriver 512² IFMAB3 32210-32871 → 32848-33620
+#ifndef SW_ROW_KC_SHORT
+#define SW_ROW_KC_SHORT 1
+#endif
+// MultiLayerQG's short rows (aliased_fraction = 0: kc = nx/2; SW_ROW_KC_MLQG).
+// Measured (tools/ab/r6_rowkc_mlqg.sh, bitwise equal): TwoLayerSimulation 512²
+// FilteredRK4 7188-7251 → 7508-7607 steps/s (row 11.0-11.4 → 9.6-9.9 µs)
+#ifndef SW_ROW_KC_MLQG
+#define SW_ROW_KC_MLQG 1
+#endif
 template <int L>
-static bool row_kc(const Geom& g, bool qg = false) {
-  return SW_ROW_KC && (!qg || SW_ROW_KC_QG) && g.kc == (1 << L) / 3;
+static bool row_kc(const Geom& g, bool qg = false, bool shortrow = false) {
+  return SW_ROW_KC && (!qg || SW_ROW_KC_QG) && (!shortrow || SW_ROW_KC_SHORT) && g.kc == (1 << L) / 3;
 }
 
 template <int L>
@@ -3438,6 +3451,9 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
     else if (row_prunable<L>(g))
       SW_LAUNCH((k_row<MODEL_RSW, L, false, true>), dim3(nrows / BR::NB), dim3(BR::THREADS), sh_rsw, s, g,
                          p, Mi, Mo, tw, y0, nullptr);
+    else if (g.rsplit && row_lds_lines<MODEL_RSW, L>() == 2 && roww<L>() == 0 && row_kc<L>(g, false, true))
+      SW_LAUNCH((k_row<MODEL_RSW, L, false, false, true, (1 << L) / 3>), dim3(nrows / BR::NB, 2),
+                         dim3(BR::THREADS), sh_rsw, s, g, p, Mi, Mo, tw, y0, nullptr);
     else if (g.rsplit && row_lds_lines<MODEL_RSW, L>() == 2 && roww<L>() == 0)
       SW_LAUNCH((k_row<MODEL_RSW, L, false, false, true>), dim3(nrows / BR::NB, 2), dim3(BR::THREADS),
                          sh_rsw, s, g, p, Mi, Mo, tw, y0, nullptr);
@@ -3448,6 +3464,9 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
     if (Ma)
       SW_LAUNCH((k_row<MODEL_TY, L, true>), dim3(nrows / BT::NB), dim3(BT::THREADS), sh_ty, s, g, p, Mi,
                          Mo, tw, y0, Ma);
+    else if (g.rsplit && row_kc<L>(g, false, true))
+      SW_LAUNCH((k_row<MODEL_TY, L, false, false, true, (1 << L) / 3>), dim3(nrows / BT::NB, 4),
+                         dim3(BT::THREADS), sh_ty, s, g, p, Mi, Mo, tw, y0, nullptr);
     else if (g.rsplit)
       SW_LAUNCH((k_row<MODEL_TY, L, false, false, true>), dim3(nrows / BT::NB, 4), dim3(BT::THREADS), sh_ty,
                          s, g, p, Mi, Mo, tw, y0, nullptr);
@@ -3479,6 +3498,10 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
   } else if (row_prunable<L>(g)) {
     SW_LAUNCH((k_row<MODEL_QG2, L, false, true>), dim3(nrows / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p,
                        Mi, Mo, tw, y0, nullptr);
+  } else if (g.rsplit && SW_ROW_KC_MLQG && g.kc == (1 << L) / 2) {
+    // (aliased_fraction = 0, TwoLayerSimulation's MultiLayerQG: kc = nx/2)
+    SW_LAUNCH((k_row<MODEL_QG2, L, false, false, true, (1 << L) / 2>), dim3(nrows / BQ::NB, 2),
+                       dim3(BQ::THREADS), sh_qg2, s, g, p, Mi, Mo, tw, y0, nullptr);
   } else if (g.rsplit) {
     SW_LAUNCH((k_row<MODEL_QG2, L, false, false, true>), dim3(nrows / BQ::NB, 2), dim3(BQ::THREADS), sh_qg2,
                        s, g, p, Mi, Mo, tw, y0, nullptr);
