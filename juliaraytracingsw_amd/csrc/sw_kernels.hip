@@ -296,10 +296,35 @@ __host__ __device__ constexpr int inv_split_per() { return MODEL == MODEL_QG2 ? 
 // Thomas–Yamada and RSW (a group's one or two outputs) — so that small grids, whose
 // one-line blocks are a single wave, put 2-3 times the waves on the chip (the
 // same arithmetic per output; Geom::isplit, sw_api.cpp make_geom)
-template <int MODEL, int LOG2N, bool SPLIT = false>
+// The column kernels' live-row band at compile time (round 6): BAND = 1 the
+// 2/3 rule (lc = N/3, lr2 = N − N/3 for every power-of-two column), 2
+// aliased_fraction = 0 (lc = N/2, lr2 = N/2 + 1), 0 the run-time g.lc, g.lr2.
+// A local copy of the geometry carries the constants into every inlined
+// helper (compact_of, the slot tests), so wholly live or dead slots resolve at
+// compile time.  Measured (tools/ab/r6_band.sh, 512² drivers' grids, three
+// interleaved rounds, bitwise equal): RSWDriver IFMAB3 33157-33375 →
+// 34548-34702 steps/s, TYdriver ETDRK4 6765-6791 → 6891-6931, TwoLayerSimulation
+// FilteredRK4 7480-7576 → 7586-7693.  SW_COL_BAND=0: never (A/B).
+#ifndef SW_COL_BAND
+#define SW_COL_BAND 1
+#endif
+template <int LOG2N, int BAND>
+__device__ __forceinline__ void band_fix(Geom& g) {
+  constexpr int N = 1 << LOG2N;
+  if constexpr (BAND == 1) {
+    g.lc = N / 3;
+    g.lr2 = N - N / 3;
+  } else if constexpr (BAND == 2) {
+    g.lc = N / 2;
+    g.lr2 = N / 2 + 1;
+  }
+}
+
+template <int MODEL, int LOG2N, bool SPLIT = false, int BAND = 0>
 static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, LOG2N))
     k_col_inv(Geom g, Phys p, const double2* __restrict__ X, double2* __restrict__ M,
               const double2* __restrict__ tw, int gbase) {
+  band_fix<LOG2N, BAND>(g);
   using B = Blk<LOG2N>;
   constexpr int NT = B::NT;
   extern __shared__ double2 smem[];
@@ -1826,11 +1851,12 @@ __device__ __forceinline__ double2 ty_linear_terms(const double2* __restrict__ X
 // term of N_f (nterms) per block — its transform and multiplier, no sum and
 // no linear terms — into N (term 0), T1 or T2; the update that consumes N
 // adds them in k_col_fwd's order (assemble_terms): bitwise the same N
-template <int MODEL, int LOG2N, bool SPLIT = false>
+template <int MODEL, int LOG2N, bool SPLIT = false, int BAND = 0>
 static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW_M(MODEL, LOG2N))
     k_col_fwd(Geom g, Phys p, const double2* __restrict__ Mf, double2* __restrict__ N,
               const double2* __restrict__ X, const double2* __restrict__ tw, int gbase,
               double2* __restrict__ T1, double2* __restrict__ T2) {
+  band_fix<LOG2N, BAND>(g);
   using B = Blk<LOG2N>;
   constexpr int NT = B::NT;
   extern __shared__ double2 smem[];
@@ -2451,10 +2477,11 @@ static __global__ void __launch_bounds__(256) k_step_elem(Geom g, Phys p, StepPt
 // INV = false: forward + update only (k_col_fwd + k_step_elem in one pass, N
 // never in HBM); the next calcN's k_col_inv runs separately.  STREAM: the
 // state/history cache policy of k_step_elem (StepPtrs::stream).
-template <int MODEL, int LOG2N, int OP, bool INV = true, bool STREAM = false>
+template <int MODEL, int LOG2N, int OP, bool INV = true, bool STREAM = false, int BAND = 0>
 static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
     k_col_step(Geom g, Phys p, StepPtrs a, const double2* __restrict__ Mf,
                double2* __restrict__ Minv, const double2* __restrict__ tw) {
+  band_fix<LOG2N, BAND>(g);
   using B = Blk<LOG2N>;
   constexpr int NT = B::NT;
   constexpr int NF = MODEL == MODEL_RSW ? 3 : 2;
@@ -2716,10 +2743,11 @@ static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, SW_MINW(LOG2N))
 #ifndef SW_MINW_CS
 #define SW_MINW_CS 2
 #endif
-template <int LOG2N, bool STREAM>
+template <int LOG2N, bool STREAM, int BAND = 0>
 static __global__ void __launch_bounds__(Blk<LOG2N>::THREADS, (Blk<LOG2N>::THREADS >= 512 ? 4 : SW_MINW_CS))
     k_col_step_fab3_rsw(Geom g, Phys p, StepPtrs a, const double2* __restrict__ Mf,
                         double2* __restrict__ Minv, const double2* __restrict__ tw, int fbase) {
+  band_fix<LOG2N, BAND>(g);
   using B = Blk<LOG2N>;
   constexpr int NT = B::NT;
   extern __shared__ double2 smem[];
@@ -3182,6 +3210,31 @@ static __global__ void k_absmax(const double* __restrict__ f, long long n, unsig
 // of one transform length per translation unit (-DSW_PART=L, L = 5 … 13), the
 // rest and the dispatch in SW_PART=0; without SW_PART one TU holds all.
 #if !defined(SW_PART) || SW_PART > 0
+// the column kernels' band (band_fix): 1 the 2/3 rule, 2 aliased_fraction = 0
+template <int L>
+static int band_of(const Geom& g) {
+  constexpr int N = 1 << L;
+  if (!SW_COL_BAND) return 0;
+  if (g.lc == N / 3 && g.lr2 == N - N / 3) return 1;
+  if (g.lc == N / 2 && g.lr2 == N / 2 + 1) return 2;
+  return 0;
+}
+// SW_LAUNCH of a kernel template expression naming SWB, the band, for the
+// band BV (one instantiation per band)
+#define SW_LAUNCH_BAND(BV, KEXPR, ...)                     \
+  do {                                                     \
+    if ((BV) == 1) {                                       \
+      constexpr int SWB = 1;                               \
+      SW_LAUNCH(KEXPR, __VA_ARGS__);                       \
+    } else if ((BV) == 2) {                                \
+      constexpr int SWB = 2;                               \
+      SW_LAUNCH(KEXPR, __VA_ARGS__);                       \
+    } else {                                               \
+      constexpr int SWB = 0;                               \
+      SW_LAUNCH(KEXPR, __VA_ARGS__);                       \
+    }                                                      \
+  } while (0)
+
 template <int L>
 static int col_blocks(const Geom& g) {
   return (g.kcl + Blk<L>::NB - 1) / Blk<L>::NB;
@@ -3206,32 +3259,33 @@ static size_t lds_bytes() {
 template <int L>
 void LenOps<L>::col_inv(int model, const Geom& g, const Phys& p, const double2* X, double2* M, const double2* tw,
                         hipStream_t s, int g0, int ng) {
+  const int bnd = band_of<L>(g);
   const dim3 grid(col_blocks<L>(g), ng);
   const dim3 grid2(col_blocks<L>(g), 2 * ng);
   if (model == MODEL_RSW && g.isplit)
-    SW_LAUNCH((k_col_inv<MODEL_RSW, L, true>), grid2, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M,
+    SW_LAUNCH_BAND(bnd, (k_col_inv<MODEL_RSW, L, true, SWB>), grid2, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M,
                        tw, g0);
   else if (model == MODEL_RSW)
-    SW_LAUNCH((k_col_inv<MODEL_RSW, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
+    SW_LAUNCH_BAND(bnd, (k_col_inv<MODEL_RSW, L, false, SWB>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
   else if (model == MODEL_RSWA && g.isplit)
-    SW_LAUNCH((k_col_inv<MODEL_RSWA, L, true>), grid2, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M,
+    SW_LAUNCH_BAND(bnd, (k_col_inv<MODEL_RSWA, L, true, SWB>), grid2, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M,
                        tw, g0);
   else if (model == MODEL_RSWA)
-    SW_LAUNCH((k_col_inv<MODEL_RSWA, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
+    SW_LAUNCH_BAND(bnd, (k_col_inv<MODEL_RSWA, L, false, SWB>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
   else if (model == MODEL_TY && g.isplit)
-    SW_LAUNCH((k_col_inv<MODEL_TY, L, true>), dim3(col_blocks<L>(g), 2 * ng), dim3(Blk<L>::THREADS),
+    SW_LAUNCH_BAND(bnd, (k_col_inv<MODEL_TY, L, true, SWB>), dim3(col_blocks<L>(g), 2 * ng), dim3(Blk<L>::THREADS),
                        lds_bytes<L>(), s, g, p, X, M, tw, g0);
   else if (model == MODEL_TY)
-    SW_LAUNCH((k_col_inv<MODEL_TY, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
+    SW_LAUNCH_BAND(bnd, (k_col_inv<MODEL_TY, L, false, SWB>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
   else if (g0 == 0 && ng == 2 && Blk<L>::NB == 1 && g.kcl % 64 == 0 &&
            (SW_QG_INV_PAIR == 2 || (SW_QG_INV_PAIR == 1 && L >= 13)))
-    SW_LAUNCH((k_col_inv<MODEL_QG2, L>), dim3(2 * g.kcl), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X,
+    SW_LAUNCH_BAND(bnd, (k_col_inv<MODEL_QG2, L, false, SWB>), dim3(2 * g.kcl), dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X,
                        M, tw, -1);
   else if (g.isplit)
-    SW_LAUNCH((k_col_inv<MODEL_QG2, L, true>), dim3(col_blocks<L>(g), 3 * ng), dim3(Blk<L>::THREADS),
+    SW_LAUNCH_BAND(bnd, (k_col_inv<MODEL_QG2, L, true, SWB>), dim3(col_blocks<L>(g), 3 * ng), dim3(Blk<L>::THREADS),
                        lds_bytes<L>(), s, g, p, X, M, tw, g0);
   else
-    SW_LAUNCH((k_col_inv<MODEL_QG2, L>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
+    SW_LAUNCH_BAND(bnd, (k_col_inv<MODEL_QG2, L, false, SWB>), grid, dim3(Blk<L>::THREADS), lds_bytes<L>(), s, g, p, X, M, tw, g0);
 }
 
 // ===========================================================================
@@ -3531,21 +3585,22 @@ void LenOps<L>::col_fwd(int model, const Geom& g, const Phys& p, const double2* 
                         const double2* tw, hipStream_t s, int f0, int nfl, double2* T1, double2* T2) {
   const dim3 grid(col_blocks<L>(g), nfl), grid3(col_blocks<L>(g), 3 * nfl), blk(Blk<L>::THREADS);
   const size_t sh = lds_bytes<L>();
+  const int bnd = band_of<L>(g);
   const bool split = T1 != nullptr;  // (RSW, 2LQG / MultiLayerQG, Thomas–Yamada)
   if (model == MODEL_RSW && split)
-    SW_LAUNCH((k_col_fwd<MODEL_RSW, L, true>), grid3, blk, sh, s, g, p, Mf, N, X, tw, f0, T1, T2);
+    SW_LAUNCH_BAND(bnd, (k_col_fwd<MODEL_RSW, L, true, SWB>), grid3, blk, sh, s, g, p, Mf, N, X, tw, f0, T1, T2);
   else if (model == MODEL_RSW)
-    SW_LAUNCH((k_col_fwd<MODEL_RSW, L>), grid, blk, sh, s, g, p, Mf, N, X, tw, f0, nullptr, nullptr);
+    SW_LAUNCH_BAND(bnd, (k_col_fwd<MODEL_RSW, L, false, SWB>), grid, blk, sh, s, g, p, Mf, N, X, tw, f0, nullptr, nullptr);
   else if (model == MODEL_RSWA)
-    SW_LAUNCH((k_col_fwd<MODEL_RSWA, L>), grid, blk, sh, s, g, p, Mf, N, X, tw, f0, nullptr, nullptr);
+    SW_LAUNCH_BAND(bnd, (k_col_fwd<MODEL_RSWA, L, false, SWB>), grid, blk, sh, s, g, p, Mf, N, X, tw, f0, nullptr, nullptr);
   else if (model == MODEL_TY && split)
-    SW_LAUNCH((k_col_fwd<MODEL_TY, L, true>), grid3, blk, sh, s, g, p, Mf, N, X, tw, f0, T1, T2);
+    SW_LAUNCH_BAND(bnd, (k_col_fwd<MODEL_TY, L, true, SWB>), grid3, blk, sh, s, g, p, Mf, N, X, tw, f0, T1, T2);
   else if (model == MODEL_TY)
-    SW_LAUNCH((k_col_fwd<MODEL_TY, L>), grid, blk, sh, s, g, p, Mf, N, X, tw, f0, nullptr, nullptr);
+    SW_LAUNCH_BAND(bnd, (k_col_fwd<MODEL_TY, L, false, SWB>), grid, blk, sh, s, g, p, Mf, N, X, tw, f0, nullptr, nullptr);
   else if (split)
-    SW_LAUNCH((k_col_fwd<MODEL_QG2, L, true>), grid3, blk, sh, s, g, p, Mf, N, X, tw, f0, T1, T2);
+    SW_LAUNCH_BAND(bnd, (k_col_fwd<MODEL_QG2, L, true, SWB>), grid3, blk, sh, s, g, p, Mf, N, X, tw, f0, T1, T2);
   else
-    SW_LAUNCH((k_col_fwd<MODEL_QG2, L>), grid, blk, sh, s, g, p, Mf, N, X, tw, f0, nullptr, nullptr);
+    SW_LAUNCH_BAND(bnd, (k_col_fwd<MODEL_QG2, L, false, SWB>), grid, blk, sh, s, g, p, Mf, N, X, tw, f0, nullptr, nullptr);
 }
 
 template <int L>
@@ -3572,9 +3627,11 @@ void LenOps<L>::col_step(int model, int op, const Geom& g, const Phys& p, const 
       const bool one = all && Blk<L>::NB == 1 && g.kcl % 64 == 0;
       const dim3 gr = one ? dim3(3 * g.kcl) : dim3(col_blocks<L>(g), nfl);
       if (a.stream)
-        SW_LAUNCH((k_col_step_fab3_rsw<L, true>), gr, blk, sh, s, g, p, a, Mf, Minv, tw, one ? -1 : f0);
+        SW_LAUNCH_BAND(band_of<L>(g), (k_col_step_fab3_rsw<L, true, SWB>), gr, blk, sh, s, g, p, a, Mf, Minv, tw,
+                       one ? -1 : f0);
       else
-        SW_LAUNCH((k_col_step_fab3_rsw<L, false>), gr, blk, sh, s, g, p, a, Mf, Minv, tw, one ? -1 : f0);
+        SW_LAUNCH_BAND(band_of<L>(g), (k_col_step_fab3_rsw<L, false, SWB>), gr, blk, sh, s, g, p, a, Mf, Minv, tw,
+                       one ? -1 : f0);
     } else if (op == OP_IFMAB3) SW_CS(MODEL_RSW, OP_IFMAB3);
     else SW_CS(MODEL_RSW, OP_RK4);
   } else {
