@@ -301,10 +301,12 @@ __host__ __device__ constexpr int inv_split_per() { return MODEL == MODEL_QG2 ? 
 // aliased_fraction = 0 (lc = N/2, lr2 = N/2 + 1), 0 the run-time g.lc, g.lr2.
 // A local copy of the geometry carries the constants into every inlined
 // helper (compact_of, the slot tests), so wholly live or dead slots resolve at
-// compile time.  Measured (tools/ab/r6_band.sh, 512² drivers' grids, three
-// interleaved rounds, bitwise equal): RSWDriver IFMAB3 33157-33375 →
-// 34548-34702 steps/s, TYdriver ETDRK4 6765-6791 → 6891-6931, TwoLayerSimulation
-// FilteredRK4 7480-7576 → 7586-7693.  SW_COL_BAND=0: never (A/B).
+// compile time.  Measured (tools/ab/r6_colband.sh, two interleaved rounds,
+// bitwise equal on eight configurations): RSWDriver 512² IFMAB3 33077-33173 →
+// 34640-34648 steps/s, TYdriver 512² 6797-6818 → 6920-6925, TwoLayerSimulation
+// 512² 7518-7604 → 7664-7682, the headline 6570-6587 → 6597-6622 (col_step
+// −1 µs), config 3 5662-5674 → 5715-5718, config 5 71.6 → 71.8-72.3 (col_inv
+// 887 → 853 µs).  SW_COL_BAND=0: never (A/B).
 #ifndef SW_COL_BAND
 #define SW_COL_BAND 1
 #endif
