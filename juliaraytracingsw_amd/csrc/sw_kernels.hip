@@ -960,7 +960,13 @@ static __global__ void __launch_bounds__((BlkRow<MODEL, LOG2N>::THREADS),
     k_row(Geom g_in, Phys p, const double2* __restrict__ Mi, double2* __restrict__ Mo,
           const double2* __restrict__ tw, int yoff, double2* __restrict__ Ma) {
   Geom g = g_in;
-  if constexpr (KC > 0) g.kc = KC;
+  // (KC is launched only on one slab: the closed-form tile offsets, no slab
+  // division — tools/ab/r6_slab1.sh: RSW 2048 row 65.7-66.7 → 64.0-65.2 µs,
+  // the drivers' 512² rows +1.3..+2.5 %)
+  if constexpr (KC > 0) {
+    g.kc = KC;
+    g.nslab = 1;
+  }
   using Bk = BlkRow<MODEL, LOG2N>;
   extern __shared__ double2 smem[];
   const LineCtx c = line_ctx<LOG2N>();
@@ -1603,8 +1609,12 @@ __device__ __forceinline__ int rowh_row(int b, int nb, int ln) {
 }
 template <int LOG2N, int KC = 0>
 static __global__ void __launch_bounds__(RowH<LOG2N>::NTH * rowh_nb<LOG2N>(), SW_MINW_ROW_H)
-    k_row_qg_h(Geom g, Phys p, const double2* __restrict__ Mi, double2* __restrict__ Mo,
+    k_row_qg_h(Geom g_in, Phys p, const double2* __restrict__ Mi, double2* __restrict__ Mo,
                const double2* __restrict__ tw, int yoff) {
+  // (KC is launched only on one slab, but telling the half rows so — their
+  // slab-division paths compiled out — measured slower: config 5 row
+  // 1550-1595 → 1626-1632 µs, tools/ab/r6_slab1.sh)
+  const Geom& g = g_in;
   using H = RowH<LOG2N>;
   constexpr int NB = rowh_nb<LOG2N>();
   extern __shared__ double2 smem_all[];
@@ -1675,8 +1685,12 @@ __host__ __device__ constexpr int rowh_nb() {
 }
 template <int LOG2N, int KC = 0>
 static __global__ void __launch_bounds__((RowH<LOG2N>::NTH * rowh_nb<LOG2N, true>()), SW_MINW_ROW_RSW_H)
-    k_row_rsw_h(Geom g, Phys p, const double2* __restrict__ Mi, double2* __restrict__ Mo,
+    k_row_rsw_h(Geom g_in, Phys p, const double2* __restrict__ Mi, double2* __restrict__ Mo,
                 const double2* __restrict__ tw, int yoff) {
+  // (KC is launched only on one slab, but telling the half rows so — their
+  // slab-division paths compiled out — measured slower: config 5 row
+  // 1550-1595 → 1626-1632 µs, tools/ab/r6_slab1.sh)
+  const Geom& g = g_in;
   using H = RowH<LOG2N>;
   constexpr int NB = rowh_nb<LOG2N, true>();
   extern __shared__ double2 smem_all[];
@@ -3435,7 +3449,7 @@ static bool row_prunable(const Geom& g) {
 #endif
 template <int L>
 static bool rowh_kc(const Geom& g) {
-  return SW_ROWH_KC && g.kc == (1 << L) / 3;
+  return SW_ROWH_KC && g.nslab == 1 && g.kc == (1 << L) / 3;
 }
 // the same for the full-length decimated rows (k_row<…, KC>; SW_ROW_KC=0:
 // never).  Measured (tools/ab/r6_rowkc2.sh, three interleaved rounds, bitwise
@@ -3464,7 +3478,7 @@ static bool rowh_kc(const Geom& g) {
 #endif
 template <int L>
 static bool row_kc(const Geom& g, bool qg = false, bool shortrow = false) {
-  return SW_ROW_KC && (!qg || SW_ROW_KC_QG) && (!shortrow || SW_ROW_KC_SHORT) && g.kc == (1 << L) / 3;
+  return SW_ROW_KC && g.nslab == 1 && (!qg || SW_ROW_KC_QG) && (!shortrow || SW_ROW_KC_SHORT) && g.kc == (1 << L) / 3;
 }
 
 template <int L>
@@ -3554,7 +3568,7 @@ void LenOps<L>::row(int model, const Geom& g, const Phys& p, const double2* Mi, 
   } else if (row_prunable<L>(g)) {
     SW_LAUNCH((k_row<MODEL_QG2, L, false, true>), dim3(nrows / BQ::NB), dim3(BQ::THREADS), sh_qg2, s, g, p,
                        Mi, Mo, tw, y0, nullptr);
-  } else if (g.rsplit && SW_ROW_KC_MLQG && g.kc == (1 << L) / 2) {
+  } else if (g.rsplit && SW_ROW_KC_MLQG && g.nslab == 1 && g.kc == (1 << L) / 2) {
     // (aliased_fraction = 0, TwoLayerSimulation's MultiLayerQG: kc = nx/2)
     SW_LAUNCH((k_row<MODEL_QG2, L, false, false, true, (1 << L) / 2>), dim3(nrows / BQ::NB, 2),
                        dim3(BQ::THREADS), sh_qg2, s, g, p, Mi, Mo, tw, y0, nullptr);
