@@ -3455,13 +3455,15 @@ static bool rowh_kc(const Geom& g) {
 // never).  Measured (tools/ab/r6_rowkc2.sh, three interleaved rounds, bitwise
 // equal): RSW 2048 row static VALU 3362 → 2536, row 66.6-67.8 → 66.1-66.7 µs
 // (6650-6684 → 6679-6691 steps/s), 1024² neutral — kept for RSW; the 2LQG
-// row (4315 → 3574) ran slower, 69.9-72.1 → 71.5-73.5 µs: off there
-// (SW_ROW_KC_QG)
+// row (4315 → 3574) ran slower, 69.9-72.1 → 71.5-73.5 µs; with the slab
+// paths compiled out as well (k_row's KC variants since) it runs level to
+// slightly faster, 71.7-73.3 → 71.1-72.3 µs, config 3 5795-5858 → 5829-5876
+// (tools/ab/r6_qgkc.sh, bitwise equal): on (SW_ROW_KC_QG)
 #ifndef SW_ROW_KC
 #define SW_ROW_KC 1
 #endif
 #ifndef SW_ROW_KC_QG
-#define SW_ROW_KC_QG 0
+#define SW_ROW_KC_QG 1
 #endif
 // short (split) rows of the drivers' 512² grids, RSW and Thomas–Yamada
 // (SW_ROW_KC_SHORT).  Measured (tools/ab/r6_rowkc9.sh, three rounds, bitwise
